@@ -1,0 +1,405 @@
+// capi.hip -- context, launch plan and the extern "C" boundary of the MSM engine.
+//
+// Boundary: halo2 `best_multiexp` ([3P], /root/reference/examples/
+// simple-example.rs:606,620,638-640,702,722); see include/pasta_msm.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/pasta_msm.h"
+#include "curve.hpp"
+#include "runtime.hpp"
+
+using namespace pm;
+
+// ------------------------------------------------------------------ errors
+namespace pm {
+thread_local std::string g_last_error;
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+}  // namespace pm
+
+// ------------------------------------------------------------------ context
+int pm::Buf::ensure(size_t bytes) {
+  if (bytes <= cap) return PM_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  size_t want = std::max<size_t>(bytes, 256);
+  hipError_t e = hipMalloc(&p, want);
+  if (e != hipSuccess) {
+    p = nullptr;
+    return set_error(PM_ERR_HIP, std::string("hipMalloc(") + std::to_string(want) + "): " + hipGetErrorString(e));
+  }
+  cap = want;
+  return PM_OK;
+}
+void pm::Buf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+}
+
+pm_ctx::~pm_ctx() {
+  (void)hipSetDevice(device);
+  for (pm::Buf* b : all_bufs()) b->release();
+  if (h_pinned) (void)hipHostFree(h_pinned);
+  for (auto& e : ev_pool) (void)hipEventDestroy(e);
+  if (own_stream) (void)hipStreamDestroy(own_stream);
+}
+
+int pm_ctx::begin_call() {
+  HIP_TRY(hipSetDevice(device));
+  pending.clear();
+  ev_used = 0;
+  return PM_OK;
+}
+
+hipEvent_t pm_ctx::next_event() {
+  if (ev_used == ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    ev_pool.push_back(e);
+  }
+  return ev_pool[ev_used++];
+}
+
+void pm_ctx::mark(const char* name, hipEvent_t a, hipEvent_t b) { pending.push_back({name, a, b}); }
+
+int pm_ctx::end_call() {
+  // called after the stream has been synchronised
+  for (auto& p : pending) {
+    float ms = 0.f;
+    if (p.a && p.b && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      auto& s = stats[p.name];
+      s.first += 1;
+      s.second += ms;
+    }
+  }
+  pending.clear();
+  return PM_OK;
+}
+
+int pm_ctx::ensure_pinned(size_t bytes) {
+  if (bytes <= h_pinned_cap) return PM_OK;
+  if (h_pinned) (void)hipHostFree(h_pinned);
+  h_pinned = nullptr;
+  h_pinned_cap = 0;
+  HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocDefault));
+  h_pinned_cap = bytes;
+  return PM_OK;
+}
+
+// ------------------------------------------------------------------- plan
+namespace pm {
+
+static int bit_length(uint32_t v) {
+  int b = 0;
+  while (v) {
+    b++;
+    v >>= 1;
+  }
+  return b;
+}
+
+MsmPlan make_plan(size_t n, int c_override) {
+  MsmPlan pl;
+  int lg = bit_length((uint32_t)std::max<size_t>(n, 1)) - 1;
+  int c = c_override > 0 ? c_override : std::max(4, std::min(18, lg - 4));
+  c = std::max(kMinC, std::min(kMaxC, c));
+  pl.c = c;
+  pl.W = (256 + c - 1) / c;
+  pl.K = 1 << (c - 1);
+  pl.L1 = std::min(16, pl.K);
+  pl.log2L1 = bit_length((uint32_t)pl.L1) - 1;
+  pl.NB = ((pl.K + 1 + pl.L1 - 1) / pl.L1) * pl.L1;
+  pl.M1 = pl.NB / pl.L1;
+  pl.NB2 = bit_length((uint32_t)(pl.M1 - 1));
+  pl.n = (uint32_t)n;
+  const size_t work = (size_t)n * pl.W;
+  const size_t target = 256 * 1024;  // lanes in flight: 256 CUs x 16 waves x 64
+  pl.chunk = (uint32_t)std::max<size_t>(16, (work + target - 1) / target);
+  pl.nthreads = (uint32_t)((work + pl.chunk - 1) / pl.chunk);
+  return pl;
+}
+
+}  // namespace pm
+
+namespace {
+
+const CurveOps* curve_ops(int curve) {
+  switch (curve) {
+    case PM_CURVE_PALLAS: return &kPallasOps;
+    case PM_CURVE_VESTA: return &kVestaOps;
+    case PM_CURVE_BN254: return &kBn254Ops;
+    default: return nullptr;
+  }
+}
+
+int dispatch_msm_device(Ctx* ctx, int curve, const void* d_s, const void* d_b, size_t n, uint32_t flags,
+                        uint64_t out[8]) {
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  return ops->msm(ctx, d_s, d_b, n, flags, out);
+}
+
+int msm_host_inputs(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
+                    uint32_t flags, uint64_t out[8]) {
+  int rc;
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  if ((rc = ctx->begin_call())) return rc;
+  if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
+  if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(ctx->in_bases.p, bases, n * 64, hipMemcpyHostToDevice, ctx->stream));
+  return dispatch_msm_device(ctx, curve, ctx->in_scalars.p, ctx->in_bases.p, n, flags, out);
+}
+
+// default context per device (lazily created, process lifetime)
+std::mutex g_default_mu;
+std::map<int, Ctx*> g_default;  // process lifetime: never freed (HIP may be torn down at exit)
+
+int default_ctx(int device, Ctx** out) {
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  auto it = g_default.find(device);
+  if (it != g_default.end()) {
+    *out = it->second;
+    return PM_OK;
+  }
+  pm_ctx* c = nullptr;
+  int rc = pm_ctx_create(device, &c);
+  if (rc) return rc;
+  g_default[device] = c;
+  *out = c;
+  return PM_OK;
+}
+
+bool valid_curve(int c) { return c == PM_CURVE_PALLAS || c == PM_CURVE_VESTA || c == PM_CURVE_BN254; }
+
+}  // namespace
+
+// ================================================================== C-ABI
+extern "C" {
+
+const char* pm_version(void) { return "pasta_msm 0.1 (gfx950)"; }
+const char* pm_last_error(void) { return pm::g_last_error.c_str(); }
+
+int pm_device_count(int* count) {
+  if (!count) return set_error(PM_ERR_ARG, "null count");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return set_error(PM_ERR_NODEV, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = c;
+  return PM_OK;
+}
+
+int pm_ctx_create(int device, pm_ctx** out) {
+  if (!out) return set_error(PM_ERR_ARG, "null out");
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) return set_error(PM_ERR_NODEV, "no HIP device");
+  if (device < 0 || device >= cnt) return set_error(PM_ERR_NODEV, "device index out of range");
+  std::unique_ptr<Ctx> c(new Ctx());
+  c->device = device;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  c->stream = c->own_stream;
+  *out = c.release();
+  return PM_OK;
+}
+
+int pm_ctx_destroy(pm_ctx* ctx) {
+  delete ctx;
+  return PM_OK;
+}
+
+int pm_ctx_set_stream(pm_ctx* ctx, void* s) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+  return PM_OK;
+}
+
+int pm_ctx_set_window(pm_ctx* ctx, int c) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  if (c != 0 && (c < kMinC || c > kMaxC)) return set_error(PM_ERR_ARG, "window width out of range");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->window_c = c;
+  return PM_OK;
+}
+
+int pm_ctx_set_timing(pm_ctx* ctx, int enable) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->timing = enable != 0;
+  return PM_OK;
+}
+
+int pm_ctx_kernel_stats(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms) {
+  if (!ctx || !kernel || !launches || !total_ms) return set_error(PM_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  auto it = ctx->stats.find(kernel);
+  *launches = it == ctx->stats.end() ? 0 : it->second.first;
+  *total_ms = it == ctx->stats.end() ? 0.0 : it->second.second;
+  return PM_OK;
+}
+
+int pm_ctx_reset_stats(pm_ctx* ctx) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->stats.clear();
+  return PM_OK;
+}
+
+int pm_msm_ctx(pm_ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
+               uint64_t out[8]) {
+  if (!ctx || !out || (n && (!scalars || !bases))) return set_error(PM_ERR_ARG, "null argument");
+  if (!valid_curve(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return msm_host_inputs(ctx, curve, scalars, bases, n, flags, out);
+}
+
+int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags, uint64_t out[8]) {
+  Ctx* ctx = nullptr;
+  int rc = default_ctx(0, &ctx);
+  if (rc) return rc;
+  return pm_msm_ctx(ctx, curve, scalars, bases, n, flags, out);
+}
+
+int pm_msm_device(pm_ctx* ctx, int curve, const void* d_scalars, const void* d_bases, size_t n, uint32_t flags,
+                  uint64_t out[8]) {
+  if (!ctx || !out || (n && (!d_scalars || !d_bases))) return set_error(PM_ERR_ARG, "null argument");
+  if (!valid_curve(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return dispatch_msm_device(ctx, curve, d_scalars, d_bases, n, flags, out);
+}
+
+int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags, int ngpu,
+                 uint64_t out[8]) {
+  if (!out || (n && (!scalars || !bases))) return set_error(PM_ERR_ARG, "null argument");
+  if (!valid_curve(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) return set_error(PM_ERR_NODEV, "no HIP device");
+  if (ngpu <= 0 || ngpu > cnt) return set_error(PM_ERR_NODEV, "ngpu out of range");
+  std::vector<uint64_t> parts((size_t)ngpu * 8, 0);
+  std::vector<int> rcs(ngpu, PM_OK);
+  std::vector<std::string> errs(ngpu);
+  std::vector<std::thread> th;
+  const size_t per = (n + ngpu - 1) / ngpu;
+  for (int g = 0; g < ngpu; g++) {
+    th.emplace_back([&, g]() {
+      const size_t lo = std::min(n, per * g), hi = std::min(n, per * (g + 1));
+      Ctx* ctx = nullptr;
+      int rc = default_ctx(g, &ctx);
+      if (!rc) rc = pm_msm_ctx(ctx, curve, scalars + 4 * lo, bases + 8 * lo, hi - lo, flags, &parts[8 * g]);
+      rcs[g] = rc;
+      if (rc) errs[g] = pm::g_last_error;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int g = 0; g < ngpu; g++)
+    if (rcs[g]) return set_error(rcs[g], "device " + std::to_string(g) + ": " + errs[g]);
+  uint64_t acc[8] = {0};
+  for (int g = 0; g < ngpu; g++) pm_point_add(curve, acc, &parts[8 * g], acc);
+  std::memcpy(out, acc, 64);
+  return PM_OK;
+}
+
+struct pm_bases {
+  int curve;
+  int device;
+  size_t n;
+  void* d;
+};
+
+int pm_bases_upload(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, pm_bases** out) {
+  if (!ctx || !out || (n && !bases)) return set_error(PM_ERR_ARG, "null argument");
+  if (!valid_curve(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  std::unique_ptr<pm_bases> b(new pm_bases{curve, ctx->device, n, nullptr});
+  HIP_TRY(hipMalloc(&b->d, std::max<size_t>(64, n * 64)));
+  HIP_TRY(hipMemcpyAsync(b->d, bases, n * 64, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  *out = b.release();
+  return PM_OK;
+}
+
+int pm_bases_release(pm_bases* b) {
+  if (!b) return PM_OK;
+  (void)hipSetDevice(b->device);
+  (void)hipFree(b->d);
+  delete b;
+  return PM_OK;
+}
+
+int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* scalars, size_t n,
+                    uint32_t flags, uint64_t out[8]) {
+  if (!ctx || !b || !out || (n && !scalars)) return set_error(PM_ERR_ARG, "null argument");
+  if (b->device != ctx->device) return set_error(PM_ERR_ARG, "bases live on another device");
+  if (offset > b->n || n > b->n - offset) return set_error(PM_ERR_ARG, "window exceeds resident bases");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  return dispatch_msm_device(ctx, b->curve, ctx->in_scalars.p, (const char*)b->d + offset * 64, n, flags, out);
+}
+
+int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {
+  if (!a || !b || !out) return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  return ops->point_add(a, b, out);
+}
+
+int pm_synth_scalars(pm_ctx* ctx, int curve, uint64_t seed, uint64_t i0, size_t n, uint32_t flags, void* d_out) {
+  if (!ctx || (n && !d_out)) return set_error(PM_ERR_ARG, "null argument");
+  if (n > 0xffffffffull) return set_error(PM_ERR_ARG, "n too large");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n == 0) return PM_OK;
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  return ops->synth_scalars(ctx, seed, i0, (uint32_t)n, (flags & PM_SCALARS_CANONICAL) ? 0u : 1u, d_out);
+}
+
+int pm_synth_bases(pm_ctx* ctx, int curve, uint64_t seed, uint64_t i0, size_t n, void* d_out) {
+  if (!ctx || (n && !d_out)) return set_error(PM_ERR_ARG, "null argument");
+  if (n > 0xffffffffull) return set_error(PM_ERR_ARG, "n too large");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n == 0) return PM_OK;
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  return ops->synth_bases(ctx, seed, i0, (uint32_t)n, d_out);
+}
+
+}  // extern "C"

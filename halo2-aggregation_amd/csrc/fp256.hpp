@@ -1,0 +1,261 @@
+// fp256.hpp -- 255/254-bit prime-field arithmetic for gfx950 (and the host).
+//
+// Replaces the Montgomery field arithmetic of pasta_curves / pairing_bn256 that
+// halo2's best_multiexp runs on ([3P], reached from
+// /root/reference/examples/simple-example.rs:606,620,638-640).  Semantics match
+// those crates: elements are kept in Montgomery form with R = 2^256, fully
+// reduced to [0, p), so the in-memory limbs of a Rust `Fp` ([u64;4] LE) are
+// bit-identical to the 8 x u32 LE limbs used here.
+//
+// Design (MI355X): one field element = 8 VGPRs per lane (32-bit limbs, since
+// CDNA has no 64x64 multiply; 32x32->64 products lower to v_mad_u64_u32).
+// Montgomery multiplication is CIOS with the modulus limbs as compile-time
+// constants, so for the Pasta primes (p = 2^254 + small, limbs 4..6 zero,
+// limb 7 = 2^30, p = 1 mod 2^32 => -p^-1 = 0xffffffff) the reduction half
+// collapses to 3 real multiplies per row instead of 8.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define PM_HD __host__ __device__ __forceinline__
+#else
+#define PM_HD inline
+#endif
+
+namespace pm {
+
+// ---------------------------------------------------------------- parameters
+// Constants derived in tests/test_constants.py from the moduli in SURVEY.md
+// Appendix A (INV = -p^-1 mod 2^32, ONE = R mod p, R2 = R^2 mod p).
+struct PallasFp {  // Pallas base field == Vesta scalar field
+  static constexpr uint32_t MOD[8] = {0x00000001u, 0x992d30edu, 0x094cf91bu, 0x224698fcu,
+                                      0x00000000u, 0x00000000u, 0x00000000u, 0x40000000u};
+  static constexpr uint32_t INV = 0xffffffffu;
+  static constexpr uint32_t ONE[8] = {0xfffffffdu, 0x34786d38u, 0xe41914adu, 0x992c350bu,
+                                      0xffffffffu, 0xffffffffu, 0xffffffffu, 0x3fffffffu};
+  static constexpr uint32_t R2[8] = {0x0000000fu, 0x8c78ecb3u, 0x8b0de0e7u, 0xd7d30dbdu,
+                                     0xc3c95d18u, 0x7797a99bu, 0x7b9cb714u, 0x096d41afu};
+  static constexpr int NBITS = 255;
+};
+struct VestaFp {  // Vesta base field == Pallas scalar field
+  static constexpr uint32_t MOD[8] = {0x00000001u, 0x8c46eb21u, 0x0994a8ddu, 0x224698fcu,
+                                      0x00000000u, 0x00000000u, 0x00000000u, 0x40000000u};
+  static constexpr uint32_t INV = 0xffffffffu;
+  static constexpr uint32_t ONE[8] = {0xfffffffdu, 0x5b2b3e9cu, 0xe3420567u, 0x992c350bu,
+                                      0xffffffffu, 0xffffffffu, 0xffffffffu, 0x3fffffffu};
+  static constexpr uint32_t R2[8] = {0x0000000fu, 0xfc9678ffu, 0x891a16e3u, 0x67bb433du,
+                                     0x04ccf590u, 0x7fae2310u, 0x7ccfdaa9u, 0x096d41afu};
+  static constexpr int NBITS = 255;
+};
+struct Bn254Fq {  // BN254 G1 base field (reference's actual curve)
+  static constexpr uint32_t MOD[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                      0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t INV = 0xe4866389u;
+  static constexpr uint32_t ONE[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                      0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                     0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+  static constexpr int NBITS = 254;
+};
+struct Bn254Fr {  // BN254 scalar field
+  static constexpr uint32_t MOD[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                      0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t INV = 0xefffffffu;
+  static constexpr uint32_t ONE[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                      0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                     0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+  static constexpr int NBITS = 254;
+};
+
+// ------------------------------------------------------------------- element
+template <class P>
+struct Fe {
+  uint32_t l[8];
+};
+
+// carry helpers (lower to v_add_co/v_addc_co, v_sub_co/v_subb_co on gfx950)
+PM_HD uint32_t addc(uint32_t a, uint32_t b, uint32_t& c) {
+  uint64_t s = (uint64_t)a + b + c;
+  c = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+PM_HD uint32_t subb(uint32_t a, uint32_t b, uint32_t& br) {
+  uint64_t d = (uint64_t)a - b - br;
+  br = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+}
+
+template <class P>
+PM_HD Fe<P> fe_zero() {
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = 0;
+  return r;
+}
+template <class P>
+PM_HD Fe<P> fe_one() {
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = P::ONE[i];
+  return r;
+}
+template <class P>
+PM_HD bool fe_is_zero(const Fe<P>& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.l[i];
+  return o == 0;
+}
+template <class P>
+PM_HD bool fe_eq(const Fe<P>& a, const Fe<P>& b) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.l[i] ^ b.l[i];
+  return o == 0;
+}
+
+// r = t - p if (hi || t >= p) else t   (t < 2p)
+template <class P>
+PM_HD Fe<P> fe_reduce_once(const uint32_t t[8], uint32_t hi) {
+  uint32_t d[8], br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = subb(t[i], P::MOD[i], br);
+  const bool take = hi || !br;
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = take ? d[i] : t[i];
+  return r;
+}
+
+template <class P>
+PM_HD Fe<P> fe_add(const Fe<P>& a, const Fe<P>& b) {
+  uint32_t t[8], c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = addc(a.l[i], b.l[i], c);
+  return fe_reduce_once<P>(t, c);
+}
+
+template <class P>
+PM_HD Fe<P> fe_sub(const Fe<P>& a, const Fe<P>& b) {
+  uint32_t t[8], br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = subb(a.l[i], b.l[i], br);
+  // if borrow: add p back (mask trick keeps it branch-free)
+  const uint32_t m = 0u - br;
+  uint32_t c = 0;
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = addc(t[i], P::MOD[i] & m, c);
+  return r;
+}
+
+template <class P>
+PM_HD Fe<P> fe_neg(const Fe<P>& a) {
+  return fe_sub<P>(fe_zero<P>(), a);
+}
+
+template <class P>
+PM_HD Fe<P> fe_dbl(const Fe<P>& a) {
+  return fe_add<P>(a, a);
+}
+
+// Montgomery product a*b*R^-1 mod p, CIOS, fully reduced.
+template <class P>
+PM_HD Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
+  uint32_t t[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint64_t s = (uint64_t)a.l[j] * b.l[i] + t[j] + c;
+      t[j] = (uint32_t)s;
+      c = s >> 32;
+    }
+    uint64_t s = (uint64_t)t[8] + c;
+    t[8] = (uint32_t)s;
+    t[9] = (uint32_t)(s >> 32);
+    const uint32_t m = t[0] * P::INV;
+    s = (uint64_t)m * P::MOD[0] + t[0];
+    c = s >> 32;
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      s = (uint64_t)m * P::MOD[j] + t[j] + c;
+      t[j - 1] = (uint32_t)s;
+      c = s >> 32;
+    }
+    s = (uint64_t)t[8] + c;
+    t[7] = (uint32_t)s;
+    t[8] = t[9] + (uint32_t)(s >> 32);
+  }
+  return fe_reduce_once<P>(t, t[8]);
+}
+
+template <class P>
+PM_HD Fe<P> fe_sqr(const Fe<P>& a) {
+  return fe_mul<P>(a, a);
+}
+
+template <class P>
+PM_HD Fe<P> fe_from_mont(const Fe<P>& a) {
+  Fe<P> one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) one.l[i] = i == 0 ? 1u : 0u;
+  return fe_mul<P>(a, one);
+}
+template <class P>
+PM_HD Fe<P> fe_to_mont(const Fe<P>& a) {
+  Fe<P> r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.l[i] = P::R2[i];
+  return fe_mul<P>(a, r2);
+}
+
+// a^(p-2) by left-to-right square-and-multiply over the compile-time exponent.
+template <class P>
+PM_HD Fe<P> fe_inv(const Fe<P>& a) {
+  uint32_t e[8], br = 0;
+  const uint32_t two[8] = {2, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = subb(P::MOD[i], two[i], br);
+  Fe<P> r = fe_one<P>();
+  bool started = false;
+  for (int i = 7; i >= 0; i--) {
+    for (int bit = 31; bit >= 0; bit--) {
+      if (started) r = fe_sqr<P>(r);
+      if ((e[i] >> bit) & 1u) {
+        r = started ? fe_mul<P>(r, a) : a;
+        started = true;
+      }
+    }
+  }
+  return r;
+}
+
+// small-constant multiple (k <= 8) by additions
+template <class P>
+PM_HD Fe<P> fe_mul_small(const Fe<P>& a, int k) {
+  Fe<P> r = fe_zero<P>();
+  for (int i = 0; i < k; i++) r = fe_add<P>(r, a);
+  return r;
+}
+
+// -------------------------------------------------------- load / store
+template <class P>
+PM_HD Fe<P> fe_load(const uint32_t* p) {
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = p[i];
+  return r;
+}
+template <class P>
+PM_HD void fe_store(uint32_t* p, const Fe<P>& a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) p[i] = a.l[i];
+}
+
+}  // namespace pm

@@ -1,0 +1,437 @@
+// msm_kernels.hpp -- Pippenger MSM kernels for gfx950.
+//
+// Replaces halo2 `best_multiexp` / `multiexp_serial` ([3P], called from
+// /root/reference/examples/simple-example.rs:606,620,638-640,702,722).  The
+// reference is a CPU bucket method (unsigned c-bit windows, one bucket array
+// per window per rayon chunk).  This is an MI355X re-design of the same math:
+//
+//   1. k_digits     one lane per scalar: Montgomery -> canonical, signed c-bit
+//                   digits for all W windows (halves the bucket count), bucket
+//                   histogram via global atomics.            [integer, HBM]
+//   2. k_scan_*     exclusive scan of the W x NB histogram -> bucket offsets.
+//   3. k_scatter    counting-sort scatter: per window, point indices grouped by
+//                   bucket (sign in bit 31).                  [integer, HBM]
+//   4. k_accumulate every lane walks an equal-length slice of the concatenated
+//                   sorted list, summing consecutive same-bucket points with
+//                   XYZZ mixed additions (load-balanced regardless of the
+//                   bucket-size distribution).      [VALU-int bound, dominant]
+//   5. k_fixup      folds the slice-boundary partial sums into their bucket.
+//   6. k_bucket_seg segment running sums: S_j = sum B, T_j = sum i*B (L1 wide).
+//   7. k_bucket_bits per window: G_b = sum_{j: bit b of j} S_j and sum T_j via
+//                   LDS tree reductions (parallel form of sum_j j*S_j).
+//   8. k_window     per window R_w = sum T + L1 * sum_b 2^b G_b.
+// The host then combines windows (Horner with c doublings per window).
+#pragma once
+#include "curve.hpp"
+
+namespace pm {
+
+constexpr uint32_t kNegBit = 0x80000000u;
+
+// ------------------------------------------------------------ vector loads
+template <class F>
+__device__ __forceinline__ Aff<F> load_aff(const uint32_t* __restrict__ p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  Aff<F> r;
+  r.x.l[0] = a.x; r.x.l[1] = a.y; r.x.l[2] = a.z; r.x.l[3] = a.w;
+  r.x.l[4] = b.x; r.x.l[5] = b.y; r.x.l[6] = b.z; r.x.l[7] = b.w;
+  r.y.l[0] = c.x; r.y.l[1] = c.y; r.y.l[2] = c.z; r.y.l[3] = c.w;
+  r.y.l[4] = d.x; r.y.l[5] = d.y; r.y.l[6] = d.z; r.y.l[7] = d.w;
+  return r;
+}
+template <class F>
+__device__ __forceinline__ void store_fe4(uint4* q, const Fe<F>& a) {
+  q[0] = make_uint4(a.l[0], a.l[1], a.l[2], a.l[3]);
+  q[1] = make_uint4(a.l[4], a.l[5], a.l[6], a.l[7]);
+}
+template <class F>
+__device__ __forceinline__ Fe<F> load_fe4(const uint4* q) {
+  uint4 a = q[0], b = q[1];
+  Fe<F> r;
+  r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
+  r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
+  return r;
+}
+template <class F>
+__device__ __forceinline__ void store_xyzz(Xyzz<F>* dst, const Xyzz<F>& p) {
+  uint4* q = reinterpret_cast<uint4*>(dst);
+  store_fe4<F>(q + 0, p.X);
+  store_fe4<F>(q + 2, p.Y);
+  store_fe4<F>(q + 4, p.ZZ);
+  store_fe4<F>(q + 6, p.ZZZ);
+}
+template <class F>
+__device__ __forceinline__ Xyzz<F> load_xyzz(const Xyzz<F>* src) {
+  const uint4* q = reinterpret_cast<const uint4*>(src);
+  Xyzz<F> p;
+  p.X = load_fe4<F>(q + 0);
+  p.Y = load_fe4<F>(q + 2);
+  p.ZZ = load_fe4<F>(q + 4);
+  p.ZZZ = load_fe4<F>(q + 6);
+  return p;
+}
+
+// --------------------------------------------------------------- 1. digits
+// Signed c-bit digits: d in [-2^(c-1)+1, 2^(c-1)], code = |d| | sign<<31,
+// code 0 = skip.  W = ceil(256 / c) windows always absorbs the final carry for
+// scalars < 2^255.
+template <class Fs, int C>
+__global__ void __launch_bounds__(256) k_digits(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                int NB, uint32_t canonical,
+                                                uint32_t* __restrict__ digits,
+                                                uint32_t* __restrict__ counts) {
+  constexpr int W = (256 + C - 1) / C;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* q = reinterpret_cast<const uint4*>(scalars + 8ull * i);
+  Fe<Fs> s = load_fe4<Fs>(q);
+  if (!canonical) s = fe_from_mont<Fs>(s);
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int bit = w * C;
+    const int limb = bit >> 5, sh = bit & 31;
+    uint32_t lo = s.l[limb] >> sh;
+    uint32_t hi = (sh != 0 && limb + 1 < 8) ? (s.l[limb + 1] << (32 - sh)) : 0u;
+    uint32_t raw = (lo | hi);
+    if (C < 32) raw &= (1u << C) - 1u;
+    uint32_t d = raw + carry;
+    uint32_t neg = 0;
+    if (w != W - 1 && d > (1u << (C - 1))) {
+      d = (1u << C) - d;
+      neg = 1;
+      carry = 1;
+    } else {
+      carry = 0;
+    }
+    const uint32_t code = d ? (d | (neg << 31)) : 0u;
+    digits[(size_t)w * n + i] = code;
+    if (d) atomicAdd(&counts[(size_t)w * NB + d], 1u);
+  }
+}
+
+// ----------------------------------------------------------------- 2. scan
+constexpr int kScanThreads = 256;
+constexpr int kScanPerThread = 16;
+constexpr int kScanChunk = kScanThreads * kScanPerThread;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// exclusive block scan; lds needs (blockDim/64 + 1) words
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, uint32_t& total) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
+  const uint32_t incl = wave_incl_scan(v);
+  if (lane == 63) lds[wave] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t s = 0;
+    for (int w = 0; w < nw; w++) {
+      uint32_t x = lds[w];
+      lds[w] = s;
+      s += x;
+    }
+    lds[nw] = s;
+  }
+  __syncthreads();
+  const uint32_t r = incl - v + lds[wave];
+  total = lds[nw];
+  __syncthreads();
+  return r;
+}
+
+static __global__ void __launch_bounds__(kScanThreads) k_scan_reduce(const uint32_t* __restrict__ in, uint32_t N,
+                                                             uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t lds[kScanThreads / 64 + 1];
+  const size_t base = (size_t)blockIdx.x * kScanChunk + (size_t)threadIdx.x * kScanPerThread;
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPerThread; k++) s += (base + k < N) ? in[base + k] : 0u;
+  uint32_t total;
+  block_excl_scan(s, lds, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// single block: exclusive scan of nb block sums in place
+static __global__ void __launch_bounds__(1024) k_scan_top(uint32_t* __restrict__ bsum, uint32_t nb) {
+  __shared__ uint32_t lds[1024 / 64 + 1];
+  uint32_t carry = 0;
+  for (uint32_t off = 0; off < nb; off += blockDim.x) {
+    const uint32_t i = off + threadIdx.x;
+    const uint32_t v = i < nb ? bsum[i] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(v, lds, total);
+    if (i < nb) bsum[i] = ex + carry;
+    carry += total;
+  }
+}
+
+static __global__ void __launch_bounds__(kScanThreads) k_scan_down(const uint32_t* __restrict__ in, uint32_t N,
+                                                           const uint32_t* __restrict__ bsum,
+                                                           uint32_t* __restrict__ offsets,
+                                                           uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t lds[kScanThreads / 64 + 1];
+  const size_t base = (size_t)blockIdx.x * kScanChunk + (size_t)threadIdx.x * kScanPerThread;
+  uint32_t v[kScanPerThread];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPerThread; k++) {
+    v[k] = (base + k < N) ? in[base + k] : 0u;
+    s += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan(s, lds, total) + bsum[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanPerThread; k++) {
+    if (base + k < N) {
+      offsets[base + k] = run;
+      cursor[base + k] = run;
+    }
+    run += v[k];
+  }
+}
+
+// -------------------------------------------------------------- 3. scatter
+static __global__ void __launch_bounds__(256) k_scatter(const uint32_t* __restrict__ digits, uint32_t n, int W,
+                                                 int NB, uint32_t* __restrict__ cursor,
+                                                 uint32_t* __restrict__ sorted) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)n * W) return;
+  const uint32_t code = digits[idx];
+  if (!code) return;
+  const uint32_t w = (uint32_t)(idx / n), i = (uint32_t)(idx - (size_t)w * n);
+  const uint32_t slot = code & ~kNegBit;
+  const uint32_t pos = atomicAdd(&cursor[(size_t)w * NB + slot], 1u);
+  sorted[pos] = i | (code & kNegBit);
+}
+
+// ----------------------------------------------------------- 4. accumulate
+// Slice t covers sorted positions [t*chunk, min((t+1)*chunk, total)).  A bucket
+// is *owned* by the slice holding its first element; the owner writes its
+// (possibly partial) sum to buckets[]; a slice whose first bucket started in an
+// earlier slice writes that partial to head[t] for k_fixup.
+__device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ offsets, uint32_t nslots,
+                                                uint32_t pos) {
+  // largest gb in [0, nslots) with offsets[gb] <= pos
+  uint32_t lo = 0, hi = nslots;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= pos) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ sorted,
+                                                    const uint32_t* __restrict__ offsets, uint32_t nslots,
+                                                    const uint32_t* __restrict__ bases, uint32_t chunk,
+                                                    Xyzz<F>* __restrict__ buckets,
+                                                    Xyzz<F>* __restrict__ head) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = offsets[nslots];
+  const uint32_t start = t * chunk;
+  if (start >= total) return;
+  const uint32_t end = min(start + chunk, total);
+  uint32_t gb = find_bucket(offsets, nslots, start);
+  uint32_t bend = offsets[gb + 1];
+  bool owned = offsets[gb] == start;
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (uint32_t p = start; p < end; p++) {
+    if (p == bend) {
+      store_xyzz<F>(owned ? &buckets[gb] : &head[t], acc);
+      acc = xyzz_inf<F>();
+      gb++;
+      while (offsets[gb + 1] <= p) gb++;
+      bend = offsets[gb + 1];
+      owned = true;
+    }
+    const uint32_t code = sorted[p];
+    Aff<F> P = load_aff<F>(bases + 16ull * (code & ~kNegBit));
+    if (code & kNegBit) P.y = fe_neg<F>(P.y);
+    acc = xyzz_add_aff<F>(acc, P);
+  }
+  store_xyzz<F>(owned ? &buckets[gb] : &head[t], acc);
+}
+
+// --------------------------------------------------------------- 5. fixup
+template <class F>
+__global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offsets, uint32_t nslots,
+                                               uint32_t chunk, uint32_t nthreads,
+                                               Xyzz<F>* __restrict__ buckets,
+                                               const Xyzz<F>* __restrict__ head) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nthreads) return;
+  const uint32_t total = offsets[nslots];
+  const uint32_t start = t * chunk;
+  if (start >= total) return;
+  const uint32_t end = min(start + chunk, total);
+  const uint32_t gb = find_bucket(offsets, nslots, end - 1);
+  const uint32_t bstart = offsets[gb], bend = offsets[gb + 1];
+  if (bstart < start || bend <= end) return;  // not owned, or fully inside
+  Xyzz<F> acc = load_xyzz<F>(&buckets[gb]);
+  for (uint32_t t2 = t + 1; t2 < nthreads && (size_t)t2 * chunk < bend; t2++)
+    acc = xyzz_add<F>(acc, load_xyzz<F>(&head[t2]));
+  store_xyzz<F>(&buckets[gb], acc);
+}
+
+// ------------------------------------------------------ 6. segment sums
+// thread (w, j): slots s = j*L1 + i, i in [0, L1):  S = sum B_s,
+// T = sum i * B_s (0-based weight inside the segment).
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__ offsets,
+                                                    const Xyzz<F>* __restrict__ buckets, int W, int NB,
+                                                    int L1, Xyzz<F>* __restrict__ S,
+                                                    Xyzz<F>* __restrict__ T) {
+  const int M1 = NB / L1;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= W * M1) return;
+  const int w = gid / M1, j = gid - w * M1;
+  const size_t base = (size_t)w * NB + (size_t)j * L1;
+  Xyzz<F> s = xyzz_inf<F>(), t = xyzz_inf<F>();
+  for (int i = L1 - 1; i >= 1; i--) {
+    if (offsets[base + i] != offsets[base + i + 1]) s = xyzz_add<F>(s, load_xyzz<F>(&buckets[base + i]));
+    t = xyzz_add<F>(t, s);
+  }
+  if (offsets[base] != offsets[base + 1]) s = xyzz_add<F>(s, load_xyzz<F>(&buckets[base]));
+  store_xyzz<F>(&S[gid], s);
+  store_xyzz<F>(&T[gid], t);
+}
+
+// ------------------------------------------------------ 7. bit sums
+// block (w, job): job < NBITS2 -> G_job = sum_{j : (j >> job) & 1} S_j;
+// job == NBITS2 -> sum_j T_j.  256 lanes, strided partial sums, LDS tree.
+constexpr int kRedThreads = 256;
+template <class F>
+__global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __restrict__ S,
+                                                             const Xyzz<F>* __restrict__ T, int M1,
+                                                             int NBITS2, Xyzz<F>* __restrict__ G) {
+  __shared__ Xyzz<F> lds[kRedThreads];
+  const int w = blockIdx.y, job = blockIdx.x, tid = threadIdx.x;
+  Xyzz<F> acc = xyzz_inf<F>();
+  if (job < NBITS2) {
+    for (int j = tid; j < M1; j += kRedThreads)
+      if ((j >> job) & 1) acc = xyzz_add<F>(acc, load_xyzz<F>(&S[(size_t)w * M1 + j]));
+  } else {
+    for (int j = tid; j < M1; j += kRedThreads) acc = xyzz_add<F>(acc, load_xyzz<F>(&T[(size_t)w * M1 + j]));
+  }
+  lds[tid] = acc;
+  __syncthreads();
+  for (int s = kRedThreads / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+      acc = xyzz_add<F>(acc, lds[tid + s]);
+      lds[tid] = acc;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) store_xyzz<F>(&G[(size_t)w * (NBITS2 + 1) + job], acc);
+}
+
+// ------------------------------------------------------ 8. window result
+template <class F>
+__global__ void k_window(const Xyzz<F>* __restrict__ G, int W, int NBITS2, int log2L1,
+                         Xyzz<F>* __restrict__ R) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  const Xyzz<F>* g = G + (size_t)w * (NBITS2 + 1);
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (int b = NBITS2 - 1; b >= 0; b--) {
+    acc = xyzz_dbl<F>(acc);
+    acc = xyzz_add<F>(acc, load_xyzz<F>(&g[b]));
+  }
+  for (int k = 0; k < log2L1; k++) acc = xyzz_dbl<F>(acc);
+  acc = xyzz_add<F>(acc, load_xyzz<F>(&g[NBITS2]));
+  store_xyzz<F>(&R[w], acc);
+}
+
+// ------------------------------------------------------ synthetic inputs
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t synth_word(uint64_t seed, uint64_t i, uint64_t j) {
+  return mix64(mix64(seed + i) + j);
+}
+// uniform in [0, MOD) (canonical), mirrors oracle/pasta.py synth_scalar
+template <class Fs>
+__host__ __device__ __forceinline__ Fe<Fs> synth_scalar(uint64_t seed, uint64_t i) {
+  for (uint64_t t = 0;; t++) {
+    uint64_t w[4];
+    for (int k = 0; k < 4; k++) w[k] = synth_word(seed, i, 4 * t + k);
+    w[3] &= (Fs::NBITS - 192 >= 64) ? ~0ull : ((1ull << (Fs::NBITS - 192)) - 1ull);
+    Fe<Fs> v;
+    for (int k = 0; k < 4; k++) {
+      v.l[2 * k] = (uint32_t)w[k];
+      v.l[2 * k + 1] = (uint32_t)(w[k] >> 32);
+    }
+    uint32_t br = 0;
+    for (int k = 0; k < 8; k++) (void)subb(v.l[k], Fs::MOD[k], br);
+    if (br) return v;  // v < MOD
+  }
+}
+
+template <class Fs>
+__global__ void k_synth_scalars(uint64_t seed, uint64_t i0, uint32_t n, uint32_t mont,
+                                uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fe<Fs> v = synth_scalar<Fs>(seed, i0 + i);
+  if (mont) v = fe_to_mont<Fs>(v);
+  store_fe4<Fs>(reinterpret_cast<uint4*>(out + 8ull * i), v);
+}
+
+template <class Cv>
+__device__ __forceinline__ Aff<typename Cv::Base> generator();
+
+template <>
+__device__ __forceinline__ Aff<PallasFp> generator<PallasCurve>() {
+  return Aff<PallasFp>{fe_neg<PallasFp>(fe_one<PallasFp>()), fe_add<PallasFp>(fe_one<PallasFp>(), fe_one<PallasFp>())};
+}
+template <>
+__device__ __forceinline__ Aff<VestaFp> generator<VestaCurve>() {
+  return Aff<VestaFp>{fe_neg<VestaFp>(fe_one<VestaFp>()), fe_add<VestaFp>(fe_one<VestaFp>(), fe_one<VestaFp>())};
+}
+template <>
+__device__ __forceinline__ Aff<Bn254Fq> generator<Bn254Curve>() {
+  return Aff<Bn254Fq>{fe_one<Bn254Fq>(), fe_add<Bn254Fq>(fe_one<Bn254Fq>(), fe_one<Bn254Fq>())};
+}
+
+// P = [k]A (k canonical), MSB-first double-and-add
+template <class F, class Fs>
+__device__ __forceinline__ Xyzz<F> scalar_mul(const Fe<Fs>& k, const Aff<F>& A) {
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (int i = 7; i >= 0; i--) {
+    for (int b = 31; b >= 0; b--) {
+      acc = xyzz_dbl<F>(acc);
+      if ((k.l[i] >> b) & 1u) acc = xyzz_add_aff<F>(acc, A);
+    }
+  }
+  return acc;
+}
+
+// synthetic base i = [a_i]G with a_i = synth_scalar(seed, i) (1 if zero)
+template <class Cv>
+__global__ void __launch_bounds__(256) k_synth_bases(uint64_t seed, uint64_t i0, uint32_t n,
+                                                     uint32_t* __restrict__ out) {
+  using F = typename Cv::Base;
+  using Fs = typename Cv::Scalar;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fe<Fs> a = synth_scalar<Fs>(seed, i0 + i);
+  if (fe_is_zero<Fs>(a)) a.l[0] = 1;
+  const Aff<F> P = xyzz_to_aff<F>(scalar_mul<F, Fs>(a, generator<Cv>()));
+  uint4* q = reinterpret_cast<uint4*>(out + 16ull * i);
+  store_fe4<F>(q, P.x);
+  store_fe4<F>(q + 2, P.y);
+}
+
+}  // namespace pm

@@ -1,0 +1,109 @@
+// runtime.hpp -- device context, workspace and launch plan of the MSM engine.
+//
+// A pm_ctx binds one device, one HIP stream and a grow-only workspace, so a
+// caller (rayon thread in the Rust shim, one rank in bench.py) reuses device
+// memory across calls and no hipMalloc happens once warm.  Calls on one
+// context are serialised by its mutex (the C-ABI is re-entrant, §8b).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/pasta_msm.h"
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace pm {
+
+int set_error(int code, const std::string& msg);
+
+constexpr int kMinC = 4;
+constexpr int kMaxC = 20;
+constexpr size_t kMaxPoints = size_t(1) << 26;
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes);
+  void release();
+};
+
+struct MsmPlan {
+  int c;          // window width (bits)
+  int W;          // windows = ceil(256 / c)
+  int K;          // max |digit| = 2^(c-1)
+  int L1;         // bucket-segment length of k_bucket_seg
+  int log2L1;
+  int NB;         // bucket slots per window (K+1 rounded up to L1)
+  int M1;         // segments per window
+  int NB2;        // bits of the segment index
+  uint32_t n;
+  uint32_t chunk;     // sorted entries per accumulate lane
+  uint32_t nthreads;  // accumulate lanes
+};
+
+MsmPlan make_plan(size_t n, int c_override);
+
+struct TimedSpan {
+  const char* name;
+  hipEvent_t a, b;
+};
+
+}  // namespace pm
+
+struct pm_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int window_c = 0;
+  bool timing = false;
+  std::mutex mu;
+  // workspace
+  pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
+      win;
+  void* h_pinned = nullptr;
+  size_t h_pinned_cap = 0;
+  // timing
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<pm::TimedSpan> pending;
+  std::map<std::string, std::pair<uint64_t, double>> stats;
+
+  std::vector<pm::Buf*> all_bufs() {
+    return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
+            &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win};
+  }
+  ~pm_ctx();
+  int begin_call();
+  int end_call();
+  int ensure_pinned(size_t bytes);
+  hipEvent_t next_event();
+  void mark(const char* name, hipEvent_t a, hipEvent_t b);
+};
+
+namespace pm {
+using Ctx = ::pm_ctx;
+}
+
+namespace pm {
+
+// Per-curve engine entry points, one translation unit per curve
+// (inst_pallas.hip, inst_vesta.hip, inst_bn254.hip) so they build in parallel.
+struct CurveOps {
+  int (*msm)(Ctx* ctx, const void* d_scalars, const void* d_bases, size_t n, uint32_t flags, uint64_t out[8]);
+  int (*point_add)(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
+  int (*synth_scalars)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, uint32_t mont, void* d_out);
+  int (*synth_bases)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, void* d_out);
+};
+extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
+
+}  // namespace pm
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return pm::set_error(PM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)

@@ -1,0 +1,520 @@
+/* msm_ref.c -- TEST INFRASTRUCTURE ONLY: C restatement of halo2 best_multiexp.
+ *
+ * Used as (a) the large-n checker in tests/ and (b) bench.py's cpu_baseline
+ * ("kind": "port").  Never linked by the product library.
+ *
+ * PARITY STATUS: parity unpinned by the reference -- the reference's MSM lives
+ * in the un-vendored halo2 fork `kzg-agg2` (/root/reference/Cargo.toml:12) and
+ * pasta_curves, neither present in /root/reference, and the reference ships no
+ * test vectors (/root/reference/src/lib.rs:43-44).  This file restates the
+ * published algorithms of those crates:
+ *   halo2 arithmetic.rs `multiexp_serial`:
+ *     c = 1 if n < 4, 3 if n < 32, else ceil(ln n);  segments = 256/c + 1;
+ *     for each segment (high to low): c doublings of acc; (2^c - 1) buckets
+ *     filled from get_at(segment, c, coeff.to_repr()) with mixed additions
+ *     (Bucket::None -> Affine -> Projective); summation by parts: running_sum
+ *     over buckets high->low, acc += running_sum after each bucket.
+ *   halo2 `best_multiexp`: if n > num_threads, chunk = n / num_threads, one
+ *     multiexp_serial per contiguous chunk (chunks(chunk), so possibly one
+ *     extra short chunk), results folded left to right; else one serial call.
+ *   pasta_curves / pairing_bn256: Montgomery form R = 2^256 in 4 x u64,
+ *     Jacobian projective points, affine identity (0, 0).
+ * It is an independent implementation from the HIP library (64-bit limbs,
+ * Jacobian coordinates, unsigned windows) and from oracle/pasta.py.
+ *
+ * Build: oracle/Makefile -> oracle/libmsm_ref.so
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+typedef uint64_t u64;
+typedef unsigned __int128 u128;
+
+typedef struct {
+  u64 p[4];
+  u64 inv;    /* -p^-1 mod 2^64 */
+  u64 one[4]; /* R mod p */
+} Field;
+
+typedef struct {
+  Field fp;   /* base field */
+  Field fr;   /* scalar field */
+  int b;      /* y^2 = x^3 + b */
+  int gx_neg_one; /* generator x = -1 (Pasta) else x = 1 (BN254) */
+} CurveDef;
+
+static const CurveDef CURVES[3] = {
+    /* Pallas: base = Fp(pallas), scalar = Fq(vesta base) */
+    {{{0x992d30ed00000001ull, 0x224698fc094cf91bull, 0x0000000000000000ull, 0x4000000000000000ull},
+      0x992d30ecffffffffull,
+      {0x34786d38fffffffdull, 0x992c350be41914adull, 0xffffffffffffffffull, 0x3fffffffffffffffull}},
+     {{0x8c46eb2100000001ull, 0x224698fc0994a8ddull, 0x0000000000000000ull, 0x4000000000000000ull},
+      0x8c46eb20ffffffffull,
+      {0x5b2b3e9cfffffffdull, 0x992c350be3420567ull, 0xffffffffffffffffull, 0x3fffffffffffffffull}},
+     5, 1},
+    /* Vesta: base = Fq, scalar = Fp */
+    {{{0x8c46eb2100000001ull, 0x224698fc0994a8ddull, 0x0000000000000000ull, 0x4000000000000000ull},
+      0x8c46eb20ffffffffull,
+      {0x5b2b3e9cfffffffdull, 0x992c350be3420567ull, 0xffffffffffffffffull, 0x3fffffffffffffffull}},
+     {{0x992d30ed00000001ull, 0x224698fc094cf91bull, 0x0000000000000000ull, 0x4000000000000000ull},
+      0x992d30ecffffffffull,
+      {0x34786d38fffffffdull, 0x992c350be41914adull, 0xffffffffffffffffull, 0x3fffffffffffffffull}},
+     5, 1},
+    /* BN254 G1 */
+    {{{0x3c208c16d87cfd47ull, 0x97816a916871ca8dull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
+      0x87d20782e4866389ull,
+      {0xd35d438dc58f0d9dull, 0x0a78eb28f5c70b3dull, 0x666ea36f7879462cull, 0x0e0a77c19a07df2full}},
+     {{0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
+      0xc2e1f593efffffffull,
+      {0xac96341c4ffffffbull, 0x36fc76959f60cd29ull, 0x666ea36f7879462eull, 0x0e0a77c19a07df2full}},
+     3, 0},
+};
+
+/* ------------------------------------------------------------- field ops */
+static int geq(const u64 a[4], const u64 b[4]) {
+  for (int i = 3; i >= 0; i--) {
+    if (a[i] > b[i]) return 1;
+    if (a[i] < b[i]) return 0;
+  }
+  return 1;
+}
+static void sub4(u64 r[4], const u64 a[4], const u64 b[4]) {
+  u64 br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 d = (u128)a[i] - b[i] - br;
+    r[i] = (u64)d;
+    br = (u64)(d >> 64) & 1;
+  }
+}
+static void f_add(const Field* F, u64 r[4], const u64 a[4], const u64 b[4]) {
+  u64 t[4], c = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 s = (u128)a[i] + b[i] + c;
+    t[i] = (u64)s;
+    c = (u64)(s >> 64);
+  }
+  if (c || geq(t, F->p)) sub4(t, t, F->p);
+  memcpy(r, t, 32);
+}
+static void f_sub(const Field* F, u64 r[4], const u64 a[4], const u64 b[4]) {
+  if (geq(a, b)) {
+    sub4(r, a, b);
+  } else {
+    u64 t[4];
+    sub4(t, b, a);
+    sub4(r, F->p, t);
+  }
+}
+static void f_mul(const Field* F, u64 r[4], const u64 a[4], const u64 b[4]) {
+  u64 t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    u64 carry = 0;
+    u128 uv;
+    for (int j = 0; j < 4; j++) {
+      uv = (u128)a[j] * b[i] + t[j] + carry;
+      t[j] = (u64)uv;
+      carry = (u64)(uv >> 64);
+    }
+    uv = (u128)t[4] + carry;
+    t[4] = (u64)uv;
+    t[5] = (u64)(uv >> 64);
+    u64 m = t[0] * F->inv;
+    uv = (u128)m * F->p[0] + t[0];
+    carry = (u64)(uv >> 64);
+    for (int j = 1; j < 4; j++) {
+      uv = (u128)m * F->p[j] + t[j] + carry;
+      t[j - 1] = (u64)uv;
+      carry = (u64)(uv >> 64);
+    }
+    uv = (u128)t[4] + carry;
+    t[3] = (u64)uv;
+    t[4] = t[5] + (u64)(uv >> 64);
+  }
+  if (t[4] || geq(t, F->p)) sub4(t, t, F->p);
+  memcpy(r, t, 32);
+}
+static int f_is_zero(const u64 a[4]) { return (a[0] | a[1] | a[2] | a[3]) == 0; }
+static void f_inv(const Field* F, u64 r[4], const u64 a[4]) {
+  u64 e[4], two[4] = {2, 0, 0, 0}, acc[4];
+  sub4(e, F->p, two);
+  memcpy(acc, F->one, 32);
+  for (int i = 3; i >= 0; i--)
+    for (int b = 63; b >= 0; b--) {
+      f_mul(F, acc, acc, acc);
+      if ((e[i] >> b) & 1) f_mul(F, acc, acc, a);
+    }
+  memcpy(r, acc, 32);
+}
+static void from_mont(const Field* F, u64 r[4], const u64 a[4]) {
+  u64 one[4] = {1, 0, 0, 0};
+  f_mul(F, r, a, one);
+}
+
+/* ------------------------------------------------------------ Jacobian ops */
+typedef struct { u64 x[4], y[4], z[4]; } Jac; /* z == 0: identity */
+
+static void j_set_aff(const Field* F, Jac* r, const u64* aff) {
+  if (f_is_zero(aff) && f_is_zero(aff + 4)) {
+    memset(r, 0, sizeof(*r));
+    memcpy(r->x, F->one, 32);
+    memcpy(r->y, F->one, 32);
+    return;
+  }
+  memcpy(r->x, aff, 32);
+  memcpy(r->y, aff + 4, 32);
+  memcpy(r->z, F->one, 32);
+}
+
+/* dbl-2009-l (a = 0) */
+static void j_dbl(const Field* F, Jac* r, const Jac* p) {
+  if (f_is_zero(p->z) || f_is_zero(p->y)) {
+    memset(r->z, 0, 32);
+    return;
+  }
+  u64 A[4], B[4], C[4], D[4], E[4], Fv[4], t[4], X3[4], Y3[4], Z3[4];
+  f_mul(F, A, p->x, p->x);
+  f_mul(F, B, p->y, p->y);
+  f_mul(F, C, B, B);
+  f_add(F, t, p->x, B);
+  f_mul(F, t, t, t);
+  f_sub(F, t, t, A);
+  f_sub(F, t, t, C);
+  f_add(F, D, t, t);
+  f_add(F, E, A, A);
+  f_add(F, E, E, A);
+  f_mul(F, Fv, E, E);
+  f_add(F, t, D, D);
+  f_sub(F, X3, Fv, t);
+  f_sub(F, t, D, X3);
+  f_mul(F, t, E, t);
+  u64 c8[4];
+  f_add(F, c8, C, C);
+  f_add(F, c8, c8, c8);
+  f_add(F, c8, c8, c8);
+  f_sub(F, Y3, t, c8);
+  f_mul(F, Z3, p->y, p->z);
+  f_add(F, Z3, Z3, Z3);
+  memcpy(r->x, X3, 32);
+  memcpy(r->y, Y3, 32);
+  memcpy(r->z, Z3, 32);
+}
+
+/* add-2007-bl */
+static void j_add(const Field* F, Jac* r, const Jac* p, const Jac* q) {
+  if (f_is_zero(p->z)) { *r = *q; return; }
+  if (f_is_zero(q->z)) { *r = *p; return; }
+  u64 Z1Z1[4], Z2Z2[4], U1[4], U2[4], S1[4], S2[4], H[4], I[4], J[4], rr[4], V[4], t[4];
+  f_mul(F, Z1Z1, p->z, p->z);
+  f_mul(F, Z2Z2, q->z, q->z);
+  f_mul(F, U1, p->x, Z2Z2);
+  f_mul(F, U2, q->x, Z1Z1);
+  f_mul(F, t, q->z, Z2Z2);
+  f_mul(F, S1, p->y, t);
+  f_mul(F, t, p->z, Z1Z1);
+  f_mul(F, S2, q->y, t);
+  if (memcmp(U1, U2, 32) == 0) {
+    if (memcmp(S1, S2, 32) == 0) { j_dbl(F, r, p); return; }
+    memset(r->z, 0, 32);
+    return;
+  }
+  f_sub(F, H, U2, U1);
+  f_add(F, I, H, H);
+  f_mul(F, I, I, I);
+  f_mul(F, J, H, I);
+  f_sub(F, rr, S2, S1);
+  f_add(F, rr, rr, rr);
+  f_mul(F, V, U1, I);
+  u64 X3[4], Y3[4], Z3[4];
+  f_mul(F, X3, rr, rr);
+  f_sub(F, X3, X3, J);
+  f_sub(F, X3, X3, V);
+  f_sub(F, X3, X3, V);
+  f_sub(F, t, V, X3);
+  f_mul(F, Y3, rr, t);
+  f_mul(F, t, S1, J);
+  f_add(F, t, t, t);
+  f_sub(F, Y3, Y3, t);
+  f_add(F, Z3, p->z, q->z);
+  f_mul(F, Z3, Z3, Z3);
+  f_sub(F, Z3, Z3, Z1Z1);
+  f_sub(F, Z3, Z3, Z2Z2);
+  f_mul(F, Z3, Z3, H);
+  memcpy(r->x, X3, 32);
+  memcpy(r->y, Y3, 32);
+  memcpy(r->z, Z3, 32);
+}
+
+/* madd-2007-bl: p + affine q (q not identity) */
+static void j_add_aff(const Field* F, Jac* r, const Jac* p, const u64* q) {
+  if (f_is_zero(q) && f_is_zero(q + 4)) { *r = *p; return; }
+  if (f_is_zero(p->z)) { j_set_aff(F, r, q); return; }
+  u64 Z1Z1[4], U2[4], S2[4], H[4], HH[4], I[4], J[4], rr[4], V[4], t[4];
+  f_mul(F, Z1Z1, p->z, p->z);
+  f_mul(F, U2, q, Z1Z1);
+  f_mul(F, t, p->z, Z1Z1);
+  f_mul(F, S2, q + 4, t);
+  if (memcmp(U2, p->x, 32) == 0) {
+    if (memcmp(S2, p->y, 32) == 0) { j_dbl(F, r, p); return; }
+    memset(r->z, 0, 32);
+    return;
+  }
+  f_sub(F, H, U2, p->x);
+  f_mul(F, HH, H, H);
+  f_add(F, I, HH, HH);
+  f_add(F, I, I, I);
+  f_mul(F, J, H, I);
+  f_sub(F, rr, S2, p->y);
+  f_add(F, rr, rr, rr);
+  f_mul(F, V, p->x, I);
+  u64 X3[4], Y3[4], Z3[4];
+  f_mul(F, X3, rr, rr);
+  f_sub(F, X3, X3, J);
+  f_sub(F, X3, X3, V);
+  f_sub(F, X3, X3, V);
+  f_sub(F, t, V, X3);
+  f_mul(F, Y3, rr, t);
+  f_mul(F, t, p->y, J);
+  f_add(F, t, t, t);
+  f_sub(F, Y3, Y3, t);
+  f_add(F, Z3, p->z, H);
+  f_mul(F, Z3, Z3, Z3);
+  f_sub(F, Z3, Z3, Z1Z1);
+  f_sub(F, Z3, Z3, HH);
+  memcpy(r->x, X3, 32);
+  memcpy(r->y, Y3, 32);
+  memcpy(r->z, Z3, 32);
+}
+
+static void j_to_aff(const Field* F, u64* out, const Jac* p) {
+  if (f_is_zero(p->z)) { memset(out, 0, 64); return; }
+  u64 zi[4], zi2[4], zi3[4];
+  f_inv(F, zi, p->z);
+  f_mul(F, zi2, zi, zi);
+  f_mul(F, zi3, zi2, zi);
+  f_mul(F, out, p->x, zi2);
+  f_mul(F, out + 4, p->y, zi3);
+}
+
+/* ------------------------------------------------------- multiexp_serial */
+static size_t get_at(size_t segment, size_t c, const uint8_t bytes[32]) {
+  size_t skip_bits = segment * c, skip_bytes = skip_bits / 8;
+  if (skip_bytes >= 32) return 0;
+  uint8_t v[8] = {0};
+  for (size_t k = 0; k < 8 && skip_bytes + k < 32; k++) v[k] = bytes[skip_bytes + k];
+  u64 tmp = 0;
+  for (int k = 7; k >= 0; k--) tmp = (tmp << 8) | v[k];
+  tmp >>= skip_bits - skip_bytes * 8;
+  tmp %= (1ull << c);
+  return (size_t)tmp;
+}
+
+enum { B_NONE = 0, B_AFF = 1, B_PROJ = 2 };
+
+static void multiexp_serial(const CurveDef* cv, const uint8_t* repr /* n x 32 canonical LE */,
+                            const u64* bases, size_t n, Jac* acc) {
+  const Field* F = &cv->fp;
+  size_t c = n < 4 ? 1 : (n < 32 ? 3 : (size_t)ceil(log((double)n)));
+  size_t segments = 256 / c + 1;
+  size_t nb = ((size_t)1 << c) - 1;
+  int* kind = (int*)malloc(nb * sizeof(int));
+  const u64** aff = (const u64**)malloc(nb * sizeof(u64*));
+  Jac* proj = (Jac*)malloc(nb * sizeof(Jac));
+  for (size_t seg = segments; seg-- > 0;) {
+    for (size_t k = 0; k < c; k++) j_dbl(F, acc, acc);
+    memset(kind, 0, nb * sizeof(int));
+    for (size_t i = 0; i < n; i++) {
+      size_t d = get_at(seg, c, repr + 32 * i);
+      if (d == 0) continue;
+      const u64* b = bases + 8 * i;
+      size_t bi = d - 1;
+      if (kind[bi] == B_NONE) {
+        kind[bi] = B_AFF;
+        aff[bi] = b;
+      } else if (kind[bi] == B_AFF) {
+        Jac t;
+        j_set_aff(F, &t, aff[bi]);
+        j_add_aff(F, &proj[bi], &t, b);
+        kind[bi] = B_PROJ;
+      } else {
+        j_add_aff(F, &proj[bi], &proj[bi], b);
+      }
+    }
+    Jac running;
+    memset(&running, 0, sizeof(running));
+    for (size_t bi = nb; bi-- > 0;) {
+      if (kind[bi] == B_AFF) j_add_aff(F, &running, &running, aff[bi]);
+      else if (kind[bi] == B_PROJ) j_add(F, &running, &running, &proj[bi]);
+      j_add(F, acc, acc, &running);
+    }
+  }
+  free(kind);
+  free(aff);
+  free(proj);
+}
+
+/* ---------------------------------------------------------- best_multiexp */
+typedef struct {
+  const CurveDef* cv;
+  const uint8_t* repr;
+  const u64* bases;
+  size_t n, chunk, nchunks;
+  Jac* results;
+  volatile size_t next;
+  pthread_mutex_t mu;
+} Job;
+
+static void* worker(void* arg) {
+  Job* job = (Job*)arg;
+  for (;;) {
+    pthread_mutex_lock(&job->mu);
+    size_t k = job->next++;
+    pthread_mutex_unlock(&job->mu);
+    if (k >= job->nchunks) break;
+    size_t lo = k * job->chunk, hi = lo + job->chunk;
+    if (hi > job->n) hi = job->n;
+    memset(&job->results[k], 0, sizeof(Jac));
+    multiexp_serial(job->cv, job->repr + 32 * lo, job->bases + 8 * lo, hi - lo, &job->results[k]);
+  }
+  return NULL;
+}
+
+static void scalars_to_repr(const CurveDef* cv, const u64* scalars, size_t n, int canonical, uint8_t* repr) {
+  for (size_t i = 0; i < n; i++) {
+    u64 v[4];
+    if (canonical) memcpy(v, scalars + 4 * i, 32);
+    else from_mont(&cv->fr, v, scalars + 4 * i);
+    for (int k = 0; k < 4; k++)
+      for (int b = 0; b < 8; b++) repr[32 * i + 8 * k + b] = (uint8_t)(v[k] >> (8 * b));
+  }
+}
+
+/* Public: halo2 best_multiexp.  scalars Montgomery unless canonical != 0;
+ * bases affine Montgomery (0,0)=identity; out affine Montgomery. */
+int msm_ref_best_multiexp(int curve, const u64* scalars, const u64* bases, size_t n, int canonical,
+                          int num_threads, u64 out[8]) {
+  if (curve < 0 || curve > 2 || num_threads < 1) return -1;
+  const CurveDef* cv = &CURVES[curve];
+  uint8_t* repr = (uint8_t*)malloc(n ? 32 * n : 32);
+  scalars_to_repr(cv, scalars, n, canonical, repr);
+  Jac acc;
+  memset(&acc, 0, sizeof(acc));
+  if (n > (size_t)num_threads) {
+    Job job;
+    job.cv = cv;
+    job.repr = repr;
+    job.bases = bases;
+    job.n = n;
+    job.chunk = n / (size_t)num_threads;
+    job.nchunks = (n + job.chunk - 1) / job.chunk;
+    job.results = (Jac*)calloc(job.nchunks, sizeof(Jac));
+    job.next = 0;
+    pthread_mutex_init(&job.mu, NULL);
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * num_threads);
+    for (int t = 0; t < num_threads; t++) pthread_create(&th[t], NULL, worker, &job);
+    for (int t = 0; t < num_threads; t++) pthread_join(th[t], NULL);
+    for (size_t k = 0; k < job.nchunks; k++) j_add(&cv->fp, &acc, &acc, &job.results[k]);
+    pthread_mutex_destroy(&job.mu);
+    free(th);
+    free(job.results);
+  } else {
+    multiexp_serial(cv, repr, bases, n, &acc);
+  }
+  j_to_aff(&cv->fp, out, &acc);
+  free(repr);
+  return 0;
+}
+
+/* ------------------------------------------------- synthetic inputs (tests) */
+static u64 mix64(u64 x) {
+  u64 z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static u64 synth_word(u64 seed, u64 i, u64 j) { return mix64(mix64(seed + i) + j); }
+
+static void synth_scalar(const Field* Fr, int nbits, u64 seed, u64 i, u64 out[4]) {
+  for (u64 t = 0;; t++) {
+    for (int k = 0; k < 4; k++) out[k] = synth_word(seed, i, 4 * t + k);
+    out[3] &= (1ull << (nbits - 192)) - 1ull;
+    if (!geq(out, Fr->p)) return;
+  }
+}
+
+/* canonical -> Montgomery: a * R2 * R^-1 with R2 = R^2 mod p computed as one^2 * ... */
+static void to_mont(const Field* F, u64 r[4], const u64 a[4]) {
+  /* R2 = (R mod p)^2 * R^-1 * R ... compute R2 by doubling `one` 256 times */
+  u64 r2[4];
+  memcpy(r2, F->one, 32);
+  for (int k = 0; k < 256; k++) f_add(F, r2, r2, r2); /* one * 2^256 = R^2 mod p */
+  f_mul(F, r, a, r2);
+}
+
+typedef struct {
+  const CurveDef* cv;
+  u64 seed, i0;
+  size_t lo, hi;
+  u64* out;
+  int kind; /* 0 scalars (Montgomery), 1 bases */
+} SynthJob;
+
+static void* synth_worker(void* arg) {
+  SynthJob* j = (SynthJob*)arg;
+  const CurveDef* cv = j->cv;
+  const Field* F = &cv->fp;
+  int nbits = (cv == &CURVES[2]) ? 254 : 255;
+  for (size_t i = j->lo; i < j->hi; i++) {
+    u64 a[4];
+    synth_scalar(&cv->fr, nbits, j->seed, j->i0 + i, a);
+    if (j->kind == 0) {
+      to_mont(&cv->fr, j->out + 4 * i, a);
+      continue;
+    }
+    if (f_is_zero(a)) a[0] = 1;
+    u64 g[8];
+    memcpy(g + 4, F->one, 32);
+    f_add(F, g + 4, g + 4, F->one); /* y = 2 */
+    if (cv->gx_neg_one) {
+      u64 z[4] = {0, 0, 0, 0};
+      f_sub(F, g, z, F->one);       /* x = -1 */
+    } else {
+      memcpy(g, F->one, 32);        /* x = 1 */
+    }
+    Jac acc;
+    memset(&acc, 0, sizeof(acc));
+    for (int k = 3; k >= 0; k--)
+      for (int b = 63; b >= 0; b--) {
+        j_dbl(F, &acc, &acc);
+        if ((a[k] >> b) & 1) j_add_aff(F, &acc, &acc, g);
+      }
+    j_to_aff(F, j->out + 8 * i, &acc);
+  }
+  return NULL;
+}
+
+static int synth_run(int curve, u64 seed, u64 i0, size_t n, int num_threads, u64* out, int kind) {
+  if (curve < 0 || curve > 2 || num_threads < 1) return -1;
+  pthread_t th[256];
+  SynthJob jobs[256];
+  if (num_threads > 256) num_threads = 256;
+  size_t per = (n + num_threads - 1) / num_threads;
+  for (int t = 0; t < num_threads; t++) {
+    size_t lo = per * t, hi = per * (t + 1);
+    if (lo > n) lo = n;
+    if (hi > n) hi = n;
+    jobs[t] = (SynthJob){&CURVES[curve], seed, i0, lo, hi, out, kind};
+    pthread_create(&th[t], NULL, synth_worker, &jobs[t]);
+  }
+  for (int t = 0; t < num_threads; t++) pthread_join(th[t], NULL);
+  return 0;
+}
+
+int msm_ref_synth_scalars(int curve, u64 seed, u64 i0, size_t n, int num_threads, u64* out) {
+  return synth_run(curve, seed, i0, n, num_threads, out, 0);
+}
+int msm_ref_synth_bases(int curve, u64 seed, u64 i0, size_t n, int num_threads, u64* out) {
+  return synth_run(curve, seed, i0, n, num_threads, out, 1);
+}

@@ -1,0 +1,170 @@
+"""Host-logic model of the HIP MSM pipeline (test helper).
+
+Mirrors halo2-aggregation_amd/csrc/{capi.hip:make_plan, msm_kernels.hpp} step
+by step, but over the additive group Z_r (a point is replaced by its discrete
+log, point addition by integer addition mod r).  It lets the CPU test-suite
+check the design's algebra -- signed digits, counting sort, slice ownership +
+fixup, segment / bit-decomposed bucket reduction and the window Horner --
+independently of any curve arithmetic.
+"""
+from __future__ import annotations
+
+import math
+
+
+def bit_length(v):
+    return int(v).bit_length()
+
+
+def make_plan(n, c_override=0, chunk_override=0):
+    lg = bit_length(max(n, 1)) - 1
+    c = c_override if c_override > 0 else max(4, min(18, lg - 4))
+    c = max(4, min(20, c))
+    W = (256 + c - 1) // c
+    K = 1 << (c - 1)
+    L1 = min(16, K)
+    NB = ((K + 1 + L1 - 1) // L1) * L1
+    M1 = NB // L1
+    NB2 = bit_length(M1 - 1)
+    work = n * W
+    target = 256 * 1024
+    chunk = max(16, (work + target - 1) // target)
+    if chunk_override:
+        chunk = chunk_override
+    nthreads = (work + chunk - 1) // chunk
+    return dict(c=c, W=W, K=K, L1=L1, log2L1=L1.bit_length() - 1, NB=NB, M1=M1, NB2=NB2, chunk=chunk,
+                nthreads=nthreads)
+
+
+def digits(s, c, W):
+    """k_digits: signed c-bit digits of canonical scalar s -> list of (|d|, neg)."""
+    out = []
+    carry = 0
+    for w in range(W):
+        raw = (s >> (w * c)) & ((1 << c) - 1) if w * c < 256 else 0
+        d = raw + carry
+        neg = 0
+        if w != W - 1 and d > (1 << (c - 1)):
+            d = (1 << c) - d
+            neg, carry = 1, 1
+        else:
+            carry = 0
+        out.append((d, neg))
+    return out
+
+
+def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
+    n = len(scalars)
+    if n == 0:
+        return 0
+    pl = make_plan(n, c_override, chunk_override)
+    c, W, NB, L1, M1, NB2 = pl["c"], pl["W"], pl["NB"], pl["L1"], pl["M1"], pl["NB2"]
+    TOT = W * NB + 1
+    counts = [0] * TOT
+    dig = [digits(s, c, W) for s in scalars]
+    for i in range(n):
+        for w, (d, _) in enumerate(dig[i]):
+            assert d <= pl["K"]
+            if d:
+                counts[w * NB + d] += 1
+    offsets, run = [], 0
+    for x in counts:
+        offsets.append(run)
+        run += x
+    cursor = list(offsets)
+    total = offsets[-1]
+    sorted_ = [None] * total
+    for w in range(W):  # scatter (any order inside a bucket is valid)
+        for i in range(n):
+            d, neg = dig[i][w]
+            if d:
+                sorted_[cursor[w * NB + d]] = (i, neg)
+                cursor[w * NB + d] += 1
+    nslots = TOT - 1
+
+    def find_bucket(pos):
+        lo, hi = 0, nslots
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if offsets[mid] <= pos:
+                lo = mid
+            else:
+                hi = mid
+        return lo
+
+    buckets = [0] * nslots
+    head = [0] * pl["nthreads"]
+    chunk = pl["chunk"]
+    for t in range(pl["nthreads"]):  # k_accumulate
+        start = t * chunk
+        if start >= total:
+            continue
+        end = min(start + chunk, total)
+        gb = find_bucket(start)
+        bend = offsets[gb + 1]
+        owned = offsets[gb] == start
+        acc = 0
+        for p in range(start, end):
+            if p == bend:
+                if owned:
+                    buckets[gb] = acc
+                else:
+                    head[t] = acc
+                acc = 0
+                gb += 1
+                while offsets[gb + 1] <= p:
+                    gb += 1
+                bend = offsets[gb + 1]
+                owned = True
+            i, neg = sorted_[p]
+            acc = (acc + (-dlogs[i] if neg else dlogs[i])) % r
+        if owned:
+            buckets[gb] = acc
+        else:
+            head[t] = acc
+    for t in range(pl["nthreads"]):  # k_fixup
+        start = t * chunk
+        if start >= total:
+            continue
+        end = min(start + chunk, total)
+        gb = find_bucket(end - 1)
+        bstart, bend = offsets[gb], offsets[gb + 1]
+        if bstart < start or bend <= end:
+            continue
+        acc = buckets[gb]
+        t2 = t + 1
+        while t2 < pl["nthreads"] and t2 * chunk < bend:
+            acc = (acc + head[t2]) % r
+            t2 += 1
+        buckets[gb] = acc
+    S = [0] * (W * M1)
+    T = [0] * (W * M1)
+    for w in range(W):  # k_bucket_seg
+        for j in range(M1):
+            base = w * NB + j * L1
+            s = t_ = 0
+            for i in range(L1 - 1, 0, -1):
+                if offsets[base + i] != offsets[base + i + 1]:
+                    s = (s + buckets[base + i]) % r
+                t_ = (t_ + s) % r
+            if offsets[base] != offsets[base + 1]:
+                s = (s + buckets[base]) % r
+            S[w * M1 + j], T[w * M1 + j] = s, t_
+    R = []
+    for w in range(W):  # k_bucket_bits + k_window
+        G = [sum(S[w * M1 + j] for j in range(M1) if (j >> b) & 1) % r for b in range(NB2)]
+        sumT = sum(T[w * M1:(w + 1) * M1]) % r
+        acc = 0
+        for b in range(NB2 - 1, -1, -1):
+            acc = (2 * acc + G[b]) % r
+        acc = (acc * L1 + sumT) % r
+        R.append(acc)
+    acc = R[W - 1]
+    for w in range(W - 2, -1, -1):  # host Horner
+        acc = (acc * (1 << c) + R[w]) % r
+    return acc
+
+
+def halo2_window(n):
+    """halo2 multiexp_serial window width (for documentation / comparison)."""
+    return 1 if n < 4 else (3 if n < 32 else int(math.ceil(math.log(n))))

@@ -1,0 +1,141 @@
+"""GPU parity tests: the HIP MSM (through the C-ABI) against the oracle.
+
+* golden vectors (Python restatement of halo2 best_multiexp), every case
+* every window width 4..20 on one vector (exercises all k_digits instances)
+* larger random sizes against the C restatement (oracle/msm_ref.c)
+* 2^20 against the known-discrete-log answer (size-independent property)
+* API surface: resident bases, multi-GPU entry, device pointers, errors
+"""
+import numpy as np
+import pytest
+
+import halo2_amd as H
+import msm_ref
+import pasta as P
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_vectors(golden):
+    for name, case in golden.items():
+        got = H.best_multiexp(case["curve"], case["scalars"], case["bases"])
+        assert np.array_equal(got, case["expected"]), name
+
+
+@pytest.mark.parametrize("c", list(range(4, 21)))
+def test_every_window_width(golden, gpu_ctx, c):
+    gpu_ctx.set_window(c)
+    try:
+        for name in ("pallas_n1024", "pallas_top_bits", "pallas_equal_scalars", "pallas_neg_pairs"):
+            case = golden[name]
+            got = gpu_ctx.msm(case["curve"], case["scalars"], case["bases"])
+            assert np.array_equal(got, case["expected"]), (name, c)
+    finally:
+        gpu_ctx.set_window(0)
+
+
+def test_canonical_scalars(golden):
+    case = golden["pallas_n4096"]
+    C = P.PALLAS
+    rinv = pow(P.R_MONT, -1, C.r)
+    canon = np.array([P.to_limbs(P.from_limbs(s) * rinv % C.r) for s in case["scalars"]], dtype=np.uint64)
+    got = H.best_multiexp(0, canon, case["bases"], canonical=True)
+    assert np.array_equal(got, case["expected"])
+
+
+def _torch_inputs(ctx, curve, n, i0=0):
+    import torch
+
+    dev = torch.device("cuda", ctx.device)
+    s = torch.empty((n, 4), dtype=torch.int64, device=dev)
+    b = torch.empty((n, 8), dtype=torch.int64, device=dev)
+    ctx.synth_scalars(curve, P.SEED_SCALARS, i0, n, s.data_ptr())
+    ctx.synth_bases(curve, P.SEED_BASES, i0, n, b.data_ptr())
+    torch.cuda.synchronize()
+    return s, b
+
+
+@pytest.mark.parametrize("curve", [0, 1, 2])
+def test_synth_on_device_matches_oracle(gpu_ctx, curve):
+    n = 3000
+    s, b = _torch_inputs(gpu_ctx, curve, n, i0=12345)
+    S = s.cpu().numpy().view(np.uint64)
+    B = b.cpu().numpy().view(np.uint64)
+    assert np.array_equal(S, msm_ref.synth_scalars(curve, P.SEED_SCALARS, 12345, n))
+    assert np.array_equal(B, msm_ref.synth_bases(curve, P.SEED_BASES, 12345, n))
+
+
+@pytest.mark.parametrize("curve,n", [(0, 5000), (0, (1 << 16) + 123), (1, 1 << 16), (2, 40000), (0, 1 << 18)])
+def test_vs_c_oracle(gpu_ctx, curve, n):
+    s, b = _torch_inputs(gpu_ctx, curve, n)
+    got = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+    S = s.cpu().numpy().view(np.uint64)
+    B = b.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, msm_ref.best_multiexp(curve, S, B))
+
+
+def test_known_dlog_2_20(gpu_ctx):
+    """2^20 Pallas MSM == [sum s_i a_i]G (a_i = discrete log of synthetic base i)."""
+    n = 1 << 20
+    s, b = _torch_inputs(gpu_ctx, 0, n)
+    got = gpu_ctx.msm_device(0, s.data_ptr(), b.data_ptr(), n)
+    C = P.PALLAS
+    S = msm_ref.synth_scalars(0, P.SEED_SCALARS, 0, n)       # Montgomery form
+    A = msm_ref.synth_scalars(0, P.SEED_BASES, 0, n)         # dlogs a_i (Montgomery)
+    rinv = pow(P.R_MONT, -1, C.r)
+    tot = 0
+    for k in range(0, n, 1 << 16):  # sum s_i a_i in R^2-scaled Montgomery domain
+        ss = [int(x) for x in _to_int(S[k:k + (1 << 16)])]
+        aa = [int(x) for x in _to_int(A[k:k + (1 << 16)])]
+        tot += sum(x * y for x, y in zip(ss, aa))
+    tot = tot * rinv * rinv % C.r
+    # a_i == 0 maps to 1 in the generator; never happens for these seeds (checked)
+    assert P.limbs_to_point(C, [int(x) for x in got]) == C.mul(tot, C.gen)
+
+
+def _to_int(L):
+    L = L.astype(object)
+    return L[:, 0] + (L[:, 1] << 64) + (L[:, 2] << 128) + (L[:, 3] << 192)
+
+
+def test_all_equal_scalars_large(gpu_ctx):
+    """One bucket per window holds every point: long fixup chains."""
+    n = 1 << 16
+    s, b = _torch_inputs(gpu_ctx, 0, n)
+    s[:] = s[7]
+    got = gpu_ctx.msm_device(0, s.data_ptr(), b.data_ptr(), n)
+    assert np.array_equal(got, msm_ref.best_multiexp(0, s.cpu().numpy().view(np.uint64),
+                                                     b.cpu().numpy().view(np.uint64)))
+
+
+def test_resident_bases_window(golden, gpu_ctx):
+    case = golden["pallas_n4096"]
+    rb = gpu_ctx.upload_bases(0, case["bases"])
+    try:
+        got = gpu_ctx.msm_resident(rb, 0, case["scalars"])
+        assert np.array_equal(got, case["expected"])
+        sub = golden["pallas_n1024"]
+        assert np.array_equal(gpu_ctx.msm_resident(rb, 0, case["scalars"][:1024]), sub["expected"])
+        with pytest.raises(H.PmError):
+            gpu_ctx.msm_resident(rb, 4000, case["scalars"][:200])
+    finally:
+        rb.release()
+
+
+def test_multi_entry_and_point_add(golden):
+    case = golden["pallas_n4096"]
+    ngpu = H.device_count()
+    got = H.msm_multi(0, case["scalars"], case["bases"], ngpu)
+    assert np.array_equal(got, case["expected"])
+    a = H.best_multiexp(0, case["scalars"][:2000], case["bases"][:2000])
+    b = H.best_multiexp(0, case["scalars"][2000:], case["bases"][2000:])
+    assert np.array_equal(H.point_add(0, a, b), case["expected"])
+
+
+def test_errors():
+    with pytest.raises(H.PmError):
+        H.best_multiexp(7, np.zeros((1, 4), np.uint64), np.zeros((1, 8), np.uint64))
+    with pytest.raises(ValueError):
+        H.best_multiexp(0, np.zeros((2, 4), np.uint64), np.zeros((1, 8), np.uint64))
+    assert np.array_equal(H.best_multiexp(0, np.zeros((0, 4), np.uint64), np.zeros((0, 8), np.uint64)),
+                          np.zeros(8, np.uint64))

@@ -1,0 +1,108 @@
+"""CPU tests: the oracle against the golden vectors and known answers, and the
+host-side logic of the HIP pipeline (tests/pipeline_model.py)."""
+import random
+
+import numpy as np
+import pytest
+
+import msm_ref
+import pasta as P
+import pipeline_model as PM
+
+
+def test_curve_constants():
+    assert P.self_check()
+
+
+def test_golden_python_oracle(golden):
+    """Recompute the small golden cases with the Python restatement of
+    best_multiexp (independent of the fixture generator's run)."""
+    for name, case in golden.items():
+        if case["scalars"].shape[0] > 255:
+            continue
+        C = P.CURVES[case["curve"]]
+        sc = [P.from_limbs(s) * pow(P.R_MONT, -1, C.r) % C.r for s in case["scalars"]]
+        pts = [P.limbs_to_point(C, list(b)) for b in case["bases"]]
+        got = C.best_multiexp(sc, pts)
+        assert P.point_to_limbs(C, got) == [int(x) for x in case["expected"]], name
+
+
+def test_golden_c_oracle(golden):
+    """The C restatement (independent field/curve code) reproduces every vector."""
+    for name, case in golden.items():
+        out = msm_ref.best_multiexp(case["curve"], case["scalars"], case["bases"], threads=4)
+        assert np.array_equal(out, case["expected"]), name
+
+
+def test_c_oracle_thread_count_invariant(golden):
+    case = golden["pallas_n1024"]
+    outs = {tuple(msm_ref.best_multiexp(0, case["scalars"], case["bases"], threads=t)) for t in (1, 3, 8, 17)}
+    assert len(outs) == 1
+
+
+def test_c_oracle_canonical_flag(golden):
+    case = golden["pallas_n255"]
+    C = P.PALLAS
+    canon = np.array([P.to_limbs(P.from_limbs(s) * pow(P.R_MONT, -1, C.r) % C.r) for s in case["scalars"]],
+                     dtype=np.uint64)
+    assert np.array_equal(msm_ref.best_multiexp(0, canon, case["bases"], canonical=True), case["expected"])
+
+
+@pytest.mark.parametrize("curve", [0, 1, 2])
+def test_synth_generators_match(curve):
+    """The C synth generator (mirrored by the HIP one) matches the Python one."""
+    C = P.CURVES[curve]
+    idx = [0, 1, 2, 77, 1000]
+    B = msm_ref.synth_bases(curve, P.SEED_BASES, 0, 1001, threads=4)
+    S = msm_ref.synth_scalars(curve, P.SEED_SCALARS, 0, 1001, threads=4)
+    for i in idx:
+        a = P.synth_base_dlog(C, P.SEED_BASES, i)
+        assert P.limbs_to_point(C, list(B[i])) == C.mul(a, C.gen)
+        s = P.synth_scalar(P.SEED_SCALARS, i, C.r, C.scalar_bits)
+        assert P.from_limbs(S[i]) == s * P.R_MONT % C.r
+
+
+def test_halo2_window_formula():
+    # 2^18 -> 13, 2^20 -> 14, 2^22 -> 16
+    assert [PM.halo2_window(1 << k) for k in (18, 20, 22)] == [13, 14, 16]
+    assert PM.halo2_window(3) == 1 and PM.halo2_window(31) == 3
+
+
+@pytest.mark.parametrize("c", [4, 5, 8, 11, 13, 15, 16, 17])
+def test_signed_digits_reconstruct(c):
+    rng = random.Random(c)
+    W = (256 + c - 1) // c
+    r = P.VESTA_P
+    for s in [0, 1, r - 1, (1 << 254), (1 << 255) - 1] + [rng.randrange(r) for _ in range(200)]:
+        ds = PM.digits(s, c, W)
+        assert all(0 <= d <= (1 << (c - 1)) for d, _ in ds)
+        assert sum((-d if neg else d) << (w * c) for w, (d, neg) in enumerate(ds)) == s
+
+
+@pytest.mark.parametrize("n,c,chunk", [(1, 0, 0), (2, 4, 16), (7, 5, 3), (64, 6, 16), (200, 8, 5),
+                                       (300, 4, 1000), (513, 7, 37), (1000, 0, 0), (1000, 10, 2)])
+def test_pipeline_model_random(n, c, chunk):
+    rng = random.Random(n * 31 + c)
+    r = P.VESTA_P
+    s = [rng.randrange(r) for _ in range(n)]
+    a = [rng.randrange(r) for _ in range(n)]
+    assert PM.msm_model(s, a, r, c, chunk) == sum(x * y for x, y in zip(s, a)) % r
+
+
+@pytest.mark.parametrize("chunk", [1, 2, 16, 100])
+def test_pipeline_model_giant_bucket(chunk):
+    """All scalars equal: one bucket per window spans many slices (fixup chain)."""
+    r = P.VESTA_P
+    n = 500
+    s = [0x1234567890ABCDEF << 100] * n
+    a = list(range(1, n + 1))
+    assert PM.msm_model(s, a, r, 6, chunk) == sum(x * y for x, y in zip(s, a)) % r
+
+
+def test_pipeline_model_sparse():
+    r = P.VESTA_P
+    s = [0, 0, 5, 0, r - 1, 0, 1 << 200]
+    a = [3, 4, 5, 6, 7, 8, 9]
+    for c in (4, 9, 16):
+        for chunk in (1, 3, 16):
+            assert PM.msm_model(s, a, r, c, chunk) == sum(x * y for x, y in zip(s, a)) % r

@@ -1,0 +1,50 @@
+"""Per-kernel timing of the MSM pipeline at several sizes (diagnostic)."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "halo2-aggregation_amd"))
+import torch  # noqa: E402
+
+import halo2_amd as H  # noqa: E402
+
+KERNELS = ["digits", "scan", "scatter", "accumulate", "fixup", "bucket_seg", "bucket_bits", "window"]
+
+
+def main():
+    curve = int(os.environ.get("CURVE", "0"))
+    sizes = [int(x) for x in os.environ.get("LOGN", "16,18,20,22").split(",")]
+    cs = [int(x) for x in os.environ.get("WINDOWS", "0").split(",")]
+    ctx = H.Context(0)
+    nmax = 1 << max(sizes)
+    s = torch.empty((nmax, 4), dtype=torch.int64, device="cuda")
+    b = torch.empty((nmax, 8), dtype=torch.int64, device="cuda")
+    ctx.synth_scalars(curve, 0x5EED, 0, nmax, s.data_ptr())
+    t = time.time()
+    ctx.synth_bases(curve, 0xA11CE, 0, nmax, b.data_ptr())
+    print(json.dumps({"synth_bases_s": time.time() - t, "n": nmax}), flush=True)
+    for lg in sizes:
+        n = 1 << lg
+        for c in cs:
+            ctx.set_window(c)
+            ctx.set_timing(False)
+            ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+            reps = 5
+            t = time.time()
+            for _ in range(reps):
+                ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+            wall = (time.time() - t) / reps
+            ctx.set_timing(True)
+            ctx.reset_stats()
+            for _ in range(reps):
+                ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+            ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}
+            print(json.dumps({"logn": lg, "c": c, "wall_ms": round(wall * 1e3, 3), "Mscalar_s": round(n / wall / 1e6, 2),
+                              "kernels_ms": ks}), flush=True)
+    ctx.set_timing(False)
+
+
+if __name__ == "__main__":
+    main()
