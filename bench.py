@@ -1,0 +1,198 @@
+"""bench.py -- Pallas MSM throughput on MI355X (BASELINE.json metric).
+
+python bench.py --gpus N --steps K --warmup W   (N>1: launched by torch.distributed.run)
+
+One step = one Pallas MSM over this rank's slice of 2^20 (scalar, base) pairs
+(rank r owns pairs [r*2^20, (r+1)*2^20) of an N*2^20-point MSM, weak scaling),
+with scalars and bases already resident in HBM, plus the exchange step: an
+all-gather of the per-rank partial points over RCCL and their fold on the host
+(EC addition is not limb-wise, so no all-reduce).  `value` = N*2^20 / step time.
+
+`roofline` is for the dominant kernel (k_accumulate), its duration measured
+live with HIP events on the context stream over the timed region.
+`cpu_baseline` times the C restatement of halo2 best_multiexp (oracle/msm_ref.c)
+on the host cores of the same box, on the same inputs, at N=1 on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "halo2-aggregation_amd"))
+
+METRIC = "Pallas MSM Mscalar/s at 2^20 (1/2/4/8 GPU); aggregated proofs verified/s"
+LOGN = 20
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_PAIR = 96            # 32 B scalar + 64 B affine base
+SEED_SCALARS, SEED_BASES = 0x5EED, 0xA11CE
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--logn", type=int, default=LOGN)
+    ap.add_argument("--window", type=int, default=0, help="force window width c (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def load_valu_peak():
+    p = os.path.join(ROOT, "profiles", "valu_peak.json")
+    if os.path.exists(p):
+        return json.load(open(p))
+    return None
+
+
+def load_pmc_traffic(workload):
+    p = os.path.join(ROOT, "profiles", "pmc_accumulate.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    import halo2_amd as H
+    from sharded import combine_partials, shard_range
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n = 1 << args.logn
+    curve = H.PALLAS
+    ctx = H.Context(local)
+    if args.window:
+        ctx.set_window(args.window)
+    dev = torch.device("cuda", local)
+    d_s = torch.empty((n, 4), dtype=torch.int64, device=dev)
+    d_b = torch.empty((n, 8), dtype=torch.int64, device=dev)
+    i0, _ = shard_range(rank, world, n)
+    ctx.synth_scalars(curve, SEED_SCALARS, i0, n, d_s.data_ptr())
+    ctx.synth_bases(curve, SEED_BASES, i0, n, d_b.data_ptr())
+    torch.cuda.synchronize()
+
+    gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
+
+    def padd(a, b):
+        return H.point_add(curve, a, b)
+
+    def step():
+        part = ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n)
+        return combine_partials(part, dist, dev, padd, world, gathered)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(True)
+    ctx.reset_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        result = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    launches, acc_ms = ctx.kernel_stats("accumulate")
+    kernels = {k: round(ctx.kernel_stats(k)[1] / max(1, ctx.kernel_stats(k)[0]), 4)
+               for k in ["digits", "scan", "scatter", "accumulate", "fixup", "bucket_seg", "bucket_bits", "window"]}
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = world * n / (elapsed / args.steps) / 1e6
+        acc_avg_ms = acc_ms / max(1, launches)
+        # algorithmic bytes of one accumulate launch: the launch consumes all n
+        # (scalar, base) pairs of the MSM (every window) -> 96 B x n
+        alg_bytes = BYTES_PER_PAIR * n
+        achieved = alg_bytes / (acc_avg_ms * 1e-3) / 1e9
+        workload = f"pallas_msm_2^{args.logn}_per_gpu"
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc_traffic(workload),
+                "kernel": "k_accumulate", "avg_launch_ms": round(acc_avg_ms, 4),
+                "alg_bytes_per_launch": alg_bytes}
+        vp = load_valu_peak()
+        if vp:
+            # The binding roofline is integer VALU: one XYZZ mixed
+            # add = 10 Montgomery products = 10 x 88 v_mad_u64_u32 (Pasta
+            # moduli); ~n*W adds per launch; peak = measured mad issue rate.
+            W = windows_for(n, args.window)
+            mads = n * W * 10 * 88
+            ach = mads / (acc_avg_ms * 1e-3) / 1e12
+            roof["valu_int"] = {"achieved": round(ach, 3), "peak": vp["v_mad_u64_u32_Tops"], "unit": "T v_mad_u64_u32/s",
+                                "frac": round(ach / vp["v_mad_u64_u32_Tops"], 4), "mads_per_launch": mads}
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mscalar/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (SplitMix64 scalars in [0,r), bases [a_i]G generated on device)",
+            "config": {"workload": workload, "curve": "pallas", "n_per_gpu": n, "n_total": world * n,
+                       "scalars": "montgomery", "bases": "affine montgomery, HBM-resident",
+                       "parallelism": f"point-slice x{world} + RCCL all-gather of partial points"},
+            "kernels_ms": kernels,
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(d_s, d_b, n, result, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def windows_for(n, c_override=0):
+    """Window count of the engine's launch plan (capi.hip make_plan)."""
+    lg = max(n, 1).bit_length() - 1
+    c = c_override if c_override > 0 else max(4, min(18, lg - 4))
+    c = max(4, min(20, c))
+    return (256 + c - 1) // c
+
+
+def cpu_baseline(d_s, d_b, n, gpu_result, budget_s):
+    """C restatement of halo2 best_multiexp on the host, same inputs."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import msm_ref
+
+    S = d_s.cpu().numpy().view(np.uint64)
+    B = d_b.cpu().numpy().view(np.uint64)
+    threads = int(os.environ.get("BENCH_CPU_THREADS", "16"))
+    reps, t0 = 0, time.perf_counter()
+    match = None
+    while True:
+        out = msm_ref.best_multiexp(0, S, B, threads=threads)
+        reps += 1
+        if match is None:
+            match = bool(np.array_equal(out, gpu_result))
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(reps * n / dt / 1e6, 4), "unit": "Mscalar/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x Pallas best_multiexp of the same 2^{n.bit_length() - 1} inputs "
+                      f"({dt:.1f} s, oracle/msm_ref.c, {threads} threads)",
+            "matches_gpu": match}
+
+
+if __name__ == "__main__":
+    main()

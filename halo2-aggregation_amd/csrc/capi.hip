@@ -15,7 +15,7 @@
 #include <vector>
 
 #include "../../include/pasta_msm.h"
-#include "curve.hpp"
+#include "msm_kernels.hpp"
 #include "runtime.hpp"
 
 using namespace pm;
@@ -119,7 +119,10 @@ MsmPlan make_plan(size_t n, int c_override) {
   c = std::max(kMinC, std::min(kMaxC, c));
   pl.c = c;
   pl.W = (256 + c - 1) / c;
-  pl.K = 1 << (c - 1);
+  pl.base = 256 / pl.W;
+  pl.extra = 256 % pl.W;
+  pl.cmax = pl.base + (pl.extra ? 1 : 0);
+  pl.K = 1 << (pl.cmax - 1);
   pl.L1 = std::min(16, pl.K);
   pl.log2L1 = bit_length((uint32_t)pl.L1) - 1;
   pl.NB = ((pl.K + 1 + pl.L1 - 1) / pl.L1) * pl.L1;
@@ -130,6 +133,7 @@ MsmPlan make_plan(size_t n, int c_override) {
   const size_t target = 256 * 1024;  // lanes in flight: 256 CUs x 16 waves x 64
   pl.chunk = (uint32_t)std::max<size_t>(16, (work + target - 1) / target);
   pl.nthreads = (uint32_t)((work + pl.chunk - 1) / pl.chunk);
+  pl.maxlong = (uint32_t)(work / ((size_t)kMaxChain * pl.chunk) + 1);
   return pl;
 }
 

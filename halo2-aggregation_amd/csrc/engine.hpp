@@ -35,22 +35,23 @@
 namespace pm {
 // ---------------------------------------------------------- MSM pipeline
 
-template <class Fs, int C>
-void launch_digits_c(const uint32_t* s, uint32_t n, int NB, uint32_t canonical, uint32_t* digits,
+template <class Fs, int W>
+void launch_digits_w(const uint32_t* s, uint32_t n, int NB, uint32_t canonical, uint32_t* digits,
                      uint32_t* counts, hipStream_t st) {
-  k_digits<Fs, C><<<(n + 255) / 256, 256, 0, st>>>(s, n, NB, canonical, digits, counts);
+  k_digits<Fs, W><<<(n + 255) / 256, 256, 0, st>>>(s, n, NB, canonical, digits, counts);
 }
 
+// one instance per window count reachable from c in [kMinC, kMaxC]
 template <class Fs>
-int launch_digits(int c, const uint32_t* s, uint32_t n, int NB, uint32_t canonical, uint32_t* digits,
+int launch_digits(int W, const uint32_t* s, uint32_t n, int NB, uint32_t canonical, uint32_t* digits,
                   uint32_t* counts, hipStream_t st) {
-  switch (c) {
-#define PM_C(k) \
-  case k: launch_digits_c<Fs, k>(s, n, NB, canonical, digits, counts, st); return PM_OK;
-    PM_C(4) PM_C(5) PM_C(6) PM_C(7) PM_C(8) PM_C(9) PM_C(10) PM_C(11) PM_C(12) PM_C(13) PM_C(14)
-    PM_C(15) PM_C(16) PM_C(17) PM_C(18) PM_C(19) PM_C(20)
-#undef PM_C
-    default: return set_error(PM_ERR_UNSUPPORTED, "window width out of range");
+  switch (W) {
+#define PM_W(k) \
+  case k: launch_digits_w<Fs, k>(s, n, NB, canonical, digits, counts, st); return PM_OK;
+    PM_W(13) PM_W(14) PM_W(15) PM_W(16) PM_W(18) PM_W(19) PM_W(20) PM_W(22) PM_W(24) PM_W(26) PM_W(29)
+    PM_W(32) PM_W(37) PM_W(43) PM_W(52) PM_W(64)
+#undef PM_W
+    default: return set_error(PM_ERR_UNSUPPORTED, "window count out of range");
   }
 }
 
@@ -83,6 +84,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->segT.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->bits.ensure((size_t)pl.W * (pl.NB2 + 1) * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->win.ensure((size_t)pl.W * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->longs.ensure(16 + (size_t)pl.maxlong * sizeof(LongChain)))) return rc;
   if ((rc = ctx->ensure_pinned((size_t)pl.W * sizeof(Xyzz<F>)))) return rc;
 
   uint32_t* digits = (uint32_t*)ctx->digits.p;
@@ -99,9 +101,12 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   Xyzz<F>* R = (Xyzz<F>*)ctx->win.p;
   const uint32_t un = (uint32_t)n;
 
+  uint32_t* nlong = (uint32_t*)ctx->longs.p;
+  LongChain* longs = (LongChain*)((char*)ctx->longs.p + 16);
   HIP_TRY(hipMemsetAsync(counts, 0, TOT * 4, st));
+  HIP_TRY(hipMemsetAsync(nlong, 0, 16, st));
   PM_LAUNCH(ctx, "digits",
-            rc = launch_digits<Fs>(pl.c, d_scalars, un, pl.NB, (flags & PM_SCALARS_CANONICAL) ? 1u : 0u,
+            rc = launch_digits<Fs>(pl.W, d_scalars, un, pl.NB, (flags & PM_SCALARS_CANONICAL) ? 1u : 0u,
                                    digits, counts, st));
   if (rc) return rc;
   PM_LAUNCH(ctx, "scan", {
@@ -115,9 +120,11 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   PM_LAUNCH(ctx, "accumulate",
             (k_accumulate<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, nslots, d_bases,
                                                                          pl.chunk, buckets, head)));
-  PM_LAUNCH(ctx, "fixup",
-            (k_fixup<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(offsets, nslots, pl.chunk, pl.nthreads,
-                                                                    buckets, head)));
+  PM_LAUNCH(ctx, "fixup", {
+    k_fixup<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(offsets, nslots, pl.chunk, pl.nthreads, buckets, head,
+                                                           longs, nlong);
+    k_fixup_long<F><<<pl.maxlong, 256, 0, st>>>(longs, nlong, buckets, head);
+  });
   PM_LAUNCH(ctx, "bucket_seg",
             (k_bucket_seg<F><<<(pl.W * pl.M1 + 255) / 256, 256, 0, st>>>(offsets, buckets, pl.W, pl.NB, pl.L1,
                                                                           S, T)));
@@ -128,11 +135,11 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   HIP_TRY(hipStreamSynchronize(st));
   ctx->end_call();
 
-  // window combine on the host: sum_w 2^(c w) R_w (Horner)
+  // window combine on the host: sum_w 2^(o_w) R_w (Horner, c_w doublings)
   const Xyzz<F>* hR = (const Xyzz<F>*)ctx->h_pinned;
   Xyzz<F> acc = hR[pl.W - 1];
   for (int w = pl.W - 2; w >= 0; w--) {
-    for (int k = 0; k < pl.c; k++) acc = xyzz_dbl<F>(acc);
+    for (int k = 0; k < pl.width(w); k++) acc = xyzz_dbl<F>(acc);
     acc = xyzz_add<F>(acc, hR[w]);
   }
   *result = acc;
@@ -193,14 +200,21 @@ int synth_bases_impl(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, void* d_o
 
 }  // namespace pm
 
-// host-only table (kept out of the device compilation pass)
+// Explicit instantiations are visible to both compilation passes, so the
+// device pass instantiates every kernel the host driver launches; the op
+// table (host function pointers) exists only in the host pass.
 #if defined(__HIP_DEVICE_COMPILE__)
-#define PM_DEFINE_CURVE_OPS(Cv, name)
+#define PM_OPS_TABLE(Cv, name)
 #else
-#define PM_DEFINE_CURVE_OPS(Cv, name)                                                        \
-  namespace pm {                                                                             \
-  extern const CurveOps name;                                                                \
-  const CurveOps name = {&msm_device_to_aff<Cv>, &point_add_impl<typename Cv::Base>,          \
-                         &synth_scalars_impl<Cv>, &synth_bases_impl<Cv>};                     \
-  }
+#define PM_OPS_TABLE(Cv, name)                                                                 \
+  extern const CurveOps name;                                                                  \
+  const CurveOps name = {&msm_device_to_aff<Cv>, &point_add_impl<typename Cv::Base>,            \
+                         &synth_scalars_impl<Cv>, &synth_bases_impl<Cv>};
 #endif
+#define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
+  namespace pm {                                                                               \
+  template int msm_device_to_aff<Cv>(Ctx*, const void*, const void*, size_t, uint32_t, uint64_t*); \
+  template int synth_scalars_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, uint32_t, void*);     \
+  template int synth_bases_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, void*);                 \
+  PM_OPS_TABLE(Cv, name)                                                                       \
+  }

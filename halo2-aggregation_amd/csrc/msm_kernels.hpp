@@ -15,12 +15,13 @@
 //                   sorted list, summing consecutive same-bucket points with
 //                   XYZZ mixed additions (load-balanced regardless of the
 //                   bucket-size distribution).      [VALU-int bound, dominant]
-//   5. k_fixup      folds the slice-boundary partial sums into their bucket.
+//   5. k_fixup      folds the slice-boundary partial sums into their bucket
+//                   (k_fixup_long: block tree for buckets spanning many slices).
 //   6. k_bucket_seg segment running sums: S_j = sum B, T_j = sum i*B (L1 wide).
 //   7. k_bucket_bits per window: G_b = sum_{j: bit b of j} S_j and sum T_j via
 //                   LDS tree reductions (parallel form of sum_j j*S_j).
 //   8. k_window     per window R_w = sum T + L1 * sum_b 2^b G_b.
-// The host then combines windows (Horner with c doublings per window).
+// The host then combines windows (Horner with c_w doublings per window).
 #pragma once
 #include "curve.hpp"
 
@@ -73,15 +74,26 @@ __device__ __forceinline__ Xyzz<F> load_xyzz(const Xyzz<F>* src) {
 }
 
 // --------------------------------------------------------------- 1. digits
-// Signed c-bit digits: d in [-2^(c-1)+1, 2^(c-1)], code = |d| | sign<<31,
-// code 0 = skip.  W = ceil(256 / c) windows always absorbs the final carry for
-// scalars < 2^255.
-template <class Fs, int C>
+// W windows split the 256-bit range evenly: window w has width
+// c_w = 256/W + (w < 256%W) and bit offset o_w = w*(256/W) + min(w, 256%W),
+// so no window is left with a handful of bits (which would make a few giant
+// buckets).  Signed digits: d in [-2^(c_w-1)+1, 2^(c_w-1)], code = |d| |
+// sign<<31, code 0 = skip.  The top window never produces a carry because
+// scalars are < 2^255.
+template <int W>
+struct WinGeom {
+  static constexpr int base = 256 / W;
+  static constexpr int extra = 256 % W;
+  static constexpr __host__ __device__ int width(int w) { return base + (w < extra ? 1 : 0); }
+  static constexpr __host__ __device__ int offset(int w) { return w * base + (w < extra ? w : extra); }
+};
+
+template <class Fs, int W>
 __global__ void __launch_bounds__(256) k_digits(const uint32_t* __restrict__ scalars, uint32_t n,
                                                 int NB, uint32_t canonical,
                                                 uint32_t* __restrict__ digits,
                                                 uint32_t* __restrict__ counts) {
-  constexpr int W = (256 + C - 1) / C;
+  using G = WinGeom<W>;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint4* q = reinterpret_cast<const uint4*>(scalars + 8ull * i);
@@ -90,12 +102,12 @@ __global__ void __launch_bounds__(256) k_digits(const uint32_t* __restrict__ sca
   uint32_t carry = 0;
 #pragma unroll
   for (int w = 0; w < W; w++) {
-    const int bit = w * C;
+    const int C = G::width(w);
+    const int bit = G::offset(w);
     const int limb = bit >> 5, sh = bit & 31;
     uint32_t lo = s.l[limb] >> sh;
     uint32_t hi = (sh != 0 && limb + 1 < 8) ? (s.l[limb + 1] << (32 - sh)) : 0u;
-    uint32_t raw = (lo | hi);
-    if (C < 32) raw &= (1u << C) - 1u;
+    const uint32_t raw = (lo | hi) & ((1u << C) - 1u);
     uint32_t d = raw + carry;
     uint32_t neg = 0;
     if (w != W - 1 && d > (1u << (C - 1))) {
@@ -262,11 +274,22 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
 }
 
 // --------------------------------------------------------------- 5. fixup
+// The owner of a bucket that runs past its slice adds the head partials of
+// the following slices.  Chains up to kMaxChain are walked serially; longer
+// ones (giant buckets: adversarial or highly repetitive scalars) are queued
+// for k_fixup_long, one workgroup per bucket with an LDS tree.
+constexpr uint32_t kMaxChain = 32;
+struct LongChain {
+  uint32_t gb, t_first, t_last;
+};
+
 template <class F>
 __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offsets, uint32_t nslots,
                                                uint32_t chunk, uint32_t nthreads,
                                                Xyzz<F>* __restrict__ buckets,
-                                               const Xyzz<F>* __restrict__ head) {
+                                               const Xyzz<F>* __restrict__ head,
+                                               LongChain* __restrict__ longs,
+                                               uint32_t* __restrict__ nlong) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nthreads) return;
   const uint32_t total = offsets[nslots];
@@ -276,10 +299,38 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offs
   const uint32_t gb = find_bucket(offsets, nslots, end - 1);
   const uint32_t bstart = offsets[gb], bend = offsets[gb + 1];
   if (bstart < start || bend <= end) return;  // not owned, or fully inside
+  const uint32_t t_last = min((bend - 1) / chunk, nthreads - 1);
+  if (t_last - t > kMaxChain) {
+    const uint32_t k = atomicAdd(nlong, 1u);
+    longs[k] = LongChain{gb, t + 1, t_last};
+    return;
+  }
   Xyzz<F> acc = load_xyzz<F>(&buckets[gb]);
-  for (uint32_t t2 = t + 1; t2 < nthreads && (size_t)t2 * chunk < bend; t2++)
-    acc = xyzz_add<F>(acc, load_xyzz<F>(&head[t2]));
+  for (uint32_t t2 = t + 1; t2 <= t_last; t2++) acc = xyzz_add<F>(acc, load_xyzz<F>(&head[t2]));
   store_xyzz<F>(&buckets[gb], acc);
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_fixup_long(const LongChain* __restrict__ longs,
+                                                    const uint32_t* __restrict__ nlong,
+                                                    Xyzz<F>* __restrict__ buckets,
+                                                    const Xyzz<F>* __restrict__ head) {
+  __shared__ Xyzz<F> lds[256];
+  if (blockIdx.x >= *nlong) return;
+  const LongChain lc = longs[blockIdx.x];
+  const int tid = threadIdx.x;
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256) acc = xyzz_add<F>(acc, load_xyzz<F>(&head[t2]));
+  lds[tid] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) {
+      acc = xyzz_add<F>(acc, lds[tid + s]);
+      lds[tid] = acc;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) store_xyzz<F>(&buckets[lc.gb], xyzz_add<F>(load_xyzz<F>(&buckets[lc.gb]), acc));
 }
 
 // ------------------------------------------------------ 6. segment sums

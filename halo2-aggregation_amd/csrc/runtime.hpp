@@ -31,9 +31,11 @@ struct Buf {
 };
 
 struct MsmPlan {
-  int c;          // window width (bits)
-  int W;          // windows = ceil(256 / c)
-  int K;          // max |digit| = 2^(c-1)
+  int c;          // target window width (bits)
+  int W;          // windows = ceil(256 / c); widths base or base+1 (WinGeom)
+  int base, extra;
+  int cmax;       // widest window
+  int K;          // max |digit| = 2^(cmax-1)
   int L1;         // bucket-segment length of k_bucket_seg
   int log2L1;
   int NB;         // bucket slots per window (K+1 rounded up to L1)
@@ -42,6 +44,8 @@ struct MsmPlan {
   uint32_t n;
   uint32_t chunk;     // sorted entries per accumulate lane
   uint32_t nthreads;  // accumulate lanes
+  uint32_t maxlong;   // bound on buckets needing k_fixup_long
+  int width(int w) const { return base + (w < extra ? 1 : 0); }
 };
 
 MsmPlan make_plan(size_t n, int c_override);
@@ -62,7 +66,7 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win;
+      win, longs;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // timing
@@ -73,7 +77,7 @@ struct pm_ctx {
 
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
-            &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win};
+            &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs};
   }
   ~pm_ctx();
   int begin_call();

@@ -37,6 +37,14 @@ class PmError(RuntimeError):
 
 
 def _load():
+    # torch wheels bundle their own libamdhip64.so.7.  Loading torch first makes
+    # the dynamic loader resolve our DT_NEEDED libamdhip64.so.7 to that same
+    # copy, so the process runs ONE HIP runtime whether or not torch is used
+    # (two runtimes in one process fail with "No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libpasta_msm.so not built at {LIB_PATH} (run __graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH)

@@ -21,7 +21,9 @@ def make_plan(n, c_override=0, chunk_override=0):
     c = c_override if c_override > 0 else max(4, min(18, lg - 4))
     c = max(4, min(20, c))
     W = (256 + c - 1) // c
-    K = 1 << (c - 1)
+    base, extra = 256 // W, 256 % W
+    cmax = base + (1 if extra else 0)
+    K = 1 << (cmax - 1)
     L1 = min(16, K)
     NB = ((K + 1 + L1 - 1) // L1) * L1
     M1 = NB // L1
@@ -32,16 +34,25 @@ def make_plan(n, c_override=0, chunk_override=0):
     if chunk_override:
         chunk = chunk_override
     nthreads = (work + chunk - 1) // chunk
-    return dict(c=c, W=W, K=K, L1=L1, log2L1=L1.bit_length() - 1, NB=NB, M1=M1, NB2=NB2, chunk=chunk,
+    widths = [base + (1 if w < extra else 0) for w in range(W)]
+    return dict(c=c, W=W, widths=widths, K=K, L1=L1, log2L1=L1.bit_length() - 1, NB=NB, M1=M1, NB2=NB2, chunk=chunk,
                 nthreads=nthreads)
 
 
-def digits(s, c, W):
-    """k_digits: signed c-bit digits of canonical scalar s -> list of (|d|, neg)."""
+def window_widths(W):
+    base, extra = 256 // W, 256 % W
+    return [base + (1 if w < extra else 0) for w in range(W)]
+
+
+def digits(s, W):
+    """k_digits: signed digits of canonical scalar s over the W balanced
+    windows (WinGeom) -> list of (|d|, neg)."""
     out = []
     carry = 0
-    for w in range(W):
-        raw = (s >> (w * c)) & ((1 << c) - 1) if w * c < 256 else 0
+    off = 0
+    for w, c in enumerate(window_widths(W)):
+        raw = (s >> off) & ((1 << c) - 1)
+        off += c
         d = raw + carry
         neg = 0
         if w != W - 1 and d > (1 << (c - 1)):
@@ -61,7 +72,7 @@ def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
     c, W, NB, L1, M1, NB2 = pl["c"], pl["W"], pl["NB"], pl["L1"], pl["M1"], pl["NB2"]
     TOT = W * NB + 1
     counts = [0] * TOT
-    dig = [digits(s, c, W) for s in scalars]
+    dig = [digits(s, W) for s in scalars]
     for i in range(n):
         for w, (d, _) in enumerate(dig[i]):
             assert d <= pl["K"]
@@ -160,8 +171,8 @@ def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
         acc = (acc * L1 + sumT) % r
         R.append(acc)
     acc = R[W - 1]
-    for w in range(W - 2, -1, -1):  # host Horner
-        acc = (acc * (1 << c) + R[w]) % r
+    for w in range(W - 2, -1, -1):  # host Horner, c_w doublings
+        acc = (acc * (1 << pl["widths"][w]) + R[w]) % r
     return acc
 
 

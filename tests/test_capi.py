@@ -36,3 +36,22 @@ def test_last_error_is_thread_local_string():
 def test_gfx950_code_object_embedded():
     blob = open(H.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
+
+
+def test_device_code_has_every_launched_kernel():
+    """Each kernel the host driver launches has a gfx950 kernel descriptor
+    (.kd) in the embedded code objects (a missing device instantiation aborts
+    at launch with 'Cannot find Symbol')."""
+    blob = open(H.LIB_PATH, "rb").read()
+    kds = set(re.findall(rb"(_ZN2pm[A-Za-z0-9_]+)\.kd", blob))
+    names = [k.decode() for k in kds]
+
+    def count(stem):
+        return sum(1 for n in names if stem in n)
+
+    assert count("8k_digits") == 3 * 16  # 3 scalar fields x 16 window counts
+    for stem in ("12k_accumulate", "7k_fixupI", "12k_fixup_long", "12k_bucket_seg", "13k_bucket_bits", "8k_window",
+                 "15k_synth_scalars", "13k_synth_bases"):
+        assert count(stem) == 3, stem
+    for stem in ("13k_scan_reduce", "10k_scan_top", "11k_scan_down", "9k_scatter"):
+        assert count(stem) == 1, stem

@@ -1,0 +1,83 @@
+"""CPU multi-process test of the N>1 path (gloo, world_size 2): each rank
+computes its slice's partial MSM (C oracle stands in for the GPU), the partials
+are all-gathered and folded by halo2-aggregation_amd/sharded.py exactly as in
+bench.py, and every rank must hold the full MSM."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_per_rank, q):
+    import sys
+
+    for p in (os.path.join(ROOT, "halo2-aggregation_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    import msm_ref
+    import pasta as P
+    from sharded import combine_partials, shard_range
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    C = P.PALLAS
+    i0, n = shard_range(rank, world, n_per_rank)
+    S = msm_ref.synth_scalars(0, P.SEED_SCALARS, i0, n, threads=2)
+    B = msm_ref.synth_bases(0, P.SEED_BASES, i0, n, threads=2)
+    part = msm_ref.best_multiexp(0, S, B, threads=2)
+
+    def padd(a, b):
+        s = C.add(P.limbs_to_point(C, [int(x) for x in a]), P.limbs_to_point(C, [int(x) for x in b]))
+        return np.array(P.point_to_limbs(C, s), dtype=np.uint64)
+
+    full = combine_partials(part, dist, torch.device("cpu"), padd, world)
+    q.put((rank, [int(x) for x in full]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_msm_gloo(world):
+    import msm_ref
+    import pasta as P
+
+    n_per_rank = 700
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = world * n_per_rank
+    S = msm_ref.synth_scalars(0, P.SEED_SCALARS, 0, n, threads=4)
+    B = msm_ref.synth_bases(0, P.SEED_BASES, 0, n, threads=4)
+    want = [int(x) for x in msm_ref.best_multiexp(0, S, B, threads=4)]
+    for r in range(world):
+        assert res[r] == want, r
+
+
+def test_split_range_covers():
+    from sharded import split_range
+
+    for n in (0, 1, 7, 1000, 1 << 20):
+        for w in (1, 2, 3, 8):
+            parts = [split_range(r, w, n) for r in range(w)]
+            assert sum(c for _, c in parts) == n
+            assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1) if parts[i + 1][1])

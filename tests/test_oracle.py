@@ -68,15 +68,28 @@ def test_halo2_window_formula():
     assert PM.halo2_window(3) == 1 and PM.halo2_window(31) == 3
 
 
-@pytest.mark.parametrize("c", [4, 5, 8, 11, 13, 15, 16, 17])
+@pytest.mark.parametrize("c", list(range(4, 21)))
 def test_signed_digits_reconstruct(c):
     rng = random.Random(c)
     W = (256 + c - 1) // c
+    widths = PM.window_widths(W)
+    assert sum(widths) == 256 and max(widths) - min(widths) <= 1
+    offs = [sum(widths[:w]) for w in range(W)]
     r = P.VESTA_P
     for s in [0, 1, r - 1, (1 << 254), (1 << 255) - 1] + [rng.randrange(r) for _ in range(200)]:
-        ds = PM.digits(s, c, W)
-        assert all(0 <= d <= (1 << (c - 1)) for d, _ in ds)
-        assert sum((-d if neg else d) << (w * c) for w, (d, neg) in enumerate(ds)) == s
+        ds = PM.digits(s, W)
+        assert all(0 <= d <= (1 << (cw - 1)) for (d, _), cw in zip(ds, widths))
+        assert sum((-d if neg else d) << o for o, (d, neg) in zip(offs, ds)) == s
+
+
+def test_balanced_windows_no_giant_buckets():
+    """Every window of a uniformly random scalar uses at least a quarter of
+    the widest window's digit range (no few-bit top window)."""
+    for c in range(4, 21):
+        W = (256 + c - 1) // c
+        widths = PM.window_widths(W)
+        top_bits = 254 - sum(widths[:-1])  # Pasta/BN254 scalars are < 2^255, bit 254 ~never set
+        assert top_bits >= max(widths) - 3, c
 
 
 @pytest.mark.parametrize("n,c,chunk", [(1, 0, 0), (2, 4, 16), (7, 5, 3), (64, 6, 16), (200, 8, 5),
