@@ -161,16 +161,14 @@ PM_HD Fe<P> fe_dbl(const Fe<P>& a) {
   return fe_add<P>(a, a);
 }
 
-// Montgomery product a*b*R^-1 mod p, CIOS, fully reduced.
+// Montgomery product a*b*R^-1 mod p, CIOS, fully reduced (portable form;
+// used on the host).
 template <class P>
-PM_HD Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
+inline Fe<P> fe_mul_portable(const Fe<P>& a, const Fe<P>& b) {
   uint32_t t[10];
-#pragma unroll
   for (int i = 0; i < 10; i++) t[i] = 0;
-#pragma unroll
   for (int i = 0; i < 8; i++) {
     uint64_t c = 0;
-#pragma unroll
     for (int j = 0; j < 8; j++) {
       uint64_t s = (uint64_t)a.l[j] * b.l[i] + t[j] + c;
       t[j] = (uint32_t)s;
@@ -182,7 +180,6 @@ PM_HD Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
     const uint32_t m = t[0] * P::INV;
     s = (uint64_t)m * P::MOD[0] + t[0];
     c = s >> 32;
-#pragma unroll
     for (int j = 1; j < 8; j++) {
       s = (uint64_t)m * P::MOD[j] + t[j] + c;
       t[j - 1] = (uint32_t)s;
@@ -193,6 +190,74 @@ PM_HD Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
     t[8] = t[9] + (uint32_t)(s >> 32);
   }
   return fe_reduce_once<P>(t, t[8]);
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// 96-bit column accumulator (acc = 64-bit VGPR pair, acc2 = overflow word):
+// acc += x*y with v_mad_u64_u32's carry-out (VCC) folded into acc2, i.e. two
+// VALU instructions per 32x32 product.  VCC is produced and consumed inside
+// one asm statement, so the compiler may interleave the statements freely.
+__device__ __forceinline__ void mac_vv(uint64_t& acc, uint32_t& acc2, uint32_t x, uint32_t y) {
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_addc_co_u32_e64 %1, %3, 0, %1, %2"
+      : "+v"(acc), "+v"(acc2), "=&s"(c0), "=&s"(c1)
+      : "v"(x), "v"(y));
+}
+// y = a modulus limb (compile-time constant, lives in an SGPR)
+__device__ __forceinline__ void mac_vs(uint64_t& acc, uint32_t& acc2, uint32_t x, uint32_t y) {
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_addc_co_u32_e64 %1, %3, 0, %1, %2"
+      : "+v"(acc), "+v"(acc2), "=&s"(c0), "=&s"(c1)
+      : "v"(x), "s"(y));
+}
+
+// Montgomery product by finely integrated product scanning (FIPS): column k
+// accumulates sum a_i b_{k-i} + sum m_i p_{k-i}; the low columns also produce
+// m_k = acc * (-p^-1) so that column k becomes divisible by 2^32.  Modulus
+// limbs that are zero (Pasta: p_4..p_6) are skipped at compile time, so a
+// Pasta product costs 64 + 32 + 8 multiply-adds.
+template <class P>
+__device__ __forceinline__ Fe<P> fe_mul_fips(const Fe<P>& a, const Fe<P>& b) {
+  uint32_t m[8], r[8];
+  uint64_t acc = 0;
+  uint32_t acc2 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) mac_vv(acc, acc2, a.l[i], b.l[k - i]);
+#pragma unroll
+    for (int i = 0; i < k; i++)
+      if (P::MOD[k - i] != 0u) mac_vs(acc, acc2, m[i], P::MOD[k - i]);
+    m[k] = (uint32_t)acc * P::INV;
+    mac_vs(acc, acc2, m[k], P::MOD[0]);
+    acc = (acc >> 32) | ((uint64_t)acc2 << 32);
+    acc2 = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int i = k - 7; i < 8; i++) mac_vv(acc, acc2, a.l[i], b.l[k - i]);
+#pragma unroll
+    for (int i = k - 7; i < 8; i++)
+      if (P::MOD[k - i] != 0u) mac_vs(acc, acc2, m[i], P::MOD[k - i]);
+    r[k - 8] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)acc2 << 32);
+    acc2 = 0;
+  }
+  r[7] = (uint32_t)acc;
+  return fe_reduce_once<P>(r, (uint32_t)(acc >> 32));
+}
+#endif
+
+template <class P>
+PM_HD Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fe_mul_fips<P>(a, b);
+#else
+  return fe_mul_portable<P>(a, b);
+#endif
 }
 
 template <class P>
