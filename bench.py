@@ -113,7 +113,7 @@ def main():
     ctx.set_timing(False)
     launches, acc_ms = ctx.kernel_stats("accumulate")
     kernels = {k: round(ctx.kernel_stats(k)[1] / max(1, ctx.kernel_stats(k)[0]), 4)
-               for k in ["digits", "scan", "scatter", "accumulate", "fixup", "bucket_seg", "bucket_bits", "window"]}
+               for k in ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg", "bucket_bits"]}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

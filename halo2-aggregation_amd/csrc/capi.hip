@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -123,7 +124,7 @@ MsmPlan make_plan(size_t n, int c_override) {
   pl.extra = 256 % pl.W;
   pl.cmax = pl.base + (pl.extra ? 1 : 0);
   pl.K = 1 << (pl.cmax - 1);
-  pl.L1 = std::min(16, pl.K);
+  pl.L1 = std::min(kL1, pl.K);
   pl.log2L1 = bit_length((uint32_t)pl.L1) - 1;
   pl.NB = ((pl.K + 1 + pl.L1 - 1) / pl.L1) * pl.L1;
   pl.M1 = pl.NB / pl.L1;
@@ -223,6 +224,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
   c->stream = c->own_stream;
+  if (const char* e = std::getenv("PM_PREFETCH")) c->prefetch = std::atoi(e);
   *out = c.release();
   return PM_OK;
 }

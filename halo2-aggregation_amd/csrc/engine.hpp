@@ -9,6 +9,7 @@
 #include <cstring>
 #include <string>
 
+#include "host_ec.hpp"
 #include "msm_kernels.hpp"
 #include "runtime.hpp"
 
@@ -36,18 +37,18 @@ namespace pm {
 // ---------------------------------------------------------- MSM pipeline
 
 template <class Fs, int W>
-void launch_digits_w(const uint32_t* s, uint32_t n, int NB, uint32_t canonical, uint32_t* digits,
-                     uint32_t* counts, hipStream_t st) {
-  k_digits<Fs, W><<<(n + 255) / 256, 256, 0, st>>>(s, n, NB, canonical, digits, counts);
+void launch_sort_hist_w(const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* digits,
+                        uint32_t* bh, hipStream_t st) {
+  k_sort_hist<Fs, W><<<g.nblk, kSortThreads, (size_t)W * g.NCB * 4, st>>>(s, n, canonical, g, digits, bh);
 }
 
 // one instance per window count reachable from c in [kMinC, kMaxC]
 template <class Fs>
-int launch_digits(int W, const uint32_t* s, uint32_t n, int NB, uint32_t canonical, uint32_t* digits,
-                  uint32_t* counts, hipStream_t st) {
+int launch_sort_hist(int W, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* digits,
+                     uint32_t* bh, hipStream_t st) {
   switch (W) {
 #define PM_W(k) \
-  case k: launch_digits_w<Fs, k>(s, n, NB, canonical, digits, counts, st); return PM_OK;
+  case k: launch_sort_hist_w<Fs, k>(s, n, canonical, g, digits, bh, st); return PM_OK;
     PM_W(13) PM_W(14) PM_W(15) PM_W(16) PM_W(18) PM_W(19) PM_W(20) PM_W(22) PM_W(24) PM_W(26) PM_W(29)
     PM_W(32) PM_W(37) PM_W(43) PM_W(52) PM_W(64)
 #undef PM_W
@@ -70,56 +71,72 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const hipStream_t st = ctx->stream;
   const size_t TOT = (size_t)pl.W * pl.NB + 1;
   const size_t nW = (size_t)n * pl.W;
+  SortGeom g;
+  g.FB = std::max(0, pl.cmax - 1 - 8);
+  g.NCB = (pl.K >> g.FB) + 1;
+  g.nblk = (int)((n + kSortB - 1) / kSortB);
+  const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
   int rc;
   if ((rc = ctx->digits.ensure(nW * 4))) return rc;
   if ((rc = ctx->sorted.ensure(nW * 4))) return rc;
-  if ((rc = ctx->counts.ensure(TOT * 4))) return rc;
+  if ((rc = ctx->mid.ensure(nW * 8))) return rc;
+  if ((rc = ctx->counts.ensure(TOTB * 4))) return rc;
+  if ((rc = ctx->cursor.ensure(TOTB * 4))) return rc;
   if ((rc = ctx->offsets.ensure(TOT * 4))) return rc;
-  if ((rc = ctx->cursor.ensure(TOT * 4))) return rc;
-  const uint32_t nb = (uint32_t)((TOT + kScanChunk - 1) / kScanChunk);
+  const uint32_t nb = (uint32_t)((TOTB + kScanChunk - 1) / kScanChunk);
   if ((rc = ctx->bsum.ensure((size_t)nb * 4))) return rc;
   if ((rc = ctx->buckets.ensure((size_t)pl.W * pl.NB * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->head.ensure((size_t)pl.nthreads * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segS.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segT.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->bits.ensure((size_t)pl.W * (pl.NB2 + 1) * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->win.ensure((size_t)pl.W * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->longs.ensure(16 + (size_t)pl.maxlong * sizeof(LongChain)))) return rc;
-  if ((rc = ctx->ensure_pinned((size_t)pl.W * sizeof(Xyzz<F>)))) return rc;
+  const size_t nG = (size_t)pl.W * (pl.NB2 + 1);
+  if ((rc = ctx->ensure_pinned(nG * sizeof(Xyzz<F>)))) return rc;
 
   uint32_t* digits = (uint32_t*)ctx->digits.p;
   uint32_t* sorted = (uint32_t*)ctx->sorted.p;
-  uint32_t* counts = (uint32_t*)ctx->counts.p;
+  uint64_t* mid = (uint64_t*)ctx->mid.p;
+  uint32_t* bh = (uint32_t*)ctx->counts.p;
+  uint32_t* bofs = (uint32_t*)ctx->cursor.p;
   uint32_t* offsets = (uint32_t*)ctx->offsets.p;
-  uint32_t* cursor = (uint32_t*)ctx->cursor.p;
   uint32_t* bsum = (uint32_t*)ctx->bsum.p;
   Xyzz<F>* buckets = (Xyzz<F>*)ctx->buckets.p;
   Xyzz<F>* head = (Xyzz<F>*)ctx->head.p;
   Xyzz<F>* S = (Xyzz<F>*)ctx->segS.p;
   Xyzz<F>* T = (Xyzz<F>*)ctx->segT.p;
   Xyzz<F>* G = (Xyzz<F>*)ctx->bits.p;
-  Xyzz<F>* R = (Xyzz<F>*)ctx->win.p;
   const uint32_t un = (uint32_t)n;
 
   uint32_t* nlong = (uint32_t*)ctx->longs.p;
   LongChain* longs = (LongChain*)((char*)ctx->longs.p + 16);
-  HIP_TRY(hipMemsetAsync(counts, 0, TOT * 4, st));
+  HIP_TRY(hipMemsetAsync(bh + (TOTB - 1), 0, 4, st));
   HIP_TRY(hipMemsetAsync(nlong, 0, 16, st));
-  PM_LAUNCH(ctx, "digits",
-            rc = launch_digits<Fs>(pl.W, d_scalars, un, pl.NB, (flags & PM_SCALARS_CANONICAL) ? 1u : 0u,
-                                   digits, counts, st));
+  PM_LAUNCH(ctx, "sort_hist",
+            rc = launch_sort_hist<Fs>(pl.W, d_scalars, un, (flags & PM_SCALARS_CANONICAL) ? 1u : 0u, g, digits,
+                                      bh, st));
   if (rc) return rc;
   PM_LAUNCH(ctx, "scan", {
-    k_scan_reduce<<<nb, kScanThreads, 0, st>>>(counts, (uint32_t)TOT, bsum);
+    k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum);
     k_scan_top<<<1, 1024, 0, st>>>(bsum, nb);
-    k_scan_down<<<nb, kScanThreads, 0, st>>>(counts, (uint32_t)TOT, bsum, offsets, cursor);
+    k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum, bofs, nullptr);
   });
-  PM_LAUNCH(ctx, "scatter",
-            (k_scatter<<<(uint32_t)((nW + 255) / 256), 256, 0, st>>>(digits, un, pl.W, pl.NB, cursor, sorted)));
+  const size_t lds_coarse = (size_t)2 * kSortB * 4 + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
+  PM_LAUNCH(ctx, "sort_coarse",
+            (k_sort_coarse<<<dim3(g.nblk, pl.W), kSortThreads, lds_coarse, st>>>(digits, un, g, bofs, mid)));
+  const size_t lds_fine = ((size_t)(1 << g.FB) + kSortThreads / 64 + 1) * 4;
+  PM_LAUNCH(ctx, "sort_fine",
+            (k_sort_fine<<<pl.W * g.NCB, kSortThreads, lds_fine, st>>>(mid, bofs, g, pl.W, pl.NB, offsets, sorted)));
   const uint32_t nslots = (uint32_t)(TOT - 1);
-  PM_LAUNCH(ctx, "accumulate",
-            (k_accumulate<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, nslots, d_bases,
-                                                                         pl.chunk, buckets, head)));
+  const bool prefetch = ctx->prefetch >= 0 ? ctx->prefetch != 0 : (size_t)n * 64 > kPrefetchBytes;
+  if (prefetch)
+    PM_LAUNCH(ctx, "accumulate",
+              (k_accumulate<F, true><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, nslots, d_bases,
+                                                                                 pl.chunk, buckets, head)));
+  else
+    PM_LAUNCH(ctx, "accumulate",
+              (k_accumulate<F, false><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, nslots, d_bases,
+                                                                                  pl.chunk, buckets, head)));
   PM_LAUNCH(ctx, "fixup", {
     k_fixup<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(offsets, nslots, pl.chunk, pl.nthreads, buckets, head,
                                                            longs, nlong);
@@ -130,18 +147,29 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
                                                                           S, T)));
   PM_LAUNCH(ctx, "bucket_bits",
             (k_bucket_bits<F><<<dim3(pl.NB2 + 1, pl.W), kRedThreads, 0, st>>>(S, T, pl.M1, pl.NB2, G)));
-  PM_LAUNCH(ctx, "window", (k_window<F><<<1, 64, 0, st>>>(G, pl.W, pl.NB2, pl.log2L1, R)));
-  HIP_TRY(hipMemcpyAsync(ctx->h_pinned, R, (size_t)pl.W * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(ctx->h_pinned, G, nG * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   ctx->end_call();
 
-  // window combine on the host: sum_w 2^(o_w) R_w (Horner, c_w doublings)
-  const Xyzz<F>* hR = (const Xyzz<F>*)ctx->h_pinned;
-  Xyzz<F> acc = hR[pl.W - 1];
-  for (int w = pl.W - 2; w >= 0; w--) {
-    for (int k = 0; k < pl.width(w); k++) acc = xyzz_dbl<F>(acc);
-    acc = xyzz_add<F>(acc, hR[w]);
+  // Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b}) as one
+  // Horner over absolute bit positions q (host_ec.hpp).
+  const Xyzz<F>* hG = (const Xyzz<F>*)ctx->h_pinned;
+  std::vector<std::vector<int>> at(256 + pl.NB2 + pl.log2L1 + 1);
+  int qmax = 0;
+  for (int w = 0; w < pl.W; w++) {
+    const int o = w * pl.base + std::min(w, pl.extra);
+    for (int b = 0; b <= pl.NB2; b++) {
+      const int q = b < pl.NB2 ? o + b + pl.log2L1 : o;
+      at[q].push_back(w * (pl.NB2 + 1) + b);
+      qmax = std::max(qmax, q);
+    }
   }
+  host::Pt<F> hacc = host::inf<F>();
+  for (int q = qmax; q >= 0; q--) {
+    hacc = host::dbl<F>(hacc);
+    for (int idx : at[q]) hacc = host::addp<F>(hacc, host::from_dev<F>(hG[idx]));
+  }
+  Xyzz<F> acc = host::to_dev<F>(hacc);
   *result = acc;
   return PM_OK;
 }

@@ -1,0 +1,191 @@
+// host_ec.hpp -- 64-bit-limb host arithmetic for the serial tail of the MSM.
+//
+// A single wave on the GPU pays ~7 us per dependent EC addition (a Montgomery
+// product is a ~100-long v_mad_u64_u32 dependency chain), while an x86 core
+// with 64x64->128 multiplies does one in well under 1 us.  The MSM therefore
+// ends on the host: the GPU delivers, per window w, the bit sums G_{w,b} and
+// sum_j T_{w,j}; the host evaluates  sum_w 2^{o_w} (sum_j T_{w,j} +
+// sum_b 2^{b + log2 L1} G_{w,b})  as ONE Horner over absolute bit positions
+// (~256 doublings + ~W*(NB2+1) additions) -- the same group element as the
+// per-window + cross-window Horner, with no per-window serial chain.
+//
+// Same representation as the device (Montgomery, R = 2^256, XYZZ); the u32
+// limb layout of Fe<P> is bit-identical to 4 x u64 little-endian.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include "curve.hpp"
+
+namespace pm {
+namespace host {
+
+typedef unsigned __int128 u128;
+
+template <class P>
+struct F64 {
+  static constexpr uint64_t mod(int i) { return (uint64_t)P::MOD[2 * i] | ((uint64_t)P::MOD[2 * i + 1] << 32); }
+  static constexpr uint64_t inv() {  // -p^-1 mod 2^64 (Newton from 1)
+    uint64_t p0 = mod(0), x = 1;
+    for (int i = 0; i < 7; i++) x *= 2 - p0 * x;
+    return (uint64_t)0 - x;
+  }
+};
+
+template <class P>
+struct E {
+  uint64_t v[4];
+};
+
+template <class P>
+inline bool is_zero(const E<P>& a) {
+  return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0;
+}
+
+template <class P>
+inline E<P> sub_p_if(const uint64_t t[4], uint64_t hi) {
+  uint64_t d[4], br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 x = (u128)t[i] - F64<P>::mod(i) - br;
+    d[i] = (uint64_t)x;
+    br = (uint64_t)(x >> 64) & 1;
+  }
+  E<P> r;
+  const bool take = hi || !br;
+  for (int i = 0; i < 4; i++) r.v[i] = take ? d[i] : t[i];
+  return r;
+}
+
+template <class P>
+inline E<P> add(const E<P>& a, const E<P>& b) {
+  uint64_t t[4], c = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 s = (u128)a.v[i] + b.v[i] + c;
+    t[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+  return sub_p_if<P>(t, c);
+}
+
+template <class P>
+inline E<P> sub(const E<P>& a, const E<P>& b) {
+  uint64_t t[4], br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 x = (u128)a.v[i] - b.v[i] - br;
+    t[i] = (uint64_t)x;
+    br = (uint64_t)(x >> 64) & 1;
+  }
+  if (br) {
+    uint64_t c = 0;
+    for (int i = 0; i < 4; i++) {
+      u128 s = (u128)t[i] + F64<P>::mod(i) + c;
+      t[i] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+  }
+  E<P> r;
+  memcpy(r.v, t, 32);
+  return r;
+}
+
+// CIOS Montgomery product, 4 x 64
+template <class P>
+inline E<P> mul(const E<P>& a, const E<P>& b) {
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  constexpr uint64_t INV = F64<P>::inv();
+  for (int i = 0; i < 4; i++) {
+    uint64_t c = 0;
+    for (int j = 0; j < 4; j++) {
+      u128 s = (u128)a.v[j] * b.v[i] + t[j] + c;
+      t[j] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    u128 s = (u128)t[4] + c;
+    t[4] = (uint64_t)s;
+    t[5] = (uint64_t)(s >> 64);
+    const uint64_t m = t[0] * INV;
+    s = (u128)m * F64<P>::mod(0) + t[0];
+    c = (uint64_t)(s >> 64);
+    for (int j = 1; j < 4; j++) {
+      s = (u128)m * F64<P>::mod(j) + t[j] + c;
+      t[j - 1] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    s = (u128)t[4] + c;
+    t[3] = (uint64_t)s;
+    t[4] = t[5] + (uint64_t)(s >> 64);
+  }
+  return sub_p_if<P>(t, t[4]);
+}
+
+template <class P>
+struct Pt {  // XYZZ, ZZ == 0 is the identity
+  E<P> X, Y, ZZ, ZZZ;
+};
+
+template <class P>
+inline Pt<P> inf() {
+  Pt<P> r;
+  memset(&r, 0, sizeof(r));
+  return r;
+}
+
+template <class P>
+inline Pt<P> dbl(const Pt<P>& p) {
+  if (is_zero(p.ZZ) || is_zero(p.Y)) return inf<P>();
+  const E<P> U = add(p.Y, p.Y);
+  const E<P> V = mul(U, U);
+  const E<P> W = mul(U, V);
+  const E<P> S = mul(p.X, V);
+  const E<P> XX = mul(p.X, p.X);
+  const E<P> M = add(add(XX, XX), XX);
+  Pt<P> r;
+  r.X = sub(mul(M, M), add(S, S));
+  r.Y = sub(mul(M, sub(S, r.X)), mul(W, p.Y));
+  r.ZZ = mul(V, p.ZZ);
+  r.ZZZ = mul(W, p.ZZZ);
+  return r;
+}
+
+template <class P>
+inline Pt<P> addp(const Pt<P>& p, const Pt<P>& q) {
+  if (is_zero(q.ZZ)) return p;
+  if (is_zero(p.ZZ)) return q;
+  const E<P> U1 = mul(p.X, q.ZZ);
+  const E<P> U2 = mul(q.X, p.ZZ);
+  const E<P> S1 = mul(p.Y, q.ZZZ);
+  const E<P> S2 = mul(q.Y, p.ZZZ);
+  const E<P> Pd = sub(U2, U1);
+  const E<P> R = sub(S2, S1);
+  if (is_zero(Pd)) {
+    if (is_zero(R)) return dbl(p);
+    return inf<P>();
+  }
+  const E<P> PP = mul(Pd, Pd);
+  const E<P> PPP = mul(Pd, PP);
+  const E<P> Q = mul(U1, PP);
+  Pt<P> r;
+  r.X = sub(sub(mul(R, R), PPP), add(Q, Q));
+  r.Y = sub(mul(R, sub(Q, r.X)), mul(S1, PPP));
+  r.ZZ = mul(mul(p.ZZ, q.ZZ), PP);
+  r.ZZZ = mul(mul(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+// reinterpret a device Xyzz<P> (8 x u32 LE limbs per coordinate)
+template <class P>
+inline Pt<P> from_dev(const Xyzz<P>& d) {
+  Pt<P> r;
+  static_assert(sizeof(Xyzz<P>) == sizeof(Pt<P>), "layout");
+  memcpy(&r, &d, sizeof(r));
+  return r;
+}
+template <class P>
+inline Xyzz<P> to_dev(const Pt<P>& h) {
+  Xyzz<P> r;
+  memcpy(&r, &h, sizeof(r));
+  return r;
+}
+
+}  // namespace host
+}  // namespace pm

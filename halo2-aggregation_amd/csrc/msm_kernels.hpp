@@ -5,12 +5,13 @@
 // reference is a CPU bucket method (unsigned c-bit windows, one bucket array
 // per window per rayon chunk).  This is an MI355X re-design of the same math:
 //
-//   1. k_digits     one lane per scalar: Montgomery -> canonical, signed c-bit
-//                   digits for all W windows (halves the bucket count), bucket
-//                   histogram via global atomics.            [integer, HBM]
-//   2. k_scan_*     exclusive scan of the W x NB histogram -> bucket offsets.
-//   3. k_scatter    counting-sort scatter: per window, point indices grouped by
-//                   bucket (sign in bit 31).                  [integer, HBM]
+//   1. k_sort_hist  one lane per scalar: Montgomery -> canonical, signed
+//                   digits for all W windows (halves the bucket count), LDS
+//                   histogram of (window, coarse bin) per block.   [HBM]
+//   2. k_scan_*     exclusive scan of the block histograms.
+//   3. k_sort_coarse / k_sort_fine: two-level LDS bucket sort -> per window,
+//                   point indices grouped by bucket (sign in bit 31) and the
+//                   bucket offsets.                                [HBM]
 //   4. k_accumulate every lane walks an equal-length slice of the concatenated
 //                   sorted list, summing consecutive same-bucket points with
 //                   XYZZ mixed additions (load-balanced regardless of the
@@ -20,8 +21,8 @@
 //   6. k_bucket_seg segment running sums: S_j = sum B, T_j = sum i*B (L1 wide).
 //   7. k_bucket_bits per window: G_b = sum_{j: bit b of j} S_j and sum T_j via
 //                   LDS tree reductions (parallel form of sum_j j*S_j).
-//   8. k_window     per window R_w = sum T + L1 * sum_b 2^b G_b.
-// The host then combines windows (Horner with c_w doublings per window).
+// The host (host_ec.hpp) then evaluates sum_w 2^{o_w} (sum T + L1 * sum_b 2^b
+// G_b) as one Horner over absolute bit positions.
 #pragma once
 #include "curve.hpp"
 
@@ -73,7 +74,7 @@ __device__ __forceinline__ Xyzz<F> load_xyzz(const Xyzz<F>* src) {
   return p;
 }
 
-// --------------------------------------------------------------- 1. digits
+// ------------------------------------------------------- 1. window geometry
 // W windows split the 256-bit range evenly: window w has width
 // c_w = 256/W + (w < 256%W) and bit offset o_w = w*(256/W) + min(w, 256%W),
 // so no window is left with a handful of bits (which would make a few giant
@@ -87,41 +88,6 @@ struct WinGeom {
   static constexpr __host__ __device__ int width(int w) { return base + (w < extra ? 1 : 0); }
   static constexpr __host__ __device__ int offset(int w) { return w * base + (w < extra ? w : extra); }
 };
-
-template <class Fs, int W>
-__global__ void __launch_bounds__(256) k_digits(const uint32_t* __restrict__ scalars, uint32_t n,
-                                                int NB, uint32_t canonical,
-                                                uint32_t* __restrict__ digits,
-                                                uint32_t* __restrict__ counts) {
-  using G = WinGeom<W>;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint4* q = reinterpret_cast<const uint4*>(scalars + 8ull * i);
-  Fe<Fs> s = load_fe4<Fs>(q);
-  if (!canonical) s = fe_from_mont<Fs>(s);
-  uint32_t carry = 0;
-#pragma unroll
-  for (int w = 0; w < W; w++) {
-    const int C = G::width(w);
-    const int bit = G::offset(w);
-    const int limb = bit >> 5, sh = bit & 31;
-    uint32_t lo = s.l[limb] >> sh;
-    uint32_t hi = (sh != 0 && limb + 1 < 8) ? (s.l[limb + 1] << (32 - sh)) : 0u;
-    const uint32_t raw = (lo | hi) & ((1u << C) - 1u);
-    uint32_t d = raw + carry;
-    uint32_t neg = 0;
-    if (w != W - 1 && d > (1u << (C - 1))) {
-      d = (1u << C) - d;
-      neg = 1;
-      carry = 1;
-    } else {
-      carry = 0;
-    }
-    const uint32_t code = d ? (d | (neg << 31)) : 0u;
-    digits[(size_t)w * n + i] = code;
-    if (d) atomicAdd(&counts[(size_t)w * NB + d], 1u);
-  }
-}
 
 // ----------------------------------------------------------------- 2. scan
 constexpr int kScanThreads = 256;
@@ -205,24 +171,173 @@ static __global__ void __launch_bounds__(kScanThreads) k_scan_down(const uint32_
   for (int k = 0; k < kScanPerThread; k++) {
     if (base + k < N) {
       offsets[base + k] = run;
-      cursor[base + k] = run;
+      if (cursor) cursor[base + k] = run;
     }
     run += v[k];
   }
 }
 
-// -------------------------------------------------------------- 3. scatter
-static __global__ void __launch_bounds__(256) k_scatter(const uint32_t* __restrict__ digits, uint32_t n, int W,
-                                                 int NB, uint32_t* __restrict__ cursor,
-                                                 uint32_t* __restrict__ sorted) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)n * W) return;
-  const uint32_t code = digits[idx];
-  if (!code) return;
-  const uint32_t w = (uint32_t)(idx / n), i = (uint32_t)(idx - (size_t)w * n);
-  const uint32_t slot = code & ~kNegBit;
-  const uint32_t pos = atomicAdd(&cursor[(size_t)w * NB + slot], 1u);
-  sorted[pos] = i | (code & kNegBit);
+// -------------------------------------------------------------- 3. sort
+// Bucket sort of the W x n digit codes without global atomics (replaces a
+// global-atomic counting sort that was 45% of the MSM at 2^20):
+//   k_sort_hist    per block of kSortB points: signed digits for all windows
+//                  (written coalesced to digits[w*n+i]) and an LDS histogram
+//                  over (window, coarse bin), coarse = slot >> FB; the block
+//                  histogram goes to bh[(w*NCB+cb)*nblk + blk] so one exclusive
+//                  scan of bh yields every block's output position.
+//   k_sort_coarse  block (blk, w): LDS-ranked, LDS-staged scatter of its codes
+//                  into the coarse segments (runs of consecutive addresses).
+//   k_sort_fine    block per (w, cb) segment: LDS counting sort on the FB fine
+//                  bits; writes the final bucket offsets and sorted[] entries.
+constexpr int kSortThreads = 256;
+constexpr int kSortPerThread = 8;
+constexpr int kSortB = kSortThreads * kSortPerThread;  // points per block
+
+struct SortGeom {
+  int FB;    // fine bits
+  int NCB;   // coarse bins per window
+  int nblk;  // point blocks
+};
+
+template <class Fs, int W>
+__global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                            uint32_t canonical, SortGeom g,
+                                                            uint32_t* __restrict__ digits,
+                                                            uint32_t* __restrict__ bh) {
+  using G = WinGeom<W>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
+  const int nbins = W * g.NCB;
+  for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
+  __syncthreads();
+  for (int r = 0; r < kSortPerThread; r++) {
+    const uint32_t i = blockIdx.x * kSortB + r * kSortThreads + threadIdx.x;
+    if (i >= n) break;
+    const uint4* q = reinterpret_cast<const uint4*>(scalars + 8ull * i);
+    Fe<Fs> s = load_fe4<Fs>(q);
+    if (!canonical) s = fe_from_mont<Fs>(s);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int C = G::width(w);
+      const int bit = G::offset(w);
+      const int limb = bit >> 5, sh = bit & 31;
+      uint32_t lo = s.l[limb] >> sh;
+      uint32_t hi = (sh != 0 && limb + 1 < 8) ? (s.l[limb + 1] << (32 - sh)) : 0u;
+      const uint32_t raw = (lo | hi) & ((1u << C) - 1u);
+      uint32_t d = raw + carry;
+      uint32_t neg = 0;
+      if (w != W - 1 && d > (1u << (C - 1))) {
+        d = (1u << C) - d;
+        neg = 1;
+        carry = 1;
+      } else {
+        carry = 0;
+      }
+      digits[(size_t)w * n + i] = d ? (d | (neg << 31)) : 0u;
+      if (d) atomicAdd(&hist[w * g.NCB + (d >> g.FB)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nbins; k += kSortThreads) bh[(size_t)k * g.nblk + blockIdx.x] = hist[k];
+}
+
+// block (blk = blockIdx.x, w = blockIdx.y)
+static __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const uint32_t* __restrict__ digits, uint32_t n,
+                                                                     SortGeom g, const uint32_t* __restrict__ bofs,
+                                                                     uint64_t* __restrict__ mid) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  uint64_t* stage = reinterpret_cast<uint64_t*>(sm);                   // kSortB entries
+  uint32_t* cnt = sm + 2 * kSortB;                                     // NCB
+  uint32_t* lstart = cnt + g.NCB;                                      // NCB + 1
+  uint32_t* scan_tmp = lstart + g.NCB + 1;                             // kSortThreads/64 + 1
+  const uint32_t w = blockIdx.y, blk = blockIdx.x;
+  for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) cnt[k] = 0;
+  __syncthreads();
+  uint32_t code[kSortPerThread];
+#pragma unroll
+  for (int r = 0; r < kSortPerThread; r++) {
+    const uint32_t i = blk * kSortB + r * kSortThreads + threadIdx.x;
+    code[r] = i < n ? digits[(size_t)w * n + i] : 0u;
+    if (code[r]) atomicAdd(&cnt[(code[r] & ~kNegBit) >> g.FB], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of cnt -> lstart (NCB <= a few hundred: one chunk per pass)
+  uint32_t carry = 0;
+  for (int base = 0; base < g.NCB; base += kSortThreads) {
+    const int k = base + threadIdx.x;
+    const uint32_t v = k < g.NCB ? cnt[k] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(v, scan_tmp, total);
+    if (k < g.NCB) lstart[k] = ex + carry;
+    carry += total;
+  }
+  if (threadIdx.x == 0) lstart[g.NCB] = carry;
+  __syncthreads();
+  for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) cnt[k] = lstart[k];  // cursors
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSortPerThread; r++) {
+    if (!code[r]) continue;
+    const uint32_t i = blk * kSortB + r * kSortThreads + threadIdx.x;
+    const uint32_t slot = code[r] & ~kNegBit;
+    const uint32_t pos = atomicAdd(&cnt[slot >> g.FB], 1u);
+    stage[pos] = ((uint64_t)slot << 32) | (i | (code[r] & kNegBit));
+  }
+  __syncthreads();
+  const uint32_t nvalid = lstart[g.NCB];
+  for (uint32_t e = threadIdx.x; e < nvalid; e += kSortThreads) {
+    const uint64_t v = stage[e];
+    const uint32_t cb = (uint32_t)(v >> 32) >> g.FB;
+    const uint32_t pos = bofs[((size_t)w * g.NCB + cb) * g.nblk + blk] + (e - lstart[cb]);
+    mid[pos] = v;
+  }
+}
+
+// block per (w, cb) segment; offsets[w*NB + slot] for its slots, sorted[]
+static __global__ void __launch_bounds__(kSortThreads) k_sort_fine(const uint64_t* __restrict__ mid,
+                                                                   const uint32_t* __restrict__ bofs, SortGeom g,
+                                                                   int W, int NB, uint32_t* __restrict__ offsets,
+                                                                   uint32_t* __restrict__ sorted) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  const int nf = 1 << g.FB;
+  uint32_t* hist = sm;                 // nf
+  uint32_t* scan_tmp = sm + nf;        // kSortThreads/64 + 1
+  const uint32_t seg = blockIdx.x;     // = w * NCB + cb
+  const uint32_t w = seg / g.NCB, cb = seg - w * g.NCB;
+  const uint32_t s0 = bofs[(size_t)seg * g.nblk];
+  const uint32_t s1 = bofs[(size_t)(seg + 1) * g.nblk];  // next segment (or total)
+  const uint32_t fmask = (uint32_t)nf - 1u;
+  for (int k = threadIdx.x; k < nf; k += kSortThreads) hist[k] = 0;
+  __syncthreads();
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += kSortThreads)
+    atomicAdd(&hist[(uint32_t)(mid[e] >> 32) & fmask], 1u);
+  __syncthreads();
+  // exclusive scan of the fine histogram; emit bucket offsets
+  uint32_t carry = 0;
+  for (int base = 0; base < nf; base += kSortThreads) {
+    const int k = base + threadIdx.x;
+    const uint32_t v = k < nf ? hist[k] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(v, scan_tmp, total);
+    if (k < nf) {
+      const uint32_t slot = (cb << g.FB) + k;
+      hist[k] = s0 + ex + carry;  // cursor
+      if (slot < (uint32_t)NB) offsets[(size_t)w * NB + slot] = s0 + ex + carry;
+    }
+    carry += total;
+  }
+  // slots beyond the coarse range (window padding) and the final sentinel
+  if (cb == (uint32_t)g.NCB - 1) {
+    for (uint32_t slot = ((uint32_t)g.NCB << g.FB) + threadIdx.x; slot < (uint32_t)NB; slot += kSortThreads)
+      offsets[(size_t)w * NB + slot] = s1;
+    if (threadIdx.x == 0 && w == (uint32_t)W - 1) offsets[(size_t)W * NB] = s1;
+  }
+  __syncthreads();
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += kSortThreads) {
+    const uint64_t v = mid[e];
+    const uint32_t pos = atomicAdd(&hist[(uint32_t)(v >> 32) & fmask], 1u);
+    sorted[pos] = (uint32_t)v;
+  }
 }
 
 // ----------------------------------------------------------- 4. accumulate
@@ -241,7 +356,10 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ off
   return lo;
 }
 
-template <class F>
+// PREFETCH: issue the next entry's index + base loads before this entry's
+// addition (hides the dependent HBM gather when the bases exceed the
+// Infinity Cache, at the cost of 16+ VGPRs).
+template <class F, bool PREFETCH>
 __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t nslots,
                                                     const uint32_t* __restrict__ bases, uint32_t chunk,
@@ -256,6 +374,9 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
   uint32_t bend = offsets[gb + 1];
   bool owned = offsets[gb] == start;
   Xyzz<F> acc = xyzz_inf<F>();
+  uint32_t code = sorted[start];
+  Aff<F> P;
+  if (PREFETCH) P = load_aff<F>(bases + 16ull * (code & ~kNegBit));
   for (uint32_t p = start; p < end; p++) {
     if (p == bend) {
       store_xyzz<F>(owned ? &buckets[gb] : &head[t], acc);
@@ -265,10 +386,20 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
       bend = offsets[gb + 1];
       owned = true;
     }
-    const uint32_t code = sorted[p];
-    Aff<F> P = load_aff<F>(bases + 16ull * (code & ~kNegBit));
-    if (code & kNegBit) P.y = fe_neg<F>(P.y);
-    acc = xyzz_add_aff<F>(acc, P);
+    Aff<F> cur;
+    uint32_t ccode = code;
+    if (PREFETCH) {
+      cur = P;
+      if (p + 1 < end) {
+        code = sorted[p + 1];
+        P = load_aff<F>(bases + 16ull * (code & ~kNegBit));
+      }
+    } else {
+      cur = load_aff<F>(bases + 16ull * (ccode & ~kNegBit));
+      if (p + 1 < end) code = sorted[p + 1];
+    }
+    if (ccode & kNegBit) cur.y = fe_neg<F>(cur.y);
+    acc = xyzz_add_aff<F>(acc, cur);
   }
   store_xyzz<F>(owned ? &buckets[gb] : &head[t], acc);
 }
@@ -383,23 +514,6 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
     __syncthreads();
   }
   if (tid == 0) store_xyzz<F>(&G[(size_t)w * (NBITS2 + 1) + job], acc);
-}
-
-// ------------------------------------------------------ 8. window result
-template <class F>
-__global__ void k_window(const Xyzz<F>* __restrict__ G, int W, int NBITS2, int log2L1,
-                         Xyzz<F>* __restrict__ R) {
-  const int w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= W) return;
-  const Xyzz<F>* g = G + (size_t)w * (NBITS2 + 1);
-  Xyzz<F> acc = xyzz_inf<F>();
-  for (int b = NBITS2 - 1; b >= 0; b--) {
-    acc = xyzz_dbl<F>(acc);
-    acc = xyzz_add<F>(acc, load_xyzz<F>(&g[b]));
-  }
-  for (int k = 0; k < log2L1; k++) acc = xyzz_dbl<F>(acc);
-  acc = xyzz_add<F>(acc, load_xyzz<F>(&g[NBITS2]));
-  store_xyzz<F>(&R[w], acc);
 }
 
 // ------------------------------------------------------ synthetic inputs

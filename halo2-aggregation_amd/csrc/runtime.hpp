@@ -22,6 +22,9 @@ int set_error(int code, const std::string& msg);
 constexpr int kMinC = 4;
 constexpr int kMaxC = 20;
 constexpr size_t kMaxPoints = size_t(1) << 26;
+constexpr int kL1 = 8;
+// bases larger than this (bytes) use the prefetching accumulate kernel
+constexpr size_t kPrefetchBytes = size_t(128) << 20;  // bucket-segment length of k_bucket_seg (latency: 2*L1-1 adds)
 
 struct Buf {
   void* p = nullptr;
@@ -62,11 +65,12 @@ struct pm_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   int window_c = 0;
+  int prefetch = -1;  // -1 auto, 0 off, 1 on (diagnostics: PM_PREFETCH env)
   bool timing = false;
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs;
+      win, longs, mid;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // timing
@@ -77,7 +81,7 @@ struct pm_ctx {
 
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
-            &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs};
+            &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid};
   }
   ~pm_ctx();
   int begin_call();

@@ -24,7 +24,7 @@ def make_plan(n, c_override=0, chunk_override=0):
     base, extra = 256 // W, 256 % W
     cmax = base + (1 if extra else 0)
     K = 1 << (cmax - 1)
-    L1 = min(16, K)
+    L1 = min(8, K)
     NB = ((K + 1 + L1 - 1) // L1) * L1
     M1 = NB // L1
     NB2 = bit_length(M1 - 1)
@@ -161,21 +161,82 @@ def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
             if offsets[base] != offsets[base + 1]:
                 s = (s + buckets[base]) % r
             S[w * M1 + j], T[w * M1 + j] = s, t_
-    R = []
-    for w in range(W):  # k_bucket_bits + k_window
+    widths = pl["widths"]
+    at = {}
+    for w in range(W):  # k_bucket_bits -> host Horner over absolute bit positions
         G = [sum(S[w * M1 + j] for j in range(M1) if (j >> b) & 1) % r for b in range(NB2)]
         sumT = sum(T[w * M1:(w + 1) * M1]) % r
-        acc = 0
-        for b in range(NB2 - 1, -1, -1):
-            acc = (2 * acc + G[b]) % r
-        acc = (acc * L1 + sumT) % r
-        R.append(acc)
-    acc = R[W - 1]
-    for w in range(W - 2, -1, -1):  # host Horner, c_w doublings
-        acc = (acc * (1 << pl["widths"][w]) + R[w]) % r
+        o = sum(widths[:w])
+        for b in range(NB2):
+            at.setdefault(o + b + pl["log2L1"], []).append(G[b])
+        at.setdefault(o, []).append(sumT)
+    acc = 0
+    for q in range(max(at), -1, -1):
+        acc = 2 * acc % r
+        for v in at.get(q, []):
+            acc = (acc + v) % r
     return acc
 
 
 def halo2_window(n):
     """halo2 multiexp_serial window width (for documentation / comparison)."""
     return 1 if n < 4 else (3 if n < 32 else int(math.ceil(math.log(n))))
+
+
+def sort_model(dig, n, W, K, cmax, NB, sort_b=2048):
+    """Two-level LDS bucket sort (k_sort_hist / k_scan / k_sort_coarse /
+    k_sort_fine) -> (offsets, sorted entries as (i, neg))."""
+    FB = max(0, cmax - 1 - 8)
+    NCB = (K >> FB) + 1
+    nblk = (n + sort_b - 1) // sort_b
+    bh = [0] * (W * NCB * nblk + 1)
+    for blk in range(nblk):
+        for i in range(blk * sort_b, min(n, (blk + 1) * sort_b)):
+            for w in range(W):
+                d, _ = dig[i][w]
+                if d:
+                    bh[(w * NCB + (d >> FB)) * nblk + blk] += 1
+    bofs, run = [], 0
+    for x in bh:
+        bofs.append(run)
+        run += x
+    total = bofs[-1]
+    mid = [None] * total
+    for blk in range(nblk):
+        for w in range(W):
+            cur = {}
+            for i in range(blk * sort_b, min(n, (blk + 1) * sort_b)):
+                d, neg = dig[i][w]
+                if d:
+                    cb = d >> FB
+                    k = cur.get(cb, 0)
+                    mid[bofs[(w * NCB + cb) * nblk + blk] + k] = (d, i, neg)
+                    cur[cb] = k + 1
+    offsets = [None] * (W * NB + 1)
+    sorted_ = [None] * total
+    nf = 1 << FB
+    for seg in range(W * NCB):
+        w, cb = divmod(seg, NCB)
+        s0, s1 = bofs[seg * nblk], bofs[(seg + 1) * nblk]
+        hist = [0] * nf
+        for e in range(s0, s1):
+            hist[mid[e][0] & (nf - 1)] += 1
+        run = s0
+        cursor = []
+        for k in range(nf):
+            slot = (cb << FB) + k
+            if slot < NB:
+                offsets[w * NB + slot] = run
+            cursor.append(run)
+            run += hist[k]
+        if cb == NCB - 1:
+            for slot in range(NCB << FB, NB):
+                offsets[w * NB + slot] = s1
+            if w == W - 1:
+                offsets[W * NB] = s1
+        for e in range(s0, s1):
+            d, i, neg = mid[e]
+            f = d & (nf - 1)
+            sorted_[cursor[f]] = (i, neg)
+            cursor[f] += 1
+    return offsets, sorted_

@@ -49,9 +49,9 @@ def test_device_code_has_every_launched_kernel():
     def count(stem):
         return sum(1 for n in names if stem in n)
 
-    assert count("8k_digits") == 3 * 16  # 3 scalar fields x 16 window counts
-    for stem in ("12k_accumulate", "7k_fixupI", "12k_fixup_long", "12k_bucket_seg", "13k_bucket_bits", "8k_window",
+    assert count("11k_sort_hist") == 3 * 16  # 3 scalar fields x 16 window counts
+    for stem in ("12k_accumulate", "7k_fixupI", "12k_fixup_long", "12k_bucket_seg", "13k_bucket_bits",
                  "15k_synth_scalars", "13k_synth_bases"):
         assert count(stem) == 3, stem
-    for stem in ("13k_scan_reduce", "10k_scan_top", "11k_scan_down", "9k_scatter"):
+    for stem in ("13k_scan_reduce", "10k_scan_top", "11k_scan_down", "13k_sort_coarse", "11k_sort_fine"):
         assert count(stem) == 1, stem

@@ -119,3 +119,34 @@ def test_pipeline_model_sparse():
     for c in (4, 9, 16):
         for chunk in (1, 3, 16):
             assert PM.msm_model(s, a, r, c, chunk) == sum(x * y for x, y in zip(s, a)) % r
+
+
+@pytest.mark.parametrize("n,c,sort_b", [(100, 4, 16), (1000, 9, 128), (3000, 12, 512), (2500, 16, 300),
+                                        (700, 18, 64), (50, 20, 2048)])
+def test_two_level_sort_model(n, c, sort_b):
+    """The LDS two-level bucket sort yields exactly the counting-sort offsets
+    and the same (point, sign) multiset in every bucket."""
+    rng = random.Random(n + c)
+    r = P.VESTA_P
+    pl = PM.make_plan(n, c)
+    W, NB = pl["W"], pl["NB"]
+    cmax = max(pl["widths"])
+    dig = [PM.digits(rng.randrange(r), W) for _ in range(n)]
+    offsets, sorted_ = PM.sort_model(dig, n, W, pl["K"], cmax, NB, sort_b)
+    counts = [0] * (W * NB + 1)
+    for i in range(n):
+        for w, (d, _) in enumerate(dig[i]):
+            if d:
+                counts[w * NB + d] += 1
+    ref, run = [], 0
+    for x in counts:
+        ref.append(run)
+        run += x
+    assert offsets == ref
+    want = {}
+    for i in range(n):
+        for w, (d, neg) in enumerate(dig[i]):
+            if d:
+                want.setdefault((w, d), []).append((i, neg))
+    for (w, slot), items in want.items():
+        assert sorted(sorted_[ref[w * NB + slot]:ref[w * NB + slot + 1]]) == sorted(items)
