@@ -50,7 +50,8 @@ def test_device_code_has_every_launched_kernel():
         return sum(1 for n in names if stem in n)
 
     assert count("11k_sort_hist") == 3 * 16  # 3 scalar fields x 16 window counts
-    for stem in ("12k_accumulate", "7k_fixupI", "12k_fixup_long", "12k_bucket_seg", "13k_bucket_bits",
+    assert count("12k_accumulate") == 3 * 2  # 3 curves x {plain, prefetch}
+    for stem in ("7k_fixupI", "12k_fixup_long", "12k_bucket_seg", "13k_bucket_bits",
                  "15k_synth_scalars", "13k_synth_bases"):
         assert count(stem) == 3, stem
     for stem in ("13k_scan_reduce", "10k_scan_top", "11k_scan_down", "13k_sort_coarse", "11k_sort_fine"):
