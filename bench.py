@@ -163,7 +163,7 @@ def main():
 def windows_for(n, c_override=0):
     """Window count of the engine's launch plan (capi.hip make_plan)."""
     lg = max(n, 1).bit_length() - 1
-    c = c_override if c_override > 0 else max(4, min(18, lg - 4))
+    c = c_override if c_override > 0 else max(4, min(16, lg - 4))
     c = max(4, min(20, c))
     return (256 + c - 1) // c
 

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/pasta_msm.h"
+#include "accum_plan.hpp"
 #include "msm_kernels.hpp"
 #include "runtime.hpp"
 
@@ -116,7 +117,7 @@ static int bit_length(uint32_t v) {
 MsmPlan make_plan(size_t n, int c_override) {
   MsmPlan pl;
   int lg = bit_length((uint32_t)std::max<size_t>(n, 1)) - 1;
-  int c = c_override > 0 ? c_override : std::max(4, std::min(18, lg - 4));
+  int c = c_override > 0 ? c_override : std::max(4, std::min(kAutoMaxC, lg - 4));
   c = std::max(kMinC, std::min(kMaxC, c));
   pl.c = c;
   pl.W = (256 + c - 1) / c;
@@ -406,6 +407,58 @@ int pm_synth_bases(pm_ctx* ctx, int curve, uint64_t seed, uint64_t i0, size_t n,
   const CurveOps* ops = curve_ops(curve);
   if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
   return ops->synth_bases(ctx, seed, i0, (uint32_t)n, d_out);
+}
+
+// ------------------------------------------------- multiopen accumulator
+int pm_shape_layout(const pm_proof_shape* shape, uint32_t* points_per_proof, uint32_t* scalars_per_proof,
+                    uint32_t* num_sets) {
+  std::vector<AccQuery> q;
+  AccLayout L;
+  const std::string err = acc_validate(shape, q, L, nullptr);
+  if (!err.empty()) return set_error(PM_ERR_ARG, "accum shape: " + err);
+  if (points_per_proof) *points_per_proof = L.npts;
+  if (scalars_per_proof) *scalars_per_proof = L.nsc;
+  if (num_sets) *num_sets = L.nsets;
+  return PM_OK;
+}
+
+int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_points,
+                          const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval) {
+  if (!ctx || !shape || (B && (!d_points || !d_scalars || !d_challenges || !d_out_quads)))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return ops->accum(ctx, shape, B, d_points, d_scalars, d_challenges, d_out_quads, d_out_h_eval);
+}
+
+int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t* points,
+                   const uint64_t* scalars, const uint64_t* challenges, uint64_t* out_quads, uint64_t* out_h_eval) {
+  if (!ctx || !shape || (B && (!points || !scalars || !challenges || !out_quads)))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  uint32_t npts = 0, nsc = 0, ns = 0;
+  int rc = pm_shape_layout(shape, &npts, &nsc, &ns);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (B == 0) return PM_OK;
+  if ((rc = ctx->begin_call())) return rc;
+  const size_t bp = B * npts * 64, bs = B * nsc * 32, bc = B * 7 * 32, bo = B * 4 * 64, bh = B * 32;
+  if ((rc = ctx->acc_io.ensure(bp + bs + bc + bo + bh))) return rc;
+  char* base = (char*)ctx->acc_io.p;
+  HIP_TRY(hipMemcpyAsync(base, points, bp, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(base + bp, scalars, bs, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(base + bp + bs, challenges, bc, hipMemcpyHostToDevice, ctx->stream));
+  char* dq = base + bp + bs + bc;
+  char* dh = dq + bo;
+  if ((rc = ops->accum(ctx, shape, B, base, base + bp, base + bp + bs, dq, dh))) return rc;
+  HIP_TRY(hipMemcpyAsync(out_quads, dq, bo, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_h_eval) HIP_TRY(hipMemcpyAsync(out_h_eval, dh, bh, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return PM_OK;
 }
 
 }  // extern "C"

@@ -228,21 +228,3 @@ int synth_bases_impl(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, void* d_o
 
 }  // namespace pm
 
-// Explicit instantiations are visible to both compilation passes, so the
-// device pass instantiates every kernel the host driver launches; the op
-// table (host function pointers) exists only in the host pass.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define PM_OPS_TABLE(Cv, name)
-#else
-#define PM_OPS_TABLE(Cv, name)                                                                 \
-  extern const CurveOps name;                                                                  \
-  const CurveOps name = {&msm_device_to_aff<Cv>, &point_add_impl<typename Cv::Base>,            \
-                         &synth_scalars_impl<Cv>, &synth_bases_impl<Cv>};
-#endif
-#define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
-  namespace pm {                                                                               \
-  template int msm_device_to_aff<Cv>(Ctx*, const void*, const void*, size_t, uint32_t, uint64_t*); \
-  template int synth_scalars_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, uint32_t, void*);     \
-  template int synth_bases_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, void*);                 \
-  PM_OPS_TABLE(Cv, name)                                                                       \
-  }

@@ -1,3 +1,3 @@
 // inst_pallas.hip -- PallasCurve instantiation of the MSM engine.
-#include "engine.hpp"
+#include "accum_engine.hpp"
 PM_DEFINE_CURVE_OPS(pm::PallasCurve, kPallasOps)

@@ -1,3 +1,3 @@
 // inst_vesta.hip -- VestaCurve instantiation of the MSM engine.
-#include "engine.hpp"
+#include "accum_engine.hpp"
 PM_DEFINE_CURVE_OPS(pm::VestaCurve, kVestaOps)

@@ -21,6 +21,11 @@ int set_error(int code, const std::string& msg);
 
 constexpr int kMinC = 4;
 constexpr int kMaxC = 20;
+// Widest automatic window.  Measured on MI355X (profiles/r01_s2/diag22): once
+// the bucket array (W * 2^(c-1) * 128 B) outgrows the caches, the scattered
+// 128-B bucket stores of k_accumulate dominate: at 2^22, c = 18 took 11.7 ms
+// in accumulate vs 6.1 ms at c = 16; at 2^20, c = 20 took 23.8 ms vs 1.4 ms.
+constexpr int kAutoMaxC = 16;
 constexpr size_t kMaxPoints = size_t(1) << 26;
 constexpr int kL1 = 8;
 // bases larger than this (bytes) use the prefetching accumulate kernel
@@ -70,7 +75,7 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid;
+      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // timing
@@ -81,7 +86,8 @@ struct pm_ctx {
 
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
-            &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid};
+            &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
+            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io};
   }
   ~pm_ctx();
   int begin_call();
@@ -104,6 +110,8 @@ struct CurveOps {
   int (*point_add)(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
   int (*synth_scalars)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, uint32_t mont, void* d_out);
   int (*synth_bases)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, void* d_out);
+  int (*accum)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const void* d_points, const void* d_scalars,
+               const void* d_challenges, void* d_out_quads, void* d_out_h);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

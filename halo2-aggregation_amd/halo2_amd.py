@@ -36,6 +36,155 @@ class PmError(RuntimeError):
     pass
 
 
+# ------------------------------------------------ accumulator shape (C mirror)
+class PmQuery(ctypes.Structure):
+    _fields_ = [("column", ctypes.c_uint32), ("rotation", ctypes.c_int32)]
+
+
+class PmPermColumn(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("query_index", ctypes.c_uint32)]
+
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+class PmProofShape(ctypes.Structure):
+    _fields_ = [
+        ("log_n", ctypes.c_uint32), ("blinding_factors", ctypes.c_uint32),
+        ("num_instance_columns", ctypes.c_uint32), ("num_advice_columns", ctypes.c_uint32),
+        ("num_fixed_columns", ctypes.c_uint32), ("num_lookups", ctypes.c_uint32),
+        ("perm_chunk_len", ctypes.c_uint32), ("quotient_degree", ctypes.c_uint32),
+        ("n_instance_queries", ctypes.c_uint32), ("n_advice_queries", ctypes.c_uint32),
+        ("n_fixed_queries", ctypes.c_uint32), ("n_perm_columns", ctypes.c_uint32),
+        ("instance_queries", ctypes.POINTER(PmQuery)), ("advice_queries", ctypes.POINTER(PmQuery)),
+        ("fixed_queries", ctypes.POINTER(PmQuery)), ("perm_columns", ctypes.POINTER(PmPermColumn)),
+        ("gate_code", _u32p), ("gate_code_len", ctypes.c_uint32),
+        ("lookup_input_code", _u32p), ("lookup_input_code_len", ctypes.c_uint32),
+        ("lookup_table_code", _u32p), ("lookup_table_code_len", ctypes.c_uint32),
+        ("constants", _u64p), ("n_constants", ctypes.c_uint32),
+        ("omega", ctypes.c_uint64 * 4), ("delta", ctypes.c_uint64 * 4), ("g1", ctypes.c_uint64 * 8),
+        ("fixed_commitments", _u64p), ("sigma_commitments", _u64p),
+    ]
+
+
+# scalar-field moduli (pasta_msm.h curve ids): the field of the accumulator's scalars
+SCALAR_MODULUS = {
+    0: 0x40000000000000000000000000000000224698FC0994A8DD8C46EB2100000001,  # Pallas -> Fq
+    1: 0x40000000000000000000000000000000224698FC094CF91B992D30ED00000001,  # Vesta -> Fp
+    2: 21888242871839275222246405745257275088548364400416034343698204186575808495617,  # BN254 Fr
+}
+EXPR_OPS = {"const": 1, "fixed": 2, "advice": 3, "instance": 4, "neg": 5, "sum": 6, "prod": 7, "scaled": 8}
+
+
+def _mont_limbs(v, r):
+    v = v * (1 << 256) % r
+    return [(v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF for k in range(4)]
+
+
+def compile_expressions(exprs, constants):
+    """halo2 Expression trees (tuples: ("const", c) ("fixed", q) ("advice", q)
+    ("instance", q) ("neg", e) ("sum", a, b) ("prod", a, b) ("scaled", e, c))
+    -> postfix pm_expr_op words; constants are appended to ``constants``."""
+    code = []
+
+    def cidx(c):
+        constants.append(c)
+        return len(constants) - 1
+
+    def walk(e):
+        op = e[0]
+        if op == "const":
+            code.append(EXPR_OPS[op] | cidx(e[1]) << 8)
+        elif op in ("fixed", "advice", "instance"):
+            code.append(EXPR_OPS[op] | e[1] << 8)
+        elif op == "neg":
+            walk(e[1])
+            code.append(EXPR_OPS[op])
+        elif op in ("sum", "prod"):
+            walk(e[1])
+            walk(e[2])
+            code.append(EXPR_OPS[op])
+        elif op == "scaled":
+            walk(e[1])
+            code.append(EXPR_OPS[op] | cidx(e[2]) << 8)
+        else:
+            raise ValueError(f"unknown expression node {op!r}")
+
+    for e in exprs:
+        walk(e)
+        code.append(0)  # PM_EXPR_END
+    return code
+
+
+class ProofShape:
+    """Owns the arrays behind one pm_proof_shape (the VerifyingKey view of
+    /root/reference/src/verifier.rs:227-285).  omega / delta / constants are
+    canonical integers of the curve's scalar field; g1 and the VK commitments
+    are (8,) / (n, 8) u64 affine Montgomery limbs."""
+
+    def __init__(self, curve, *, log_n, blinding_factors, num_instance_columns, num_advice_columns,
+                 num_fixed_columns, num_lookups, perm_chunk_len, quotient_degree, instance_queries,
+                 advice_queries, fixed_queries, perm_columns, gates, lookup_inputs, lookup_tables, omega, delta,
+                 g1, fixed_commitments, sigma_commitments):
+        r = SCALAR_MODULUS[curve]
+        self.curve = curve
+        consts = []
+        gate_code = compile_expressions(gates, consts)
+        lkin = compile_expressions(lookup_inputs, consts)
+        lktab = compile_expressions(lookup_tables, consts)
+
+        def qarr(qs):
+            a = (PmQuery * max(1, len(qs)))()
+            for i, (c, rot) in enumerate(qs):
+                a[i] = PmQuery(c, rot)
+            return a
+
+        self._keep = []
+
+        def u32(xs):
+            a = np.ascontiguousarray(np.array(xs if xs else [0], dtype=np.uint32))
+            self._keep.append(a)
+            return a.ctypes.data_as(_u32p)
+
+        def u64(a):
+            a = np.ascontiguousarray(np.array(a, dtype=np.uint64).reshape(-1))
+            if a.size == 0:
+                a = np.zeros(8, dtype=np.uint64)
+            self._keep.append(a)
+            return a.ctypes.data_as(_u64p)
+
+        iq, aq, fq = qarr(instance_queries), qarr(advice_queries), qarr(fixed_queries)
+        pc = (PmPermColumn * max(1, len(perm_columns)))()
+        for i, (k, q) in enumerate(perm_columns):
+            pc[i] = PmPermColumn(k, q)
+        self._keep += [iq, aq, fq, pc]
+        cl = [_mont_limbs(c % r, r) for c in consts]
+        s = PmProofShape()
+        s.log_n, s.blinding_factors = log_n, blinding_factors
+        s.num_instance_columns, s.num_advice_columns = num_instance_columns, num_advice_columns
+        s.num_fixed_columns, s.num_lookups = num_fixed_columns, num_lookups
+        s.perm_chunk_len, s.quotient_degree = perm_chunk_len, quotient_degree
+        s.n_instance_queries, s.n_advice_queries = len(instance_queries), len(advice_queries)
+        s.n_fixed_queries, s.n_perm_columns = len(fixed_queries), len(perm_columns)
+        s.instance_queries, s.advice_queries, s.fixed_queries, s.perm_columns = iq, aq, fq, pc
+        s.gate_code, s.gate_code_len = u32(gate_code), len(gate_code)
+        s.lookup_input_code, s.lookup_input_code_len = u32(lkin), len(lkin)
+        s.lookup_table_code, s.lookup_table_code_len = u32(lktab), len(lktab)
+        s.constants, s.n_constants = u64(cl), len(cl)
+        s.omega[:] = _mont_limbs(omega % r, r)
+        s.delta[:] = _mont_limbs(delta % r, r)
+        s.g1[:] = [int(x) for x in np.asarray(g1, dtype=np.uint64).reshape(8)]
+        s.fixed_commitments = u64(fixed_commitments)
+        s.sigma_commitments = u64(sigma_commitments)
+        self.c = s
+
+    def layout(self):
+        """(points_per_proof, scalars_per_proof, num_sets)"""
+        a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().pm_shape_layout(ctypes.byref(self.c), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+
 def _load():
     # torch wheels bundle their own libamdhip64.so.7.  Loading torch first makes
     # the dynamic loader resolve our DT_NEEDED libamdhip64.so.7 to that same
@@ -73,6 +222,12 @@ def _load():
                               _vp], ctypes.c_int),
         "pm_synth_bases": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, _vp],
                            ctypes.c_int),
+        "pm_shape_layout": ([ctypes.POINTER(PmProofShape), ctypes.POINTER(ctypes.c_uint32),
+                             ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+        "pm_accum_batch": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p, _u64p, _u64p,
+                            _u64p, _u64p], ctypes.c_int),
+        "pm_accum_batch_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _vp, _vp, _vp,
+                                   _vp, _vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -226,6 +381,25 @@ class Context:
     def synth_scalars(self, curve, seed, i0, n, d_out, canonical=False):
         _check(lib().pm_synth_scalars(self.h, curve, seed, i0, n, SCALARS_CANONICAL if canonical else 0,
                                       _vp(d_out)))
+
+    def accum_batch(self, shape: ProofShape, points, scalars, challenges):
+        """Batch multiopen accumulator (pm_accum_batch): points (B, npts, 8),
+        scalars (B, nsc, 4), challenges (B, 7, 4) u64 Montgomery ->
+        (quads (B, 4, 8): w, zw, f, e affine; h_eval (B, 4))."""
+        npts, nsc, _ = shape.layout()
+        p = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1, npts, 8)
+        B = p.shape[0]
+        s = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(B, nsc, 4)
+        c = np.ascontiguousarray(challenges, dtype=np.uint64).reshape(B, 7, 4)
+        quads = np.zeros((B, 4, 8), dtype=np.uint64)
+        hev = np.zeros((B, 4), dtype=np.uint64)
+        _check(lib().pm_accum_batch(self.h, shape.curve, ctypes.byref(shape.c), B, _p(p), _p(s), _p(c), _p(quads),
+                                    _p(hev)))
+        return quads, hev
+
+    def accum_batch_device(self, shape: ProofShape, B, d_points, d_scalars, d_challenges, d_quads, d_h=0):
+        _check(lib().pm_accum_batch_device(self.h, shape.curve, ctypes.byref(shape.c), B, _vp(d_points),
+                                           _vp(d_scalars), _vp(d_challenges), _vp(d_quads), _vp(d_h or None)))
 
     def synth_bases(self, curve, seed, i0, n, d_out):
         _check(lib().pm_synth_bases(self.h, curve, seed, i0, n, _vp(d_out)))

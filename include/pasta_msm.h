@@ -103,6 +103,98 @@ int pm_synth_scalars(pm_ctx* ctx, int curve, uint64_t seed, uint64_t i0, size_t 
                      void* d_out);
 int pm_synth_bases(pm_ctx* ctx, int curve, uint64_t seed, uint64_t i0, size_t n, void* d_out);
 
+/* ------------------------------------------------- multiopen accumulator
+ * Boundary 2: the native meaning of the reference's in-circuit
+ * verifier for a batch of B inner proofs that share one verifying key.
+ * Per proof it evaluates the scalar block of VerifierChip::_verify_proof
+ * (/root/reference/src/verifier.rs:512-652: x^n, l_0 / l_last / l_blind,
+ * gate, permutation (src/permutation.rs:190-324) and lookup
+ * (src/lookup.rs:173-311) expressions, vanishing h_eval
+ * (src/vanishing.rs:136-201)), assembles the queries in the reference order
+ * (verifier.rs:654-715), groups them by rotation (src/multiopen.rs:19-45) and
+ * produces MultiopenChip::calc_witness's accumulator (src/multiopen.rs:271-509)
+ *     w  = sum_j u^{S-1-j} W_j          zw = sum_j u^{S-1-j} z_j W_j
+ *     f  = sum_j u^{S-1-j} sum_i v^{m_j-1-i} C_{j,i}   (H = sum_i x^{n i} h_i)
+ *     e  = [-sum_j u^{S-1-j} sum_i v^{m_j-1-i} e_{j,i}] g1
+ * as exact affine points, plus h_eval.  The Rust side replays the transcript
+ * and passes the challenges in; the EccChip / Transcript / VerifyingKey
+ * surfaces stay unchanged.
+ *
+ * Expression code (halo2 plonk::Expression, compute_expr verifier.rs:58-151)
+ * is postfix, one u32 word per node: op | arg << 8.  Each expression ends with
+ * PM_EXPR_END.  Leaves index the query evals (advice/fixed/instance query
+ * index) or the shape's constant table (CONST, SCALED). */
+enum pm_expr_op {
+  PM_EXPR_END = 0,
+  PM_EXPR_CONST = 1,    /* push constants[arg] */
+  PM_EXPR_FIXED = 2,    /* push fixed_evals[arg] */
+  PM_EXPR_ADVICE = 3,   /* push advice_evals[arg] */
+  PM_EXPR_INSTANCE = 4, /* push instance_evals[arg] */
+  PM_EXPR_NEG = 5,
+  PM_EXPR_SUM = 6,
+  PM_EXPR_PROD = 7,
+  PM_EXPR_SCALED = 8    /* top *= constants[arg] */
+};
+enum pm_column_kind { PM_COL_ADVICE = 0, PM_COL_FIXED = 1, PM_COL_INSTANCE = 2 };
+
+typedef struct pm_query {
+  uint32_t column;
+  int32_t rotation;
+} pm_query;
+
+typedef struct pm_perm_column {
+  uint32_t kind;        /* pm_column_kind */
+  uint32_t query_index; /* index into that kind's query evals */
+} pm_perm_column;
+
+/* What the accumulator reads from VerifyingKey / ConstraintSystem
+ * (verifier.rs:227-285).  Scalars are 4 x u64 Montgomery, points 8 x u64
+ * affine Montgomery, (0,0) = identity. */
+typedef struct pm_proof_shape {
+  uint32_t log_n;
+  uint32_t blinding_factors;     /* cs.blinding_factors() */
+  uint32_t num_instance_columns;
+  uint32_t num_advice_columns;
+  uint32_t num_fixed_columns;
+  uint32_t num_lookups;
+  uint32_t perm_chunk_len;       /* cs.degree() - 2 */
+  uint32_t quotient_degree;      /* number of h pieces */
+  uint32_t n_instance_queries, n_advice_queries, n_fixed_queries, n_perm_columns;
+  const pm_query* instance_queries;
+  const pm_query* advice_queries;
+  const pm_query* fixed_queries;
+  const pm_perm_column* perm_columns;
+  const uint32_t* gate_code;         /* all gate polynomials, in gate order */
+  uint32_t gate_code_len;
+  const uint32_t* lookup_input_code; /* flattened over lookups (verifier.rs:244-251) */
+  uint32_t lookup_input_code_len;
+  const uint32_t* lookup_table_code;
+  uint32_t lookup_table_code_len;
+  const uint64_t* constants;         /* n_constants x 4 */
+  uint32_t n_constants;
+  uint64_t omega[4];                 /* vk.get_domain().get_omega() */
+  uint64_t delta[4];                 /* C::ScalarExt::DELTA */
+  uint64_t g1[8];                    /* C::generator() */
+  const uint64_t* fixed_commitments; /* num_fixed_columns x 8 */
+  const uint64_t* sigma_commitments; /* n_perm_columns x 8 */
+} pm_proof_shape;
+
+/* Per-proof layout implied by a shape (transcript read order, see
+ * oracle/accum.py): points, scalars, and rotation sets S (= number of W_j). */
+int pm_shape_layout(const pm_proof_shape* shape, uint32_t* points_per_proof, uint32_t* scalars_per_proof,
+                    uint32_t* num_sets);
+
+/* Batch accumulator, host buffers.  points: B x points_per_proof x 8;
+ * scalars: B x scalars_per_proof x 4; challenges: B x 7 x 4 (theta, beta,
+ * gamma, y, x, v, u); out_quads: B x 4 x 8 (w, zw, f, e); out_h_eval: B x 4
+ * (may be NULL).  curve selects the group (PM_CURVE_*); its scalar field is
+ * the field of every scalar above. */
+int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t* points,
+                   const uint64_t* scalars, const uint64_t* challenges, uint64_t* out_quads, uint64_t* out_h_eval);
+/* Same with every buffer in device memory of ctx's device. */
+int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_points,
+                          const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval);
+
 #ifdef __cplusplus
 }
 #endif
