@@ -12,6 +12,14 @@ all-gather of the per-rank partial points over RCCL and their fold on the host
 live with HIP events on the context stream over the timed region.
 `cpu_baseline` times the C restatement of halo2 best_multiexp (oracle/msm_ref.c)
 on the host cores of the same box, on the same inputs, at N=1 on rank 0.
+
+`accumulator` is the second half of the BASELINE metric ("aggregated proofs
+verified/s"): each rank runs the batch multiopen accumulator (pm_accum_batch,
+SURVEY §8 rows a-3..a-9) over its own B = 256 synthetic simple-example proofs
+(BN254, k = 17; weak scaling, proofs are independent), followed by an
+all-gather of the B x 4 accumulator points over RCCL.  Its cpu_baseline is the
+Python oracle (oracle/accum.py) on a bounded sample of the same proofs, with a
+bit-exact spot check of the GPU results.
 """
 import argparse
 import json
@@ -38,6 +46,8 @@ def parse():
     ap.add_argument("--window", type=int, default=0, help="force window width c (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--accum-batch", type=int, default=256, help="proofs per GPU for the accumulator leg (0 = skip)")
+    ap.add_argument("--accum-logn", type=int, default=17)
     return ap.parse_args()
 
 
@@ -118,6 +128,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
@@ -155,9 +166,110 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(d_s, d_b, n, result, args.cpu_seconds)
+        if accum is not None:
+            if world == 1 and not args.no_cpu:
+                accum["cpu_baseline"] = accum_cpu_baseline(*accum.pop("_state"), budget_s=8.0)
+            else:
+                accum.pop("_state", None)
+            out["accumulator"] = accum
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def run_accumulator(args, ctx, dist, dev, rank, world):
+    """Batch multiopen accumulator: B proofs per rank, timed like the MSM leg."""
+    import numpy as np
+    import torch
+
+    import halo2_amd as H
+    import workloads as Wk
+
+    curve, B = H.BN254, args.accum_batch
+    shape = Wk.simple_example_shape(ctx, curve, args.accum_logn)
+    batch = Wk.SyntheticBatch(ctx, shape, B, i0=rank * B)
+    gathered = [torch.zeros_like(batch.quads) for _ in range(world)] if dist else None
+
+    def step():
+        batch.run(ctx, shape)
+        if dist:
+            dist.all_gather(gathered, batch.quads)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(True)
+    ctx.reset_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kernels = {k: round(ctx.kernel_stats(k)[1] / max(1, ctx.kernel_stats(k)[0]), 4)
+               for k in ("acc_scalars", "acc_termmul", "acc_sum")}
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed * 1e3 / args.steps
+    out = {"metric": "aggregated proofs verified/s", "value": round(world * B / (ms * 1e-3), 1), "unit": "proofs/s",
+           "ms_per_batch": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+           "config": {"workload": f"multiopen_accumulator_simple_example_k{args.accum_logn}", "curve": "bn254",
+                      "proofs_per_gpu": B, "proofs_total": world * B,
+                      "parallelism": f"proof-batch x{world} + RCCL all-gather of B x 4 points"},
+           "kernels_ms": kernels}
+    if rank == 0:
+        pick = [0, B - 1]
+        host = {k: getattr(batch, k)[pick].cpu().numpy().view(np.uint64)
+                for k in ("points", "scalars", "challenges", "quads", "h_eval")}
+        vk = (np.ctypeslib.as_array(shape.c.fixed_commitments, shape=(shape.c.num_fixed_columns * 8,)).copy(),
+              np.ctypeslib.as_array(shape.c.sigma_commitments, shape=(shape.c.n_perm_columns * 8,)).copy())
+        out["_state"] = (curve, args.accum_logn, host, vk, B)
+    return out
+
+
+def accum_cpu_baseline(curve, log_n, host, vk, B, budget_s):
+    """Python oracle (oracle/accum.py, closed form) on the GPU's own proofs:
+    bit-exact spot check + throughput on a bounded sample."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import accum as A
+    import pasta as P
+
+    C = P.CURVES[curve]
+    sh = A.simple_example_shape(C, log_n)
+    sh.fixed_commitments = [P.limbs_to_point(C, [int(x) for x in vk[0][8 * i:8 * i + 8]])
+                            for i in range(sh.num_fixed_columns)]
+    sh.sigma_commitments = [P.limbs_to_point(C, [int(x) for x in vk[1][8 * i:8 * i + 8]])
+                            for i in range(len(sh.perm_columns))]
+    rinv = pow(P.R_MONT, -1, C.r)
+    proofs = []
+    for b in range(host["points"].shape[0]):
+        proofs.append(A.Proof(points=[P.limbs_to_point(C, [int(x) for x in q]) for q in host["points"][b]],
+                              scalars=[P.from_limbs([int(x) for x in v]) * rinv % C.r for v in host["scalars"][b]],
+                              challenges=[P.from_limbs([int(x) for x in v]) * rinv % C.r
+                                          for v in host["challenges"][b]]))
+    match = True
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        for b, pf in enumerate(proofs):
+            q, h = A.pack_result(C, A.accumulate_msm(C, sh, pf))
+            if reps < len(proofs):
+                match &= bool(np.array_equal(q, host["quads"][b]) and np.array_equal(h, host["h_eval"][b]))
+            reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(reps / dt, 2), "unit": "proofs/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} proofs (2 distinct, from the GPU batch) through oracle/accum.py accumulate_msm "
+                      f"({dt:.1f} s, Python big-int, 1 thread)",
+            "matches_gpu": match}
 
 
 def windows_for(n, c_override=0):

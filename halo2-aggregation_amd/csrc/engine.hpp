@@ -89,9 +89,9 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->head.ensure((size_t)pl.nthreads * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segS.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segT.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->bits.ensure((size_t)pl.W * (pl.NB2 + 1) * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->bits.ensure((size_t)pl.W * (pl.NB2 + kTJobs) * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->longs.ensure(16 + (size_t)pl.maxlong * sizeof(LongChain)))) return rc;
-  const size_t nG = (size_t)pl.W * (pl.NB2 + 1);
+  const size_t nG = (size_t)pl.W * (pl.NB2 + kTJobs);
   if ((rc = ctx->ensure_pinned(nG * sizeof(Xyzz<F>)))) return rc;
 
   uint32_t* digits = (uint32_t*)ctx->digits.p;
@@ -146,7 +146,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
             (k_bucket_seg<F><<<(pl.W * pl.M1 + 255) / 256, 256, 0, st>>>(offsets, buckets, pl.W, pl.NB, pl.L1,
                                                                           S, T)));
   PM_LAUNCH(ctx, "bucket_bits",
-            (k_bucket_bits<F><<<dim3(pl.NB2 + 1, pl.W), kRedThreads, 0, st>>>(S, T, pl.M1, pl.NB2, G)));
+            (k_bucket_bits<F><<<dim3(pl.NB2 + kTJobs, pl.W), kRedThreads, 0, st>>>(S, T, pl.M1, pl.NB2, G)));
   HIP_TRY(hipMemcpyAsync(ctx->h_pinned, G, nG * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   ctx->end_call();
@@ -158,9 +158,9 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   int qmax = 0;
   for (int w = 0; w < pl.W; w++) {
     const int o = w * pl.base + std::min(w, pl.extra);
-    for (int b = 0; b <= pl.NB2; b++) {
+    for (int b = 0; b < pl.NB2 + kTJobs; b++) {
       const int q = b < pl.NB2 ? o + b + pl.log2L1 : o;
-      at[q].push_back(w * (pl.NB2 + 1) + b);
+      at[q].push_back(w * (pl.NB2 + kTJobs) + b);
       qmax = std::max(qmax, q);
     }
   }

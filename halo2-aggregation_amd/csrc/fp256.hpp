@@ -213,6 +213,99 @@ __device__ __forceinline__ void mac_vs(uint64_t& acc, uint32_t& acc2, uint32_t x
       : "v"(x), "s"(y));
 }
 
+// Grouped forms: up to four products per asm statement.  The compiler pads
+// every inline-asm statement that writes an SGPR with an s_nop before the next
+// VALU statement; grouping keeps the (hazard-free) mad -> addc pairs inside one
+// statement and removes 3 of every 4 of those pads.
+#define PM_MAD2(X, Y) "v_mad_u64_u32 %0, %2, " X ", " Y ", %0\n\tv_addc_co_u32_e64 %1, %3, 0, %1, %2\n\t"
+__device__ __forceinline__ void mac4_vv(uint64_t& acc, uint32_t& acc2, uint32_t x0, uint32_t y0, uint32_t x1,
+                                        uint32_t y1, uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+  uint64_t c0, c1;
+  asm(PM_MAD2("%4", "%5") PM_MAD2("%6", "%7") PM_MAD2("%8", "%9") PM_MAD2("%10", "%11")
+      : "+v"(acc), "+v"(acc2), "=&s"(c0), "=&s"(c1)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2), "v"(x3), "v"(y3));
+}
+__device__ __forceinline__ void mac2_vv(uint64_t& acc, uint32_t& acc2, uint32_t x0, uint32_t y0, uint32_t x1,
+                                        uint32_t y1) {
+  uint64_t c0, c1;
+  asm(PM_MAD2("%4", "%5") PM_MAD2("%6", "%7")
+      : "+v"(acc), "+v"(acc2), "=&s"(c0), "=&s"(c1)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+}
+__device__ __forceinline__ void mac4_vs(uint64_t& acc, uint32_t& acc2, uint32_t x0, uint32_t y0, uint32_t x1,
+                                        uint32_t y1, uint32_t x2, uint32_t y2, uint32_t x3, uint32_t y3) {
+  uint64_t c0, c1;
+  asm(PM_MAD2("%4", "%5") PM_MAD2("%6", "%7") PM_MAD2("%8", "%9") PM_MAD2("%10", "%11")
+      : "+v"(acc), "+v"(acc2), "=&s"(c0), "=&s"(c1)
+      : "v"(x0), "s"(y0), "v"(x1), "s"(y1), "v"(x2), "s"(y2), "v"(x3), "s"(y3));
+}
+__device__ __forceinline__ void mac2_vs(uint64_t& acc, uint32_t& acc2, uint32_t x0, uint32_t y0, uint32_t x1,
+                                        uint32_t y1) {
+  uint64_t c0, c1;
+  asm(PM_MAD2("%4", "%5") PM_MAD2("%6", "%7")
+      : "+v"(acc), "+v"(acc2), "=&s"(c0), "=&s"(c1)
+      : "v"(x0), "s"(y0), "v"(x1), "s"(y1));
+}
+// acc += sum_{t<n} xs[t] * ys[t] in groups of 4 / 2 / 1 (n is a compile-time
+// constant after unrolling)
+template <bool YS>
+__device__ __forceinline__ void mac_n(uint64_t& acc, uint32_t& acc2, const uint32_t* xs, const uint32_t* ys, int n) {
+  int t = 0;
+#pragma unroll
+  for (; t + 4 <= n; t += 4) {
+    if (YS) mac4_vs(acc, acc2, xs[t], ys[t], xs[t + 1], ys[t + 1], xs[t + 2], ys[t + 2], xs[t + 3], ys[t + 3]);
+    else mac4_vv(acc, acc2, xs[t], ys[t], xs[t + 1], ys[t + 1], xs[t + 2], ys[t + 2], xs[t + 3], ys[t + 3]);
+  }
+  if (t + 2 <= n) {
+    if (YS) mac2_vs(acc, acc2, xs[t], ys[t], xs[t + 1], ys[t + 1]);
+    else mac2_vv(acc, acc2, xs[t], ys[t], xs[t + 1], ys[t + 1]);
+    t += 2;
+  }
+  if (t < n) {
+    if (YS) mac_vs(acc, acc2, xs[t], ys[t]);
+    else mac_vv(acc, acc2, xs[t], ys[t]);
+  }
+}
+
+// FIPS with grouped asm statements (same arithmetic as fe_mul_fips).
+template <class P>
+__device__ __forceinline__ Fe<P> fe_mul_fips_g(const Fe<P>& a, const Fe<P>& b) {
+  uint32_t m[8], r[8];
+  uint64_t acc = 0;
+  uint32_t acc2 = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    uint32_t xs[8], ys[8], ms[8], ps[8];
+    int n = 0, nr = 0;
+    const int lo = k < 8 ? 0 : k - 7, hi = k < 8 ? k : 7;
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      xs[n] = a.l[i];
+      ys[n] = b.l[k - i];
+      n++;
+    }
+#pragma unroll
+    for (int i = lo; i <= hi && i < 8; i++)
+      if (i < k && P::MOD[k - i] != 0u) {
+        ms[nr] = m[i];
+        ps[nr] = P::MOD[k - i];
+        nr++;
+      }
+    mac_n<false>(acc, acc2, xs, ys, n);
+    mac_n<true>(acc, acc2, ms, ps, nr);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac_vs(acc, acc2, m[k], P::MOD[0]);
+    } else {
+      r[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)acc2 << 32);
+    acc2 = 0;
+  }
+  r[7] = (uint32_t)acc;
+  return fe_reduce_once<P>(r, (uint32_t)(acc >> 32));
+}
+
 // Montgomery product by finely integrated product scanning (FIPS): column k
 // accumulates sum a_i b_{k-i} + sum m_i p_{k-i}; the low columns also produce
 // m_k = acc * (-p^-1) so that column k becomes divisible by 2^32.  Modulus
@@ -249,12 +342,13 @@ __device__ __forceinline__ Fe<P> fe_mul_fips(const Fe<P>& a, const Fe<P>& b) {
   r[7] = (uint32_t)acc;
   return fe_reduce_once<P>(r, (uint32_t)(acc >> 32));
 }
+
 #endif
 
 template <class P>
 PM_HD Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return fe_mul_fips<P>(a, b);
+  return fe_mul_fips_g<P>(a, b);
 #else
   return fe_mul_portable<P>(a, b);
 #endif

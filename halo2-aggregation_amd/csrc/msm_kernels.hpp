@@ -488,21 +488,31 @@ __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------ 7. bit sums
-// block (w, job): job < NBITS2 -> G_job = sum_{j : (j >> job) & 1} S_j;
-// job == NBITS2 -> sum_j T_j.  256 lanes, strided partial sums, LDS tree.
-constexpr int kRedThreads = 256;
+// block (job, w): job < NB2 -> G_job = sum_{j : (j >> job) & 1} S_j (only
+// the j with that bit set are enumerated, so no lane idles); job >= NB2 ->
+// partial sum of T_j over part (job - NB2) of kTJobs equal ranges.
+// kRedThreads lanes: strided partial sums, then an LDS tree.  Serial depth
+// ~ M1/2/kRedThreads + log2(kRedThreads) additions.
+constexpr int kRedThreads = 512;
+constexpr int kTJobs = 2;
 template <class F>
 __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __restrict__ S,
                                                              const Xyzz<F>* __restrict__ T, int M1,
-                                                             int NBITS2, Xyzz<F>* __restrict__ G) {
+                                                             int NB2, Xyzz<F>* __restrict__ G) {
   __shared__ Xyzz<F> lds[kRedThreads];
   const int w = blockIdx.y, job = blockIdx.x, tid = threadIdx.x;
   Xyzz<F> acc = xyzz_inf<F>();
-  if (job < NBITS2) {
-    for (int j = tid; j < M1; j += kRedThreads)
-      if ((j >> job) & 1) acc = xyzz_add<F>(acc, load_xyzz<F>(&S[(size_t)w * M1 + j]));
+  if (job < NB2) {
+    const int low = (1 << job) - 1;
+    for (int m = tid;; m += kRedThreads) {
+      const int j = ((m & ~low) << 1) | (1 << job) | (m & low);  // m-th index with bit `job` set
+      if (j >= M1) break;
+      acc = xyzz_add<F>(acc, load_xyzz<F>(&S[(size_t)w * M1 + j]));
+    }
   } else {
-    for (int j = tid; j < M1; j += kRedThreads) acc = xyzz_add<F>(acc, load_xyzz<F>(&T[(size_t)w * M1 + j]));
+    const int per = (M1 + kTJobs - 1) / kTJobs;
+    const int j0 = (job - NB2) * per, j1 = min(M1, j0 + per);
+    for (int j = j0 + tid; j < j1; j += kRedThreads) acc = xyzz_add<F>(acc, load_xyzz<F>(&T[(size_t)w * M1 + j]));
   }
   lds[tid] = acc;
   __syncthreads();
@@ -513,7 +523,7 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
     }
     __syncthreads();
   }
-  if (tid == 0) store_xyzz<F>(&G[(size_t)w * (NBITS2 + 1) + job], acc);
+  if (tid == 0) store_xyzz<F>(&G[(size_t)w * (NB2 + kTJobs) + job], acc);
 }
 
 // ------------------------------------------------------ synthetic inputs

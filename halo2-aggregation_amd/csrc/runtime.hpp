@@ -27,9 +27,9 @@ constexpr int kMaxC = 20;
 // in accumulate vs 6.1 ms at c = 16; at 2^20, c = 20 took 23.8 ms vs 1.4 ms.
 constexpr int kAutoMaxC = 16;
 constexpr size_t kMaxPoints = size_t(1) << 26;
-constexpr int kL1 = 8;
+constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg (serial chain: 2*L1-1 adds)
 // bases larger than this (bytes) use the prefetching accumulate kernel
-constexpr size_t kPrefetchBytes = size_t(128) << 20;  // bucket-segment length of k_bucket_seg (latency: 2*L1-1 adds)
+constexpr size_t kPrefetchBytes = size_t(128) << 20;
 
 struct Buf {
   void* p = nullptr;

@@ -24,7 +24,7 @@ def make_plan(n, c_override=0, chunk_override=0):
     base, extra = 256 // W, 256 % W
     cmax = base + (1 if extra else 0)
     K = 1 << (cmax - 1)
-    L1 = min(8, K)
+    L1 = min(4, K)
     NB = ((K + 1 + L1 - 1) // L1) * L1
     M1 = NB // L1
     NB2 = bit_length(M1 - 1)
