@@ -58,11 +58,13 @@ def load_valu_peak():
     return None
 
 
-def load_pmc_traffic(workload):
+def load_pmc_traffic(workload, launches_per_msm):
+    """HBM bytes per k_accumulate launch from the committed PMC passes, if they
+    were taken on this workload with the same launch structure."""
     p = os.path.join(ROOT, "profiles", "pmc_accumulate.json")
     if os.path.exists(p):
         d = json.load(open(p))
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and d.get("launches_per_msm", 1) == launches_per_msm:
             return d.get("hbm_bytes_per_launch")
     return None
 
@@ -122,8 +124,11 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     launches, acc_ms = ctx.kernel_stats("accumulate")
-    kernels = {k: round(ctx.kernel_stats(k)[1] / max(1, ctx.kernel_stats(k)[0]), 4)
+    # per-MSM kernel time (the pipelined engine launches accumulate / fixup /
+    # bucket_* once per window group)
+    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4)
                for k in ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg", "bucket_bits"]}
+    acc_launches_per_msm = max(1, launches) / args.steps
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -134,22 +139,23 @@ def main():
         ms_per_step = elapsed * 1e3 / args.steps
         value = world * n / (elapsed / args.steps) / 1e6
         acc_avg_ms = acc_ms / max(1, launches)
-        # algorithmic bytes of one accumulate launch: the launch consumes all n
-        # (scalar, base) pairs of the MSM (every window) -> 96 B x n
-        alg_bytes = BYTES_PER_PAIR * n
+        # algorithmic bytes of one accumulate launch: the MSM consumes all n
+        # (scalar, base) pairs -> 96 B x n; one launch covers one
+        # window group, i.e. 1 / (launches per MSM) of it
+        alg_bytes = BYTES_PER_PAIR * n / acc_launches_per_msm
         achieved = alg_bytes / (acc_avg_ms * 1e-3) / 1e9
         workload = f"pallas_msm_2^{args.logn}_per_gpu"
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc_traffic(workload),
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc_traffic(workload, acc_launches_per_msm),
                 "kernel": "k_accumulate", "avg_launch_ms": round(acc_avg_ms, 4),
-                "alg_bytes_per_launch": alg_bytes}
+                "launches_per_msm": acc_launches_per_msm, "alg_bytes_per_launch": int(alg_bytes)}
         vp = load_valu_peak()
         if vp:
             # The binding roofline is integer VALU: one XYZZ mixed
             # add = 10 Montgomery products = 10 x 88 v_mad_u64_u32 (Pasta
             # moduli); ~n*W adds per launch; peak = measured mad issue rate.
             W = windows_for(n, args.window)
-            mads = n * W * 10 * 88
+            mads = int(n * W * 10 * 88 / acc_launches_per_msm)
             ach = mads / (acc_avg_ms * 1e-3) / 1e12
             roof["valu_int"] = {"achieved": round(ach, 3), "peak": vp["v_mad_u64_u32_Tops"], "unit": "T v_mad_u64_u32/s",
                                 "frac": round(ach / vp["v_mad_u64_u32_Tops"], 4), "mads_per_launch": mads}
@@ -210,8 +216,7 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
-    kernels = {k: round(ctx.kernel_stats(k)[1] / max(1, ctx.kernel_stats(k)[0]), 4)
-               for k in ("acc_scalars", "acc_termmul", "acc_sum")}
+    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4) for k in ("acc_scalars", "acc_termmul", "acc_sum")}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -57,6 +57,8 @@ pm_ctx::~pm_ctx() {
   for (pm::Buf* b : all_bufs()) b->release();
   if (h_pinned) (void)hipHostFree(h_pinned);
   for (auto& e : ev_pool) (void)hipEventDestroy(e);
+  for (auto& e : grp_ev) (void)hipEventDestroy(e);
+  if (red_stream) (void)hipStreamDestroy(red_stream);
   if (own_stream) (void)hipStreamDestroy(own_stream);
 }
 
@@ -92,6 +94,15 @@ int pm_ctx::end_call() {
   return PM_OK;
 }
 
+int pm_ctx::ensure_group_events(int n) {
+  while ((int)grp_ev.size() < n) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    grp_ev.push_back(e);
+  }
+  return PM_OK;
+}
+
 int pm_ctx::ensure_pinned(size_t bytes) {
   if (bytes <= h_pinned_cap) return PM_OK;
   if (h_pinned) (void)hipHostFree(h_pinned);
@@ -114,7 +125,7 @@ static int bit_length(uint32_t v) {
   return b;
 }
 
-MsmPlan make_plan(size_t n, int c_override) {
+MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk) {
   MsmPlan pl;
   int lg = bit_length((uint32_t)std::max<size_t>(n, 1)) - 1;
   int c = c_override > 0 ? c_override : std::max(4, std::min(kAutoMaxC, lg - 4));
@@ -131,9 +142,19 @@ MsmPlan make_plan(size_t n, int c_override) {
   pl.M1 = pl.NB / pl.L1;
   pl.NB2 = bit_length((uint32_t)(pl.M1 - 1));
   pl.n = (uint32_t)n;
-  const size_t work = (size_t)n * pl.W;
+  // window groups: the bucket reduction (+ host Horner) of group g runs while
+  // group g-1 accumulates.  Measured on MI355X (profiles/r01_s2/pipe2): no
+  // gain -- the reduction kernels compete with accumulate for the same VALU
+  // slots and each smaller accumulate launch loses occupancy -- so the
+  // default is one group (2^20: G=1 2.29 ms, G=2 2.43, G=4 2.95).
+  int G = groups_override > 0 ? groups_override : 1;
+  G = std::max(1, std::min(G, pl.W));
+  pl.wpg = (pl.W + G - 1) / G;
+  pl.G = (pl.W + pl.wpg - 1) / pl.wpg;
+  const size_t work = (size_t)n * pl.wpg;
   const size_t target = 256 * 1024;  // lanes in flight: 256 CUs x 16 waves x 64
-  pl.chunk = (uint32_t)std::max<size_t>(16, (work + target - 1) / target);
+  const size_t mc = min_chunk > 0 ? (size_t)min_chunk : 16;
+  pl.chunk = (uint32_t)std::max<size_t>(mc, (work + target - 1) / target);
   pl.nthreads = (uint32_t)((work + pl.chunk - 1) / pl.chunk);
   pl.maxlong = (uint32_t)(work / ((size_t)kMaxChain * pl.chunk) + 1);
   return pl;
@@ -225,7 +246,10 @@ int pm_ctx_create(int device, pm_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
   c->stream = c->own_stream;
+  HIP_TRY(hipStreamCreateWithFlags(&c->red_stream, hipStreamNonBlocking));
   if (const char* e = std::getenv("PM_PREFETCH")) c->prefetch = std::atoi(e);
+  if (const char* e = std::getenv("PM_GROUPS")) c->groups = std::atoi(e);
+  if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   *out = c.release();
   return PM_OK;
 }
@@ -247,6 +271,16 @@ int pm_ctx_set_window(pm_ctx* ctx, int c) {
   if (c != 0 && (c < kMinC || c > kMaxC)) return set_error(PM_ERR_ARG, "window width out of range");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->window_c = c;
+  return PM_OK;
+}
+
+int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  if (groups < 0 || groups > 64 || min_chunk < 0 || min_chunk > (1 << 20))
+    return set_error(PM_ERR_ARG, "pipeline setting out of range");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->groups = groups;
+  ctx->min_chunk = min_chunk;
   return PM_OK;
 }
 

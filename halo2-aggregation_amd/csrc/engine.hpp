@@ -13,14 +13,14 @@
 #include "msm_kernels.hpp"
 #include "runtime.hpp"
 
-// time a launch on the context stream when timing is enabled
-#define PM_LAUNCH(ctx, name, ...)                                        \
+// time a launch on stream `st_` when timing is enabled
+#define PM_LAUNCH_ST(ctx, st_, name, ...)                                \
   do {                                                                   \
     hipEvent_t a_ = nullptr, b_ = nullptr;                               \
     if ((ctx)->timing) {                                                 \
       a_ = (ctx)->next_event();                                          \
       b_ = (ctx)->next_event();                                          \
-      (void)hipEventRecord(a_, (ctx)->stream);                           \
+      (void)hipEventRecord(a_, (st_));                                   \
     }                                                                    \
     __VA_ARGS__;                                                         \
     hipError_t le_ = hipGetLastError();                                  \
@@ -28,10 +28,11 @@
       return pm::set_error(PM_ERR_HIP, std::string("launch ") + (name) + \
                                            ": " + hipGetErrorString(le_)); \
     if ((ctx)->timing) {                                                 \
-      (void)hipEventRecord(b_, (ctx)->stream);                           \
+      (void)hipEventRecord(b_, (st_));                                   \
       (ctx)->mark((name), a_, b_);                                       \
     }                                                                    \
   } while (0)
+#define PM_LAUNCH(ctx, name, ...) PM_LAUNCH_ST(ctx, (ctx)->stream, name, __VA_ARGS__)
 
 namespace pm {
 // ---------------------------------------------------------- MSM pipeline
@@ -57,6 +58,14 @@ int launch_sort_hist(int W, const uint32_t* s, uint32_t n, uint32_t canonical, S
 }
 
 // Run the device pipeline; result = host XYZZ point (sum over windows).
+//
+// Sort once, then the windows are processed in G groups from the top window
+// down.  Group g is accumulated on the context stream; its fixup, segment and
+// bit sums and the D2H copy of its G_{w,b} run on red_stream while group g-1
+// accumulates, and the host Horner over group g's bit positions runs while the
+// GPU works on the lower groups (window w's terms sit at bit positions
+// [o_w, o_w + cmax), so a group's positions are final once every group above
+// it has arrived).
 template <class Cv>
 int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases, size_t n, uint32_t flags,
                     Xyzz<typename Cv::Base>* result) {
@@ -67,15 +76,17 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     return PM_OK;
   }
   if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "n exceeds 2^26 points per device call");
-  const MsmPlan pl = make_plan(n, ctx->window_c);
-  const hipStream_t st = ctx->stream;
+  const MsmPlan pl = make_plan(n, ctx->window_c, ctx->groups, ctx->min_chunk);
+  const hipStream_t st = ctx->stream, st2 = ctx->red_stream;
   const size_t TOT = (size_t)pl.W * pl.NB + 1;
   const size_t nW = (size_t)n * pl.W;
+  const int NJ = pl.NB2 + kTJobs;
   SortGeom g;
   g.FB = std::max(0, pl.cmax - 1 - 8);
   g.NCB = (pl.K >> g.FB) + 1;
   g.nblk = (int)((n + kSortB - 1) / kSortB);
   const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
+  const size_t longs_stride = 16 + (size_t)pl.maxlong * sizeof(LongChain);
   int rc;
   if ((rc = ctx->digits.ensure(nW * 4))) return rc;
   if ((rc = ctx->sorted.ensure(nW * 4))) return rc;
@@ -86,13 +97,14 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const uint32_t nb = (uint32_t)((TOTB + kScanChunk - 1) / kScanChunk);
   if ((rc = ctx->bsum.ensure((size_t)nb * 4))) return rc;
   if ((rc = ctx->buckets.ensure((size_t)pl.W * pl.NB * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->head.ensure((size_t)pl.nthreads * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->head.ensure((size_t)pl.G * pl.nthreads * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segS.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segT.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->bits.ensure((size_t)pl.W * (pl.NB2 + kTJobs) * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->longs.ensure(16 + (size_t)pl.maxlong * sizeof(LongChain)))) return rc;
-  const size_t nG = (size_t)pl.W * (pl.NB2 + kTJobs);
+  if ((rc = ctx->bits.ensure((size_t)pl.W * NJ * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->longs.ensure((size_t)pl.G * longs_stride))) return rc;
+  const size_t nG = (size_t)pl.W * NJ;
   if ((rc = ctx->ensure_pinned(nG * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->ensure_group_events(2 * pl.G))) return rc;
 
   uint32_t* digits = (uint32_t*)ctx->digits.p;
   uint32_t* sorted = (uint32_t*)ctx->sorted.p;
@@ -108,10 +120,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   Xyzz<F>* G = (Xyzz<F>*)ctx->bits.p;
   const uint32_t un = (uint32_t)n;
 
-  uint32_t* nlong = (uint32_t*)ctx->longs.p;
-  LongChain* longs = (LongChain*)((char*)ctx->longs.p + 16);
   HIP_TRY(hipMemsetAsync(bh + (TOTB - 1), 0, 4, st));
-  HIP_TRY(hipMemsetAsync(nlong, 0, 16, st));
+  for (int gi = 0; gi < pl.G; gi++) HIP_TRY(hipMemsetAsync((char*)ctx->longs.p + gi * longs_stride, 0, 16, st));
   PM_LAUNCH(ctx, "sort_hist",
             rc = launch_sort_hist<Fs>(pl.W, d_scalars, un, (flags & PM_SCALARS_CANONICAL) ? 1u : 0u, g, digits,
                                       bh, st));
@@ -127,50 +137,66 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const size_t lds_fine = ((size_t)(1 << g.FB) + kSortThreads / 64 + 1) * 4;
   PM_LAUNCH(ctx, "sort_fine",
             (k_sort_fine<<<pl.W * g.NCB, kSortThreads, lds_fine, st>>>(mid, bofs, g, pl.W, pl.NB, offsets, sorted)));
-  const uint32_t nslots = (uint32_t)(TOT - 1);
   const bool prefetch = ctx->prefetch >= 0 ? ctx->prefetch != 0 : (size_t)n * 64 > kPrefetchBytes;
-  if (prefetch)
-    PM_LAUNCH(ctx, "accumulate",
-              (k_accumulate<F, true><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, nslots, d_bases,
-                                                                                 pl.chunk, buckets, head)));
-  else
-    PM_LAUNCH(ctx, "accumulate",
-              (k_accumulate<F, false><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, nslots, d_bases,
-                                                                                  pl.chunk, buckets, head)));
-  PM_LAUNCH(ctx, "fixup", {
-    k_fixup<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(offsets, nslots, pl.chunk, pl.nthreads, buckets, head,
-                                                           longs, nlong);
-    k_fixup_long<F><<<pl.maxlong, 256, 0, st>>>(longs, nlong, buckets, head);
-  });
-  PM_LAUNCH(ctx, "bucket_seg",
-            (k_bucket_seg<F><<<(pl.W * pl.M1 + 255) / 256, 256, 0, st>>>(offsets, buckets, pl.W, pl.NB, pl.L1,
-                                                                          S, T)));
-  PM_LAUNCH(ctx, "bucket_bits",
-            (k_bucket_bits<F><<<dim3(pl.NB2 + kTJobs, pl.W), kRedThreads, 0, st>>>(S, T, pl.M1, pl.NB2, G)));
-  HIP_TRY(hipMemcpyAsync(ctx->h_pinned, G, nG * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  ctx->end_call();
+  const unsigned ablocks = (pl.nthreads + 255) / 256;
+  for (int gi = pl.G - 1; gi >= 0; gi--) {
+    const int w0 = gi * pl.wpg, w1 = std::min(pl.W, w0 + pl.wpg), nw = w1 - w0;
+    const uint32_t s0 = (uint32_t)((size_t)w0 * pl.NB), s1 = (uint32_t)((size_t)w1 * pl.NB);
+    Xyzz<F>* hg = head + (size_t)gi * pl.nthreads;
+    uint32_t* nlong = (uint32_t*)((char*)ctx->longs.p + gi * longs_stride);
+    LongChain* longs = (LongChain*)((char*)nlong + 16);
+    if (prefetch)
+      PM_LAUNCH(ctx, "accumulate",
+                (k_accumulate<F, true><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, d_bases, pl.chunk, buckets, hg)));
+    else
+      PM_LAUNCH(ctx, "accumulate",
+                (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, d_bases, pl.chunk, buckets, hg)));
+    HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi], st));
+    HIP_TRY(hipStreamWaitEvent(st2, ctx->grp_ev[2 * gi], 0));
+    PM_LAUNCH_ST(ctx, st2, "fixup", {
+      k_fixup<F><<<ablocks, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg, longs, nlong);
+      k_fixup_long<F><<<pl.maxlong, 256, 0, st2>>>(longs, nlong, buckets, hg);
+    });
+    PM_LAUNCH_ST(ctx, st2, "bucket_seg",
+                 (k_bucket_seg<F><<<(nw * pl.M1 + 255) / 256, 256, 0, st2>>>(offsets, buckets, w0, nw, pl.NB, pl.L1,
+                                                                               S, T)));
+    PM_LAUNCH_ST(ctx, st2, "bucket_bits",
+                 (k_bucket_bits<F><<<dim3(NJ, nw), kRedThreads, 0, st2>>>(S, T, w0, pl.M1, pl.NB2, G)));
+    HIP_TRY(hipMemcpyAsync((Xyzz<F>*)ctx->h_pinned + (size_t)w0 * NJ, G + (size_t)w0 * NJ,
+                           (size_t)nw * NJ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st2));
+    HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi + 1], st2));
+  }
 
   // Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b}) as one
-  // Horner over absolute bit positions q (host_ec.hpp).
+  // Horner over absolute bit positions q (host_ec.hpp), consumed group by group.
   const Xyzz<F>* hG = (const Xyzz<F>*)ctx->h_pinned;
-  std::vector<std::vector<int>> at(256 + pl.NB2 + pl.log2L1 + 1);
+  std::vector<std::vector<int>> at(256 + NJ + pl.log2L1 + 1);
+  std::vector<int> gmax(pl.G, -1);  // highest position of any term of group g
   int qmax = 0;
   for (int w = 0; w < pl.W; w++) {
     const int o = w * pl.base + std::min(w, pl.extra);
-    for (int b = 0; b < pl.NB2 + kTJobs; b++) {
+    for (int b = 0; b < NJ; b++) {
       const int q = b < pl.NB2 ? o + b + pl.log2L1 : o;
-      at[q].push_back(w * (pl.NB2 + kTJobs) + b);
+      at[q].push_back(w * NJ + b);
       qmax = std::max(qmax, q);
+      gmax[w / pl.wpg] = std::max(gmax[w / pl.wpg], q);
     }
   }
   host::Pt<F> hacc = host::inf<F>();
-  for (int q = qmax; q >= 0; q--) {
-    hacc = host::dbl<F>(hacc);
-    for (int idx : at[q]) hacc = host::addp<F>(hacc, host::from_dev<F>(hG[idx]));
+  int q = qmax;
+  for (int gi = pl.G - 1; gi >= 0; gi--) {
+    HIP_TRY(hipEventSynchronize(ctx->grp_ev[2 * gi + 1]));
+    int low = 0;  // positions above every lower group's terms are final now
+    for (int gj = 0; gj < gi; gj++) low = std::max(low, gmax[gj] + 1);
+    for (; q >= low; q--) {
+      hacc = host::dbl<F>(hacc);
+      for (int idx : at[q]) hacc = host::addp<F>(hacc, host::from_dev<F>(hG[idx]));
+    }
   }
-  Xyzz<F> acc = host::to_dev<F>(hacc);
-  *result = acc;
+  HIP_TRY(hipStreamSynchronize(st2));
+  HIP_TRY(hipStreamSynchronize(st));
+  ctx->end_call();
+  *result = host::to_dev<F>(hacc);
   return PM_OK;
 }
 

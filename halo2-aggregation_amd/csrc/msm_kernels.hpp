@@ -341,14 +341,15 @@ static __global__ void __launch_bounds__(kSortThreads) k_sort_fine(const uint64_
 }
 
 // ----------------------------------------------------------- 4. accumulate
-// Slice t covers sorted positions [t*chunk, min((t+1)*chunk, total)).  A bucket
-// is *owned* by the slice holding its first element; the owner writes its
-// (possibly partial) sum to buckets[]; a slice whose first bucket started in an
-// earlier slice writes that partial to head[t] for k_fixup.
-__device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ offsets, uint32_t nslots,
+// One launch covers the windows [w0, w1) of a window group, i.e. the sorted
+// positions [offsets[s0], offsets[s1]) with s0 = w0*NB, s1 = w1*NB.  Slice t
+// covers positions [start + t*chunk, ...).  A bucket is *owned* by the slice
+// holding its first element; the owner writes its (possibly partial) sum to
+// buckets[]; a slice whose first bucket started in an earlier slice writes
+// that partial to head[t] for k_fixup.
+__device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ offsets, uint32_t lo, uint32_t hi,
                                                 uint32_t pos) {
-  // largest gb in [0, nslots) with offsets[gb] <= pos
-  uint32_t lo = 0, hi = nslots;
+  // largest gb in [lo, hi) with offsets[gb] <= pos
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
     if (offsets[mid] <= pos) lo = mid; else hi = mid;
@@ -361,16 +362,16 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ off
 // Infinity Cache, at the cost of 16+ VGPRs).
 template <class F, bool PREFETCH>
 __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ sorted,
-                                                    const uint32_t* __restrict__ offsets, uint32_t nslots,
+                                                    const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
                                                     const uint32_t* __restrict__ bases, uint32_t chunk,
                                                     Xyzz<F>* __restrict__ buckets,
                                                     Xyzz<F>* __restrict__ head) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t total = offsets[nslots];
-  const uint32_t start = t * chunk;
+  const uint32_t base = offsets[s0], total = offsets[s1];
+  const uint32_t start = base + t * chunk;
   if (start >= total) return;
   const uint32_t end = min(start + chunk, total);
-  uint32_t gb = find_bucket(offsets, nslots, start);
+  uint32_t gb = find_bucket(offsets, s0, s1, start);
   uint32_t bend = offsets[gb + 1];
   bool owned = offsets[gb] == start;
   Xyzz<F> acc = xyzz_inf<F>();
@@ -415,7 +416,7 @@ struct LongChain {
 };
 
 template <class F>
-__global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offsets, uint32_t nslots,
+__global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
                                                uint32_t chunk, uint32_t nthreads,
                                                Xyzz<F>* __restrict__ buckets,
                                                const Xyzz<F>* __restrict__ head,
@@ -423,14 +424,14 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offs
                                                uint32_t* __restrict__ nlong) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nthreads) return;
-  const uint32_t total = offsets[nslots];
-  const uint32_t start = t * chunk;
+  const uint32_t base = offsets[s0], total = offsets[s1];
+  const uint32_t start = base + t * chunk;
   if (start >= total) return;
   const uint32_t end = min(start + chunk, total);
-  const uint32_t gb = find_bucket(offsets, nslots, end - 1);
+  const uint32_t gb = find_bucket(offsets, s0, s1, end - 1);
   const uint32_t bstart = offsets[gb], bend = offsets[gb + 1];
   if (bstart < start || bend <= end) return;  // not owned, or fully inside
-  const uint32_t t_last = min((bend - 1) / chunk, nthreads - 1);
+  const uint32_t t_last = min((bend - 1 - base) / chunk, nthreads - 1);
   if (t_last - t > kMaxChain) {
     const uint32_t k = atomicAdd(nlong, 1u);
     longs[k] = LongChain{gb, t + 1, t_last};
@@ -465,16 +466,17 @@ __global__ void __launch_bounds__(256) k_fixup_long(const LongChain* __restrict_
 }
 
 // ------------------------------------------------------ 6. segment sums
-// thread (w, j): slots s = j*L1 + i, i in [0, L1):  S = sum B_s,
-// T = sum i * B_s (0-based weight inside the segment).
+// thread (w, j), w in [w0, w0 + nw): slots s = j*L1 + i, i in [0, L1):
+// S = sum B_s, T = sum i * B_s (0-based weight inside the segment).
 template <class F>
 __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__ offsets,
-                                                    const Xyzz<F>* __restrict__ buckets, int W, int NB,
+                                                    const Xyzz<F>* __restrict__ buckets, int w0, int nw, int NB,
                                                     int L1, Xyzz<F>* __restrict__ S,
                                                     Xyzz<F>* __restrict__ T) {
   const int M1 = NB / L1;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= W * M1) return;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nw * M1) return;
+  const int gid = w0 * M1 + g;
   const int w = gid / M1, j = gid - w * M1;
   const size_t base = (size_t)w * NB + (size_t)j * L1;
   Xyzz<F> s = xyzz_inf<F>(), t = xyzz_inf<F>();
@@ -488,7 +490,7 @@ __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------ 7. bit sums
-// block (job, w): job < NB2 -> G_job = sum_{j : (j >> job) & 1} S_j (only
+// block (job, w - w0): job < NB2 -> G_job = sum_{j : (j >> job) & 1} S_j (only
 // the j with that bit set are enumerated, so no lane idles); job >= NB2 ->
 // partial sum of T_j over part (job - NB2) of kTJobs equal ranges.
 // kRedThreads lanes: strided partial sums, then an LDS tree.  Serial depth
@@ -497,10 +499,10 @@ constexpr int kRedThreads = 512;
 constexpr int kTJobs = 2;
 template <class F>
 __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __restrict__ S,
-                                                             const Xyzz<F>* __restrict__ T, int M1,
+                                                             const Xyzz<F>* __restrict__ T, int w0, int M1,
                                                              int NB2, Xyzz<F>* __restrict__ G) {
   __shared__ Xyzz<F> lds[kRedThreads];
-  const int w = blockIdx.y, job = blockIdx.x, tid = threadIdx.x;
+  const int w = w0 + blockIdx.y, job = blockIdx.x, tid = threadIdx.x;
   Xyzz<F> acc = xyzz_inf<F>();
   if (job < NB2) {
     const int low = (1 << job) - 1;

@@ -50,13 +50,15 @@ struct MsmPlan {
   int M1;         // segments per window
   int NB2;        // bits of the segment index
   uint32_t n;
+  int G;              // window groups (pipelined, processed from the top window down)
+  int wpg;            // windows per group
   uint32_t chunk;     // sorted entries per accumulate lane
-  uint32_t nthreads;  // accumulate lanes
-  uint32_t maxlong;   // bound on buckets needing k_fixup_long
+  uint32_t nthreads;  // accumulate lanes per group
+  uint32_t maxlong;   // bound on buckets needing k_fixup_long, per group
   int width(int w) const { return base + (w < extra ? 1 : 0); }
 };
 
-MsmPlan make_plan(size_t n, int c_override);
+MsmPlan make_plan(size_t n, int c_override, int groups_override = 0, int min_chunk = 0);
 
 struct TimedSpan {
   const char* name;
@@ -69,8 +71,12 @@ struct pm_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  hipStream_t red_stream = nullptr;  // bucket reduction of window group g overlaps accumulation of g-1
+  std::vector<hipEvent_t> grp_ev;    // 2 per window group (accumulated, reduced+copied)
   int window_c = 0;
   int prefetch = -1;  // -1 auto, 0 off, 1 on (diagnostics: PM_PREFETCH env)
+  int groups = 0;     // window groups, 0 = auto (diagnostics: PM_GROUPS env)
+  int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
   bool timing = false;
   std::mutex mu;
   // workspace
@@ -93,6 +99,7 @@ struct pm_ctx {
   int begin_call();
   int end_call();
   int ensure_pinned(size_t bytes);
+  int ensure_group_events(int n);
   hipEvent_t next_event();
   void mark(const char* name, hipEvent_t a, hipEvent_t b);
 };

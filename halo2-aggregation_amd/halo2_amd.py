@@ -205,6 +205,7 @@ def _load():
         "pm_ctx_destroy": ([_vp], ctypes.c_int),
         "pm_ctx_set_stream": ([_vp, _vp], ctypes.c_int),
         "pm_ctx_set_window": ([_vp, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_kernel_stats": ([_vp, ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "pm_ctx_reset_stats": ([_vp], ctypes.c_int),
@@ -342,6 +343,9 @@ class Context:
 
     def set_window(self, c):
         _check(lib().pm_ctx_set_window(self.h, c))
+
+    def set_pipeline(self, groups=0, min_chunk=0):
+        _check(lib().pm_ctx_set_pipeline(self.h, groups, min_chunk))
 
     def set_timing(self, on=True):
         _check(lib().pm_ctx_set_timing(self.h, 1 if on else 0))

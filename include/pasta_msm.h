@@ -57,6 +57,10 @@ int pm_ctx_destroy(pm_ctx* ctx);
 int pm_ctx_set_stream(pm_ctx* ctx, void* hip_stream);
 /* Force the window width c (0 = automatic). */
 int pm_ctx_set_window(pm_ctx* ctx, int c);
+/* Pipeline tuning: number of window groups whose bucket reduction overlaps
+ * the next group's accumulation (0 = automatic, 1 = no pipelining) and the
+ * minimum accumulate slice per lane (0 = automatic). */
+int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk);
 /* Per-kernel HIP-event timing on the context stream (for bench/profiling). */
 int pm_ctx_set_timing(pm_ctx* ctx, int enable);
 int pm_ctx_kernel_stats(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms);

@@ -16,7 +16,7 @@ def bit_length(v):
     return int(v).bit_length()
 
 
-def make_plan(n, c_override=0, chunk_override=0):
+def make_plan(n, c_override=0, chunk_override=0, groups_override=0):
     lg = bit_length(max(n, 1)) - 1
     c = c_override if c_override > 0 else max(4, min(16, lg - 4))
     c = max(4, min(20, c))
@@ -28,7 +28,11 @@ def make_plan(n, c_override=0, chunk_override=0):
     NB = ((K + 1 + L1 - 1) // L1) * L1
     M1 = NB // L1
     NB2 = bit_length(M1 - 1)
-    work = n * W
+    G = groups_override if groups_override > 0 else 1
+    G = max(1, min(G, W))
+    wpg = (W + G - 1) // G
+    G = (W + wpg - 1) // wpg
+    work = n * wpg
     target = 256 * 1024
     chunk = max(16, (work + target - 1) // target)
     if chunk_override:
@@ -36,7 +40,7 @@ def make_plan(n, c_override=0, chunk_override=0):
     nthreads = (work + chunk - 1) // chunk
     widths = [base + (1 if w < extra else 0) for w in range(W)]
     return dict(c=c, W=W, widths=widths, K=K, L1=L1, log2L1=L1.bit_length() - 1, NB=NB, M1=M1, NB2=NB2, chunk=chunk,
-                nthreads=nthreads)
+                nthreads=nthreads, G=G, wpg=wpg)
 
 
 def window_widths(W):
@@ -64,11 +68,11 @@ def digits(s, W):
     return out
 
 
-def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
+def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0, groups_override=0):
     n = len(scalars)
     if n == 0:
         return 0
-    pl = make_plan(n, c_override, chunk_override)
+    pl = make_plan(n, c_override, chunk_override, groups_override)
     c, W, NB, L1, M1, NB2 = pl["c"], pl["W"], pl["NB"], pl["L1"], pl["M1"], pl["NB2"]
     TOT = W * NB + 1
     counts = [0] * TOT
@@ -93,8 +97,7 @@ def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
                 cursor[w * NB + d] += 1
     nslots = TOT - 1
 
-    def find_bucket(pos):
-        lo, hi = 0, nslots
+    def find_bucket(lo, hi, pos):
         while hi - lo > 1:
             mid = (lo + hi) // 2
             if offsets[mid] <= pos:
@@ -104,50 +107,53 @@ def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
         return lo
 
     buckets = [0] * nslots
-    head = [0] * pl["nthreads"]
     chunk = pl["chunk"]
-    for t in range(pl["nthreads"]):  # k_accumulate
-        start = t * chunk
-        if start >= total:
-            continue
-        end = min(start + chunk, total)
-        gb = find_bucket(start)
-        bend = offsets[gb + 1]
-        owned = offsets[gb] == start
-        acc = 0
-        for p in range(start, end):
-            if p == bend:
-                if owned:
-                    buckets[gb] = acc
-                else:
-                    head[t] = acc
-                acc = 0
-                gb += 1
-                while offsets[gb + 1] <= p:
+    for g in range(pl["G"] - 1, -1, -1):  # window groups, top down (engine.hpp)
+        w0, w1 = g * pl["wpg"], min(W, (g + 1) * pl["wpg"])
+        s0, s1 = w0 * NB, w1 * NB
+        base, total = offsets[s0], offsets[s1]
+        head = [0] * pl["nthreads"]
+        for t in range(pl["nthreads"]):  # k_accumulate
+            start = base + t * chunk
+            if start >= total:
+                continue
+            end = min(start + chunk, total)
+            gb = find_bucket(s0, s1, start)
+            bend = offsets[gb + 1]
+            owned = offsets[gb] == start
+            acc = 0
+            for p in range(start, end):
+                if p == bend:
+                    if owned:
+                        buckets[gb] = acc
+                    else:
+                        head[t] = acc
+                    acc = 0
                     gb += 1
-                bend = offsets[gb + 1]
-                owned = True
-            i, neg = sorted_[p]
-            acc = (acc + (-dlogs[i] if neg else dlogs[i])) % r
-        if owned:
+                    while offsets[gb + 1] <= p:
+                        gb += 1
+                    bend = offsets[gb + 1]
+                    owned = True
+                i, neg = sorted_[p]
+                acc = (acc + (-dlogs[i] if neg else dlogs[i])) % r
+            if owned:
+                buckets[gb] = acc
+            else:
+                head[t] = acc
+        for t in range(pl["nthreads"]):  # k_fixup
+            start = base + t * chunk
+            if start >= total:
+                continue
+            end = min(start + chunk, total)
+            gb = find_bucket(s0, s1, end - 1)
+            bstart, bend = offsets[gb], offsets[gb + 1]
+            if bstart < start or bend <= end:
+                continue
+            acc = buckets[gb]
+            t_last = min((bend - 1 - base) // chunk, pl["nthreads"] - 1)
+            for t2 in range(t + 1, t_last + 1):
+                acc = (acc + head[t2]) % r
             buckets[gb] = acc
-        else:
-            head[t] = acc
-    for t in range(pl["nthreads"]):  # k_fixup
-        start = t * chunk
-        if start >= total:
-            continue
-        end = min(start + chunk, total)
-        gb = find_bucket(end - 1)
-        bstart, bend = offsets[gb], offsets[gb + 1]
-        if bstart < start or bend <= end:
-            continue
-        acc = buckets[gb]
-        t2 = t + 1
-        while t2 < pl["nthreads"] and t2 * chunk < bend:
-            acc = (acc + head[t2]) % r
-            t2 += 1
-        buckets[gb] = acc
     S = [0] * (W * M1)
     T = [0] * (W * M1)
     for w in range(W):  # k_bucket_seg

@@ -34,6 +34,25 @@ def test_every_window_width(golden, gpu_ctx, c):
         gpu_ctx.set_window(0)
 
 
+@pytest.mark.parametrize("groups,min_chunk", [(1, 0), (2, 1), (3, 7), (5, 0), (16, 64), (64, 2)])
+def test_pipeline_groups(golden, gpu_ctx, groups, min_chunk):
+    """Window-group pipelining (reduction of group g overlapping accumulation
+    of g-1, host Horner per group) and slice lengths do not change results."""
+    gpu_ctx.set_pipeline(groups, min_chunk)
+    try:
+        for name in ("pallas_n4096", "pallas_equal_scalars", "pallas_neg_pairs", "vesta_n1024", "bn254_n1024"):
+            if name not in golden:
+                continue
+            case = golden[name]
+            for c in (0, 5, 11):
+                gpu_ctx.set_window(c)
+                got = gpu_ctx.msm(case["curve"], case["scalars"], case["bases"])
+                assert np.array_equal(got, case["expected"]), (name, groups, min_chunk, c)
+    finally:
+        gpu_ctx.set_window(0)
+        gpu_ctx.set_pipeline(0, 0)
+
+
 def test_canonical_scalars(golden):
     case = golden["pallas_n4096"]
     C = P.PALLAS

@@ -17,6 +17,8 @@ def main():
     curve = int(os.environ.get("CURVE", "0"))
     sizes = [int(x) for x in os.environ.get("LOGN", "16,18,20,22").split(",")]
     cs = [int(x) for x in os.environ.get("WINDOWS", "0").split(",")]
+    gs = [int(x) for x in os.environ.get("PM_SWEEP_GROUPS", "0").split(",")]
+    mcs = [int(x) for x in os.environ.get("PM_SWEEP_MINCHUNK", "0").split(",")]
     ctx = H.Context(0)
     nmax = 1 << max(sizes)
     s = torch.empty((nmax, 4), dtype=torch.int64, device="cuda")
@@ -27,8 +29,9 @@ def main():
     print(json.dumps({"synth_bases_s": time.time() - t, "n": nmax}), flush=True)
     for lg in sizes:
         n = 1 << lg
-        for c in cs:
+        for c, G, mc in [(c, G, mc) for c in cs for G in gs for mc in mcs]:
             ctx.set_window(c)
+            ctx.set_pipeline(G, mc)
             ctx.set_timing(False)
             ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
             reps = 5
@@ -40,8 +43,8 @@ def main():
             ctx.reset_stats()
             for _ in range(reps):
                 ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
-            ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}
-            print(json.dumps({"logn": lg, "c": c, "wall_ms": round(wall * 1e3, 3), "Mscalar_s": round(n / wall / 1e6, 2),
+            ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}  # per MSM (sum over groups)
+            print(json.dumps({"logn": lg, "c": c, "groups": G, "min_chunk": mc, "wall_ms": round(wall * 1e3, 3), "Mscalar_s": round(n / wall / 1e6, 2),
                               "kernels_ms": ks}), flush=True)
     ctx.set_timing(False)
 
