@@ -10,6 +10,7 @@
 
 #include "accum_kernels.hpp"
 #include "engine.hpp"
+#include "selftest.hpp"
 
 namespace pm {
 
@@ -208,7 +209,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   extern const CurveOps name;                                                                  \
   const CurveOps name = {&msm_device_to_aff<Cv>, &point_add_impl<typename Cv::Base>,            \
                          &synth_scalars_impl<Cv>, &synth_bases_impl<Cv>,  \
-                         &accum_device_impl<Cv>};
+                         &accum_device_impl<Cv>, &selftest_field_impl<Cv>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
@@ -217,5 +218,6 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   template int synth_bases_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, void*);                 \
   template int accum_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, const void*, \
                                      void*, void*);                                              \
+  template int selftest_field_impl<Cv>(Ctx*, uint64_t, uint32_t, uint64_t*);                      \
   PM_OPS_TABLE(Cv, name)                                                                       \
   }

@@ -443,6 +443,17 @@ int pm_synth_bases(pm_ctx* ctx, int curve, uint64_t seed, uint64_t i0, size_t n,
   return ops->synth_bases(ctx, seed, i0, (uint32_t)n, d_out);
 }
 
+int pm_selftest_field(pm_ctx* ctx, int curve, uint64_t seed, size_t n, uint64_t* mismatches) {
+  if (!ctx || !mismatches) return set_error(PM_ERR_ARG, "null argument");
+  if (n > (1u << 24)) return set_error(PM_ERR_ARG, "n too large");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return ops->selftest_field(ctx, seed, (uint32_t)n, mismatches);
+}
+
 // ------------------------------------------------- multiopen accumulator
 int pm_shape_layout(const pm_proof_shape* shape, uint32_t* points_per_proof, uint32_t* scalars_per_proof,
                     uint32_t* num_sets) {

@@ -1,0 +1,156 @@
+// curve29.hpp -- XYZZ group law on the radix-2^29 lazy field (fp29.hpp), used
+// by every MSM device kernel after the base conversion.  Same formulas as
+// curve.hpp (madd-2008-s, add-2008-s, dbl-2008-s-1, a = 0); the bounds in the
+// comments keep every coordinate Norm with X, Y < 3p and ZZ, ZZZ < 2p, so a
+// point packs into the 128-byte Xyzz<F> layout (3p < 2^256).  The identity has
+// ZZ == 0 exactly (every routine writes an exact zero when its result is O).
+#pragma once
+#include "curve.hpp"
+#include "fp29.hpp"
+
+namespace pm {
+
+template <class F>
+struct Xyzz29 {
+  F29<F> X, Y, ZZ, ZZZ;
+};
+
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_inf() {
+  return Xyzz29<F>{f29_const<F>(F29Consts<F>::ONE), f29_const<F>(F29Consts<F>::ONE), f29_zero<F>(), f29_zero<F>()};
+}
+template <class F>
+__device__ __forceinline__ bool xyzz29_is_inf(const Xyzz29<F>& p) {
+  return f29_is_zero_exact<F>(p.ZZ);
+}
+
+// ---------------------------------------------------------- packed storage
+template <class F>
+__device__ __forceinline__ F29<F> ld29(const uint4* q) {
+  const uint4 a = q[0], b = q[1];
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return f29_unpack<F>(w);
+}
+template <class F>
+__device__ __forceinline__ void st29(uint4* q, const F29<F>& v) {
+  uint32_t w[8];
+  f29_pack<F>(v, w);
+  q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+template <class F>
+__device__ __forceinline__ Xyzz29<F> load_xyzz29(const Xyzz<F>* src) {
+  const uint4* q = reinterpret_cast<const uint4*>(src);
+  return Xyzz29<F>{ld29<F>(q), ld29<F>(q + 2), ld29<F>(q + 4), ld29<F>(q + 6)};
+}
+template <class F>
+__device__ __forceinline__ void store_xyzz29(Xyzz<F>* dst, const Xyzz29<F>& p) {
+  uint4* q = reinterpret_cast<uint4*>(dst);
+  st29<F>(q, p.X);
+  st29<F>(q + 2, p.Y);
+  st29<F>(q + 4, p.ZZ);
+  st29<F>(q + 6, p.ZZZ);
+}
+// affine base in the converted (R261, canonical) packed layout
+template <class F>
+__device__ __forceinline__ void load_aff29(const uint32_t* p, F29<F>& x, F29<F>& y) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  x = ld29<F>(q);
+  y = ld29<F>(q + 2);
+}
+
+// ------------------------------------------------------------ doubling
+// dbl-2008-s-1 on (X, Y, ZZ, ZZZ); AFF: ZZ = ZZZ = 1 (skips two products).
+// Inputs Norm, X, Y < 4p; valid points only (no y = 0 points: odd order).
+template <class F, bool AFF>
+__device__ __forceinline__ Xyzz29<F> xyzz29_dbl_impl(const F29<F>& X, const F29<F>& Y, const F29<F>& ZZ,
+                                                     const F29<F>& ZZZ) {
+  using K = F29Consts<F>;
+  const F29<F> U = f29_norm<F>(f29_add<F>(Y, Y));              // < 8p
+  const F29<F> V = f29_sqr_c<F>(U);                              // < 2p
+  const F29<F> W = f29_mul_c<F>(U, V);                           // < 2p
+  const F29<F> S = f29_mul_c<F>(X, V);                           // < 2p
+  const F29<F> XX = f29_sqr_c<F>(X);                             // < 2p
+  const F29<F> M = f29_norm<F>(f29_add<F>(f29_add<F>(XX, XX), XX));  // < 6p
+  Xyzz29<F> r;
+  r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(M), f29_add<F>(S, S), K::K8x3)));  // < 3p
+  const F29<F> D = f29_sub<F>(S, r.X, K::K6);                  // loose, < 8p
+  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_mul_c<F>(M, D), f29_mul_c<F>(W, Y), K::K6)));
+  r.ZZ = AFF ? V : f29_mul_c<F>(V, ZZ);
+  r.ZZZ = AFF ? W : f29_mul_c<F>(W, ZZZ);
+  return r;
+}
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_dbl(const Xyzz29<F>& p) {
+  if (xyzz29_is_inf<F>(p)) return p;
+  return xyzz29_dbl_impl<F, false>(p.X, p.Y, p.ZZ, p.ZZZ);
+}
+
+// ------------------------------------------------------------ mixed add
+// madd-2008-s: acc + (x2, y2) with the base (canonical, R261) negated when
+// `neg`.  The caller tracks the identity of acc (acc_inf) and of the base.
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_madd(const Xyzz29<F>& acc, const F29<F>& x2, const F29<F>& y2in,
+                                                 bool& acc_inf) {
+  using K = F29Consts<F>;
+  if (acc_inf) {
+    acc_inf = false;
+    return Xyzz29<F>{x2, y2in, f29_const<F>(K::ONE), f29_const<F>(K::ONE)};
+  }
+  const F29<F> U2 = f29_mul_c<F>(x2, acc.ZZ);                    // < 2p
+  const F29<F> S2 = f29_mul_c<F>(y2in, acc.ZZZ);                 // < 2p
+  const F29<F> P = f29_norm<F>(f29_sub<F>(U2, acc.X, K::K6));  // < 8p
+  const F29<F> R = f29_norm<F>(f29_sub<F>(S2, acc.Y, K::K6));  // < 8p
+  if (f29_is_zero_mod<F>(P)) {
+    if (f29_is_zero_mod<F>(R)) return xyzz29_dbl_impl<F, true>(x2, y2in, x2, x2);
+    acc_inf = true;
+    return xyzz29_inf<F>();
+  }
+  const F29<F> PP = f29_sqr_c<F>(P);                             // 64p^2 < R p
+  const F29<F> PPP = f29_mul_c<F>(P, PP);
+  const F29<F> Q = f29_mul_c<F>(acc.X, PP);
+  Xyzz29<F> r;
+  r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
+  const F29<F> D = f29_sub<F>(Q, r.X, K::K6);                  // loose limbs < 2^31, < 8p
+  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_mul_c<F>(R, D), f29_mul_c<F>(acc.Y, PPP), K::K6)));
+  r.ZZ = f29_mul_c<F>(acc.ZZ, PP);
+  r.ZZZ = f29_mul_c<F>(acc.ZZZ, PPP);
+  return r;
+}
+
+// ------------------------------------------------------------ full add
+// add-2008-s: p + q, both packed-storage points (identity = ZZ exactly 0).
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_add(const Xyzz29<F>& p, const Xyzz29<F>& q) {
+  using K = F29Consts<F>;
+  if (xyzz29_is_inf<F>(q)) return p;
+  if (xyzz29_is_inf<F>(p)) return q;
+  const F29<F> U1 = f29_mul_c<F>(p.X, q.ZZ);
+  const F29<F> U2 = f29_mul_c<F>(q.X, p.ZZ);
+  const F29<F> S1 = f29_mul_c<F>(p.Y, q.ZZZ);
+  const F29<F> S2 = f29_mul_c<F>(q.Y, p.ZZZ);
+  const F29<F> P = f29_norm<F>(f29_sub<F>(U2, U1, K::K6));
+  const F29<F> R = f29_norm<F>(f29_sub<F>(S2, S1, K::K6));
+  if (f29_is_zero_mod<F>(P)) {
+    if (f29_is_zero_mod<F>(R)) return xyzz29_dbl<F>(p);
+    return xyzz29_inf<F>();
+  }
+  const F29<F> PP = f29_sqr_c<F>(P);
+  const F29<F> PPP = f29_mul_c<F>(P, PP);
+  const F29<F> Q = f29_mul_c<F>(U1, PP);
+  Xyzz29<F> r;
+  r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
+  const F29<F> D = f29_sub<F>(Q, r.X, K::K6);
+  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_mul_c<F>(R, D), f29_mul_c<F>(S1, PPP), K::K6)));
+  r.ZZ = f29_mul_c<F>(f29_mul_c<F>(p.ZZ, q.ZZ), PP);
+  r.ZZZ = f29_mul_c<F>(f29_mul_c<F>(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+// y -> (2p - y) for a canonical y (the negated base of a signed digit), Norm
+template <class F>
+__device__ __forceinline__ F29<F> f29_neg_canon(const F29<F>& y) {
+  return f29_norm<F>(f29_sub<F>(f29_zero<F>(), y, F29Consts<F>::K2));
+}
+
+}  // namespace pm

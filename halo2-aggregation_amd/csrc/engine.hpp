@@ -138,6 +138,10 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   PM_LAUNCH(ctx, "sort_fine",
             (k_sort_fine<<<pl.W * g.NCB, kSortThreads, lds_fine, st>>>(mid, bofs, g, pl.W, pl.NB, offsets, sorted)));
   const bool prefetch = ctx->prefetch >= 0 ? ctx->prefetch != 0 : (size_t)n * 64 > kPrefetchBytes;
+  if ((rc = ctx->bases29.ensure((size_t)n * 64))) return rc;
+  const uint32_t* bases29 = (const uint32_t*)ctx->bases29.p;
+  PM_LAUNCH(ctx, "bases_r261",
+            (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
   const unsigned ablocks = (pl.nthreads + 255) / 256;
   for (int gi = pl.G - 1; gi >= 0; gi--) {
     const int w0 = gi * pl.wpg, w1 = std::min(pl.W, w0 + pl.wpg), nw = w1 - w0;
@@ -147,10 +151,10 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     LongChain* longs = (LongChain*)((char*)nlong + 16);
     if (prefetch)
       PM_LAUNCH(ctx, "accumulate",
-                (k_accumulate<F, true><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, d_bases, pl.chunk, buckets, hg)));
+                (k_accumulate<F, true><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg)));
     else
       PM_LAUNCH(ctx, "accumulate",
-                (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, d_bases, pl.chunk, buckets, hg)));
+                (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg)));
     HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi], st));
     HIP_TRY(hipStreamWaitEvent(st2, ctx->grp_ev[2 * gi], 0));
     PM_LAUNCH_ST(ctx, st2, "fixup", {

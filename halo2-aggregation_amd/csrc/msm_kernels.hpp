@@ -24,7 +24,7 @@
 // The host (host_ec.hpp) then evaluates sum_w 2^{o_w} (sum T + L1 * sum_b 2^b
 // G_b) as one Horner over absolute bit positions.
 #pragma once
-#include "curve.hpp"
+#include "curve29.hpp"
 
 namespace pm {
 
@@ -374,35 +374,55 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__
   uint32_t gb = find_bucket(offsets, s0, s1, start);
   uint32_t bend = offsets[gb + 1];
   bool owned = offsets[gb] == start;
-  Xyzz<F> acc = xyzz_inf<F>();
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  bool acc_inf = true;
   uint32_t code = sorted[start];
-  Aff<F> P;
-  if (PREFETCH) P = load_aff<F>(bases + 16ull * (code & ~kNegBit));
+  F29<F> px, py;
+  if (PREFETCH) load_aff29<F>(bases + 16ull * (code & ~kNegBit), px, py);
   for (uint32_t p = start; p < end; p++) {
     if (p == bend) {
-      store_xyzz<F>(owned ? &buckets[gb] : &head[t], acc);
-      acc = xyzz_inf<F>();
+      store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc_inf ? xyzz29_inf<F>() : acc);
+      acc_inf = true;
       gb++;
       while (offsets[gb + 1] <= p) gb++;
       bend = offsets[gb + 1];
       owned = true;
     }
-    Aff<F> cur;
-    uint32_t ccode = code;
+    F29<F> x, y;
+    const uint32_t ccode = code;
     if (PREFETCH) {
-      cur = P;
+      x = px;
+      y = py;
       if (p + 1 < end) {
         code = sorted[p + 1];
-        P = load_aff<F>(bases + 16ull * (code & ~kNegBit));
+        load_aff29<F>(bases + 16ull * (code & ~kNegBit), px, py);
       }
     } else {
-      cur = load_aff<F>(bases + 16ull * (ccode & ~kNegBit));
+      load_aff29<F>(bases + 16ull * (ccode & ~kNegBit), x, y);
       if (p + 1 < end) code = sorted[p + 1];
     }
-    if (ccode & kNegBit) cur.y = fe_neg<F>(cur.y);
-    acc = xyzz_add_aff<F>(acc, cur);
+    if (f29_is_zero_exact<F>(x) && f29_is_zero_exact<F>(y)) continue;  // identity base (0, 0)
+    if (ccode & kNegBit) y = f29_neg_canon<F>(y);
+    acc = xyzz29_madd<F>(acc, x, y, acc_inf);
   }
-  store_xyzz<F>(owned ? &buckets[gb] : &head[t], acc);
+  store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc_inf ? xyzz29_inf<F>() : acc);
+}
+
+// Base conversion (once per MSM): Rust-layout R = 2^256 Montgomery -> the
+// radix-2^29 pipeline's R = 2^261 form, canonical, same packed 64-B layout.
+template <class F>
+__global__ void __launch_bounds__(256) k_bases_to_r261(const uint32_t* __restrict__ in, uint32_t n,
+                                                       uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* q = reinterpret_cast<const uint4*>(in + 16ull * i);
+  uint4* o = reinterpret_cast<uint4*>(out + 16ull * i);
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const uint4 a = q[2 * c], b = q[2 * c + 1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    st29<F>(o + 2 * c, f29_canon<F>(f29_from_r256<F>(w)));
+  }
 }
 
 // --------------------------------------------------------------- 5. fixup
@@ -437,9 +457,9 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offs
     longs[k] = LongChain{gb, t + 1, t_last};
     return;
   }
-  Xyzz<F> acc = load_xyzz<F>(&buckets[gb]);
-  for (uint32_t t2 = t + 1; t2 <= t_last; t2++) acc = xyzz_add<F>(acc, load_xyzz<F>(&head[t2]));
-  store_xyzz<F>(&buckets[gb], acc);
+  Xyzz29<F> acc = load_xyzz29<F>(&buckets[gb]);
+  for (uint32_t t2 = t + 1; t2 <= t_last; t2++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
+  store_xyzz29<F>(&buckets[gb], acc);
 }
 
 template <class F>
@@ -447,22 +467,23 @@ __global__ void __launch_bounds__(256) k_fixup_long(const LongChain* __restrict_
                                                     const uint32_t* __restrict__ nlong,
                                                     Xyzz<F>* __restrict__ buckets,
                                                     const Xyzz<F>* __restrict__ head) {
-  __shared__ Xyzz<F> lds[256];
+  __shared__ Xyzz29<F> lds[256];
   if (blockIdx.x >= *nlong) return;
   const LongChain lc = longs[blockIdx.x];
   const int tid = threadIdx.x;
-  Xyzz<F> acc = xyzz_inf<F>();
-  for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256) acc = xyzz_add<F>(acc, load_xyzz<F>(&head[t2]));
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256)
+    acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
   lds[tid] = acc;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (tid < s) {
-      acc = xyzz_add<F>(acc, lds[tid + s]);
+      acc = xyzz29_add<F>(acc, lds[tid + s]);
       lds[tid] = acc;
     }
     __syncthreads();
   }
-  if (tid == 0) store_xyzz<F>(&buckets[lc.gb], xyzz_add<F>(load_xyzz<F>(&buckets[lc.gb]), acc));
+  if (tid == 0) store_xyzz29<F>(&buckets[lc.gb], xyzz29_add<F>(load_xyzz29<F>(&buckets[lc.gb]), acc));
 }
 
 // ------------------------------------------------------ 6. segment sums
@@ -479,14 +500,14 @@ __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__
   const int gid = w0 * M1 + g;
   const int w = gid / M1, j = gid - w * M1;
   const size_t base = (size_t)w * NB + (size_t)j * L1;
-  Xyzz<F> s = xyzz_inf<F>(), t = xyzz_inf<F>();
+  Xyzz29<F> s = xyzz29_inf<F>(), t = xyzz29_inf<F>();
   for (int i = L1 - 1; i >= 1; i--) {
-    if (offsets[base + i] != offsets[base + i + 1]) s = xyzz_add<F>(s, load_xyzz<F>(&buckets[base + i]));
-    t = xyzz_add<F>(t, s);
+    if (offsets[base + i] != offsets[base + i + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base + i]));
+    t = xyzz29_add<F>(t, s);
   }
-  if (offsets[base] != offsets[base + 1]) s = xyzz_add<F>(s, load_xyzz<F>(&buckets[base]));
-  store_xyzz<F>(&S[gid], s);
-  store_xyzz<F>(&T[gid], t);
+  if (offsets[base] != offsets[base + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base]));
+  store_xyzz29<F>(&S[gid], s);
+  store_xyzz29<F>(&T[gid], t);
 }
 
 // ------------------------------------------------------ 7. bit sums
@@ -501,31 +522,42 @@ template <class F>
 __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __restrict__ S,
                                                              const Xyzz<F>* __restrict__ T, int w0, int M1,
                                                              int NB2, Xyzz<F>* __restrict__ G) {
-  __shared__ Xyzz<F> lds[kRedThreads];
+  __shared__ Xyzz29<F> lds[kRedThreads];
   const int w = w0 + blockIdx.y, job = blockIdx.x, tid = threadIdx.x;
-  Xyzz<F> acc = xyzz_inf<F>();
+  Xyzz29<F> acc = xyzz29_inf<F>();
   if (job < NB2) {
     const int low = (1 << job) - 1;
     for (int m = tid;; m += kRedThreads) {
       const int j = ((m & ~low) << 1) | (1 << job) | (m & low);  // m-th index with bit `job` set
       if (j >= M1) break;
-      acc = xyzz_add<F>(acc, load_xyzz<F>(&S[(size_t)w * M1 + j]));
+      acc = xyzz29_add<F>(acc, load_xyzz29<F>(&S[(size_t)w * M1 + j]));
     }
   } else {
     const int per = (M1 + kTJobs - 1) / kTJobs;
     const int j0 = (job - NB2) * per, j1 = min(M1, j0 + per);
-    for (int j = j0 + tid; j < j1; j += kRedThreads) acc = xyzz_add<F>(acc, load_xyzz<F>(&T[(size_t)w * M1 + j]));
+    for (int j = j0 + tid; j < j1; j += kRedThreads) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&T[(size_t)w * M1 + j]));
   }
   lds[tid] = acc;
   __syncthreads();
   for (int s = kRedThreads / 2; s > 0; s >>= 1) {
     if (tid < s) {
-      acc = xyzz_add<F>(acc, lds[tid + s]);
+      acc = xyzz29_add<F>(acc, lds[tid + s]);
       lds[tid] = acc;
     }
     __syncthreads();
   }
-  if (tid == 0) store_xyzz<F>(&G[(size_t)w * (NB2 + kTJobs) + job], acc);
+  if (tid == 0) {
+    // back to the Rust-layout R = 2^256 Montgomery form for the host tail
+    uint4* q = reinterpret_cast<uint4*>(&G[(size_t)w * (NB2 + kTJobs) + job]);
+    const F29<F>* c[4] = {&acc.X, &acc.Y, &acc.ZZ, &acc.ZZZ};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t o[8];
+      f29_to_r256<F>(*c[k], o);
+      q[2 * k] = make_uint4(o[0], o[1], o[2], o[3]);
+      q[2 * k + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+    }
+  }
 }
 
 // ------------------------------------------------------ synthetic inputs

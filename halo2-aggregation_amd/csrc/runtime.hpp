@@ -81,7 +81,7 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io;
+      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // timing
@@ -93,7 +93,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io};
+            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29};
   }
   ~pm_ctx();
   int begin_call();
@@ -119,6 +119,7 @@ struct CurveOps {
   int (*synth_bases)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, void* d_out);
   int (*accum)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const void* d_points, const void* d_scalars,
                const void* d_challenges, void* d_out_quads, void* d_out_h);
+  int (*selftest_field)(Ctx* ctx, uint64_t seed, uint32_t n, uint64_t* mismatches);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

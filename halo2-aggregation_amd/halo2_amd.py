@@ -219,6 +219,7 @@ def _load():
         "pm_msm_resident": ([_vp, _vp, ctypes.c_size_t, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p],
                             ctypes.c_int),
         "pm_point_add": ([ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
+        "pm_selftest_field": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_synth_scalars": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
                               _vp], ctypes.c_int),
         "pm_synth_bases": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, _vp],
@@ -404,6 +405,11 @@ class Context:
     def accum_batch_device(self, shape: ProofShape, B, d_points, d_scalars, d_challenges, d_quads, d_h=0):
         _check(lib().pm_accum_batch_device(self.h, shape.curve, ctypes.byref(shape.c), B, _vp(d_points),
                                            _vp(d_scalars), _vp(d_challenges), _vp(d_quads), _vp(d_h or None)))
+
+    def selftest_field(self, curve, seed, n):
+        m = ctypes.c_uint64(0)
+        _check(lib().pm_selftest_field(self.h, curve, seed, n, ctypes.byref(m)))
+        return m.value
 
     def synth_bases(self, curve, seed, i0, n, d_out):
         _check(lib().pm_synth_bases(self.h, curve, seed, i0, n, _vp(d_out)))

@@ -95,6 +95,11 @@ int pm_bases_release(pm_bases* b);
 int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* scalars,
                     size_t n, uint32_t flags, uint64_t out[8]);
 
+/* Device self-test of the MSM pipeline's radix-2^29 lazy field arithmetic
+ * against the 32-bit Montgomery arithmetic (n random + edge operand pairs of
+ * the curve's base field); *mismatches = number of failed checks. */
+int pm_selftest_field(pm_ctx* ctx, int curve, uint64_t seed, size_t n, uint64_t* mismatches);
+
 /* Affine helpers (host) for combining partial results: out = a + b. */
 int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
 

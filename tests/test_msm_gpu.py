@@ -53,6 +53,14 @@ def test_pipeline_groups(golden, gpu_ctx, groups, min_chunk):
         gpu_ctx.set_pipeline(0, 0)
 
 
+@pytest.mark.parametrize("curve", [0, 1, 2])
+def test_radix29_field_selftest(gpu_ctx, curve):
+    """The MSM pipeline's radix-2^29 lazy Montgomery arithmetic agrees with the
+    32-bit arithmetic on 2^16 random + edge operand pairs, including loose
+    operands at the limb bound and the 16p -> 3p reduction."""
+    assert gpu_ctx.selftest_field(curve, 0x29 + curve, 1 << 16) == 0
+
+
 def test_canonical_scalars(golden):
     case = golden["pallas_n4096"]
     C = P.PALLAS
