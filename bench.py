@@ -34,6 +34,7 @@ METRIC = "Pallas MSM Mscalar/s at 2^20 (1/2/4/8 GPU); aggregated proofs verified
 LOGN = 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_PAIR = 96            # 32 B scalar + 64 B affine base
+MADS_PER_MADD = 8 * 117 + 2 * 81  # v_mad_u64_u32 per XYZZ mixed add, radix-2^29 Pasta (fp29.hpp)
 SEED_SCALARS, SEED_BASES = 0x5EED, 0xA11CE
 
 
@@ -152,10 +153,11 @@ def main():
         vp = load_valu_peak()
         if vp:
             # The binding roofline is integer VALU: one XYZZ mixed
-            # add = 10 Montgomery products = 10 x 88 v_mad_u64_u32 (Pasta
-            # moduli); ~n*W adds per launch; peak = measured mad issue rate.
+            # add = 8 products + 2 squares in the radix-2^29 arithmetic
+            # (fp29.hpp): 8 x 117 + 2 x 81 = 1098 v_mad_u64_u32 for the Pasta
+            # moduli; ~n*W adds per launch; peak = measured mad issue rate.
             W = windows_for(n, args.window)
-            mads = int(n * W * 10 * 88 / acc_launches_per_msm)
+            mads = int(n * W * MADS_PER_MADD / acc_launches_per_msm)
             ach = mads / (acc_avg_ms * 1e-3) / 1e12
             roof["valu_int"] = {"achieved": round(ach, 3), "peak": vp["v_mad_u64_u32_Tops"], "unit": "T v_mad_u64_u32/s",
                                 "frac": round(ach / vp["v_mad_u64_u32_Tops"], 4), "mads_per_launch": mads}

@@ -361,7 +361,7 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ off
 // addition (hides the dependent HBM gather when the bases exceed the
 // Infinity Cache, at the cost of 16+ VGPRs).
 template <class F, bool PREFETCH>
-__global__ void __launch_bounds__(256) k_accumulate(const uint32_t* __restrict__ sorted,
+__global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
                                                     const uint32_t* __restrict__ bases, uint32_t chunk,
                                                     Xyzz<F>* __restrict__ buckets,

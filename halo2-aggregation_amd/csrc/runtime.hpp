@@ -28,8 +28,11 @@ constexpr int kMaxC = 20;
 constexpr int kAutoMaxC = 16;
 constexpr size_t kMaxPoints = size_t(1) << 26;
 constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg (serial chain: 2*L1-1 adds)
-// bases larger than this (bytes) use the prefetching accumulate kernel
-constexpr size_t kPrefetchBytes = size_t(128) << 20;
+// bases larger than this (bytes) use the prefetching accumulate kernel.  With
+// the radix-2^29 arithmetic the plain kernel is faster at every size measured
+// (2^22: 4.91 vs 5.30 ms, profiles/r01_s2), so auto-prefetch is off; PM_PREFETCH=1
+// still selects it.
+constexpr size_t kPrefetchBytes = ~size_t(0);
 
 struct Buf {
   void* p = nullptr;
