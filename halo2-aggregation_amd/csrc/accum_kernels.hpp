@@ -19,6 +19,7 @@
 #pragma once
 #include "accum_plan.hpp"
 #include "msm_kernels.hpp"
+#include "curve29.hpp"
 
 namespace pm {
 
@@ -109,7 +110,7 @@ __global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* 
     den[i] = i + 1 < K ? fe_mul<Fs>(nfe, fe_sub<Fs>(x, ldfe<Fs>(consts, h.c_wpow + i))) : xn1;
     pre[i] = i ? fe_mul<Fs>(pre[i - 1], den[i]) : den[i];
   }
-  Fe<Fs> inv = fe_inv<Fs>(pre[K - 1]);
+  Fe<Fs> inv = fe_inv_fast<Fs>(pre[K - 1]);
   for (uint32_t i = K - 1; i > 0; i--) {
     const Fe<Fs> t = fe_mul<Fs>(inv, pre[i - 1]);
     inv = fe_mul<Fs>(inv, den[i]);
@@ -217,6 +218,7 @@ template <class Cv>
 struct Glv;
 // PallasCurve: phi(x, y) = (beta x, y) = [lambda](x, y), lambda = 0x397e65a7d7c1ad71aee24b27e308f0a61259527ec1d4752e619d1840af55f1b1
 template <> struct Glv<PallasCurve> {
+  static constexpr uint32_t BETA29[9] = {0x0cbd58ebu, 0x1a2f8f16u, 0x0d140efau, 0x007bdfb9u, 0x1333ecadu, 0x0a33785bu, 0x04eacc49u, 0x09617a1eu, 0x0004ff6cu};  // beta * 2^261 mod p, radix 2^29
   static constexpr uint32_t BETA[8] = {0x9e65eac8u, 0xfbdfd7aau, 0xe50025fbu, 0x0cd4d654u, 0x3785b99au, 0xd59892a3u, 0x585e8789u, 0x2a27fb62u};  // Montgomery
   static constexpr uint32_t A1[4] = {0x00000000u, 0x8cb12793u, 0x40a89953u, 0x49e69d16u};
   static constexpr uint32_t NB1[4] = {0x00000001u, 0x7fcae1c7u, 0x40f04915u, 0x49e69d16u};  // -b1 > 0
@@ -227,6 +229,7 @@ template <> struct Glv<PallasCurve> {
 };
 // VestaCurve: phi(x, y) = (beta x, y) = [lambda](x, y), lambda = 0x12ccca834acdba712caad5dc57aab1b01d1f8bd237ad31491dad5ebdfdfe4ab9
 template <> struct Glv<VestaCurve> {
+  static constexpr uint32_t BETA29[9] = {0x02222437u, 0x00286338u, 0x1ad2e167u, 0x0c255d0eu, 0x16526d7eu, 0x1fb135b2u, 0x0801613au, 0x0220916cu, 0x0003a53fu};  // beta * 2^261 mod p, radix 2^29
   static constexpr uint32_t BETA[8] = {0x80111122u, 0x7c541a84u, 0x56ed29dau, 0x40630b9cu, 0x135b2b29u, 0x02c275fbu, 0x88245b10u, 0x121d29f8u};  // Montgomery
   static constexpr uint32_t A1[4] = {0x00000000u, 0x7fcae1c7u, 0x40f04915u, 0x49e69d16u};
   static constexpr uint32_t NB1[4] = {0x00000001u, 0x8cb12793u, 0x40a89953u, 0x49e69d16u};  // -b1 > 0
@@ -237,6 +240,7 @@ template <> struct Glv<VestaCurve> {
 };
 // Bn254Curve: phi(x, y) = (beta x, y) = [lambda](x, y), lambda = 0x30644e72e131a029048b6e193fd84104cc37a73fec2bc5e9b8ca0b2d36636f23
 template <> struct Glv<Bn254Curve> {
+  static constexpr uint32_t BETA29[9] = {0x18ccb791u, 0x175b1c3au, 0x0b83d6e2u, 0x0e8ed071u, 0x1282bee2u, 0x04220e84u, 0x1fe4017fu, 0x15084d4au, 0x00169119u};  // beta * 2^261 mod p, radix 2^29
   static constexpr uint32_t BETA[8] = {0x13e80b9cu, 0x3350c88eu, 0xdb5e56b9u, 0x7dce557cu, 0xb615564au, 0x6001b4b8u, 0x020217e0u, 0x2682e617u};  // Montgomery
   static constexpr uint32_t A1[4] = {0x7d4f1128u, 0x8211bbebu, 0xeeb859fcu, 0x6f4d8248u};
   static constexpr uint32_t NB1[4] = {0x94d213e3u, 0x89d32568u, 0x00000000u, 0x00000000u};  // -b1 > 0
@@ -319,35 +323,49 @@ __device__ __forceinline__ void glv_split(const Fe<typename Cv::Scalar>& k, uint
   n2 = mp_abs6(k2);
 }
 
-// [k]P by GLV + Shamir: one 130-step joint double-and-add over (k1, k2) with
-// the affine table {P1, P2, P1 + P2} (P1 = +-P, P2 = +-phi(P)); P1 + P2 costs
-// one inversion.  Every step does the same dbl + mixed add (branch-free point
-// select), so lanes of a wave do not diverge.
+// affine (R261) of an XYZZ point that is not the identity
+template <class F>
+__device__ __forceinline__ void xyzz29_to_aff(const Xyzz29<F>& p, F29<F>& x, F29<F>& y) {
+  const F29<F> inv = f29_inv<F>(f29_mul_c<F>(p.ZZ, p.ZZZ));  // 1 / (ZZ ZZZ)
+  x = f29_canon<F>(f29_mul_c<F>(p.X, f29_mul_c<F>(inv, p.ZZZ)));
+  y = f29_canon<F>(f29_mul_c<F>(p.Y, f29_mul_c<F>(inv, p.ZZ)));
+}
+
+// [k]P by GLV + Shamir on the radix-2^29 arithmetic: one 130-step joint
+// double-and-add over (k1, k2) with the canonical affine table {P1, P2,
+// P1 + P2} (P1 = +-P, P2 = +-phi(P)); P1 + P2 costs one inversion.  Every
+// step does one dbl and (unless both bits are 0) one mixed add of a selected
+// table point, so lanes of a wave stay convergent.  Result in packed R261.
 template <class Cv>
-__device__ Xyzz<typename Cv::Base> glv_mul(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P) {
+__device__ Xyzz29<typename Cv::Base> glv_mul(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P) {
   using F = typename Cv::Base;
   uint32_t k1[6], k2[6];
   bool n1, n2;
   glv_split<Cv>(k, k1, k2, n1, n2);
-  Fe<F> beta;
-#pragma unroll
-  for (int i = 0; i < 8; i++) beta.l[i] = Glv<Cv>::BETA[i];
-  const Aff<F> P1 = n1 ? aff_neg<F>(P) : P;
-  Aff<F> P2{fe_mul<F>(beta, P.x), P.y};
-  if (n2) P2 = aff_neg<F>(P2);
-  const Aff<F> P12 = xyzz_to_aff<F>(xyzz_add_aff<F>(xyzz_from_aff<F>(P1), P2));
-  Xyzz<F> acc = xyzz_inf<F>();
+  const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
+  const F29<F> bx = f29_canon<F>(f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), px));  // phi(P).x
+  const F29<F> y1 = n1 ? f29_canon<F>(f29_neg_canon<F>(py)) : py;
+  const F29<F> y2 = n2 ? f29_canon<F>(f29_neg_canon<F>(py)) : py;
+  // P12 = P1 + P2 (x1 != x2 for a non-identity P: beta != 1)
+  bool inf12 = true;
+  Xyzz29<F> s12 = xyzz29_madd<F>(xyzz29_inf<F>(), px, y1, inf12);
+  s12 = xyzz29_madd<F>(s12, bx, y2, inf12);
+  F29<F> x12 = f29_zero<F>(), y12 = f29_zero<F>();
+  if (!inf12) xyzz29_to_aff<F>(s12, x12, y12);
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  bool acc_inf = true;
   for (int i = kGlvBits - 1; i >= 0; i--) {
-    acc = xyzz_dbl<F>(acc);
+    acc = xyzz29_dbl<F>(acc);
     const uint32_t b1 = (k1[i >> 5] >> (i & 31)) & 1u, b2 = (k2[i >> 5] >> (i & 31)) & 1u;
     const uint32_t sel = b1 | (b2 << 1);
-    Aff<F> Q;
+    if (sel == 0 || (sel == 3 && inf12)) continue;
+    F29<F> qx, qy;
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
-      Q.x.l[t] = sel == 1 ? P1.x.l[t] : sel == 2 ? P2.x.l[t] : sel == 3 ? P12.x.l[t] : 0u;
-      Q.y.l[t] = sel == 1 ? P1.y.l[t] : sel == 2 ? P2.y.l[t] : sel == 3 ? P12.y.l[t] : 0u;
+    for (int t = 0; t < 9; t++) {
+      qx.l[t] = sel == 1 ? px.l[t] : sel == 2 ? bx.l[t] : x12.l[t];
+      qy.l[t] = sel == 1 ? y1.l[t] : sel == 2 ? y2.l[t] : y12.l[t];
     }
-    acc = xyzz_add_aff<F>(acc, Q);
+    acc = xyzz29_madd<F>(acc, qx, qy, acc_inf);
   }
   return acc;
 }
@@ -359,7 +377,7 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
                                                      const uint32_t* __restrict__ vk,
                                                      Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
-  using Fs = typename Cv::Scalar;
+  using Fs = typename Cv::Scalar;  // part[] holds packed R261 (curve29.hpp) points
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= h.B * h.T) return;
   const uint32_t b = g / h.T, t = g - b * h.T;
@@ -368,7 +386,7 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
   const uint32_t* pp = (src >> 28) == 0 ? points + 16ull * ((size_t)h.npts * b + idx) : vk + 16ull * idx;
   const Aff<F> P = load_aff<F>(pp);
   const Fe<Fs> c = ldfe<Fs>(coef, g);
-  store_xyzz<F>(&part[g], aff_is_inf<F>(P) ? xyzz_inf<F>() : glv_mul<Cv>(c, P));
+  store_xyzz29<F>(&part[g], aff_is_inf<F>(P) ? xyzz29_inf<F>() : glv_mul<Cv>(c, P));
 }
 
 template <class Cv>
@@ -381,12 +399,20 @@ __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename 
   // MultiopenVar order: w, zw, f, e
   const uint32_t lo = o == 0 ? h.nslots : o == 1 ? h.nslots + h.nsets : o == 2 ? 0 : h.T - 1;
   const uint32_t hi = o == 0 ? h.nslots + h.nsets : o == 1 ? h.nslots + 2 * h.nsets : o == 2 ? h.nslots : h.T;
-  Xyzz<F> acc = xyzz_inf<F>();
-  for (uint32_t t = lo; t < hi; t++) acc = xyzz_add<F>(acc, load_xyzz<F>(&part[(size_t)b * h.T + t]));
-  const Aff<F> a = xyzz_to_aff<F>(acc);
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  for (uint32_t t = lo; t < hi; t++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
+  uint32_t wx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!xyzz29_is_inf<F>(acc)) {
+    F29<F> x, y;
+    xyzz29_to_aff<F>(acc, x, y);
+    f29_to_r256<F>(x, wx);
+    f29_to_r256<F>(y, wy);
+  }
   uint4* q = reinterpret_cast<uint4*>(out + 16ull * g);
-  store_fe4<F>(q, a.x);
-  store_fe4<F>(q + 2, a.y);
+  q[0] = make_uint4(wx[0], wx[1], wx[2], wx[3]);
+  q[1] = make_uint4(wx[4], wx[5], wx[6], wx[7]);
+  q[2] = make_uint4(wy[0], wy[1], wy[2], wy[3]);
+  q[3] = make_uint4(wy[4], wy[5], wy[6], wy[7]);
 }
 
 }  // namespace pm
