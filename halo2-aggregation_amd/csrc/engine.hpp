@@ -38,18 +38,25 @@ namespace pm {
 // ---------------------------------------------------------- MSM pipeline
 
 template <class Fs, int W>
-void launch_sort_hist_w(const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* digits,
-                        uint32_t* bh, hipStream_t st) {
-  k_sort_hist<Fs, W><<<g.nblk, kSortThreads, (size_t)W * g.NCB * 4, st>>>(s, n, canonical, g, digits, bh);
+void launch_sort_w(bool coarse, bool wide, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g,
+                   uint32_t* bh, const uint32_t* bofs, void* digits, void* mid, hipStream_t st) {
+  if (!coarse) {
+    const size_t lds = (size_t)W * g.NCB * 4;
+    if (d16)
+      k_sort_hist<Fs, W, true><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint16_t*)digits, bh);
+    else
+      k_sort_hist<Fs, W, false><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint32_t*)digits, bh);
+    return;
+  }
 }
 
 // one instance per window count reachable from c in [kMinC, kMaxC]
 template <class Fs>
-int launch_sort_hist(int W, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* digits,
-                     uint32_t* bh, hipStream_t st) {
+int launch_sort(int W, bool coarse, bool wide, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical,
+                SortGeom g, uint32_t* bh, const uint32_t* bofs, void* digits, void* mid, hipStream_t st) {
   switch (W) {
 #define PM_W(k) \
-  case k: launch_sort_hist_w<Fs, k>(s, n, canonical, g, digits, bh, st); return PM_OK;
+  case k: launch_sort_w<Fs, k>(coarse, wide, d16, s, n, canonical, g, bh, bofs, digits, mid, st); return PM_OK;
     PM_W(13) PM_W(14) PM_W(15) PM_W(16) PM_W(18) PM_W(19) PM_W(20) PM_W(22) PM_W(24) PM_W(26) PM_W(29)
     PM_W(32) PM_W(37) PM_W(43) PM_W(52) PM_W(64)
 #undef PM_W
@@ -80,17 +87,20 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const hipStream_t st = ctx->stream, st2 = ctx->red_stream;
   const size_t TOT = (size_t)pl.W * pl.NB + 1;
   const size_t nW = (size_t)n * pl.W;
+  // 4-B coarse entries when the point index fits beside the fine bits and the sign
   const int NJ = pl.NB2 + kTJobs;
   SortGeom g;
   g.FB = std::max(0, pl.cmax - 1 - 8);
   g.NCB = (pl.K >> g.FB) + 1;
   g.nblk = (int)((n + kSortB - 1) / kSortB);
   const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
+  const bool wide = n > (size_t(1) << (31 - g.FB));
+  const bool d16 = pl.cmax <= 16;
   const size_t longs_stride = 16 + (size_t)pl.maxlong * sizeof(LongChain);
   int rc;
-  if ((rc = ctx->digits.ensure(nW * 4))) return rc;
+  if ((rc = ctx->digits.ensure(nW * (d16 ? 2 : 4)))) return rc;
   if ((rc = ctx->sorted.ensure(nW * 4))) return rc;
-  if ((rc = ctx->mid.ensure(nW * 8))) return rc;
+  if ((rc = ctx->mid.ensure(nW * (wide ? 8 : 4)))) return rc;
   if ((rc = ctx->counts.ensure(TOTB * 4))) return rc;
   if ((rc = ctx->cursor.ensure(TOTB * 4))) return rc;
   if ((rc = ctx->offsets.ensure(TOT * 4))) return rc;
@@ -106,9 +116,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->ensure_pinned(nG * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->ensure_group_events(2 * pl.G))) return rc;
 
-  uint32_t* digits = (uint32_t*)ctx->digits.p;
   uint32_t* sorted = (uint32_t*)ctx->sorted.p;
-  uint64_t* mid = (uint64_t*)ctx->mid.p;
+  void* mid = ctx->mid.p;
   uint32_t* bh = (uint32_t*)ctx->counts.p;
   uint32_t* bofs = (uint32_t*)ctx->cursor.p;
   uint32_t* offsets = (uint32_t*)ctx->offsets.p;
@@ -122,21 +131,44 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
 
   HIP_TRY(hipMemsetAsync(bh + (TOTB - 1), 0, 4, st));
   for (int gi = 0; gi < pl.G; gi++) HIP_TRY(hipMemsetAsync((char*)ctx->longs.p + gi * longs_stride, 0, 16, st));
+  const uint32_t canon = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
   PM_LAUNCH(ctx, "sort_hist",
-            rc = launch_sort_hist<Fs>(pl.W, d_scalars, un, (flags & PM_SCALARS_CANONICAL) ? 1u : 0u, g, digits,
-                                      bh, st));
+            rc = launch_sort<Fs>(pl.W, false, wide, d16, d_scalars, un, canon, g, bh, bofs, ctx->digits.p, mid, st));
   if (rc) return rc;
   PM_LAUNCH(ctx, "scan", {
     k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum);
     k_scan_top<<<1, 1024, 0, st>>>(bsum, nb);
     k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum, bofs, nullptr);
   });
-  const size_t lds_coarse = (size_t)2 * kSortB * 4 + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
-  PM_LAUNCH(ctx, "sort_coarse",
-            (k_sort_coarse<<<dim3(g.nblk, pl.W), kSortThreads, lds_coarse, st>>>(digits, un, g, bofs, mid)));
-  const size_t lds_fine = ((size_t)(1 << g.FB) + kSortThreads / 64 + 1) * 4;
-  PM_LAUNCH(ctx, "sort_fine",
-            (k_sort_fine<<<pl.W * g.NCB, kSortThreads, lds_fine, st>>>(mid, bofs, g, pl.W, pl.NB, offsets, sorted)));
+  {
+    const size_t lds = (size_t)kSortB * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
+    const dim3 grid(g.nblk, pl.W);
+    void* dg = ctx->digits.p;
+    if (d16 && !wide)
+      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<true, false><<<grid, kSortThreads, lds, st>>>(
+                                        (const uint16_t*)dg, un, g, bofs, (uint32_t*)mid)));
+    else if (d16)
+      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<true, true><<<grid, kSortThreads, lds, st>>>(
+                                        (const uint16_t*)dg, un, g, bofs, (uint64_t*)mid)));
+    else if (!wide)
+      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<false, false><<<grid, kSortThreads, lds, st>>>(
+                                        (const uint32_t*)dg, un, g, bofs, (uint32_t*)mid)));
+    else
+      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<false, true><<<grid, kSortThreads, lds, st>>>(
+                                        (const uint32_t*)dg, un, g, bofs, (uint64_t*)mid)));
+  }
+  // LDS cache: room for 1.5x the mean segment (random digits fill segments
+  // evenly; a skewed segment falls back to re-reading mid), capped at 64 KiB
+  const size_t esz = wide ? 8 : 4;
+  const size_t mean_seg = (size_t)n / std::max(1, g.NCB - 1) + 1;
+  const uint32_t cache_n = (uint32_t)std::min<size_t>(kFineCacheBytes / esz, (mean_seg * 3 / 2 + 63) & ~size_t(63));
+  const size_t lds_fine = (size_t)cache_n * esz + ((size_t)(1 << g.FB) + kFineThreads / 64 + 1) * 4;
+  if (wide)
+    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<true><<<pl.W * g.NCB, kFineThreads, lds_fine, st>>>(
+                                    (const uint64_t*)mid, bofs, g, pl.W, pl.NB, cache_n, offsets, sorted)));
+  else
+    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<false><<<pl.W * g.NCB, kFineThreads, lds_fine, st>>>(
+                                    (const uint32_t*)mid, bofs, g, pl.W, pl.NB, cache_n, offsets, sorted)));
   const bool prefetch = ctx->prefetch >= 0 ? ctx->prefetch != 0 : (size_t)n * 64 > kPrefetchBytes;
   if ((rc = ctx->bases29.ensure((size_t)n * 64))) return rc;
   const uint32_t* bases29 = (const uint32_t*)ctx->bases29.p;

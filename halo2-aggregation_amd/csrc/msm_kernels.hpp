@@ -178,20 +178,28 @@ static __global__ void __launch_bounds__(kScanThreads) k_scan_down(const uint32_
 }
 
 // -------------------------------------------------------------- 3. sort
-// Bucket sort of the W x n digit codes without global atomics (replaces a
-// global-atomic counting sort that was 45% of the MSM at 2^20):
-//   k_sort_hist    per block of kSortB points: signed digits for all windows
-//                  (written coalesced to digits[w*n+i]) and an LDS histogram
-//                  over (window, coarse bin), coarse = slot >> FB; the block
-//                  histogram goes to bh[(w*NCB+cb)*nblk + blk] so one exclusive
-//                  scan of bh yields every block's output position.
+// Bucket sort of the W x n digit codes without global atomics:
+//   k_sort_hist    per block of kSortB points: signed digits of all windows,
+//                  stored window-major as 2 B codes (c <= 16) or 4 B, and an LDS
+//                  histogram over (window, coarse bin), coarse = slot >> FB;
+//                  the block histogram goes to bh[(w*NCB+cb)*nblk + blk] so one
+//                  exclusive scan of bh yields every block's output position.
 //   k_sort_coarse  block (blk, w): LDS-ranked, LDS-staged scatter of its codes
 //                  into the coarse segments (runs of consecutive addresses).
+//                  Entries are 4 B (fine | sign | index) when the point index
+//                  fits, else 8 B.  (Recomputing the digits here instead of
+//                  storing them was measured slower: profiles/r01_s2.)
 //   k_sort_fine    block per (w, cb) segment: LDS counting sort on the FB fine
-//                  bits; writes the final bucket offsets and sorted[] entries.
+//                  bits, the segment cached in LDS between the two passes;
+//                  writes the bucket offsets and sorted[] (index | sign << 31).
+// Traffic per scalar at c = 16 (W = 16): 32 B read, 32 B digits written and
+// read, 64 B entries written and read once, 64 B sorted written (~290 B; was
+// ~600 B with 4-B digits, 8-B entries and two global passes in k_sort_fine).
 constexpr int kSortThreads = 256;
 constexpr int kSortPerThread = 8;
 constexpr int kSortB = kSortThreads * kSortPerThread;  // points per block
+constexpr uint32_t kFineCacheBytes = 65536;            // max LDS cache of one fine segment (64 KiB)
+constexpr int kFineThreads = 512;
 
 struct SortGeom {
   int FB;    // fine bits
@@ -199,12 +207,61 @@ struct SortGeom {
   int nblk;  // point blocks
 };
 
-template <class Fs, int W>
+// signed digit of window w (WinGeom), carry in/out; returns |d| | neg << 31
+// (0 = no contribution).  The top window never carries (scalars < 2^255).
+template <int W, class Fs>
+__device__ __forceinline__ uint32_t signed_digit(const Fe<Fs>& s, int w, uint32_t& carry) {
+  using G = WinGeom<W>;
+  const int C = G::width(w);
+  const int bit = G::offset(w);
+  const int limb = bit >> 5, sh = bit & 31;
+  const uint32_t lo = s.l[limb] >> sh;
+  const uint32_t hi = (sh != 0 && limb + 1 < 8) ? (s.l[limb + 1] << (32 - sh)) : 0u;
+  const uint32_t raw = (lo | hi) & ((1u << C) - 1u);
+  uint32_t d = raw + carry;
+  uint32_t neg = 0;
+  if (w != W - 1 && d > (1u << (C - 1))) {
+    d = (1u << C) - d;
+    neg = 1;
+    carry = 1;
+  } else {
+    carry = 0;
+  }
+  return d ? (d | (neg << 31)) : 0u;
+}
+
+template <class Fs>
+__device__ __forceinline__ Fe<Fs> load_canonical(const uint32_t* scalars, uint32_t i, uint32_t canonical) {
+  Fe<Fs> s = load_fe4<Fs>(reinterpret_cast<const uint4*>(scalars + 8ull * i));
+  return canonical ? s : fe_from_mont<Fs>(s);
+}
+
+// stored digit: D16 (cmax <= 16): (|d| - 1) | neg << 15, 0xFFFF = zero
+// (|d| = 2^15 only occurs positive, so that code is free); else |d| | neg << 31
+template <bool D16>
+struct DigitCode;
+template <>
+struct DigitCode<true> {
+  using T = uint16_t;
+  static __device__ __forceinline__ T enc(uint32_t code) {
+    return code ? (uint16_t)(((code & ~kNegBit) - 1u) | ((code >> 31) << 15)) : (uint16_t)0xFFFFu;
+  }
+  static __device__ __forceinline__ uint32_t dec(T v) {
+    return v == 0xFFFFu ? 0u : (((uint32_t)v & 0x7FFFu) + 1u) | (((uint32_t)v >> 15) << 31);
+  }
+};
+template <>
+struct DigitCode<false> {
+  using T = uint32_t;
+  static __device__ __forceinline__ T enc(uint32_t code) { return code; }
+  static __device__ __forceinline__ uint32_t dec(T v) { return v; }
+};
+
+template <class Fs, int W, bool D16>
 __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __restrict__ scalars, uint32_t n,
                                                             uint32_t canonical, SortGeom g,
-                                                            uint32_t* __restrict__ digits,
+                                                            typename DigitCode<D16>::T* __restrict__ digits,
                                                             uint32_t* __restrict__ bh) {
-  using G = WinGeom<W>;
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
   const int nbins = W * g.NCB;
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
@@ -212,44 +269,60 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
   for (int r = 0; r < kSortPerThread; r++) {
     const uint32_t i = blockIdx.x * kSortB + r * kSortThreads + threadIdx.x;
     if (i >= n) break;
-    const uint4* q = reinterpret_cast<const uint4*>(scalars + 8ull * i);
-    Fe<Fs> s = load_fe4<Fs>(q);
-    if (!canonical) s = fe_from_mont<Fs>(s);
+    const Fe<Fs> s = load_canonical<Fs>(scalars, i, canonical);
     uint32_t carry = 0;
 #pragma unroll
     for (int w = 0; w < W; w++) {
-      const int C = G::width(w);
-      const int bit = G::offset(w);
-      const int limb = bit >> 5, sh = bit & 31;
-      uint32_t lo = s.l[limb] >> sh;
-      uint32_t hi = (sh != 0 && limb + 1 < 8) ? (s.l[limb + 1] << (32 - sh)) : 0u;
-      const uint32_t raw = (lo | hi) & ((1u << C) - 1u);
-      uint32_t d = raw + carry;
-      uint32_t neg = 0;
-      if (w != W - 1 && d > (1u << (C - 1))) {
-        d = (1u << C) - d;
-        neg = 1;
-        carry = 1;
-      } else {
-        carry = 0;
-      }
-      digits[(size_t)w * n + i] = d ? (d | (neg << 31)) : 0u;
-      if (d) atomicAdd(&hist[w * g.NCB + (d >> g.FB)], 1u);
+      const uint32_t code = signed_digit<W, Fs>(s, w, carry);
+      digits[(size_t)w * n + i] = DigitCode<D16>::enc(code);
+      if (code) atomicAdd(&hist[w * g.NCB + ((code & ~kNegBit) >> g.FB)], 1u);
     }
   }
   __syncthreads();
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) bh[(size_t)k * g.nblk + blockIdx.x] = hist[k];
 }
 
+// coarse-segment entry: WIDE = slot << 32 | index | sign << 31;
+// narrow = fine << (32 - FB) | sign << (31 - FB) | index  (index < 2^(31 - FB))
+template <bool WIDE>
+struct SortEntry;
+template <>
+struct SortEntry<true> {
+  using T = uint64_t;
+  static __device__ __forceinline__ T make(uint32_t slot, uint32_t i, uint32_t neg, int) {
+    return ((uint64_t)slot << 32) | (i | (neg << 31));
+  }
+  static __device__ __forceinline__ uint32_t fine(T v, uint32_t fmask, int) { return (uint32_t)(v >> 32) & fmask; }
+  static __device__ __forceinline__ uint32_t code(T v, int) { return (uint32_t)v; }
+};
+template <>
+struct SortEntry<false> {
+  using T = uint32_t;
+  static __device__ __forceinline__ T make(uint32_t slot, uint32_t i, uint32_t neg, int FB) {
+    const uint32_t fm = (1u << FB) - 1u;
+    return (FB ? ((slot & fm) << (32 - FB)) : 0u) | (neg << (31 - FB)) | i;
+  }
+  static __device__ __forceinline__ uint32_t fine(T v, uint32_t, int FB) { return FB ? v >> (32 - FB) : 0u; }
+  static __device__ __forceinline__ uint32_t code(T v, int FB) {
+    const uint32_t imask = (1u << (31 - FB)) - 1u;
+    return (v & imask) | (((v >> (31 - FB)) & 1u) << 31);
+  }
+};
+
 // block (blk = blockIdx.x, w = blockIdx.y)
-static __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const uint32_t* __restrict__ digits, uint32_t n,
-                                                                     SortGeom g, const uint32_t* __restrict__ bofs,
-                                                                     uint64_t* __restrict__ mid) {
+template <bool D16, bool WIDE>
+__global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename DigitCode<D16>::T* __restrict__ digits,
+                                                              uint32_t n, SortGeom g,
+                                                              const uint32_t* __restrict__ bofs,
+                                                              typename SortEntry<WIDE>::T* __restrict__ mid) {
+  using E = SortEntry<WIDE>;
+  using T = typename E::T;
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-  uint64_t* stage = reinterpret_cast<uint64_t*>(sm);                   // kSortB entries
-  uint32_t* cnt = sm + 2 * kSortB;                                     // NCB
-  uint32_t* lstart = cnt + g.NCB;                                      // NCB + 1
-  uint32_t* scan_tmp = lstart + g.NCB + 1;                             // kSortThreads/64 + 1
+  T* stage = reinterpret_cast<T*>(sm);                                        // kSortB entries
+  uint16_t* stage_cb = reinterpret_cast<uint16_t*>(stage + kSortB);          // kSortB coarse bins
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(stage_cb + kSortB);            // NCB
+  uint32_t* lstart = cnt + g.NCB;                                            // NCB + 1
+  uint32_t* scan_tmp = lstart + g.NCB + 1;                                   // kSortThreads/64 + 1
   const uint32_t w = blockIdx.y, blk = blockIdx.x;
   for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) cnt[k] = 0;
   __syncthreads();
@@ -257,21 +330,20 @@ static __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const uint3
 #pragma unroll
   for (int r = 0; r < kSortPerThread; r++) {
     const uint32_t i = blk * kSortB + r * kSortThreads + threadIdx.x;
-    code[r] = i < n ? digits[(size_t)w * n + i] : 0u;
+    code[r] = i < n ? DigitCode<D16>::dec(digits[(size_t)w * n + i]) : 0u;
     if (code[r]) atomicAdd(&cnt[(code[r] & ~kNegBit) >> g.FB], 1u);
   }
   __syncthreads();
-  // exclusive scan of cnt -> lstart (NCB <= a few hundred: one chunk per pass)
-  uint32_t carry = 0;
+  uint32_t run = 0;
   for (int base = 0; base < g.NCB; base += kSortThreads) {
     const int k = base + threadIdx.x;
     const uint32_t v = k < g.NCB ? cnt[k] : 0u;
     uint32_t total;
     const uint32_t ex = block_excl_scan(v, scan_tmp, total);
-    if (k < g.NCB) lstart[k] = ex + carry;
-    carry += total;
+    if (k < g.NCB) lstart[k] = ex + run;
+    run += total;
   }
-  if (threadIdx.x == 0) lstart[g.NCB] = carry;
+  if (threadIdx.x == 0) lstart[g.NCB] = run;
   __syncthreads();
   for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) cnt[k] = lstart[k];  // cursors
   __syncthreads();
@@ -280,63 +352,73 @@ static __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const uint3
     if (!code[r]) continue;
     const uint32_t i = blk * kSortB + r * kSortThreads + threadIdx.x;
     const uint32_t slot = code[r] & ~kNegBit;
-    const uint32_t pos = atomicAdd(&cnt[slot >> g.FB], 1u);
-    stage[pos] = ((uint64_t)slot << 32) | (i | (code[r] & kNegBit));
+    const uint32_t cb = slot >> g.FB;
+    const uint32_t pos = atomicAdd(&cnt[cb], 1u);
+    stage[pos] = E::make(slot, i, code[r] >> 31, g.FB);
+    stage_cb[pos] = (uint16_t)cb;
   }
   __syncthreads();
   const uint32_t nvalid = lstart[g.NCB];
   for (uint32_t e = threadIdx.x; e < nvalid; e += kSortThreads) {
-    const uint64_t v = stage[e];
-    const uint32_t cb = (uint32_t)(v >> 32) >> g.FB;
+    const uint32_t cb = stage_cb[e];
     const uint32_t pos = bofs[((size_t)w * g.NCB + cb) * g.nblk + blk] + (e - lstart[cb]);
-    mid[pos] = v;
+    mid[pos] = stage[e];
   }
 }
 
 // block per (w, cb) segment; offsets[w*NB + slot] for its slots, sorted[]
-static __global__ void __launch_bounds__(kSortThreads) k_sort_fine(const uint64_t* __restrict__ mid,
-                                                                   const uint32_t* __restrict__ bofs, SortGeom g,
-                                                                   int W, int NB, uint32_t* __restrict__ offsets,
-                                                                   uint32_t* __restrict__ sorted) {
+// (cache_n: entries of the LDS segment cache, sized from the mean segment)
+template <bool WIDE>
+__global__ void __launch_bounds__(kFineThreads) k_sort_fine(const typename SortEntry<WIDE>::T* __restrict__ mid,
+                                                            const uint32_t* __restrict__ bofs, SortGeom g, int W,
+                                                            int NB, uint32_t cache_n, uint32_t* __restrict__ offsets,
+                                                            uint32_t* __restrict__ sorted) {
+  using E = SortEntry<WIDE>;
+  using T = typename E::T;
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int nf = 1 << g.FB;
-  uint32_t* hist = sm;                 // nf
-  uint32_t* scan_tmp = sm + nf;        // kSortThreads/64 + 1
+  T* cache = reinterpret_cast<T*>(sm);                                 // cache_n entries
+  uint32_t* hist = reinterpret_cast<uint32_t*>(cache + cache_n);       // nf
+  uint32_t* scan_tmp = hist + nf;                                      // kFineThreads/64 + 1
   const uint32_t seg = blockIdx.x;     // = w * NCB + cb
   const uint32_t w = seg / g.NCB, cb = seg - w * g.NCB;
   const uint32_t s0 = bofs[(size_t)seg * g.nblk];
   const uint32_t s1 = bofs[(size_t)(seg + 1) * g.nblk];  // next segment (or total)
+  const bool cached = s1 - s0 <= cache_n;
   const uint32_t fmask = (uint32_t)nf - 1u;
-  for (int k = threadIdx.x; k < nf; k += kSortThreads) hist[k] = 0;
+  for (int k = threadIdx.x; k < nf; k += kFineThreads) hist[k] = 0;
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += kSortThreads)
-    atomicAdd(&hist[(uint32_t)(mid[e] >> 32) & fmask], 1u);
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += kFineThreads) {
+    const T v = mid[e];
+    if (cached) cache[e - s0] = v;
+    atomicAdd(&hist[E::fine(v, fmask, g.FB)], 1u);
+  }
   __syncthreads();
   // exclusive scan of the fine histogram; emit bucket offsets
-  uint32_t carry = 0;
-  for (int base = 0; base < nf; base += kSortThreads) {
+  uint32_t run = 0;
+  for (int base = 0; base < nf; base += kFineThreads) {
     const int k = base + threadIdx.x;
     const uint32_t v = k < nf ? hist[k] : 0u;
     uint32_t total;
     const uint32_t ex = block_excl_scan(v, scan_tmp, total);
     if (k < nf) {
       const uint32_t slot = (cb << g.FB) + k;
-      hist[k] = s0 + ex + carry;  // cursor
-      if (slot < (uint32_t)NB) offsets[(size_t)w * NB + slot] = s0 + ex + carry;
+      hist[k] = s0 + ex + run;  // cursor
+      if (slot < (uint32_t)NB) offsets[(size_t)w * NB + slot] = s0 + ex + run;
     }
-    carry += total;
+    run += total;
   }
   // slots beyond the coarse range (window padding) and the final sentinel
   if (cb == (uint32_t)g.NCB - 1) {
-    for (uint32_t slot = ((uint32_t)g.NCB << g.FB) + threadIdx.x; slot < (uint32_t)NB; slot += kSortThreads)
+    for (uint32_t slot = ((uint32_t)g.NCB << g.FB) + threadIdx.x; slot < (uint32_t)NB; slot += kFineThreads)
       offsets[(size_t)w * NB + slot] = s1;
     if (threadIdx.x == 0 && w == (uint32_t)W - 1) offsets[(size_t)W * NB] = s1;
   }
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += kSortThreads) {
-    const uint64_t v = mid[e];
-    const uint32_t pos = atomicAdd(&hist[(uint32_t)(v >> 32) & fmask], 1u);
-    sorted[pos] = (uint32_t)v;
+  for (uint32_t e = s0 + threadIdx.x; e < s1; e += kFineThreads) {
+    const T v = cached ? cache[e - s0] : mid[e];
+    const uint32_t pos = atomicAdd(&hist[E::fine(v, fmask, g.FB)], 1u);
+    sorted[pos] = E::code(v, g.FB);
   }
 }
 
