@@ -128,7 +128,8 @@ def main():
     # per-MSM kernel time (the pipelined engine launches accumulate / fixup /
     # bucket_* once per window group)
     kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4)
-               for k in ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg", "bucket_bits"]}
+               for k in ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg",
+                         "bucket_bits", "host_tail"]}
     acc_launches_per_msm = max(1, launches) / args.steps
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

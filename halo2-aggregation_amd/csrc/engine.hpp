@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 
@@ -220,14 +221,22 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   }
   host::Pt<F> hacc = host::inf<F>();
   int q = qmax;
+  double tail_ms = 0.0;
   for (int gi = pl.G - 1; gi >= 0; gi--) {
     HIP_TRY(hipEventSynchronize(ctx->grp_ev[2 * gi + 1]));
+    const auto t0 = std::chrono::steady_clock::now();
     int low = 0;  // positions above every lower group's terms are final now
     for (int gj = 0; gj < gi; gj++) low = std::max(low, gmax[gj] + 1);
     for (; q >= low; q--) {
       hacc = host::dbl<F>(hacc);
       for (int idx : at[q]) hacc = host::addp<F>(hacc, host::from_dev<F>(hG[idx]));
     }
+    tail_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  if (ctx->timing) {
+    auto& stt = ctx->stats["host_tail"];
+    stt.first += 1;
+    stt.second += tail_ms;
   }
   HIP_TRY(hipStreamSynchronize(st2));
   HIP_TRY(hipStreamSynchronize(st));
