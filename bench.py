@@ -14,12 +14,14 @@ live with HIP events on the context stream over the timed region.
 on the host cores of the same box, on the same inputs, at N=1 on rank 0.
 
 `accumulator` is the second half of the BASELINE metric ("aggregated proofs
-verified/s"): each rank runs the batch multiopen accumulator (pm_accum_batch,
-SURVEY §8 rows a-3..a-9) over its own B = 256 synthetic simple-example proofs
-(BN254, k = 17; weak scaling, proofs are independent), followed by an
-all-gather of the B x 4 accumulator points over RCCL.  Its cpu_baseline is the
-Python oracle (oracle/accum.py) on a bounded sample of the same proofs, with a
-bit-exact spot check of the GPU results.
+verified/s"): each rank replays the Blake2b transcript of its own B = 256
+synthetic simple-example proofs and runs the batch multiopen accumulator on the
+replayed challenges (pm_accum_batch_transcript_device, SURVEY §8 rows
+a-3..a-9 + §8f-2; BN254, k = 17; weak scaling, proofs are independent),
+followed by an all-gather of the B x 4 accumulator points over RCCL.  Its
+cpu_baseline is the Python oracle (oracle/transcript.py + oracle/accum.py) on a
+bounded sample of the same proofs, with a bit-exact spot check of the GPU's
+challenges and results.
 """
 import argparse
 import json
@@ -219,7 +221,8 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
-    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4) for k in ("acc_scalars", "acc_termmul", "acc_sum")}
+    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4)
+               for k in ("transcript", "acc_scalars", "acc_termmul", "acc_sum")}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -229,12 +232,14 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
            "ms_per_batch": round(ms, 4), "higher_is_better": True, "scaling": "weak",
            "config": {"workload": f"multiopen_accumulator_simple_example_k{args.accum_logn}", "curve": "bn254",
                       "proofs_per_gpu": B, "proofs_total": world * B,
+                      "challenges": "Blake2b transcript replayed on the device (pm_accum_batch_transcript_device)",
                       "parallelism": f"proof-batch x{world} + RCCL all-gather of B x 4 points"},
            "kernels_ms": kernels}
     if rank == 0:
         pick = [0, B - 1]
         host = {k: getattr(batch, k)[pick].cpu().numpy().view(np.uint64)
                 for k in ("points", "scalars", "challenges", "quads", "h_eval")}
+        host["vk_repr"] = np.asarray(batch.vk_repr, dtype=np.uint64)
         vk = (np.ctypeslib.as_array(shape.c.fixed_commitments, shape=(shape.c.num_fixed_columns * 8,)).copy(),
               np.ctypeslib.as_array(shape.c.sigma_commitments, shape=(shape.c.n_perm_columns * 8,)).copy())
         out["_state"] = (curve, args.accum_logn, host, vk, B)
@@ -242,13 +247,15 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
 
 
 def accum_cpu_baseline(curve, log_n, host, vk, B, budget_s):
-    """Python oracle (oracle/accum.py, closed form) on the GPU's own proofs:
-    bit-exact spot check + throughput on a bounded sample."""
+    """Python oracle (oracle/transcript.py replay + oracle/accum.py closed
+    form) on the GPU's own proofs: bit-exact spot check of challenges, quads
+    and h_eval + throughput on a bounded sample."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import accum as A
     import pasta as P
+    import transcript as T
 
     C = P.CURVES[curve]
     sh = A.simple_example_shape(C, log_n)
@@ -263,19 +270,24 @@ def accum_cpu_baseline(curve, log_n, host, vk, B, budget_s):
                               scalars=[P.from_limbs([int(x) for x in v]) * rinv % C.r for v in host["scalars"][b]],
                               challenges=[P.from_limbs([int(x) for x in v]) * rinv % C.r
                                           for v in host["challenges"][b]]))
+    vkr = P.from_limbs([int(x) for x in host["vk_repr"]]) * rinv % C.r
     match = True
     reps, t0 = 0, time.perf_counter()
     while True:
         for b, pf in enumerate(proofs):
-            q, h = A.pack_result(C, A.accumulate_msm(C, sh, pf))
+            ch, _ = T.replay_challenges(C, sh, pf, vkr)
+            pf2 = A.Proof(points=pf.points, scalars=pf.scalars, challenges=ch)
+            q, h = A.pack_result(C, A.accumulate_msm(C, sh, pf2))
             if reps < len(proofs):
+                match &= ch == pf.challenges
                 match &= bool(np.array_equal(q, host["quads"][b]) and np.array_equal(h, host["h_eval"][b]))
             reps += 1
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
     return {"value": round(reps / dt, 2), "unit": "proofs/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} proofs (2 distinct, from the GPU batch) through oracle/accum.py accumulate_msm "
+            "sample": f"{reps} proofs (2 distinct, from the GPU batch) through oracle/transcript.py replay + "
+                      f"oracle/accum.py accumulate_msm "
                       f"({dt:.1f} s, Python big-int, 1 thread)",
             "matches_gpu": match}
 

@@ -11,6 +11,7 @@
 #include "accum_kernels.hpp"
 #include "engine.hpp"
 #include "selftest.hpp"
+#include "transcript_kernels.hpp"
 
 namespace pm {
 
@@ -197,6 +198,72 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   return PM_OK;
 }
 
+// Batched Blake2b transcript replay (transcript_kernels.hpp): absorb program
+// in verifier read order, one lane per proof, challenges written in the
+// (B, 7, 4) layout pm_accum_batch reads.
+template <class Cv>
+int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
+                           const void* d_scalars, void* d_ch, void* d_status) {
+  using Fs = typename Cv::Scalar;
+  std::vector<AccQuery> q;
+  AccLayout L;
+  const std::string err = acc_validate(s, q, L, nullptr);
+  if (!err.empty()) return set_error(PM_ERR_ARG, "transcript shape: " + err);
+  if (B == 0) return PM_OK;
+  if (B > (1u << 20)) return set_error(PM_ERR_UNSUPPORTED, "transcript batch larger than 2^20 proofs");
+  std::vector<uint32_t> prog;
+  auto pts = [&](uint32_t p0, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) prog.push_back((kTrPoint << 24) | (p0 + i));
+  };
+  auto squeeze = [&](uint32_t slot) { prog.push_back((kTrSqueeze << 24) | slot); };
+  prog.push_back(kTrVk << 24);                             // verifier.rs:341-358
+  pts(L.p_inst, s->num_instance_columns);                  // :360-363
+  pts(L.p_adv, s->num_advice_columns);                     // :365-376
+  squeeze(0);                                              // theta :378
+  pts(L.p_lkperm, 2 * s->num_lookups);                     // :381-387
+  squeeze(1);                                              // beta :390
+  squeeze(2);                                              // gamma :393
+  pts(L.p_permz, L.n_perm_sets);                           // :402-409
+  pts(L.p_lkz, s->num_lookups);                            // :411-417
+  pts(L.p_rand, 1);                                        // :419-421
+  squeeze(3);                                              // y :423
+  pts(L.p_h, s->quotient_degree);                          // :425-434
+  squeeze(4);                                              // x :436
+  for (uint32_t i = 0; i < L.nsc; i++) prog.push_back((kTrScalar << 24) | i);  // :438-509
+  squeeze(5);                                              // v :718
+  squeeze(6);                                              // u :719
+
+  TranscriptHdr hd{};
+  hd.B = (uint32_t)B;
+  hd.npts = L.npts;
+  hd.nsc = L.nsc;
+  hd.nprog = (uint32_t)prog.size();
+  blake2b_init_personal(hd.h0, (const uint8_t*)kTranscriptPersonal);
+  const Fe<Fs> vk = fe_from_mont<Fs>(fe_from_u64<Fs>(vk_repr));
+  for (int i = 0; i < 8; i++) hd.vk[i] = vk.l[i];
+
+  const hipStream_t st = ctx->stream;
+  int rc;
+  if ((rc = ctx->tr_prog.ensure(prog.size() * 4))) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->tr_prog.p, prog.data(), prog.size() * 4, hipMemcpyHostToDevice, st));
+  PM_LAUNCH(ctx, "transcript",
+            (k_transcript<Cv><<<(unsigned)((B + 63) / 64), 64, 0, st>>>(
+                hd, (const uint32_t*)ctx->tr_prog.p, (const uint32_t*)d_points, (const uint32_t*)d_scalars,
+                (uint32_t*)d_ch, (uint32_t*)d_status)));
+  return PM_OK;
+}
+
+// vk_repr = from_bytes_wide(Blake2b("Halo2-Verify-Key", ...)) (verifier.rs:347-354)
+template <class Cv>
+int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
+  using Fs = typename Cv::Scalar;
+  uint32_t d[16];
+  memcpy(d, digest, 64);
+  const Fe<Fs> v = fe_from_bytes_wide<Fs>(d);
+  for (int k = 0; k < 4; k++) out[k] = (uint64_t)v.l[2 * k] | ((uint64_t)v.l[2 * k + 1] << 32);
+  return PM_OK;
+}
+
 }  // namespace pm
 
 // Explicit instantiations are visible to both compilation passes, so the
@@ -209,7 +276,8 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   extern const CurveOps name;                                                                  \
   const CurveOps name = {&msm_device_to_aff<Cv>, &point_add_impl<typename Cv::Base>,            \
                          &synth_scalars_impl<Cv>, &synth_bases_impl<Cv>,  \
-                         &accum_device_impl<Cv>, &selftest_field_impl<Cv>};
+                         &accum_device_impl<Cv>, &selftest_field_impl<Cv>,           \
+                         &transcript_device_impl<Cv>, &vk_repr_impl<Cv>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
@@ -219,5 +287,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   template int accum_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, const void*, \
                                      void*, void*);                                              \
   template int selftest_field_impl<Cv>(Ctx*, uint64_t, uint32_t, uint64_t*);                      \
+  template int transcript_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const uint64_t*, const void*, \
+                                          const void*, void*, void*);                            \
   PM_OPS_TABLE(Cv, name)                                                                       \
   }

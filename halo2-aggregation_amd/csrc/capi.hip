@@ -19,6 +19,7 @@
 #include "accum_plan.hpp"
 #include "msm_kernels.hpp"
 #include "runtime.hpp"
+#include "blake2b.hpp"
 
 using namespace pm;
 
@@ -504,6 +505,104 @@ int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B
   if (out_h_eval) HIP_TRY(hipMemcpyAsync(out_h_eval, dh, bh, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return PM_OK;
+}
+
+// ------------------------------------------------- Blake2b transcript replay
+int pm_vk_transcript_repr(int curve, const uint8_t* pinned, size_t len, uint64_t out[4]) {
+  if (!out || (len && !pinned)) return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  Blake2bHost hs(kVerifyKeyPersonal);
+  uint8_t le[8];
+  for (int i = 0; i < 8; i++) le[i] = (uint8_t)((uint64_t)len >> (8 * i));
+  hs.update(le, 8);
+  hs.update(pinned, len);
+  uint8_t d[64];
+  hs.finalize(d);
+  return ops->vk_repr(d, out);
+}
+
+int pm_transcript_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                               const uint64_t vk_repr[4], const void* d_points, const void* d_scalars,
+                               void* d_out_challenges, void* d_out_status) {
+  if (!ctx || !shape || !vk_repr || (B && (!d_points || !d_scalars || !d_out_challenges)))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  if ((rc = ops->transcript(ctx, shape, B, vk_repr, d_points, d_scalars, d_out_challenges, d_out_status))) return rc;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->end_call();
+  return PM_OK;
+}
+
+int pm_accum_batch_transcript_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                                     const uint64_t vk_repr[4], const void* d_points, const void* d_scalars,
+                                     void* d_challenges, void* d_out_quads, void* d_out_h_eval,
+                                     void* d_out_status) {
+  if (!ctx || !shape || !vk_repr || (B && (!d_points || !d_scalars || !d_challenges || !d_out_quads)))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  if ((rc = ops->transcript(ctx, shape, B, vk_repr, d_points, d_scalars, d_challenges, d_out_status))) return rc;
+  return ops->accum(ctx, shape, B, d_points, d_scalars, d_challenges, d_out_quads, d_out_h_eval);
+}
+
+// Host-buffer variants share one staging layout in acc_io:
+// points | scalars | challenges | quads | h_eval | status.
+static int transcript_host(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4],
+                           const uint64_t* points, const uint64_t* scalars, uint64_t* out_challenges,
+                           uint64_t* out_quads, uint64_t* out_h_eval, uint32_t* out_status, bool accum) {
+  if (!ctx || !shape || !vk_repr || (B && (!points || !scalars || (accum ? !out_quads : !out_challenges))))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  uint32_t npts = 0, nsc = 0, ns = 0;
+  int rc = pm_shape_layout(shape, &npts, &nsc, &ns);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (B == 0) return PM_OK;
+  if (B > (1u << 20)) return set_error(PM_ERR_UNSUPPORTED, "transcript batch larger than 2^20 proofs");
+  if ((rc = ctx->begin_call())) return rc;
+  const size_t bp = B * npts * 64, bs = B * nsc * 32, bc = B * 7 * 32, bo = B * 4 * 64, bh = B * 32, bst = B * 4;
+  if ((rc = ctx->acc_io.ensure(bp + bs + bc + bo + bh + bst))) return rc;
+  char* dp = (char*)ctx->acc_io.p;
+  char* ds = dp + bp;
+  char* dc = ds + bs;
+  char* dq = dc + bc;
+  char* dh = dq + bo;
+  char* dst = dh + bh;
+  HIP_TRY(hipMemcpyAsync(dp, points, bp, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(ds, scalars, bs, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = ops->transcript(ctx, shape, B, vk_repr, dp, ds, dc, dst))) return rc;
+  if (accum && (rc = ops->accum(ctx, shape, B, dp, ds, dc, dq, dh))) return rc;
+  if (out_challenges) HIP_TRY(hipMemcpyAsync(out_challenges, dc, bc, hipMemcpyDeviceToHost, ctx->stream));
+  if (accum) HIP_TRY(hipMemcpyAsync(out_quads, dq, bo, hipMemcpyDeviceToHost, ctx->stream));
+  if (accum && out_h_eval) HIP_TRY(hipMemcpyAsync(out_h_eval, dh, bh, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_status) HIP_TRY(hipMemcpyAsync(out_status, dst, bst, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (!accum) ctx->end_call();
+  return PM_OK;
+}
+
+int pm_transcript_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4],
+                        const uint64_t* points, const uint64_t* scalars, uint64_t* out_challenges,
+                        uint32_t* out_status) {
+  return transcript_host(ctx, curve, shape, B, vk_repr, points, scalars, out_challenges, nullptr, nullptr,
+                         out_status, false);
+}
+
+int pm_accum_batch_transcript(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                              const uint64_t vk_repr[4], const uint64_t* points, const uint64_t* scalars,
+                              uint64_t* out_challenges, uint64_t* out_quads, uint64_t* out_h_eval,
+                              uint32_t* out_status) {
+  return transcript_host(ctx, curve, shape, B, vk_repr, points, scalars, out_challenges, out_quads, out_h_eval,
+                         out_status, true);
 }
 
 }  // extern "C"

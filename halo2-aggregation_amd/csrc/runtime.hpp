@@ -84,7 +84,7 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29;
+      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // timing
@@ -96,7 +96,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29};
+            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io};
   }
   ~pm_ctx();
   int begin_call();
@@ -123,6 +123,9 @@ struct CurveOps {
   int (*accum)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const void* d_points, const void* d_scalars,
                const void* d_challenges, void* d_out_quads, void* d_out_h);
   int (*selftest_field)(Ctx* ctx, uint64_t seed, uint32_t n, uint64_t* mismatches);
+  int (*transcript)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4], const void* d_points,
+                    const void* d_scalars, void* d_challenges, void* d_status);
+  int (*vk_repr)(const uint8_t digest[64], uint64_t out[4]);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

@@ -230,6 +230,15 @@ def _load():
                             _u64p, _u64p], ctypes.c_int),
         "pm_accum_batch_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _vp, _vp, _vp,
                                    _vp, _vp], ctypes.c_int),
+        "pm_vk_transcript_repr": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, _u64p], ctypes.c_int),
+        "pm_transcript_batch": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p, _u64p,
+                                 _u64p, _u64p, _u32p], ctypes.c_int),
+        "pm_transcript_batch_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p,
+                                        _vp, _vp, _vp, _vp], ctypes.c_int),
+        "pm_accum_batch_transcript": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p,
+                                       _u64p, _u64p, _u64p, _u64p, _u64p, _u32p], ctypes.c_int),
+        "pm_accum_batch_transcript_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t,
+                                              _u64p, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -290,6 +299,14 @@ def point_add(curve, a, b):
     a, b = _as_u64(a, 8)[0].copy(), _as_u64(b, 8)[0].copy()
     out = np.zeros(8, dtype=np.uint64)
     _check(lib().pm_point_add(curve, _p(a), _p(b), _p(out)))
+    return out
+
+
+def vk_transcript_repr(curve, pinned: bytes):
+    """pm_vk_transcript_repr: the scalar the verifier absorbs first
+    (src/verifier.rs:341-358), Montgomery limbs (4,) u64.  Host only."""
+    out = np.zeros(4, dtype=np.uint64)
+    _check(lib().pm_vk_transcript_repr(curve, pinned, len(pinned), _p(out)))
     return out
 
 
@@ -405,6 +422,51 @@ class Context:
     def accum_batch_device(self, shape: ProofShape, B, d_points, d_scalars, d_challenges, d_quads, d_h=0):
         _check(lib().pm_accum_batch_device(self.h, shape.curve, ctypes.byref(shape.c), B, _vp(d_points),
                                            _vp(d_scalars), _vp(d_challenges), _vp(d_quads), _vp(d_h or None)))
+
+    def _proof_buffers(self, shape, points, scalars):
+        npts, nsc, _ = shape.layout()
+        p = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1, npts, 8)
+        s = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(p.shape[0], nsc, 4)
+        return p, s
+
+    def transcript_batch(self, shape: ProofShape, points, scalars, vk_repr):
+        """Blake2b transcript replay (pm_transcript_batch) -> (challenges
+        (B, 7, 4) Montgomery, status (B,) u32)."""
+        p, s = self._proof_buffers(shape, points, scalars)
+        B = p.shape[0]
+        vk = np.ascontiguousarray(vk_repr, dtype=np.uint64).reshape(4)
+        ch = np.zeros((B, 7, 4), dtype=np.uint64)
+        st = np.zeros(B, dtype=np.uint32)
+        _check(lib().pm_transcript_batch(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk), _p(p), _p(s),
+                                         _p(ch), st.ctypes.data_as(_u32p)))
+        return ch, st
+
+    def accum_batch_transcript(self, shape: ProofShape, points, scalars, vk_repr):
+        """Transcript replay + accumulator (pm_accum_batch_transcript) ->
+        (quads (B, 4, 8), h_eval (B, 4), challenges (B, 7, 4), status (B,))."""
+        p, s = self._proof_buffers(shape, points, scalars)
+        B = p.shape[0]
+        vk = np.ascontiguousarray(vk_repr, dtype=np.uint64).reshape(4)
+        ch = np.zeros((B, 7, 4), dtype=np.uint64)
+        quads = np.zeros((B, 4, 8), dtype=np.uint64)
+        hev = np.zeros((B, 4), dtype=np.uint64)
+        st = np.zeros(B, dtype=np.uint32)
+        _check(lib().pm_accum_batch_transcript(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk), _p(p), _p(s),
+                                               _p(ch), _p(quads), _p(hev), st.ctypes.data_as(_u32p)))
+        return quads, hev, ch, st
+
+    def transcript_batch_device(self, shape: ProofShape, B, vk_repr, d_points, d_scalars, d_challenges, d_status=0):
+        vk = np.ascontiguousarray(vk_repr, dtype=np.uint64).reshape(4)
+        _check(lib().pm_transcript_batch_device(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk),
+                                                _vp(d_points), _vp(d_scalars), _vp(d_challenges),
+                                                _vp(d_status or None)))
+
+    def accum_batch_transcript_device(self, shape: ProofShape, B, vk_repr, d_points, d_scalars, d_challenges,
+                                      d_quads, d_h=0, d_status=0):
+        vk = np.ascontiguousarray(vk_repr, dtype=np.uint64).reshape(4)
+        _check(lib().pm_accum_batch_transcript_device(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk),
+                                                      _vp(d_points), _vp(d_scalars), _vp(d_challenges),
+                                                      _vp(d_quads), _vp(d_h or None), _vp(d_status or None)))
 
     def selftest_field(self, curve, seed, n):
         m = ctypes.c_uint64(0)

@@ -75,9 +75,14 @@ def simple_example_shape(ctx, curve, log_n, seed=0x7EC):
                         **args)
 
 
+SYNTH_PINNED_VK = b"simple-example pinned verifying key (synthetic)"
+
+
 class SyntheticBatch:
     """B shape-conformant proofs resident in HBM (points [a]G on the device;
-    scalars and challenges uniform), plus output buffers."""
+    scalars uniform), plus output buffers.  With ``transcript`` (default) the
+    challenges are replayed from the Blake2b transcript on the device
+    (pm_accum_batch_transcript_device); otherwise they are drawn uniformly."""
 
     def __init__(self, ctx, shape, B, seed=0xACC, i0=0):
         import torch
@@ -90,12 +95,19 @@ class SyntheticBatch:
         self.challenges = torch.empty((B, 7, 4), dtype=torch.int64, device=dev)
         self.quads = torch.empty((B, 4, 8), dtype=torch.int64, device=dev)
         self.h_eval = torch.empty((B, 4), dtype=torch.int64, device=dev)
+        self.status = torch.empty((B,), dtype=torch.int32, device=dev)
         c = shape.curve
+        self.vk_repr = H.vk_transcript_repr(c, SYNTH_PINNED_VK)
         ctx.synth_bases(c, seed, i0 * npts, B * npts, self.points.data_ptr())
         ctx.synth_scalars(c, seed ^ 0x5CA1A, i0 * nsc, B * nsc, self.scalars.data_ptr())
         ctx.synth_scalars(c, seed ^ 0xC4A1, i0 * 7, B * 7, self.challenges.data_ptr())
         torch.cuda.synchronize()
 
-    def run(self, ctx, shape):
-        ctx.accum_batch_device(shape, self.B, self.points.data_ptr(), self.scalars.data_ptr(),
-                               self.challenges.data_ptr(), self.quads.data_ptr(), self.h_eval.data_ptr())
+    def run(self, ctx, shape, transcript=True):
+        if transcript:
+            ctx.accum_batch_transcript_device(shape, self.B, self.vk_repr, self.points.data_ptr(),
+                                              self.scalars.data_ptr(), self.challenges.data_ptr(),
+                                              self.quads.data_ptr(), self.h_eval.data_ptr(), self.status.data_ptr())
+        else:
+            ctx.accum_batch_device(shape, self.B, self.points.data_ptr(), self.scalars.data_ptr(),
+                                   self.challenges.data_ptr(), self.quads.data_ptr(), self.h_eval.data_ptr())

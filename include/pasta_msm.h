@@ -204,6 +204,46 @@ int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B
 int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_points,
                           const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval);
 
+/* ---- Blake2b transcript replay ------------------------------
+ * The verifier squeezes theta, beta, gamma, y, x, v, u from a halo2
+ * Blake2bWrite/Challenge255 transcript (TranscriptChip,
+ * /root/reference/src/transcript.rs:57-145) fed in the verifier's read order
+ * (src/verifier.rs:341-719).  These entry points replay it for B proofs at
+ * once, one GPU lane per proof, from the same points / scalars buffers
+ * pm_accum_batch reads (the W_j are not absorbed).
+ *
+ * vk_repr: the scalar the verifier absorbs first, Montgomery form; it is
+ *   pm_vk_transcript_repr() of the pinned-VK debug string (verifier.rs:341-358).
+ * out_status (may be NULL): B x uint32; bit 0 = an identity point was
+ *   skipped (TranscriptChip::common_point rejects the identity before hashing,
+ *   transcript.rs:101-110).  Such a proof's challenges differ from an honest
+ *   prover's; the caller should reject it. */
+#define PM_TRANSCRIPT_IDENTITY_SKIPPED 1u
+
+/* vk_repr = from_bytes_wide(Blake2b-512(personal "Halo2-Verify-Key",
+ *   le_u64(len) || pinned[0..len))) in Montgomery form (verifier.rs:341-358).
+ *   Host only; needs no device. */
+int pm_vk_transcript_repr(int curve, const uint8_t* pinned, size_t len, uint64_t out[4]);
+/* out_challenges: B x 7 x 4 (theta, beta, gamma, y, x, v, u), Montgomery. */
+int pm_transcript_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4],
+                        const uint64_t* points, const uint64_t* scalars, uint64_t* out_challenges,
+                        uint32_t* out_status);
+int pm_transcript_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                               const uint64_t vk_repr[4], const void* d_points, const void* d_scalars,
+                               void* d_out_challenges, void* d_out_status);
+/* Transcript replay + accumulator in one call (challenges stay on the
+ * device).  out_challenges, out_h_eval and out_status may be NULL. */
+int pm_accum_batch_transcript(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                              const uint64_t vk_repr[4], const uint64_t* points, const uint64_t* scalars,
+                              uint64_t* out_challenges, uint64_t* out_quads, uint64_t* out_h_eval,
+                              uint32_t* out_status);
+/* Device-buffer variant; d_challenges is caller-provided B x 7 x 4 scratch
+ * (it receives the replayed challenges). */
+int pm_accum_batch_transcript_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                                     const uint64_t vk_repr[4], const void* d_points, const void* d_scalars,
+                                     void* d_challenges, void* d_out_quads, void* d_out_h_eval,
+                                     void* d_out_status);
+
 #ifdef __cplusplus
 }
 #endif

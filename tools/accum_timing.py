@@ -12,7 +12,7 @@ import torch  # noqa: E402
 import accum_util as U  # noqa: E402
 import halo2_amd as H  # noqa: E402
 
-KERNELS = ["acc_scalars", "acc_termmul", "acc_sum"]
+KERNELS = ["transcript", "acc_scalars", "acc_termmul", "acc_sum"]
 
 
 def main():
@@ -32,8 +32,16 @@ def main():
         dq = torch.empty((B, 4, 8), dtype=torch.int64, device=dev)
         dh = torch.empty((B, 4), dtype=torch.int64, device=dev)
 
+        fused = os.environ.get("TRANSCRIPT", "1") == "1"
+        vk = U.np.array([1, 2, 3, 4], dtype=U.np.uint64)
+
         def run():
-            ctx.accum_batch_device(ps, B, pts.data_ptr(), scs.data_ptr(), chs.data_ptr(), dq.data_ptr(), dh.data_ptr())
+            if fused:   # challenges replayed from the Blake2b transcript on the device
+                ctx.accum_batch_transcript_device(ps, B, vk, pts.data_ptr(), scs.data_ptr(), chs.data_ptr(),
+                                                  dq.data_ptr(), dh.data_ptr())
+            else:
+                ctx.accum_batch_device(ps, B, pts.data_ptr(), scs.data_ptr(), chs.data_ptr(), dq.data_ptr(),
+                                       dh.data_ptr())
 
         run()
         reps = 5
@@ -47,7 +55,7 @@ def main():
             run()
         ctx.set_timing(False)
         ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}
-        print(json.dumps({"shape": shape, "log_n": log_n, "B": B, "wall_ms": round(wall * 1e3, 3),
+        print(json.dumps({"transcript": fused, "shape": shape, "log_n": log_n, "B": B, "wall_ms": round(wall * 1e3, 3),
                           "proofs_per_s": round(B / wall, 1), "kernels_ms": ks}), flush=True)
 
 
