@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--window", type=int, default=0, help="force window width c (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--fixed", type=int, default=1, help="also time the fixed-base MSM (1) or skip it (0)")
     ap.add_argument("--accum-batch", type=int, default=256, help="proofs per GPU for the accumulator leg (0 = skip)")
     ap.add_argument("--accum-logn", type=int, default=17)
     return ap.parse_args()
@@ -137,6 +138,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    fixed = run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, result) if args.fixed else None
     accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
 
     if rank == 0:
@@ -177,6 +179,8 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(d_s, d_b, n, result, args.cpu_seconds)
+        if fixed is not None:
+            out["fixed_base"] = fixed
         if accum is not None:
             if world == 1 and not args.no_cpu:
                 accum["cpu_baseline"] = accum_cpu_baseline(*accum.pop("_state"), budget_s=8.0)
@@ -186,6 +190,55 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, want):
+    """Fixed-base MSM over the same scalars and bases: the
+    SRS table [2^{o_w}] P_i is built once (untimed, reported as build_ms),
+    then each step is pm_msm_fixed_device + the same all-gather / fold."""
+    import numpy as np
+    import torch
+
+    from sharded import combine_partials
+
+    t0 = time.perf_counter()
+    fb = ctx.fixed_bases(0, d_bases=d_b.data_ptr(), n=n)
+    build_ms = (time.perf_counter() - t0) * 1e3
+
+    def step():
+        part = fb.msm_device(d_s.data_ptr(), n)
+        return combine_partials(part, dist, dev, padd, world, gathered)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(True)
+    ctx.reset_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4)
+               for k in ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg",
+                         "bucket_bits", "host_tail"]}
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    out = {"metric": f"Pallas fixed-base MSM Mscalar/s at 2^{args.logn} (precomputed SRS table)",
+           "value": round(world * n / (elapsed / args.steps) / 1e6, 3), "unit": "Mscalar/s",
+           "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "c": fb.c, "windows": fb.windows,
+           "table_GiB_per_gpu": round(fb.table_bytes / 2**30, 3), "build_ms": round(build_ms, 2),
+           "matches_variable_base": bool(np.array_equal(np.asarray(got), np.asarray(want))),
+           "kernels_ms": kernels}
+    fb.release()
+    return out
 
 
 def run_accumulator(args, ctx, dist, dev, rank, world):

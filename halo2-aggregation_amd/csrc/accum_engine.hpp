@@ -277,7 +277,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
   const CurveOps name = {&msm_device_to_aff<Cv>, &point_add_impl<typename Cv::Base>,            \
                          &synth_scalars_impl<Cv>, &synth_bases_impl<Cv>,  \
                          &accum_device_impl<Cv>, &selftest_field_impl<Cv>,           \
-                         &transcript_device_impl<Cv>, &vk_repr_impl<Cv>};
+                         &transcript_device_impl<Cv>, &vk_repr_impl<Cv>,                   \
+                         &fixed_table_impl<Cv>, &msm_fixed_to_aff<Cv>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
@@ -287,6 +288,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
   template int accum_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, const void*, \
                                      void*, void*);                                              \
   template int selftest_field_impl<Cv>(Ctx*, uint64_t, uint32_t, uint64_t*);                      \
+  template int fixed_table_impl<Cv>(Ctx*, const void*, pm_fixed_bases*);                          \
+  template int msm_fixed_to_aff<Cv>(Ctx*, const pm_fixed_bases*, const void*, size_t, uint32_t, uint64_t*); \
   template int transcript_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const uint64_t*, const void*, \
                                           const void*, void*, void*);                            \
   PM_OPS_TABLE(Cv, name)                                                                       \

@@ -323,14 +323,6 @@ __device__ __forceinline__ void glv_split(const Fe<typename Cv::Scalar>& k, uint
   n2 = mp_abs6(k2);
 }
 
-// affine (R261) of an XYZZ point that is not the identity
-template <class F>
-__device__ __forceinline__ void xyzz29_to_aff(const Xyzz29<F>& p, F29<F>& x, F29<F>& y) {
-  const F29<F> inv = f29_inv<F>(f29_mul_c<F>(p.ZZ, p.ZZZ));  // 1 / (ZZ ZZZ)
-  x = f29_canon<F>(f29_mul_c<F>(p.X, f29_mul_c<F>(inv, p.ZZZ)));
-  y = f29_canon<F>(f29_mul_c<F>(p.Y, f29_mul_c<F>(inv, p.ZZ)));
-}
-
 // [k]P by GLV + Shamir on the radix-2^29 arithmetic: one 130-step joint
 // double-and-add over (k1, k2) with the canonical affine table {P1, P2,
 // P1 + P2} (P1 = +-P, P2 = +-phi(P)); P1 + P2 costs one inversion.  Every

@@ -161,6 +161,19 @@ MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk) 
   return pl;
 }
 
+MsmPlan make_plan_fixed(size_t npad, int c, int min_chunk) {
+  MsmPlan pl = make_plan(npad, c, 1, min_chunk);
+  pl.G = 1;
+  pl.wpg = pl.W;
+  const size_t work = npad * pl.W;  // every window's entries in one bucket set
+  const size_t target = 256 * 1024;
+  const size_t mc = min_chunk > 0 ? (size_t)min_chunk : 16;
+  pl.chunk = (uint32_t)std::max<size_t>(mc, (work + target - 1) / target);
+  pl.nthreads = (uint32_t)((work + pl.chunk - 1) / pl.chunk);
+  pl.maxlong = (uint32_t)(work / ((size_t)kMaxChain * pl.chunk) + 1);
+  return pl;
+}
+
 }  // namespace pm
 
 namespace {
@@ -411,6 +424,93 @@ int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
   HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
   return dispatch_msm_device(ctx, b->curve, ctx->in_scalars.p, (const char*)b->d + offset * 64, n, flags, out);
+}
+
+// ------------------------------------------------- fixed-base MSM (§8f-3)
+static int fixed_create(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, int c,
+                        pm_fixed_bases** out) {
+  if (!ctx || !out || (n && !bases)) return set_error(PM_ERR_ARG, "null argument");
+  *out = nullptr;
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  if (n == 0) return set_error(PM_ERR_ARG, "empty base set");
+  if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "more than 2^26 fixed bases");
+  if (c == 0) c = kAutoFixedC;
+  if (c < kMinC || c > kFixedMaxC) return set_error(PM_ERR_ARG, "fixed-base window out of range");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  std::unique_ptr<pm_fixed_bases> ft(new pm_fixed_bases{curve, ctx->device, c, 0, n, 0, nullptr});
+  const void* d = bases;
+  if (host) {
+    if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->in_bases.p, bases, n * 64, hipMemcpyHostToDevice, ctx->stream));
+    d = ctx->in_bases.p;
+  }
+  if ((rc = ops->fixed_table(ctx, d, ft.get()))) {
+    if (ft->d) (void)hipFree(ft->d);
+    return rc;
+  }
+  *out = ft.release();
+  return PM_OK;
+}
+
+int pm_fixed_bases_create(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, int c, pm_fixed_bases** out) {
+  return fixed_create(ctx, curve, bases, true, n, c, out);
+}
+
+int pm_fixed_bases_create_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, int c,
+                                 pm_fixed_bases** out) {
+  return fixed_create(ctx, curve, d_bases, false, n, c, out);
+}
+
+int pm_fixed_bases_info(const pm_fixed_bases* fb, size_t* n, int* c, int* windows, size_t* table_bytes) {
+  if (!fb) return set_error(PM_ERR_ARG, "null argument");
+  if (n) *n = fb->n;
+  if (c) *c = fb->c;
+  if (windows) *windows = fb->W;
+  if (table_bytes) *table_bytes = (size_t)fb->W * fb->npad * 64;
+  return PM_OK;
+}
+
+int pm_fixed_bases_release(pm_fixed_bases* fb) {
+  if (!fb) return PM_OK;
+  (void)hipSetDevice(fb->device);
+  (void)hipFree(fb->d);
+  delete fb;
+  return PM_OK;
+}
+
+int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_scalars, size_t n, uint32_t flags,
+                        uint64_t out[8]) {
+  if (!ctx || !fb || !out || (n && !d_scalars)) return set_error(PM_ERR_ARG, "null argument");
+  if (fb->device != ctx->device) return set_error(PM_ERR_ARG, "fixed bases live on another device");
+  if (n > fb->n) return set_error(PM_ERR_ARG, "more scalars than fixed bases");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return curve_ops(fb->curve)->msm_fixed(ctx, fb, d_scalars, n, flags, out);
+}
+
+int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars, size_t n, uint32_t flags,
+                 uint64_t out[8]) {
+  if (!ctx || !fb || !out || (n && !scalars)) return set_error(PM_ERR_ARG, "null argument");
+  if (fb->device != ctx->device) return set_error(PM_ERR_ARG, "fixed bases live on another device");
+  if (n > fb->n) return set_error(PM_ERR_ARG, "more scalars than fixed bases");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  return curve_ops(fb->curve)->msm_fixed(ctx, fb, ctx->in_scalars.p, n, flags, out);
 }
 
 int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {

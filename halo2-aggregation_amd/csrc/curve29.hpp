@@ -153,4 +153,12 @@ __device__ __forceinline__ F29<F> f29_neg_canon(const F29<F>& y) {
   return f29_norm<F>(f29_sub<F>(f29_zero<F>(), y, F29Consts<F>::K2));
 }
 
+// affine (R261) of an XYZZ point that is not the identity
+template <class F>
+__device__ __forceinline__ void xyzz29_to_aff(const Xyzz29<F>& p, F29<F>& x, F29<F>& y) {
+  const F29<F> inv = f29_inv<F>(f29_mul_c<F>(p.ZZ, p.ZZZ));  // 1 / (ZZ ZZZ)
+  x = f29_canon<F>(f29_mul_c<F>(p.X, f29_mul_c<F>(inv, p.ZZZ)));
+  y = f29_canon<F>(f29_mul_c<F>(p.Y, f29_mul_c<F>(inv, p.ZZ)));
+}
+
 }  // namespace pm

@@ -39,25 +39,24 @@ namespace pm {
 // ---------------------------------------------------------- MSM pipeline
 
 template <class Fs, int W>
-void launch_sort_w(bool coarse, bool wide, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g,
-                   uint32_t* bh, const uint32_t* bofs, void* digits, void* mid, hipStream_t st) {
-  if (!coarse) {
-    const size_t lds = (size_t)W * g.NCB * 4;
-    if (d16)
-      k_sort_hist<Fs, W, true><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint16_t*)digits, bh);
-    else
-      k_sort_hist<Fs, W, false><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint32_t*)digits, bh);
-    return;
-  }
+void launch_sort_w(bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* bh,
+                   void* digits, uint32_t stride, uint32_t merged, hipStream_t st) {
+  const size_t lds = (size_t)W * g.NCB * 4;
+  if (d16)
+    k_sort_hist<Fs, W, true><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint16_t*)digits, bh, stride,
+                                                                merged);
+  else
+    k_sort_hist<Fs, W, false><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint32_t*)digits, bh, stride,
+                                                                 merged);
 }
 
 // one instance per window count reachable from c in [kMinC, kMaxC]
 template <class Fs>
-int launch_sort(int W, bool coarse, bool wide, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical,
-                SortGeom g, uint32_t* bh, const uint32_t* bofs, void* digits, void* mid, hipStream_t st) {
+int launch_sort(int W, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* bh,
+                void* digits, uint32_t stride, uint32_t merged, hipStream_t st) {
   switch (W) {
 #define PM_W(k) \
-  case k: launch_sort_w<Fs, k>(coarse, wide, d16, s, n, canonical, g, bh, bofs, digits, mid, st); return PM_OK;
+  case k: launch_sort_w<Fs, k>(d16, s, n, canonical, g, bh, digits, stride, merged, st); return PM_OK;
     PM_W(13) PM_W(14) PM_W(15) PM_W(16) PM_W(18) PM_W(19) PM_W(20) PM_W(22) PM_W(24) PM_W(26) PM_W(29)
     PM_W(32) PM_W(37) PM_W(43) PM_W(52) PM_W(64)
 #undef PM_W
@@ -74,9 +73,16 @@ int launch_sort(int W, bool coarse, bool wide, bool d16, const uint32_t* s, uint
 // GPU works on the lower groups (window w's terms sit at bit positions
 // [o_w, o_w + cmax), so a group's positions are final once every group above
 // it has arrived).
+//
+// Fixed-base mode (ft != nullptr, pm_msm_fixed): the bases are a precomputed
+// table ft->d with entry w * npad + i = [2^{o_w}] P_i (k_fixed_table), so the
+// digits of all W windows index ONE bucket set: the sort runs over the W * npad
+// entries as a single window (merged histogram rows), and the bucket
+// reduction and host tail handle one window at offset 0 -- no per-window
+// reduction and no cross-window doublings.
 template <class Cv>
 int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases, size_t n, uint32_t flags,
-                    Xyzz<typename Cv::Base>* result) {
+                    Xyzz<typename Cv::Base>* result, const pm_fixed_bases* ft = nullptr) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   if (n == 0) {
@@ -84,18 +90,26 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     return PM_OK;
   }
   if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "n exceeds 2^26 points per device call");
-  const MsmPlan pl = make_plan(n, ctx->window_c, ctx->groups, ctx->min_chunk);
+  const bool fixed = ft != nullptr;
+  const MsmPlan pl = fixed ? make_plan_fixed(ft->npad, ft->c, ctx->min_chunk)
+                           : make_plan(n, ctx->window_c, ctx->groups, ctx->min_chunk);
   const hipStream_t st = ctx->stream, st2 = ctx->red_stream;
-  const size_t TOT = (size_t)pl.W * pl.NB + 1;
-  const size_t nW = (size_t)n * pl.W;
-  // 4-B coarse entries when the point index fits beside the fine bits and the sign
+  const int Wr = fixed ? 1 : pl.W;                  // bucket sets (reduced windows)
+  const int wpg = fixed ? 1 : pl.wpg;
+  const size_t stride = fixed ? ft->npad : n;       // digit row length
+  const size_t E = fixed ? (size_t)pl.W * stride : n;  // entries of one sort row
+  const size_t TOT = (size_t)Wr * pl.NB + 1;
+  const size_t nW = (size_t)stride * pl.W;
   const int NJ = pl.NB2 + kTJobs;
-  SortGeom g;
+  SortGeom g;  // histogram geometry (blocks of scalars)
   g.FB = std::max(0, pl.cmax - 1 - 8);
   g.NCB = (pl.K >> g.FB) + 1;
-  g.nblk = (int)((n + kSortB - 1) / kSortB);
+  g.nblk = (int)((stride + kSortB - 1) / kSortB);
+  SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
+  if (fixed) gm.nblk = g.nblk * pl.W;
   const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
-  const bool wide = n > (size_t(1) << (31 - g.FB));
+  // 4-B coarse entries when the entry index fits beside the fine bits and the sign
+  const bool wide = E > (size_t(1) << (31 - g.FB));
   const bool d16 = pl.cmax <= 16;
   const size_t longs_stride = 16 + (size_t)pl.maxlong * sizeof(LongChain);
   int rc;
@@ -107,13 +121,13 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->offsets.ensure(TOT * 4))) return rc;
   const uint32_t nb = (uint32_t)((TOTB + kScanChunk - 1) / kScanChunk);
   if ((rc = ctx->bsum.ensure((size_t)nb * 4))) return rc;
-  if ((rc = ctx->buckets.ensure((size_t)pl.W * pl.NB * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->buckets.ensure((size_t)Wr * pl.NB * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->head.ensure((size_t)pl.G * pl.nthreads * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->segS.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->segT.ensure((size_t)pl.W * pl.M1 * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->bits.ensure((size_t)pl.W * NJ * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->segS.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->segT.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->bits.ensure((size_t)Wr * NJ * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->longs.ensure((size_t)pl.G * longs_stride))) return rc;
-  const size_t nG = (size_t)pl.W * NJ;
+  const size_t nG = (size_t)Wr * NJ;
   if ((rc = ctx->ensure_pinned(nG * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->ensure_group_events(2 * pl.G))) return rc;
 
@@ -133,8 +147,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   HIP_TRY(hipMemsetAsync(bh + (TOTB - 1), 0, 4, st));
   for (int gi = 0; gi < pl.G; gi++) HIP_TRY(hipMemsetAsync((char*)ctx->longs.p + gi * longs_stride, 0, 16, st));
   const uint32_t canon = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
-  PM_LAUNCH(ctx, "sort_hist",
-            rc = launch_sort<Fs>(pl.W, false, wide, d16, d_scalars, un, canon, g, bh, bofs, ctx->digits.p, mid, st));
+  PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, bh, ctx->digits.p,
+                                                   (uint32_t)stride, fixed ? 1u : 0u, st));
   if (rc) return rc;
   PM_LAUNCH(ctx, "scan", {
     k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum);
@@ -143,41 +157,59 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   });
   {
     const size_t lds = (size_t)kSortB * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
-    const dim3 grid(g.nblk, pl.W);
+    const dim3 grid(gm.nblk, Wr);
     void* dg = ctx->digits.p;
+    const uint32_t ue = (uint32_t)E;
     if (d16 && !wide)
       PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<true, false><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint16_t*)dg, un, g, bofs, (uint32_t*)mid)));
+                                        (const uint16_t*)dg, ue, gm, bofs, (uint32_t*)mid)));
     else if (d16)
       PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<true, true><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint16_t*)dg, un, g, bofs, (uint64_t*)mid)));
+                                        (const uint16_t*)dg, ue, gm, bofs, (uint64_t*)mid)));
     else if (!wide)
       PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<false, false><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint32_t*)dg, un, g, bofs, (uint32_t*)mid)));
+                                        (const uint32_t*)dg, ue, gm, bofs, (uint32_t*)mid)));
     else
       PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<false, true><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint32_t*)dg, un, g, bofs, (uint64_t*)mid)));
+                                        (const uint32_t*)dg, ue, gm, bofs, (uint64_t*)mid)));
   }
   // LDS cache: room for 1.5x the mean segment (random digits fill segments
   // evenly; a skewed segment falls back to re-reading mid), capped at 64 KiB
   const size_t esz = wide ? 8 : 4;
-  const size_t mean_seg = (size_t)n / std::max(1, g.NCB - 1) + 1;
+  const size_t mean_seg = E / std::max(1, g.NCB - 1) + 1;
   const uint32_t cache_n = (uint32_t)std::min<size_t>(kFineCacheBytes / esz, (mean_seg * 3 / 2 + 63) & ~size_t(63));
   const size_t lds_fine = (size_t)cache_n * esz + ((size_t)(1 << g.FB) + kFineThreads / 64 + 1) * 4;
   if (wide)
-    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<true><<<pl.W * g.NCB, kFineThreads, lds_fine, st>>>(
-                                    (const uint64_t*)mid, bofs, g, pl.W, pl.NB, cache_n, offsets, sorted)));
+    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<true><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
+                                    (const uint64_t*)mid, bofs, gm, Wr, pl.NB, cache_n, offsets, sorted)));
   else
-    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<false><<<pl.W * g.NCB, kFineThreads, lds_fine, st>>>(
-                                    (const uint32_t*)mid, bofs, g, pl.W, pl.NB, cache_n, offsets, sorted)));
+    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<false><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
+                                    (const uint32_t*)mid, bofs, gm, Wr, pl.NB, cache_n, offsets, sorted)));
   const bool prefetch = ctx->prefetch >= 0 ? ctx->prefetch != 0 : (size_t)n * 64 > kPrefetchBytes;
-  if ((rc = ctx->bases29.ensure((size_t)n * 64))) return rc;
-  const uint32_t* bases29 = (const uint32_t*)ctx->bases29.p;
-  PM_LAUNCH(ctx, "bases_r261",
-            (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
+  const uint32_t* bases29;
+  if (fixed) {
+    bases29 = (const uint32_t*)ft->d;
+  } else {
+    if ((rc = ctx->bases29.ensure((size_t)n * 64))) return rc;
+    bases29 = (const uint32_t*)ctx->bases29.p;
+    PM_LAUNCH(ctx, "bases_r261",
+              (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
+  }
   const unsigned ablocks = (pl.nthreads + 255) / 256;
+  // bit sums of few windows (fixed-base: one) are split over more blocks
+  const int nsplit = std::max(1, std::min(kMaxSplit, 16 / wpg));
+  Xyzz<F>* bitsP = nullptr;
+  uint32_t* tickets = nullptr;
+  if (nsplit > 1) {
+    if ((rc = ctx->bitsP.ensure((size_t)Wr * NJ * nsplit * sizeof(Xyzz<F>)))) return rc;
+    const size_t old_cap = ctx->tickets.cap;  // tickets are self-resetting; zero fresh allocations
+    if ((rc = ctx->tickets.ensure((size_t)Wr * NJ * 4))) return rc;
+    if (ctx->tickets.cap != old_cap) HIP_TRY(hipMemsetAsync(ctx->tickets.p, 0, ctx->tickets.cap, st2));
+    bitsP = (Xyzz<F>*)ctx->bitsP.p;
+    tickets = (uint32_t*)ctx->tickets.p;
+  }
   for (int gi = pl.G - 1; gi >= 0; gi--) {
-    const int w0 = gi * pl.wpg, w1 = std::min(pl.W, w0 + pl.wpg), nw = w1 - w0;
+    const int w0 = gi * wpg, w1 = std::min(Wr, w0 + wpg), nw = w1 - w0;
     const uint32_t s0 = (uint32_t)((size_t)w0 * pl.NB), s1 = (uint32_t)((size_t)w1 * pl.NB);
     Xyzz<F>* hg = head + (size_t)gi * pl.nthreads;
     uint32_t* nlong = (uint32_t*)((char*)ctx->longs.p + gi * longs_stride);
@@ -191,14 +223,20 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi], st));
     HIP_TRY(hipStreamWaitEvent(st2, ctx->grp_ev[2 * gi], 0));
     PM_LAUNCH_ST(ctx, st2, "fixup", {
-      k_fixup<F><<<ablocks, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg, longs, nlong);
+      if (fixed)  // merged buckets span ~W*n/2^(c-1)/chunk slices each: one lane per bucket
+        k_fixup<F><<<(s1 - s0 + 255) / 256, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg,
+                                                           longs, nlong);
+      else
+        k_fixup_slice<F><<<ablocks, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg, longs,
+                                                   nlong);
       k_fixup_long<F><<<pl.maxlong, 256, 0, st2>>>(longs, nlong, buckets, hg);
     });
     PM_LAUNCH_ST(ctx, st2, "bucket_seg",
                  (k_bucket_seg<F><<<(nw * pl.M1 + 255) / 256, 256, 0, st2>>>(offsets, buckets, w0, nw, pl.NB, pl.L1,
                                                                                S, T)));
     PM_LAUNCH_ST(ctx, st2, "bucket_bits",
-                 (k_bucket_bits<F><<<dim3(NJ, nw), kRedThreads, 0, st2>>>(S, T, w0, pl.M1, pl.NB2, G)));
+                 (k_bucket_bits<F><<<dim3(NJ, nw, nsplit), kRedThreads, 0, st2>>>(S, T, w0, pl.M1, pl.NB2, G, nsplit,
+                                                                                      bitsP, tickets)));
     HIP_TRY(hipMemcpyAsync((Xyzz<F>*)ctx->h_pinned + (size_t)w0 * NJ, G + (size_t)w0 * NJ,
                            (size_t)nw * NJ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st2));
     HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi + 1], st2));
@@ -210,13 +248,13 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   std::vector<std::vector<int>> at(256 + NJ + pl.log2L1 + 1);
   std::vector<int> gmax(pl.G, -1);  // highest position of any term of group g
   int qmax = 0;
-  for (int w = 0; w < pl.W; w++) {
-    const int o = w * pl.base + std::min(w, pl.extra);
+  for (int w = 0; w < Wr; w++) {
+    const int o = fixed ? 0 : w * pl.base + std::min(w, pl.extra);
     for (int b = 0; b < NJ; b++) {
       const int q = b < pl.NB2 ? o + b + pl.log2L1 : o;
       at[q].push_back(w * NJ + b);
       qmax = std::max(qmax, q);
-      gmax[w / pl.wpg] = std::max(gmax[w / pl.wpg], q);
+      gmax[w / wpg] = std::max(gmax[w / wpg], q);
     }
   }
   host::Pt<F> hacc = host::inf<F>();
@@ -269,6 +307,33 @@ int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint
   using F = typename Cv::Base;
   Xyzz<F> r;
   int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, (const uint32_t*)d_b, n, flags, &r);
+  if (rc) return rc;
+  aff_to_u64<F>(xyzz_to_aff<F>(r), out);
+  return PM_OK;
+}
+
+// Build a fixed-base table (pm_fixed_bases_create): ft->n, ft->c set by the
+// caller; fills W, npad and the device table.
+template <class Cv>
+int fixed_table_impl(Ctx* ctx, const void* d_bases, pm_fixed_bases* ft) {
+  using F = typename Cv::Base;
+  const MsmPlan pl = make_plan_fixed(kSortB, ft->c);
+  ft->W = pl.W;
+  ft->npad = std::max<size_t>(kSortB, (ft->n + kSortB - 1) / kSortB * kSortB);
+  const size_t bytes = (size_t)pl.W * ft->npad * 64;
+  HIP_TRY(hipMalloc(&ft->d, bytes));
+  k_fixed_table<F><<<(unsigned)((ft->npad + 255) / 256), 256, 0, ctx->stream>>>(
+      (const uint32_t*)d_bases, (uint32_t)ft->n, (uint32_t)ft->npad, pl.W, pl.base, pl.extra, (uint32_t*)ft->d);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return PM_OK;
+}
+
+template <class Cv>
+int msm_fixed_to_aff(Ctx* ctx, const pm_fixed_bases* ft, const void* d_s, size_t n, uint32_t flags, uint64_t out[8]) {
+  using F = typename Cv::Base;
+  Xyzz<F> r;
+  int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, nullptr, n, flags, &r, ft);
   if (rc) return rc;
   aff_to_u64<F>(xyzz_to_aff<F>(r), out);
   return PM_OK;

@@ -257,29 +257,43 @@ struct DigitCode<false> {
   static __device__ __forceinline__ uint32_t dec(T v) { return v; }
 };
 
+// stride: digit row length (n, or the fixed-base table's padded length with
+// zero codes written for i in [n, stride)); merged: histogram rows laid out
+// (coarse bin, window, block) so the windows share one bucket set
+// (fixed-base MSM: entry w * stride + i is table point [2^{o_w}] P_i).
 template <class Fs, int W, bool D16>
 __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __restrict__ scalars, uint32_t n,
                                                             uint32_t canonical, SortGeom g,
                                                             typename DigitCode<D16>::T* __restrict__ digits,
-                                                            uint32_t* __restrict__ bh) {
+                                                            uint32_t* __restrict__ bh, uint32_t stride,
+                                                            uint32_t merged) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
   const int nbins = W * g.NCB;
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
   __syncthreads();
   for (int r = 0; r < kSortPerThread; r++) {
     const uint32_t i = blockIdx.x * kSortB + r * kSortThreads + threadIdx.x;
-    if (i >= n) break;
+    if (i >= stride) break;
+    if (i >= n) {
+#pragma unroll
+      for (int w = 0; w < W; w++) digits[(size_t)w * stride + i] = DigitCode<D16>::enc(0u);
+      continue;
+    }
     const Fe<Fs> s = load_canonical<Fs>(scalars, i, canonical);
     uint32_t carry = 0;
 #pragma unroll
     for (int w = 0; w < W; w++) {
       const uint32_t code = signed_digit<W, Fs>(s, w, carry);
-      digits[(size_t)w * n + i] = DigitCode<D16>::enc(code);
+      digits[(size_t)w * stride + i] = DigitCode<D16>::enc(code);
       if (code) atomicAdd(&hist[w * g.NCB + ((code & ~kNegBit) >> g.FB)], 1u);
     }
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < nbins; k += kSortThreads) bh[(size_t)k * g.nblk + blockIdx.x] = hist[k];
+  for (int k = threadIdx.x; k < nbins; k += kSortThreads) {
+    const uint32_t w = k / g.NCB, cb = k - w * g.NCB;
+    const size_t row = merged ? (size_t)cb * W + w : (size_t)k;
+    bh[row * g.nblk + blockIdx.x] = hist[k];
+  }
 }
 
 // coarse-segment entry: WIDE = slot << 32 | index | sign << 31;
@@ -507,6 +521,56 @@ __global__ void __launch_bounds__(256) k_bases_to_r261(const uint32_t* __restric
   }
 }
 
+// Fixed-base table (pm_fixed_bases_create): entry (w, i) at w * npad + i is
+// [2^{o_w}] P_i as a canonical affine point in the pipeline's R = 2^261 form,
+// o_w the bit offset of window w (WinGeom).  One lane per base: repeated
+// XYZZ doublings, one Fermat inversion per window.  Identity bases and the
+// padding rows [n, npad) stay (0, 0), which k_accumulate skips.
+template <class F>
+__global__ void __launch_bounds__(256) k_fixed_table(const uint32_t* __restrict__ in, uint32_t n, uint32_t npad,
+                                                     int W, int base, int extra, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npad) return;
+  F29<F> x = f29_zero<F>(), y = f29_zero<F>();
+  bool ident = true;
+  if (i < n) {
+    const uint4* q = reinterpret_cast<const uint4*>(in + 16ull * i);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+    uint32_t z = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) z |= wx[k] | wy[k];
+    ident = z == 0;
+    if (!ident) {
+      x = f29_canon<F>(f29_from_r256<F>(wx));
+      y = f29_canon<F>(f29_from_r256<F>(wy));
+    }
+  }
+  uint4* o = reinterpret_cast<uint4*>(out + 16ull * i);
+  st29<F>(o, x);
+  st29<F>(o + 2, y);
+  if (ident) {
+    for (int w = 1; w < W; w++) {
+      uint4* ow = reinterpret_cast<uint4*>(out + 16ull * ((size_t)w * npad + i));
+      st29<F>(ow, x);
+      st29<F>(ow + 2, y);
+    }
+    return;
+  }
+  bool acc_inf = true;
+  Xyzz29<F> acc = xyzz29_madd<F>(xyzz29_inf<F>(), x, y, acc_inf);
+  for (int w = 1; w < W; w++) {
+    const int steps = base + (w - 1 < extra ? 1 : 0);
+    for (int k = 0; k < steps; k++) acc = xyzz29_dbl<F>(acc);  // P has odd prime order: never the identity
+    F29<F> ax, ay;
+    xyzz29_to_aff<F>(acc, ax, ay);
+    uint4* ow = reinterpret_cast<uint4*>(out + 16ull * ((size_t)w * npad + i));
+    st29<F>(ow, ax);
+    st29<F>(ow + 2, ay);
+  }
+}
+
 // --------------------------------------------------------------- 5. fixup
 // The owner of a bucket that runs past its slice adds the head partials of
 // the following slices.  Chains up to kMaxChain are walked serially; longer
@@ -517,13 +581,16 @@ struct LongChain {
   uint32_t gb, t_first, t_last;
 };
 
+// One lane per accumulate slice t: the slice holding the end of a bucket's
+// first partial walks the following slices' head partials (variable-base
+// MSM: buckets average ~2 slices or fewer, so chains are short and rare).
 template <class F>
-__global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
-                                               uint32_t chunk, uint32_t nthreads,
-                                               Xyzz<F>* __restrict__ buckets,
-                                               const Xyzz<F>* __restrict__ head,
-                                               LongChain* __restrict__ longs,
-                                               uint32_t* __restrict__ nlong) {
+__global__ void __launch_bounds__(256) k_fixup_slice(const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
+                                                     uint32_t chunk, uint32_t nthreads,
+                                                     Xyzz<F>* __restrict__ buckets,
+                                                     const Xyzz<F>* __restrict__ head,
+                                                     LongChain* __restrict__ longs,
+                                                     uint32_t* __restrict__ nlong) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nthreads) return;
   const uint32_t base = offsets[s0], total = offsets[s1];
@@ -541,6 +608,36 @@ __global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offs
   }
   Xyzz29<F> acc = load_xyzz29<F>(&buckets[gb]);
   for (uint32_t t2 = t + 1; t2 <= t_last; t2++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
+  store_xyzz29<F>(&buckets[gb], acc);
+}
+
+// One lane per bucket gb in [s0, s1): a bucket whose sorted run crosses
+// slice boundaries was started by slice t_first (which stored its partial in
+// buckets[gb]); every later slice it reaches stored its first partial in
+// head[].  Bucket-parallel, so the lanes that walk a chain are dense even
+// when every bucket spans several slices (fixed-base MSM: ~8 per bucket).
+template <class F>
+__global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
+                                               uint32_t chunk, uint32_t nthreads,
+                                               Xyzz<F>* __restrict__ buckets,
+                                               const Xyzz<F>* __restrict__ head,
+                                               LongChain* __restrict__ longs,
+                                               uint32_t* __restrict__ nlong) {
+  const uint32_t gb = s0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (gb >= s1) return;
+  const uint32_t base = offsets[s0];
+  const uint32_t bstart = offsets[gb], bend = offsets[gb + 1];
+  if (bstart == bend) return;
+  const uint32_t t_first = (bstart - base) / chunk;
+  const uint32_t t_last = min((bend - 1 - base) / chunk, nthreads - 1);
+  if (t_last == t_first) return;
+  if (t_last - t_first > kMaxChain) {
+    const uint32_t k = atomicAdd(nlong, 1u);
+    longs[k] = LongChain{gb, t_first + 1, t_last};
+    return;
+  }
+  Xyzz29<F> acc = load_xyzz29<F>(&buckets[gb]);
+  for (uint32_t t2 = t_first + 1; t2 <= t_last; t2++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
   store_xyzz29<F>(&buckets[gb], acc);
 }
 
@@ -593,23 +690,30 @@ __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------ 7. bit sums
-// block (job, w - w0): job < NB2 -> G_job = sum_{j : (j >> job) & 1} S_j (only
-// the j with that bit set are enumerated, so no lane idles); job >= NB2 ->
-// partial sum of T_j over part (job - NB2) of kTJobs equal ranges.
-// kRedThreads lanes: strided partial sums, then an LDS tree.  Serial depth
-// ~ M1/2/kRedThreads + log2(kRedThreads) additions.
+// block (job, w - w0, z): job < NB2 -> G_job = sum_{j : (j >> job) & 1} S_j
+// (only the j with that bit set are enumerated, so no lane idles); job >= NB2
+// -> partial sum of T_j over part (job - NB2) of kTJobs equal ranges.
+// kRedThreads lanes: strided partial sums, then an LDS tree.  With nsplit > 1
+// (few windows, e.g. the fixed-base MSM's single bucket set) nsplit blocks
+// share a job: each reduces every nsplit-th stride, parks its partial in P,
+// and the last block to finish (atomic ticket) folds the nsplit partials.
+// Serial depth ~ M1/2/(kRedThreads nsplit) + log2(kRedThreads) + log2(nsplit).
 constexpr int kRedThreads = 512;
 constexpr int kTJobs = 2;
+constexpr int kMaxSplit = 64;
 template <class F>
 __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __restrict__ S,
                                                              const Xyzz<F>* __restrict__ T, int w0, int M1,
-                                                             int NB2, Xyzz<F>* __restrict__ G) {
+                                                             int NB2, Xyzz<F>* __restrict__ G, int nsplit,
+                                                             Xyzz<F>* __restrict__ P, uint32_t* __restrict__ tickets) {
   __shared__ Xyzz29<F> lds[kRedThreads];
-  const int w = w0 + blockIdx.y, job = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint32_t last;
+  const int w = w0 + blockIdx.y, job = blockIdx.x, tid = threadIdx.x, z = blockIdx.z;
+  const int lane = z * kRedThreads + tid, stride = kRedThreads * nsplit;
   Xyzz29<F> acc = xyzz29_inf<F>();
   if (job < NB2) {
     const int low = (1 << job) - 1;
-    for (int m = tid;; m += kRedThreads) {
+    for (int m = lane;; m += stride) {
       const int j = ((m & ~low) << 1) | (1 << job) | (m & low);  // m-th index with bit `job` set
       if (j >= M1) break;
       acc = xyzz29_add<F>(acc, load_xyzz29<F>(&S[(size_t)w * M1 + j]));
@@ -617,7 +721,7 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
   } else {
     const int per = (M1 + kTJobs - 1) / kTJobs;
     const int j0 = (job - NB2) * per, j1 = min(M1, j0 + per);
-    for (int j = j0 + tid; j < j1; j += kRedThreads) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&T[(size_t)w * M1 + j]));
+    for (int j = j0 + lane; j < j1; j += stride) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&T[(size_t)w * M1 + j]));
   }
   lds[tid] = acc;
   __syncthreads();
@@ -628,9 +732,31 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
     }
     __syncthreads();
   }
+  const size_t out = (size_t)w * (NB2 + kTJobs) + job;
+  if (nsplit > 1) {
+    if (tid == 0) {
+      store_xyzz29<F>(&P[out * nsplit + z], acc);
+      __threadfence();
+      last = atomicAdd(&tickets[out], 1u) == (uint32_t)nsplit - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    acc = tid < nsplit ? load_xyzz29<F>(&P[out * nsplit + tid]) : xyzz29_inf<F>();
+    if (tid < kMaxSplit) lds[tid] = acc;
+    __syncthreads();
+    for (int s = kMaxSplit / 2; s > 0; s >>= 1) {
+      if (tid < s) {
+        acc = xyzz29_add<F>(acc, lds[tid + s]);
+        lds[tid] = acc;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) tickets[out] = 0;  // ready for the next MSM
+  }
   if (tid == 0) {
     // back to the Rust-layout R = 2^256 Montgomery form for the host tail
-    uint4* q = reinterpret_cast<uint4*>(&G[(size_t)w * (NB2 + kTJobs) + job]);
+    uint4* q = reinterpret_cast<uint4*>(&G[out]);
     const F29<F>* c[4] = {&acc.X, &acc.Y, &acc.ZZ, &acc.ZZZ};
 #pragma unroll
     for (int k = 0; k < 4; k++) {

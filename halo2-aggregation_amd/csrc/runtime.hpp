@@ -62,6 +62,12 @@ struct MsmPlan {
 };
 
 MsmPlan make_plan(size_t n, int c_override, int groups_override = 0, int min_chunk = 0);
+// fixed-base MSM over a table of npad rows per window (one window group,
+// accumulate work = W * npad entries)
+MsmPlan make_plan_fixed(size_t npad, int c, int min_chunk = 0);
+// fixed-base windows: one bucket set of 2^(c-1) buckets
+constexpr int kFixedMaxC = 20;
+constexpr int kAutoFixedC = 16;
 
 struct TimedSpan {
   const char* name;
@@ -69,6 +75,16 @@ struct TimedSpan {
 };
 
 }  // namespace pm
+
+// Fixed-base table (pm_fixed_bases_create): W x npad affine points in the
+// pipeline's R = 2^261 form, row w = [2^{o_w}] P_i.
+struct pm_fixed_bases {
+  int curve;
+  int device;
+  int c, W;
+  size_t n, npad;
+  void* d;
+};
 
 struct pm_ctx {
   int device = 0;
@@ -84,7 +100,7 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io;
+      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // timing
@@ -96,7 +112,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io};
+            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets};
   }
   ~pm_ctx();
   int begin_call();
@@ -126,6 +142,9 @@ struct CurveOps {
   int (*transcript)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4], const void* d_points,
                     const void* d_scalars, void* d_challenges, void* d_status);
   int (*vk_repr)(const uint8_t digest[64], uint64_t out[4]);
+  int (*fixed_table)(Ctx* ctx, const void* d_bases, pm_fixed_bases* ft);
+  int (*msm_fixed)(Ctx* ctx, const pm_fixed_bases* ft, const void* d_scalars, size_t n, uint32_t flags,
+                   uint64_t out[8]);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

@@ -230,6 +230,15 @@ def _load():
                             _u64p, _u64p], ctypes.c_int),
         "pm_accum_batch_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _vp, _vp, _vp,
                                    _vp, _vp], ctypes.c_int),
+        "pm_fixed_bases_create": ([_vp, ctypes.c_int, _u64p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_vp)],
+                                  ctypes.c_int),
+        "pm_fixed_bases_create_device": ([_vp, ctypes.c_int, _vp, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.POINTER(_vp)], ctypes.c_int),
+        "pm_fixed_bases_info": ([_vp, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "pm_fixed_bases_release": ([_vp], ctypes.c_int),
+        "pm_msm_fixed": ([_vp, _vp, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
+        "pm_msm_fixed_device": ([_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_vk_transcript_repr": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_transcript_batch": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p, _u64p,
                                  _u64p, _u64p, _u32p], ctypes.c_int),
@@ -336,6 +345,49 @@ class Bases:
             pass
 
 
+class FixedBases:
+    """Fixed-base table (pm_fixed_bases_create*): [2^{o_w}] P_i for every
+    window offset, resident on ctx's device.  ``bases`` is a host (n, 8) u64
+    array, or a device pointer with ``n`` given."""
+
+    def __init__(self, ctx, curve, bases=None, c=0, d_bases=None, n=None):
+        self.ctx, self.curve = ctx, curve
+        h = _vp()
+        if d_bases is not None:
+            _check(lib().pm_fixed_bases_create_device(ctx.h, curve, _vp(d_bases), n, c, ctypes.byref(h)))
+        else:
+            b = _as_u64(bases, 8)
+            _check(lib().pm_fixed_bases_create(ctx.h, curve, _p(b), b.shape[0], c, ctypes.byref(h)))
+        self.h = h
+        nn, cc, ww, tb = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
+        _check(lib().pm_fixed_bases_info(h, ctypes.byref(nn), ctypes.byref(cc), ctypes.byref(ww), ctypes.byref(tb)))
+        self.n, self.c, self.windows, self.table_bytes = nn.value, cc.value, ww.value, tb.value
+
+    def msm(self, coeffs, canonical=False):
+        s = _as_u64(coeffs, 4)
+        out = np.zeros(8, dtype=np.uint64)
+        _check(lib().pm_msm_fixed(self.ctx.h, self.h, _p(s), s.shape[0], SCALARS_CANONICAL if canonical else 0,
+                                  _p(out)))
+        return out
+
+    def msm_device(self, d_scalars, n, canonical=False):
+        out = np.zeros(8, dtype=np.uint64)
+        _check(lib().pm_msm_fixed_device(self.ctx.h, self.h, _vp(d_scalars), n,
+                                         SCALARS_CANONICAL if canonical else 0, _p(out)))
+        return out
+
+    def release(self):
+        if self.h:
+            lib().pm_fixed_bases_release(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
 class Context:
     """One device + HIP stream + workspace (pm_ctx)."""
 
@@ -392,6 +444,9 @@ class Context:
 
     def upload_bases(self, curve, bases):
         return Bases(self, curve, bases)
+
+    def fixed_bases(self, curve, bases=None, c=0, d_bases=None, n=None):
+        return FixedBases(self, curve, bases, c, d_bases, n)
 
     def msm_resident(self, bases: Bases, offset, coeffs, canonical=False):
         s = _as_u64(coeffs, 4)

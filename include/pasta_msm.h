@@ -204,6 +204,27 @@ int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B
 int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_points,
                           const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval);
 
+/* ---- Fixed-base MSM ----------------------------------------
+ * The prover's commitments (Params::commit / commit_lagrange,
+ * examples/simple-example.rs:638-640,702) are MSMs against the static SRS
+ * bases.  pm_fixed_bases_create precomputes, once per SRS, the table
+ * [2^{o_w}] P_i for every window offset o_w (W = ceil(256 / c) windows, c = 0
+ * picks the default); every later MSM then sorts all W digits of every scalar
+ * into ONE set of 2^(c-1) buckets and skips the per-window bucket reduction
+ * and the cross-window doublings.  Table size: W x n x 64 bytes of device
+ * memory (2^20 bases, c = 16: 1 GiB).  pm_msm_fixed* use the first n bases
+ * (n <= the table's n); results are bit-identical to pm_msm. */
+typedef struct pm_fixed_bases pm_fixed_bases;
+int pm_fixed_bases_create(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, int c, pm_fixed_bases** out);
+int pm_fixed_bases_create_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, int c,
+                                 pm_fixed_bases** out);
+int pm_fixed_bases_info(const pm_fixed_bases* fb, size_t* n, int* c, int* windows, size_t* table_bytes);
+int pm_fixed_bases_release(pm_fixed_bases* fb);
+int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars, size_t n, uint32_t flags,
+                 uint64_t out[8]);
+int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_scalars, size_t n, uint32_t flags,
+                        uint64_t out[8]);
+
 /* ---- Blake2b transcript replay ------------------------------
  * The verifier squeezes theta, beta, gamma, y, x, v, u from a halo2
  * Blake2bWrite/Challenge255 transcript (TranscriptChip,
