@@ -435,7 +435,7 @@ static int fixed_create(pm_ctx* ctx, int curve, const void* bases, bool host, si
   if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
   if (n == 0) return set_error(PM_ERR_ARG, "empty base set");
   if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "more than 2^26 fixed bases");
-  if (c == 0) c = kAutoFixedC;
+  if (c == 0) c = n > (size_t(1) << 21) ? kAutoFixedCLarge : kAutoFixedC;
   if (c < kMinC || c > kFixedMaxC) return set_error(PM_ERR_ARG, "fixed-base window out of range");
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();

@@ -67,7 +67,8 @@ MsmPlan make_plan(size_t n, int c_override, int groups_override = 0, int min_chu
 MsmPlan make_plan_fixed(size_t npad, int c, int min_chunk = 0);
 // fixed-base windows: one bucket set of 2^(c-1) buckets
 constexpr int kFixedMaxC = 20;
-constexpr int kAutoFixedC = 16;
+constexpr int kAutoFixedC = 16;       // n <= 2^21
+constexpr int kAutoFixedCLarge = 20;  // n > 2^21 (fewer windows: 13 instead of 16)
 
 struct TimedSpan {
   const char* name;
