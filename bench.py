@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fixed", type=int, default=1, help="also time the fixed-base MSM (1) or skip it (0)")
+    ap.add_argument("--ntt-logn", type=int, default=20, help="NTT leg size (0 = skip)")
     ap.add_argument("--accum-batch", type=int, default=256, help="proofs per GPU for the accumulator leg (0 = skip)")
     ap.add_argument("--accum-logn", type=int, default=17)
     return ap.parse_args()
@@ -139,6 +140,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     fixed = run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, result) if args.fixed else None
+    ntt = run_ntt(args, ctx, dist, dev, world) if args.ntt_logn > 0 else None
     accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
 
     if rank == 0:
@@ -181,6 +183,12 @@ def main():
             out["cpu_baseline"] = cpu_baseline(d_s, d_b, n, result, args.cpu_seconds)
         if fixed is not None:
             out["fixed_base"] = fixed
+        if ntt is not None:
+            if world == 1 and not args.no_cpu:
+                ntt["cpu_baseline"] = ntt_cpu_baseline(*ntt.pop("_state"), budget_s=6.0)
+            else:
+                ntt.pop("_state", None)
+            out["ntt"] = ntt
         if accum is not None:
             if world == 1 and not args.no_cpu:
                 accum["cpu_baseline"] = accum_cpu_baseline(*accum.pop("_state"), budget_s=8.0)
@@ -239,6 +247,90 @@ def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, wan
            "kernels_ms": kernels}
     fb.release()
     return out
+
+
+def run_ntt(args, ctx, dist, dev, world):
+    """NTT over the BN254 scalar field (halo2 best_fft): one step
+    = one in-place pm_fft_device of 2^k HBM-resident elements per rank
+    (independent transforms, weak scaling; the omega table is built in the
+    warmup)."""
+    import numpy as np
+    import torch
+
+    import halo2_amd as H
+    import workloads as Wk
+
+    curve, k = H.BN254, args.ntt_logn
+    n = 1 << k
+    r = H.SCALAR_MODULUS[curve]
+    wv = Wk.domain_omega(curve, k) * (1 << 256) % r
+    w = np.array([(wv >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+    a = torch.empty((n, 4), dtype=torch.int64, device=dev)
+    ctx.synth_scalars(curve, 0x77, 0, n, a.data_ptr())
+    torch.cuda.synchronize()
+    src = a.cpu().numpy().view(np.uint64).copy() if args.gpus == 1 or world == 1 else None
+    ctx.fft_device(curve, a.data_ptr(), k, w)
+    first = a.cpu().numpy().view(np.uint64).copy() if src is not None else None
+    for _ in range(args.warmup):
+        ctx.fft_device(curve, a.data_ptr(), k, w)
+    ctx.set_timing(True)
+    ctx.reset_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.fft_device(curve, a.data_ptr(), k, w)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kernels = {kk: round(ctx.kernel_stats(kk)[1] / args.steps, 4) for kk in ("ntt_cols", "ntt_rows")}
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed * 1e3 / args.steps
+    gpu_ms = kernels["ntt_cols"] + kernels["ntt_rows"]
+    # algorithmic bytes: read + write every 32-B element once; the two-pass
+    # four-step form moves each element twice (4 x 32 B) through HBM
+    alg = 2 * 32 * n
+    out = {"metric": f"NTT 2^{k} over the BN254 scalar field (halo2 best_fft)", "value": round(world * n / (ms * 1e-3) / 1e6, 1),
+           "unit": "Melem/s", "ms_per_ntt": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+           "kernels_ms": kernels,
+           "roofline": {"bound": "hbm", "achieved": round(alg / (gpu_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": 4 * 32 * n, "note": "achieved = 64 B/element (read + write once) over both "
+                        "passes' kernel time; traffic = the two passes' 128 B/element (not PMC-measured)"}}
+    if src is not None:
+        out["_state"] = (curve, k, src, w, first)
+    return out
+
+
+def ntt_cpu_baseline(curve, k, src, w, first, budget_s):
+    """C restatement of halo2 best_fft (oracle/msm_ref.c, halo2's own
+    parallel_fft split over 16 threads) on the same input; bit-exact check of
+    the GPU's first transform."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import msm_ref
+
+    threads = int(os.environ.get("BENCH_CPU_THREADS", "16"))
+    reps, t0 = 0, time.perf_counter()
+    match = None
+    while True:
+        got = msm_ref.best_fft(curve, src, k, w, threads)
+        if match is None:
+            match = bool(np.array_equal(got, first))
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round((1 << k) / dt / 1e6, 3), "unit": "Melem/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x best_fft(2^{k}) in oracle/msm_ref.c ({dt * 1e3:.1f} ms each)",
+            "matches_gpu": match}
 
 
 def run_accumulator(args, ctx, dist, dev, rank, world):

@@ -56,6 +56,7 @@ void pm::Buf::release() {
 pm_ctx::~pm_ctx() {
   (void)hipSetDevice(device);
   for (pm::Buf* b : all_bufs()) b->release();
+  for (auto& t : ntt_tw) t.buf.release();
   if (h_pinned) (void)hipHostFree(h_pinned);
   for (auto& e : ev_pool) (void)hipEventDestroy(e);
   for (auto& e : grp_ev) (void)hipEventDestroy(e);
@@ -424,6 +425,36 @@ int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
   HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
   return dispatch_msm_device(ctx, b->curve, ctx->in_scalars.p, (const char*)b->d + offset * 64, n, flags, out);
+}
+
+// ------------------------------------------------- NTT (§8f-4)
+int pm_fft_device(pm_ctx* ctx, int curve, void* d_data, uint32_t log_n, const uint64_t omega[4],
+                  const uint64_t* scale) {
+  if (!ctx || !d_data || !omega) return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  if (log_n > 24) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^24");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return ops->ntt(ctx, curve, d_data, log_n, omega, scale);
+}
+
+int pm_fft(pm_ctx* ctx, int curve, uint64_t* data, uint32_t log_n, const uint64_t omega[4], const uint64_t* scale) {
+  if (!ctx || !data || !omega) return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  if (log_n > 24) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^24");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  const size_t bytes = ((size_t)1 << log_n) * 32;
+  if ((rc = ctx->in_scalars.ensure(bytes))) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, data, bytes, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = ops->ntt(ctx, curve, ctx->in_scalars.p, log_n, omega, scale))) return rc;
+  HIP_TRY(hipMemcpyAsync(data, ctx->in_scalars.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return PM_OK;
 }
 
 // ------------------------------------------------- fixed-base MSM (§8f-3)

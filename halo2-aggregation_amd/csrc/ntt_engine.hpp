@@ -1,0 +1,119 @@
+// ntt_engine.hpp -- host driver of the NTT (pm_fft*).
+// Boundary: halo2 `best_fft(a: &mut [G], omega: G::Scalar, log_n: u32)` [3P],
+// reached from EvaluationDomain::{fft, ifft, coeff_to_extended,
+// extended_to_coeff} inside create_proof (examples/simple-example.rs:606,702).
+#pragma once
+#include <cstring>
+
+#include "engine.hpp"
+#include "ntt_kernels.hpp"
+
+namespace pm {
+
+// Up to 2^7 elements one block does the whole transform; above that the
+// two-pass form spreads it over many blocks (a single block for 2^12 took
+// 0.14 ms, two passes 0.03 ms).
+constexpr uint32_t kNttOnePassLog = 7;
+
+template <class Fs>
+FeArg fearg_from_u64(const uint64_t* p) {
+  FeArg a;
+  for (int k = 0; k < 4; k++) {
+    a.l[2 * k] = (uint32_t)p[k];
+    a.l[2 * k + 1] = (uint32_t)(p[k] >> 32);
+  }
+  return a;
+}
+
+// twiddle table omega^i (i < n/2), cached per (curve, log_n, omega)
+inline int ntt_twiddles_lookup(Ctx* ctx, int curve, uint32_t logn, const uint64_t omega[4], const uint32_t** out,
+                               bool* fresh) {
+  for (auto& e : ctx->ntt_tw) {
+    if (e.curve == curve && e.logn == logn && std::memcmp(e.omega, omega, 32) == 0) {
+      e.stamp = ++ctx->ntt_clock;
+      *out = (const uint32_t*)e.buf.p;
+      *fresh = false;
+      return PM_OK;
+    }
+  }
+  NttTwiddles* slot = nullptr;
+  if (ctx->ntt_tw.size() < kNttTwiddleSlots) {
+    ctx->ntt_tw.emplace_back();
+    slot = &ctx->ntt_tw.back();
+  } else {
+    slot = &ctx->ntt_tw[0];
+    for (auto& e : ctx->ntt_tw)
+      if (e.stamp < slot->stamp) slot = &e;
+  }
+  slot->curve = curve;
+  slot->logn = logn;
+  std::memcpy(slot->omega, omega, 32);
+  slot->stamp = ++ctx->ntt_clock;
+  int rc = slot->buf.ensure(std::max<size_t>(32, ((size_t)1 << (logn ? logn - 1 : 0)) * 32));
+  if (rc) {
+    slot->curve = -1;
+    return rc;
+  }
+  *out = (const uint32_t*)slot->buf.p;
+  *fresh = true;
+  return PM_OK;
+}
+
+template <class Cv>
+int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint64_t omega[4],
+                    const uint64_t* scale) {
+  using Fs = typename Cv::Scalar;
+  if (logn > 2 * kNttMaxLogL) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^24");
+  if (logn == 0) {
+    if (scale) {  // a_0 *= scale
+      // a one-element transform is the identity; apply the scale on the host
+      uint64_t v[4];
+      HIP_TRY(hipMemcpyAsync(v, d_data, 32, hipMemcpyDeviceToHost, ctx->stream));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+      const Fe<Fs> r = fe_mul<Fs>(fe_from_u64<Fs>(v), fe_from_u64<Fs>(scale));
+      for (int k = 0; k < 4; k++) v[k] = (uint64_t)r.l[2 * k] | ((uint64_t)r.l[2 * k + 1] << 32);
+      HIP_TRY(hipMemcpyAsync(d_data, v, 32, hipMemcpyHostToDevice, ctx->stream));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    return PM_OK;
+  }
+  const hipStream_t st = ctx->stream;
+  const size_t n = (size_t)1 << logn;
+  const uint32_t half = (uint32_t)(n >> 1);
+  const uint32_t* tw = nullptr;
+  bool fresh = false;
+  int rc = ntt_twiddles_lookup(ctx, curve, logn, omega, &tw, &fresh);
+  if (rc) return rc;
+  if (fresh)
+    PM_LAUNCH(ctx, "ntt_twiddles", (k_ntt_twiddles<Fs><<<(half + 255) / 256, 256, 0, st>>>(
+                                       fearg_from_u64<Fs>(omega), half, (uint32_t*)tw)));
+  const FeArg sc = scale ? fearg_from_u64<Fs>(scale) : FeArg{};
+  uint32_t* data = (uint32_t*)d_data;
+  if (logn <= (uint32_t)kNttOnePassLog) {
+    // one sub-transform in LDS (pass A with a single column, in place)
+    const size_t lds = n * 32;
+    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<1, kNttThreads, lds, st>>>(data, data, (int)logn, (int)logn, 0, tw)));
+    if (scale) {
+      // scaling rides on a rows pass of length 1 would be wasteful: fold it in
+      // with a trivial rows pass of log2 = 0 (one element per row)
+      PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> std::min<uint32_t>(logn, 8)), kNttThreads,
+                                                   ((size_t)1 << std::min<uint32_t>(logn, 8)) * 32, st>>>(
+                                     data, data, (int)logn, 0, (int)std::min<uint32_t>(logn, 8), tw, sc, 1u)));
+    }
+  } else {
+    const int log1 = (int)(logn + 1) / 2, log2 = (int)logn - log1;
+    const int logC = std::max(0, std::min(2, 11 - log1)), logR = std::max(0, std::min(2, 11 - log2));
+    if ((rc = ctx->ntt_scratch.ensure(n * 32))) return rc;
+    uint32_t* tmp = (uint32_t*)ctx->ntt_scratch.p;
+    const size_t ldsA = ((size_t)1 << (log1 + logC)) * 32, ldsB = ((size_t)1 << (log2 + logR)) * 32;
+    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)((size_t)1 << (log2 - logC)), kNttThreads, ldsA, st>>>(
+                                   data, tmp, (int)logn, log1, logC, tw)));
+    PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)((size_t)1 << (log1 - logR)), kNttThreads, ldsB, st>>>(
+                                   tmp, data, (int)logn, log2, logR, tw, sc, scale ? 1u : 0u)));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  ctx->end_call();
+  return PM_OK;
+}
+
+}  // namespace pm

@@ -87,6 +87,17 @@ struct pm_fixed_bases {
   void* d;
 };
 
+namespace pm {
+constexpr size_t kNttTwiddleSlots = 4;
+struct NttTwiddles {
+  int curve = -1;
+  uint32_t logn = 0;
+  uint64_t omega[4] = {0, 0, 0, 0};
+  uint64_t stamp = 0;
+  Buf buf;
+};
+}  // namespace pm
+
 struct pm_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -101,7 +112,9 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets;
+      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets, ntt_scratch;
+  std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
+  uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // timing
@@ -113,7 +126,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets};
+            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets, &ntt_scratch};
   }
   ~pm_ctx();
   int begin_call();
@@ -144,6 +157,7 @@ struct CurveOps {
                     const void* d_scalars, void* d_challenges, void* d_status);
   int (*vk_repr)(const uint8_t digest[64], uint64_t out[4]);
   int (*fixed_table)(Ctx* ctx, const void* d_bases, pm_fixed_bases* ft);
+  int (*ntt)(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint64_t omega[4], const uint64_t* scale);
   int (*msm_fixed)(Ctx* ctx, const pm_fixed_bases* ft, const void* d_scalars, size_t n, uint32_t flags,
                    uint64_t out[8]);
 };

@@ -239,6 +239,8 @@ def _load():
         "pm_fixed_bases_release": ([_vp], ctypes.c_int),
         "pm_msm_fixed": ([_vp, _vp, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_msm_fixed_device": ([_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
+        "pm_fft": ([_vp, ctypes.c_int, _u64p, ctypes.c_uint32, _u64p, _u64p], ctypes.c_int),
+        "pm_fft_device": ([_vp, ctypes.c_int, _vp, ctypes.c_uint32, _u64p, _u64p], ctypes.c_int),
         "pm_vk_transcript_repr": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_transcript_batch": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p, _u64p,
                                  _u64p, _u64p, _u32p], ctypes.c_int),
@@ -522,6 +524,24 @@ class Context:
         _check(lib().pm_accum_batch_transcript_device(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk),
                                                       _vp(d_points), _vp(d_scalars), _vp(d_challenges),
                                                       _vp(d_quads), _vp(d_h or None), _vp(d_status or None)))
+
+    def fft(self, curve, values, omega, scale=None):
+        """pm_fft: natural-order NTT of values ((2^k, 4) u64 Montgomery) with
+        root omega (4,) u64 Montgomery; returns a new array."""
+        a = np.ascontiguousarray(values, dtype=np.uint64).reshape(-1, 4).copy()
+        n = a.shape[0]
+        k = n.bit_length() - 1
+        if n != 1 << k:
+            raise ValueError("length must be a power of two")
+        w = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+        sc = None if scale is None else np.ascontiguousarray(scale, dtype=np.uint64).reshape(4)
+        _check(lib().pm_fft(self.h, curve, _p(a), k, _p(w), None if sc is None else _p(sc)))
+        return a
+
+    def fft_device(self, curve, d_data, log_n, omega, scale=None):
+        w = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+        sc = None if scale is None else np.ascontiguousarray(scale, dtype=np.uint64).reshape(4)
+        _check(lib().pm_fft_device(self.h, curve, _vp(d_data), log_n, _p(w), None if sc is None else _p(sc)))
 
     def selftest_field(self, curve, seed, n):
         m = ctypes.c_uint64(0)

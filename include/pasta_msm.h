@@ -225,6 +225,19 @@ int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars,
 int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_scalars, size_t n, uint32_t flags,
                         uint64_t out[8]);
 
+/* ---- NTT over the scalar field -------------------------------
+ * halo2 `best_fft(a, omega, log_n)` [3P] (EvaluationDomain::fft / ifft /
+ * coset conversions inside create_proof): in place, natural order in and out,
+ * a_k <- sum_j a_j omega^{jk} over the scalar field of `curve` (Montgomery
+ * 4 x u64 per element, like pm_msm's scalars).  omega must be a primitive
+ * 2^log_n-th root of unity.  scale (may be NULL) multiplies every output:
+ * EvaluationDomain::ifft is pm_fft(omega_inv, scale = 1/n).  log_n <= 24;
+ * the omega^i table is cached in the context (4 most recent (curve, log_n,
+ * omega)). */
+int pm_fft(pm_ctx* ctx, int curve, uint64_t* data, uint32_t log_n, const uint64_t omega[4], const uint64_t* scale);
+int pm_fft_device(pm_ctx* ctx, int curve, void* d_data, uint32_t log_n, const uint64_t omega[4],
+                  const uint64_t* scale);
+
 /* ---- Blake2b transcript replay ------------------------------
  * The verifier squeezes theta, beta, gamma, y, x, v, u from a halo2
  * Blake2bWrite/Challenge255 transcript (TranscriptChip,

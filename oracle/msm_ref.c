@@ -518,3 +518,127 @@ int msm_ref_synth_scalars(int curve, u64 seed, u64 i0, size_t n, int num_threads
 int msm_ref_synth_bases(int curve, u64 seed, u64 i0, size_t n, int num_threads, u64* out) {
   return synth_run(curve, seed, i0, n, num_threads, out, 1);
 }
+
+/* ------------------------------------------------------------------ NTT
+ * C restatement of halo2 arithmetic.rs `best_fft` [3P] (checker for pm_fft at
+ * sizes the Python oracle cannot reach, and bench.py's NTT cpu_baseline):
+ *   serial_fft: bit-reverse swap, radix-2 DIT, w_m = omega^(n/2m), w *= w_m;
+ *   best_fft: log_threads = floor(log2 threads); if log_n <= log_threads the
+ *     serial form, else parallel_fft: for each thread j a sub-array
+ *     tmp_j[i] = sum_s a[(i + s 2^{log_n - log_threads}) mod n] * elt with
+ *     elt walking omega_step = omega^(j 2^{log_new_n}) and omega_j = omega^j,
+ *     a serial sub-FFT with omega^threads, then a[idx] = tmp[idx & mask]
+ *     [idx >> log_threads].
+ * Elements are scalar-field values in Montgomery form (4 x u64). */
+static void f_pow(const Field* F, u64 r[4], const u64 base[4], u64 e) {
+  u64 b[4], acc[4];
+  memcpy(b, base, 32);
+  memcpy(acc, F->one, 32);
+  while (e) {
+    if (e & 1) f_mul(F, acc, acc, b);
+    f_mul(F, b, b, b);
+    e >>= 1;
+  }
+  memcpy(r, acc, 32);
+}
+
+static size_t brev_bits(size_t x, unsigned bits) {
+  size_t r = 0;
+  for (unsigned i = 0; i < bits; i++) {
+    r = (r << 1) | (x & 1);
+    x >>= 1;
+  }
+  return r;
+}
+
+static void serial_fft(const Field* F, u64* a, unsigned log_n, const u64 omega[4]) {
+  const size_t n = (size_t)1 << log_n;
+  for (size_t k = 0; k < n; k++) {
+    size_t rk = brev_bits(k, log_n);
+    if (k < rk) {
+      u64 t[4];
+      memcpy(t, a + 4 * k, 32);
+      memcpy(a + 4 * k, a + 4 * rk, 32);
+      memcpy(a + 4 * rk, t, 32);
+    }
+  }
+  size_t m = 1;
+  for (unsigned s = 0; s < log_n; s++) {
+    u64 w_m[4];
+    f_pow(F, w_m, omega, n / (2 * m));
+    for (size_t k = 0; k < n; k += 2 * m) {
+      u64 w[4];
+      memcpy(w, F->one, 32);
+      for (size_t j = 0; j < m; j++) {
+        u64 t[4];
+        f_mul(F, t, a + 4 * (k + j + m), w);
+        f_sub(F, a + 4 * (k + j + m), a + 4 * (k + j), t);
+        f_add(F, a + 4 * (k + j), a + 4 * (k + j), t);
+        f_mul(F, w, w, w_m);
+      }
+    }
+    m *= 2;
+  }
+}
+
+typedef struct {
+  const Field* F;
+  const u64* a;
+  u64* tmp;
+  unsigned log_n, log_threads;
+  size_t j;
+  const u64* omega;
+} FftJob;
+
+static void* fft_worker(void* arg) {
+  FftJob* J = (FftJob*)arg;
+  const Field* F = J->F;
+  const unsigned log_new_n = J->log_n - J->log_threads;
+  const size_t num_threads = (size_t)1 << J->log_threads, new_n = (size_t)1 << log_new_n;
+  const size_t mask_n = ((size_t)1 << J->log_n) - 1;
+  u64 omega_j[4], omega_step[4], new_omega[4], elt[4];
+  f_pow(F, omega_j, J->omega, J->j);
+  f_pow(F, omega_step, J->omega, J->j << log_new_n);
+  f_pow(F, new_omega, J->omega, num_threads);
+  memcpy(elt, F->one, 32);
+  for (size_t i = 0; i < new_n; i++) {
+    u64 acc[4] = {0, 0, 0, 0};
+    for (size_t s = 0; s < num_threads; s++) {
+      const size_t idx = (i + (s << log_new_n)) & mask_n;
+      u64 t[4];
+      f_mul(F, t, J->a + 4 * idx, elt);
+      f_add(F, acc, acc, t);
+      f_mul(F, elt, elt, omega_step);
+    }
+    memcpy(J->tmp + 4 * i, acc, 32);
+    f_mul(F, elt, elt, omega_j);
+  }
+  serial_fft(F, J->tmp, log_new_n, new_omega);
+  return NULL;
+}
+
+int ntt_ref_best_fft(int curve, u64* a, unsigned log_n, const u64 omega[4], int num_threads) {
+  if (curve < 0 || curve > 2 || num_threads < 1 || log_n > 30) return -1;
+  const Field* F = &CURVES[curve].fr;
+  unsigned log_threads = 0;
+  while ((2u << log_threads) <= (unsigned)num_threads) log_threads++;
+  if (log_n <= log_threads) {
+    serial_fft(F, a, log_n, omega);
+    return 0;
+  }
+  const size_t T = (size_t)1 << log_threads, new_n = (size_t)1 << (log_n - log_threads);
+  u64* tmp = (u64*)malloc(T * new_n * 32);
+  FftJob* jobs = (FftJob*)malloc(T * sizeof(FftJob));
+  pthread_t* th = (pthread_t*)malloc(T * sizeof(pthread_t));
+  for (size_t j = 0; j < T; j++) {
+    jobs[j] = (FftJob){F, a, tmp + 4 * new_n * j, log_n, log_threads, j, omega};
+    pthread_create(&th[j], NULL, fft_worker, &jobs[j]);
+  }
+  for (size_t j = 0; j < T; j++) pthread_join(th[j], NULL);
+  const size_t n = (size_t)1 << log_n, mask = T - 1;
+  for (size_t idx = 0; idx < n; idx++) memcpy(a + 4 * idx, tmp + 4 * (new_n * (idx & mask) + (idx >> log_threads)), 32);
+  free(th);
+  free(jobs);
+  free(tmp);
+  return 0;
+}

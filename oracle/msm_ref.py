@@ -28,6 +28,8 @@ def lib():
         L.msm_ref_best_multiexp.argtypes = [ctypes.c_int, u64p, u64p, ctypes.c_size_t, ctypes.c_int,
                                             ctypes.c_int, u64p]
         L.msm_ref_best_multiexp.restype = ctypes.c_int
+        L.ntt_ref_best_fft.argtypes = [ctypes.c_int, u64p, ctypes.c_uint, u64p, ctypes.c_int]
+        L.ntt_ref_best_fft.restype = ctypes.c_int
         for f in (L.msm_ref_synth_scalars, L.msm_ref_synth_bases):
             f.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int, u64p]
             f.restype = ctypes.c_int
@@ -63,3 +65,13 @@ def synth_bases(curve: int, seed: int, i0: int, n: int, threads=None):
     rc = lib().msm_ref_synth_bases(curve, seed, i0, n, int(threads or os.cpu_count() or 1), _p(out))
     assert rc == 0
     return out
+
+
+def best_fft(curve, values, log_n, omega, threads=1):
+    """C restatement of halo2 best_fft (in a copy); values (2^log_n, 4) u64
+    Montgomery scalars of `curve`'s scalar field, omega (4,) Montgomery."""
+    a = np.ascontiguousarray(values, dtype=np.uint64).reshape(-1, 4).copy()
+    w = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+    if lib().ntt_ref_best_fft(curve, _p(a), log_n, _p(w), threads) != 0:
+        raise ValueError("ntt_ref_best_fft failed")
+    return a
