@@ -115,7 +115,9 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    ctx.set_timing(True)
+    # timed region: HIP events only around the roofline kernel (every event
+    # pair costs ~10 us of stream time on MI355X)
+    ctx.set_timing(True, only="accumulate")
     ctx.reset_stats()
     if dist:
         dist.barrier()
@@ -129,12 +131,12 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     launches, acc_ms = ctx.kernel_stats("accumulate")
-    # per-MSM kernel time (the pipelined engine launches accumulate / fixup /
-    # bucket_* once per window group)
-    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4)
-               for k in ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg",
-                         "bucket_bits", "host_tail"]}
     acc_launches_per_msm = max(1, launches) / args.steps
+    # per-MSM kernel breakdown from a separate, untimed diagnostic run with
+    # events around every launch (the pipelined engine launches accumulate /
+    # fixup / bucket_* once per window group)
+    kernels = kernel_breakdown(ctx, step, ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate",
+                                           "fixup", "bucket_seg", "bucket_bits", "host_tail"])
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -200,6 +202,17 @@ def main():
         dist.destroy_process_group()
 
 
+def kernel_breakdown(ctx, step, names, reps=5):
+    """Per-step kernel times from `reps` extra (untimed) steps with HIP events
+    around every launch; every rank runs the same steps (collectives inside)."""
+    ctx.set_timing(True)
+    ctx.reset_stats()
+    for _ in range(reps):
+        step()
+    ctx.set_timing(False)
+    return {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in names}
+
+
 def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, want):
     """Fixed-base MSM over the same scalars and bases: the
     SRS table [2^{o_w}] P_i is built once (untimed, reported as build_ms),
@@ -219,8 +232,6 @@ def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, wan
 
     for _ in range(args.warmup):
         step()
-    ctx.set_timing(True)
-    ctx.reset_stats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -231,10 +242,8 @@ def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, wan
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
-    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4)
-               for k in ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg",
-                         "bucket_bits", "host_tail"]}
+    kernels = kernel_breakdown(ctx, step, ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup",
+                                           "bucket_seg", "bucket_bits", "host_tail"])
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -271,22 +280,22 @@ def run_ntt(args, ctx, dist, dev, world):
     src = a.cpu().numpy().view(np.uint64).copy() if args.gpus == 1 or world == 1 else None
     ctx.fft_device(curve, a.data_ptr(), k, w)
     first = a.cpu().numpy().view(np.uint64).copy() if src is not None else None
-    for _ in range(args.warmup):
+    def step():
         ctx.fft_device(curve, a.data_ptr(), k, w)
-    ctx.set_timing(True)
-    ctx.reset_stats()
+
+    for _ in range(args.warmup):
+        step()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ctx.fft_device(curve, a.data_ptr(), k, w)
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
-    kernels = {kk: round(ctx.kernel_stats(kk)[1] / args.steps, 4) for kk in ("ntt_cols", "ntt_rows")}
+    kernels = kernel_breakdown(ctx, step, ("ntt_cols", "ntt_rows"))
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -353,8 +362,6 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
 
     for _ in range(args.warmup):
         step()
-    ctx.set_timing(True)
-    ctx.reset_stats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -365,9 +372,7 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
-    kernels = {k: round(ctx.kernel_stats(k)[1] / args.steps, 4)
-               for k in ("transcript", "acc_scalars", "acc_termmul", "acc_sum")}
+    kernels = kernel_breakdown(ctx, step, ("transcript", "acc_scalars", "acc_termmul", "acc_sum"))
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

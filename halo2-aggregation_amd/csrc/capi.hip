@@ -306,6 +306,13 @@ int pm_ctx_set_timing(pm_ctx* ctx, int enable) {
   return PM_OK;
 }
 
+int pm_ctx_set_timing_filter(pm_ctx* ctx, const char* kernel) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->timing_filter = kernel ? kernel : "";
+  return PM_OK;
+}
+
 int pm_ctx_kernel_stats(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms) {
   if (!ctx || !kernel || !launches || !total_ms) return set_error(PM_ERR_ARG, "null argument");
   std::lock_guard<std::mutex> lk(ctx->mu);

@@ -18,7 +18,8 @@
 #define PM_LAUNCH_ST(ctx, st_, name, ...)                                \
   do {                                                                   \
     hipEvent_t a_ = nullptr, b_ = nullptr;                               \
-    if ((ctx)->timing) {                                                 \
+    const bool tm_ = (ctx)->timed(name);                                 \
+    if (tm_) {                                                           \
       a_ = (ctx)->next_event();                                          \
       b_ = (ctx)->next_event();                                          \
       (void)hipEventRecord(a_, (st_));                                   \
@@ -28,7 +29,7 @@
     if (le_ != hipSuccess)                                               \
       return pm::set_error(PM_ERR_HIP, std::string("launch ") + (name) + \
                                            ": " + hipGetErrorString(le_)); \
-    if ((ctx)->timing) {                                                 \
+    if (tm_) {                                                           \
       (void)hipEventRecord(b_, (st_));                                   \
       (ctx)->mark((name), a_, b_);                                       \
     }                                                                    \

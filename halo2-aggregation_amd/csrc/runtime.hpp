@@ -109,6 +109,8 @@ struct pm_ctx {
   int groups = 0;     // window groups, 0 = auto (diagnostics: PM_GROUPS env)
   int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
   bool timing = false;
+  std::string timing_filter;  // time only launches with this name ("" = all)
+  bool timed(const char* name) const { return timing && (timing_filter.empty() || timing_filter == name); }
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,

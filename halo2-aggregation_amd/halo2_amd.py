@@ -207,6 +207,7 @@ def _load():
         "pm_ctx_set_window": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing": ([_vp, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_timing_filter": ([_vp, ctypes.c_char_p], ctypes.c_int),
         "pm_ctx_kernel_stats": ([_vp, ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "pm_ctx_reset_stats": ([_vp], ctypes.c_int),
         "pm_msm": ([ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
@@ -419,7 +420,10 @@ class Context:
     def set_pipeline(self, groups=0, min_chunk=0):
         _check(lib().pm_ctx_set_pipeline(self.h, groups, min_chunk))
 
-    def set_timing(self, on=True):
+    def set_timing(self, on=True, only=None):
+        """HIP-event timing; `only` restricts events to one kernel name (each
+        event pair adds ~10 us of stream time)."""
+        _check(lib().pm_ctx_set_timing_filter(self.h, (only or "").encode()))
         _check(lib().pm_ctx_set_timing(self.h, 1 if on else 0))
 
     def reset_stats(self):

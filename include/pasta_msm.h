@@ -61,8 +61,12 @@ int pm_ctx_set_window(pm_ctx* ctx, int c);
  * the next group's accumulation (0 = automatic, 1 = no pipelining) and the
  * minimum accumulate slice per lane (0 = automatic). */
 int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk);
-/* Per-kernel HIP-event timing on the context stream (for bench/profiling). */
+/* Per-kernel HIP-event timing on the context stream (for bench/profiling).
+ * Every event pair costs ~10 us of stream time on MI355X, so a timed region
+ * should restrict events to the kernel it measures:
+ * pm_ctx_set_timing_filter(ctx, "accumulate") (NULL or "" = every kernel). */
 int pm_ctx_set_timing(pm_ctx* ctx, int enable);
+int pm_ctx_set_timing_filter(pm_ctx* ctx, const char* kernel);
 int pm_ctx_kernel_stats(pm_ctx* ctx, const char* kernel, uint64_t* launches, double* total_ms);
 int pm_ctx_reset_stats(pm_ctx* ctx);
 
