@@ -136,7 +136,7 @@ def main():
     # events around every launch (the pipelined engine launches accumulate /
     # fixup / bucket_* once per window group)
     kernels = kernel_breakdown(ctx, step, ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate",
-                                           "fixup", "bucket_seg", "bucket_bits", "host_tail"])
+                                           "fixup", "bucket_seg", "bucket_bits", "bits_combine", "host_tail"])
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -243,7 +243,7 @@ def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, wan
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernels = kernel_breakdown(ctx, step, ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup",
-                                           "bucket_seg", "bucket_bits", "host_tail"])
+                                           "bucket_seg", "bucket_bits", "bits_combine", "host_tail"])
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

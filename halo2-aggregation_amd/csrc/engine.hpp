@@ -101,7 +101,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const size_t E = fixed ? (size_t)pl.W * stride : n;  // entries of one sort row
   const size_t TOT = (size_t)Wr * pl.NB + 1;
   const size_t nW = (size_t)stride * pl.W;
-  const int NJ = pl.NB2 + kTJobs;
+  const int NJ = pl.NB2 + kTJobs;                        // bit-sum jobs per window
+  const int NQ = (pl.NB2 + kBitsFold - 1) / kBitsFold + 1;  // folded terms per window (host Horner)
   SortGeom g;  // histogram geometry (blocks of scalars)
   g.FB = std::max(0, pl.cmax - 1 - 8);
   g.NCB = (pl.K >> g.FB) + 1;
@@ -127,6 +128,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->segS.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segT.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->bits.ensure((size_t)Wr * NJ * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->bitsQ.ensure((size_t)Wr * NQ * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->longs.ensure((size_t)pl.G * longs_stride))) return rc;
   const size_t nG = (size_t)Wr * NJ;
   if ((rc = ctx->ensure_pinned(nG * sizeof(Xyzz<F>)))) return rc;
@@ -143,6 +145,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   Xyzz<F>* S = (Xyzz<F>*)ctx->segS.p;
   Xyzz<F>* T = (Xyzz<F>*)ctx->segT.p;
   Xyzz<F>* G = (Xyzz<F>*)ctx->bits.p;
+  Xyzz<F>* Qb = (Xyzz<F>*)ctx->bitsQ.p;
   const uint32_t un = (uint32_t)n;
 
   HIP_TRY(hipMemsetAsync(bh + (TOTB - 1), 0, 4, st));
@@ -241,22 +244,24 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     PM_LAUNCH_ST(ctx, st2, "bucket_bits",
                  (k_bucket_bits<F><<<dim3(NJ, nw, nsplit), kRedThreads, 0, st2>>>(S, T, w0, pl.M1, pl.NB2, G, nsplit,
                                                                                       bitsP, tickets)));
-    HIP_TRY(hipMemcpyAsync((Xyzz<F>*)ctx->h_pinned + (size_t)w0 * NJ, G + (size_t)w0 * NJ,
-                           (size_t)nw * NJ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st2));
+    PM_LAUNCH_ST(ctx, st2, "bits_combine",
+                 (k_bits_combine<F><<<(nw * NQ + 63) / 64, 64, 0, st2>>>(G, w0, nw, pl.NB2, Qb)));
+    HIP_TRY(hipMemcpyAsync((Xyzz<F>*)ctx->h_pinned + (size_t)w0 * NQ, Qb + (size_t)w0 * NQ,
+                           (size_t)nw * NQ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st2));
     HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi + 1], st2));
   }
 
   // Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b}) as one
   // Horner over absolute bit positions q (host_ec.hpp), consumed group by group.
   const Xyzz<F>* hG = (const Xyzz<F>*)ctx->h_pinned;
-  std::vector<std::vector<int>> at(256 + NJ + pl.log2L1 + 1);
+  std::vector<std::vector<int>> at(256 + NJ + pl.log2L1 + kBitsFold + 1);
   std::vector<int> gmax(pl.G, -1);  // highest position of any term of group g
   int qmax = 0;
   for (int w = 0; w < Wr; w++) {
     const int o = fixed ? 0 : w * pl.base + std::min(w, pl.extra);
-    for (int b = 0; b < NJ; b++) {
-      const int q = b < pl.NB2 ? o + b + pl.log2L1 : o;
-      at[q].push_back(w * NJ + b);
+    for (int b = 0; b < NQ; b++) {
+      const int q = b < NQ - 1 ? o + kBitsFold * b + pl.log2L1 : o;
+      at[q].push_back(w * NQ + b);
       qmax = std::max(qmax, q);
       gmax[w / wpg] = std::max(gmax[w / wpg], q);
     }

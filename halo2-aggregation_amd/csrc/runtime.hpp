@@ -114,7 +114,7 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets, ntt_scratch;
+      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets, ntt_scratch, bitsQ;
   std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;
@@ -128,7 +128,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets, &ntt_scratch};
+            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ};
   }
   ~pm_ctx();
   int begin_call();
