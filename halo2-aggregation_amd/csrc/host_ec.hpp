@@ -88,34 +88,41 @@ inline E<P> sub(const E<P>& a, const E<P>& b) {
   return r;
 }
 
-// CIOS Montgomery product, 4 x 64
+// CIOS Montgomery product, 4 x 64, "no-carry" form: every modulus here has
+// its top limb below 2^63 - 1, so the running t never needs a fifth word
+// (t < 2p throughout) and one conditional subtraction finishes.
 template <class P>
 inline E<P> mul(const E<P>& a, const E<P>& b) {
-  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
   constexpr uint64_t INV = F64<P>::inv();
+  constexpr uint64_t p0 = F64<P>::mod(0), p1 = F64<P>::mod(1), p2 = F64<P>::mod(2), p3 = F64<P>::mod(3);
+  static_assert(p3 < (1ull << 63) - 1, "no-carry CIOS needs a spare top bit");
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   for (int i = 0; i < 4; i++) {
-    uint64_t c = 0;
-    for (int j = 0; j < 4; j++) {
-      u128 s = (u128)a.v[j] * b.v[i] + t[j] + c;
-      t[j] = (uint64_t)s;
-      c = (uint64_t)(s >> 64);
-    }
-    u128 s = (u128)t[4] + c;
-    t[4] = (uint64_t)s;
-    t[5] = (uint64_t)(s >> 64);
-    const uint64_t m = t[0] * INV;
-    s = (u128)m * F64<P>::mod(0) + t[0];
-    c = (uint64_t)(s >> 64);
-    for (int j = 1; j < 4; j++) {
-      s = (u128)m * F64<P>::mod(j) + t[j] + c;
-      t[j - 1] = (uint64_t)s;
-      c = (uint64_t)(s >> 64);
-    }
-    s = (u128)t[4] + c;
-    t[3] = (uint64_t)s;
-    t[4] = t[5] + (uint64_t)(s >> 64);
+    const uint64_t bi = b.v[i];
+    u128 A = (u128)a.v[0] * bi + t0;
+    const uint64_t m = (uint64_t)A * INV;
+    u128 C = (u128)m * p0 + (uint64_t)A;
+    A >>= 64;
+    C >>= 64;
+    A += (u128)a.v[1] * bi + t1;
+    C += (u128)m * p1 + (uint64_t)A;
+    t0 = (uint64_t)C;
+    A >>= 64;
+    C >>= 64;
+    A += (u128)a.v[2] * bi + t2;
+    C += (u128)m * p2 + (uint64_t)A;
+    t1 = (uint64_t)C;
+    A >>= 64;
+    C >>= 64;
+    A += (u128)a.v[3] * bi + t3;
+    C += (u128)m * p3 + (uint64_t)A;
+    t2 = (uint64_t)C;
+    A >>= 64;
+    C >>= 64;
+    t3 = (uint64_t)C + (uint64_t)A;
   }
-  return sub_p_if<P>(t, t[4]);
+  const uint64_t t[4] = {t0, t1, t2, t3};
+  return sub_p_if<P>(t, 0);
 }
 
 template <class P>

@@ -757,11 +757,13 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
   if (tid == 0) store_xyzz29<F>(&G[out], acc);  // packed R261; k_bits_combine converts
 }
 
-// Per window: the NB2 bit sums folded four at a time, Q_j = G_{4j} + 2 G_{4j+1}
-// + 4 G_{4j+2} + 8 G_{4j+3} (Horner: 3 doublings, 3 additions), plus T = the
-// kTJobs T-partials; converted to the Rust-layout R = 2^256 form for the host
-// Horner.  Cuts the host's serial additions ~3x for a few us of GPU latency.
-constexpr int kBitsFold = 4;
+// Per window: the NB2 bit sums folded kBitsFold at a time by Horner,
+// Q_j = G_{2j} + 2 G_{2j+1} (one doubling, one addition), plus T = the kTJobs
+// T-partials; converted to the Rust-layout R = 2^256 form for the host Horner.
+// A dependent EC operation costs one wave ~8 us, so folding pays only while
+// the chain stays short: 4 at a time (3 dbl + 3 add) cost as much GPU time as
+// it saved on the host; 2 at a time halves the host's additions for ~2 ops.
+constexpr int kBitsFold = 2;
 template <class F>
 __global__ void __launch_bounds__(64) k_bits_combine(const Xyzz<F>* __restrict__ G, int w0, int nw, int NB2,
                                                      Xyzz<F>* __restrict__ Q) {
