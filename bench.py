@@ -353,12 +353,13 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
     curve, B = H.BN254, args.accum_batch
     shape = Wk.simple_example_shape(ctx, curve, args.accum_logn)
     batch = Wk.SyntheticBatch(ctx, shape, B, i0=rank * B)
+    from sharded import gather_batches
+
     gathered = [torch.zeros_like(batch.quads) for _ in range(world)] if dist else None
 
     def step():
         batch.run(ctx, shape)
-        if dist:
-            dist.all_gather(gathered, batch.quads)
+        gather_batches(batch.quads, dist, world, gathered)
 
     for _ in range(args.warmup):
         step()

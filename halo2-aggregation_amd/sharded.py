@@ -42,3 +42,18 @@ def combine_partials(part, dist, device, point_add, world: int, gathered=None):
     for g in gathered:
         acc = point_add(acc, g.cpu().numpy().view(np.uint64))
     return acc
+
+
+def gather_batches(local, dist, world: int, gathered=None):
+    """Accumulator batches: proofs are independent, so rank r
+    owns its own B proofs and the only collective is an all-gather of the
+    (B, 4, 8) accumulator points.  `local` is a torch tensor; returns the
+    (world * B, 4, 8) tensor in rank order (the local tensor when world == 1)."""
+    import torch
+
+    if world == 1:
+        return local
+    if gathered is None:
+        gathered = [torch.zeros_like(local) for _ in range(world)]
+    dist.all_gather(gathered, local)
+    return torch.cat(gathered, dim=0)

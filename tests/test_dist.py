@@ -81,3 +81,58 @@ def test_split_range_covers():
             parts = [split_range(r, w, n) for r in range(w)]
             assert sum(c for _, c in parts) == n
             assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1) if parts[i + 1][1])
+
+
+def _accum_worker(rank, world, port, B, q):
+    import sys
+
+    for p in (os.path.join(ROOT, "halo2-aggregation_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    import accum as A
+    import accum_util as U
+    import transcript as T
+    from sharded import gather_batches
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    C, sh, proofs = U.make_case(2, "simple", 10, world * B, 0xD15)
+    mine = proofs[rank * B:(rank + 1) * B]           # rank r owns proofs [rB, (r+1)B)
+    T.with_replayed_challenges(C, sh, mine, T.vk_repr(C.r, b"vk"))
+    quads = np.stack([A.pack_result(C, A.accumulate_msm(C, sh, pf))[0] for pf in mine])
+    full = gather_batches(torch.from_numpy(quads.view(np.int64)), dist, world)
+    q.put((rank, full.numpy().view(np.uint64).tolist()))
+    dist.destroy_process_group()
+
+
+def test_sharded_accumulator_gloo():
+    """Proof-batch sharding of the accumulator (bench.py's accumulator leg):
+    every rank ends with all world x B quads, in rank order, equal to the
+    oracle on the whole batch."""
+    import sys
+
+    for p in (os.path.join(ROOT, "halo2-aggregation_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import accum as A
+    import accum_util as U
+    import transcript as T
+
+    world, B = 2, 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    C, sh, proofs = U.make_case(2, "simple", 10, world * B, 0xD15)
+    T.with_replayed_challenges(C, sh, proofs, T.vk_repr(C.r, b"vk"))
+    want = np.stack([A.pack_result(C, A.accumulate_msm(C, sh, pf))[0] for pf in proofs])
+    for r in range(world):
+        assert np.array_equal(np.array(res[r], dtype=np.uint64), want), r
