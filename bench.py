@@ -74,6 +74,15 @@ def load_pmc_traffic(workload, launches_per_msm):
     return None
 
 
+def load_ntt_traffic(workload):
+    p = os.path.join(ROOT, "profiles", "pmc_ntt.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_ntt")
+    return None
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -310,8 +319,10 @@ def run_ntt(args, ctx, dist, dev, world):
            "kernels_ms": kernels,
            "roofline": {"bound": "hbm", "achieved": round(alg / (gpu_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": 4 * 32 * n, "note": "achieved = 64 B/element (read + write once) over both "
-                        "passes' kernel time; traffic = the two passes' 128 B/element (not PMC-measured)"}}
+                        "traffic": load_ntt_traffic(f"ntt_bn254_2^{k}"),
+                        "note": "achieved = 64 B/element (read + write once) over both passes' kernel time; "
+                                "traffic = PMC FETCH+WRITE of both passes (profiles/pmc_ntt.json); the NTT is "
+                                "VALU-bound (n/2 log n Montgomery products)"}}
     if src is not None:
         out["_state"] = (curve, k, src, w, first)
     return out
