@@ -40,8 +40,24 @@ void push_fe(std::vector<uint32_t>& v, const Fe<Fs>& a) {
 }
 
 template <class Cv>
+int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
+                           const void* d_scalars, void* d_ch, void* d_status);
+
+// Lanes per term of the split ladder: the largest power of two (<= 16) that
+// keeps B T S within about two waves per SIMD of the 1024 on an MI355X.
+constexpr size_t kAccLaneBudget = 1024 * 2 * 64;
+inline uint32_t acc_auto_split(size_t nterm) {
+  uint32_t lg = 0;
+  while (lg < 4 && (nterm << (lg + 1)) <= kAccLaneBudget) lg++;
+  return lg;
+}
+
+// vk_repr != nullptr: the challenges are first replayed into d_ch on the
+// device (transcript_device_impl); the split ladder then runs concurrently
+// with the replay and k_acc_scalars on the reduction stream.
+template <class Cv>
 int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d_points, const void* d_scalars,
-                      const void* d_ch, void* d_out, void* d_hout) {
+                      void* d_ch, void* d_out, void* d_hout, const uint64_t* vk_repr, void* d_status) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
@@ -50,6 +66,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   if (!err.empty()) return set_error(PM_ERR_ARG, "accum shape: " + err);
   if (B == 0) return PM_OK;
   if (B > (1u << 20)) return set_error(PM_ERR_UNSUPPORTED, "accum batch larger than 2^20 proofs");
+  if (vk_repr && !d_ch) return set_error(PM_ERR_ARG, "null challenge buffer");
 
   std::vector<int32_t> rots;
   std::vector<std::vector<AccQuery>> sets;
@@ -183,14 +200,38 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   const uint32_t* dprog = (const uint32_t*)ctx->acc_prog.p;
   uint32_t* dcoef = (uint32_t*)ctx->acc_coef.p;
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
+  const size_t nterm = (size_t)B * T;
+  const uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_split(nterm);
+  const uint32_t S = 1u << lgS, Lb = (kGlvBits + S - 1) / S;
+  hipEvent_t lad_done = nullptr;
+  if (lgS > 0) {  // ladder on the reduction stream, after this call's uploads
+    if ((rc = ctx->acc_lad.ensure(nterm * S * sizeof(Xyzz<F>)))) return rc;
+    hipEvent_t up = ctx->next_event();
+    lad_done = ctx->next_event();
+    if (!up || !lad_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+    HIP_TRY(hipEventRecord(up, st));
+    HIP_TRY(hipStreamWaitEvent(ctx->red_stream, up, 0));
+    PM_LAUNCH_ST(ctx, ctx->red_stream, "acc_ladder",
+                 (k_acc_ladder<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, ctx->red_stream>>>(
+                     h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.p, S, Lb,
+                     (Xyzz<F>*)ctx->acc_lad.p)));
+    HIP_TRY(hipEventRecord(lad_done, ctx->red_stream));
+  }
+  if (vk_repr && (rc = transcript_device_impl<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status))) return rc;
   PM_LAUNCH(ctx, "acc_scalars",
             (k_acc_scalars<Fs><<<(unsigned)((B + 63) / 64), 64, 0, st>>>(
                 h, dprog, (const uint32_t*)ctx->acc_const.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
                 dcoef, (uint32_t*)d_hout)));
-  const size_t nterm = (size_t)B * T;
-  PM_LAUNCH(ctx, "acc_termmul",
-            (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
-                h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.p, dpart)));
+  if (lgS > 0) {
+    HIP_TRY(hipStreamWaitEvent(st, lad_done, 0));
+    PM_LAUNCH(ctx, "acc_termmul",
+              (k_acc_termmul_split<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
+                  h, dcoef, (const Xyzz<F>*)ctx->acc_lad.p, lgS, Lb, dpart)));
+  } else {
+    PM_LAUNCH(ctx, "acc_termmul",
+              (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
+                  h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.p, dpart)));
+  }
   PM_LAUNCH(ctx, "acc_sum",
             (k_acc_sum<Cv><<<(unsigned)((B * 4 + 63) / 64), 64, 0, st>>>(h, dpart, (uint32_t*)d_out)));
   HIP_TRY(hipStreamSynchronize(st));
@@ -287,8 +328,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
   template int msm_device_to_aff<Cv>(Ctx*, const void*, const void*, size_t, uint32_t, uint64_t*); \
   template int synth_scalars_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, uint32_t, void*);     \
   template int synth_bases_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, void*);                 \
-  template int accum_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, const void*, \
-                                     void*, void*);                                              \
+  template int accum_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, void*, void*, \
+                                     void*, const uint64_t*, void*);                             \
   template int selftest_field_impl<Cv>(Ctx*, uint64_t, uint32_t, uint64_t*);                      \
   template int fixed_table_impl<Cv>(Ctx*, const void*, pm_fixed_bases*);                          \
   template int ntt_device_impl<Cv>(Ctx*, int, void*, uint32_t, const uint64_t*, const uint64_t*);  \

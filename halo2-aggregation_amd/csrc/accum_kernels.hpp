@@ -381,6 +381,106 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
   store_xyzz29<F>(&part[g], aff_is_inf<F>(P) ? xyzz29_inf<F>() : glv_mul<Cv>(c, P));
 }
 
+// ---------------------------------------------------------------- split ladder
+// At small batches one lane per term leaves most SIMDs idle and the term
+// multiplication is a 130-step latency chain.  The split form gives each term
+// S lanes: lane j owns bits [j L, (j + 1) L) of both GLV halves and multiplies
+// Q_j = [2^{j L}] P by them (L steps); the S partials are summed by a
+// butterfly of cross-lane shuffles.  The Q_j come from k_acc_ladder, which
+// depends only on the points, so it runs on a second stream while the
+// transcript replay and k_acc_scalars derive the coefficients.
+//
+// k_acc_ladder: one lane per (proof, term): Q_0 = P, Q_{j+1} = [2^L] Q_j,
+// stored packed (R261 XYZZ, storage bounds of curve29.hpp) at lad[g S + j].
+template <class Cv>
+__global__ void __launch_bounds__(256) k_acc_ladder(AccumHdr h, const uint32_t* __restrict__ prog,
+                                                    const uint32_t* __restrict__ points,
+                                                    const uint32_t* __restrict__ vk, uint32_t S, uint32_t L,
+                                                    Xyzz<typename Cv::Base>* __restrict__ lad) {
+  using F = typename Cv::Base;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= h.B * h.T) return;
+  const uint32_t b = g / h.T, t = g - b * h.T;
+  const uint32_t src = prog[h.p_termsrc + t];
+  const uint32_t idx = src & 0x0FFFFFFFu;
+  const uint32_t* pp = (src >> 28) == 0 ? points + 16ull * ((size_t)h.npts * b + idx) : vk + 16ull * idx;
+  const Aff<F> P = load_aff<F>(pp);
+  Xyzz<F>* out = lad + (size_t)g * S;
+  const uint32_t nq = (kGlvBits + L - 1) / L;  // Q_j actually used (nq <= S)
+  if (aff_is_inf<F>(P)) {
+    for (uint32_t j = 0; j < nq; j++) store_xyzz29<F>(&out[j], xyzz29_inf<F>());
+    return;
+  }
+  const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
+  Xyzz29<F> q{px, py, f29_const<F>(F29Consts<F>::ONE), f29_const<F>(F29Consts<F>::ONE)};
+  store_xyzz29<F>(&out[0], q);
+  for (uint32_t j = 1; j < nq; j++) {
+    for (uint32_t d = 0; d < L; d++) q = xyzz29_dbl_impl<F, false>(q.X, q.Y, q.ZZ, q.ZZZ);
+    store_xyzz29<F>(&out[j], q);
+  }
+}
+
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_shfl_xor(const Xyzz29<F>& p, int m) {
+  Xyzz29<F> r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    r.X.l[i] = __shfl_xor(p.X.l[i], m, 64);
+    r.Y.l[i] = __shfl_xor(p.Y.l[i], m, 64);
+    r.ZZ.l[i] = __shfl_xor(p.ZZ.l[i], m, 64);
+    r.ZZZ.l[i] = __shfl_xor(p.ZZZ.l[i], m, 64);
+  }
+  return r;
+}
+
+// k_acc_termmul_split: S lanes per (proof, term) (S a power of two <= 64, so a
+// group never straddles a wave); lane j: sum over i in [j L, (j + 1) L) of
+// [k1_i 2^{i - j L}] (+-Q_j) + [k2_i 2^{i - j L}] (+-phi(Q_j)), joint
+// double-and-add with full XYZZ additions; then log2(S) butterfly steps and
+// lane 0 stores the term's point.  phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ).
+template <class Cv>
+__global__ void __launch_bounds__(256) k_acc_termmul_split(AccumHdr h, const uint32_t* __restrict__ coef,
+                                                           const Xyzz<typename Cv::Base>* __restrict__ lad,
+                                                           uint32_t lgS, uint32_t L,
+                                                           Xyzz<typename Cv::Base>* __restrict__ part) {
+  using F = typename Cv::Base;
+  using Fs = typename Cv::Scalar;
+  using K = F29Consts<F>;
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t S = 1u << lgS, g = gl >> lgS, j = gl & (S - 1);
+  if (g >= h.B * h.T) return;  // whole groups only: B T S lanes, groups aligned
+  uint32_t k1[6], k2[6];
+  bool n1, n2;
+  glv_split<Cv>(ldfe<Fs>(coef, g), k1, k2, n1, n2);
+  const uint32_t lo = j * L, hi = min(lo + L, (uint32_t)kGlvBits);
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  if (lo < hi) {
+    const Xyzz29<F> Q = load_xyzz29<F>(&lad[(size_t)g * S + j]);
+    // Y < 3p -> 6p - Y reduced below 3p (dbl needs Y < 4p)
+    const F29<F> yneg = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), Q.Y, K::K6)));
+    const Xyzz29<F> T1{Q.X, n1 ? yneg : Q.Y, Q.ZZ, Q.ZZZ};
+    const Xyzz29<F> T2{f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), Q.X), n2 ? yneg : Q.Y, Q.ZZ, Q.ZZZ};
+    const Xyzz29<F> T3 = xyzz29_add<F>(T1, T2);
+    for (int i = (int)hi - 1; i >= (int)lo; i--) {
+      acc = xyzz29_dbl<F>(acc);
+      const uint32_t b1 = (k1[i >> 5] >> (i & 31)) & 1u, b2 = (k2[i >> 5] >> (i & 31)) & 1u;
+      const uint32_t sel = b1 | (b2 << 1);
+      if (sel == 0) continue;
+      Xyzz29<F> q;
+#pragma unroll
+      for (int t = 0; t < 9; t++) {
+        q.X.l[t] = sel == 1 ? T1.X.l[t] : sel == 2 ? T2.X.l[t] : T3.X.l[t];
+        q.Y.l[t] = sel == 1 ? T1.Y.l[t] : sel == 2 ? T2.Y.l[t] : T3.Y.l[t];
+        q.ZZ.l[t] = sel == 3 ? T3.ZZ.l[t] : T1.ZZ.l[t];
+        q.ZZZ.l[t] = sel == 3 ? T3.ZZZ.l[t] : T1.ZZZ.l[t];
+      }
+      acc = xyzz29_add<F>(acc, q);
+    }
+  }
+  for (uint32_t m = 1; m < S; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
+  if (j == 0) store_xyzz29<F>(&part[g], acc);
+}
+
 template <class Cv>
 __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename Cv::Base>* __restrict__ part,
                                                 uint32_t* __restrict__ out) {

@@ -265,6 +265,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_PREFETCH")) c->prefetch = std::atoi(e);
   if (const char* e = std::getenv("PM_GROUPS")) c->groups = std::atoi(e);
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
+  if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   *out = c.release();
   return PM_OK;
 }
@@ -278,6 +279,14 @@ int pm_ctx_set_stream(pm_ctx* ctx, void* s) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+  return PM_OK;
+}
+
+int pm_ctx_set_accum_split(pm_ctx* ctx, int lg_lanes) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  if (lg_lanes < -1 || lg_lanes > 6) return set_error(PM_ERR_ARG, "accum split out of range (-1 auto, 0..6)");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->acc_split = lg_lanes;
   return PM_OK;
 }
 
@@ -615,7 +624,8 @@ int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, s
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();
   if (rc) return rc;
-  return ops->accum(ctx, shape, B, d_points, d_scalars, d_challenges, d_out_quads, d_out_h_eval);
+  return ops->accum(ctx, shape, B, d_points, d_scalars, const_cast<void*>(d_challenges), d_out_quads, d_out_h_eval, nullptr,
+                    nullptr);
 }
 
 int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t* points,
@@ -638,7 +648,7 @@ int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B
   HIP_TRY(hipMemcpyAsync(base + bp + bs, challenges, bc, hipMemcpyHostToDevice, ctx->stream));
   char* dq = base + bp + bs + bc;
   char* dh = dq + bo;
-  if ((rc = ops->accum(ctx, shape, B, base, base + bp, base + bp + bs, dq, dh))) return rc;
+  if ((rc = ops->accum(ctx, shape, B, base, base + bp, base + bp + bs, dq, dh, nullptr, nullptr))) return rc;
   HIP_TRY(hipMemcpyAsync(out_quads, dq, bo, hipMemcpyDeviceToHost, ctx->stream));
   if (out_h_eval) HIP_TRY(hipMemcpyAsync(out_h_eval, dh, bh, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -687,8 +697,7 @@ int pm_accum_batch_transcript_device(pm_ctx* ctx, int curve, const pm_proof_shap
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();
   if (rc) return rc;
-  if ((rc = ops->transcript(ctx, shape, B, vk_repr, d_points, d_scalars, d_challenges, d_out_status))) return rc;
-  return ops->accum(ctx, shape, B, d_points, d_scalars, d_challenges, d_out_quads, d_out_h_eval);
+  return ops->accum(ctx, shape, B, d_points, d_scalars, d_challenges, d_out_quads, d_out_h_eval, vk_repr, d_out_status);
 }
 
 // Host-buffer variants share one staging layout in acc_io:
@@ -717,8 +726,11 @@ static int transcript_host(pm_ctx* ctx, int curve, const pm_proof_shape* shape, 
   char* dst = dh + bh;
   HIP_TRY(hipMemcpyAsync(dp, points, bp, hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipMemcpyAsync(ds, scalars, bs, hipMemcpyHostToDevice, ctx->stream));
-  if ((rc = ops->transcript(ctx, shape, B, vk_repr, dp, ds, dc, dst))) return rc;
-  if (accum && (rc = ops->accum(ctx, shape, B, dp, ds, dc, dq, dh))) return rc;
+  if (accum) {
+    if ((rc = ops->accum(ctx, shape, B, dp, ds, dc, dq, dh, vk_repr, dst))) return rc;
+  } else if ((rc = ops->transcript(ctx, shape, B, vk_repr, dp, ds, dc, dst))) {
+    return rc;
+  }
   if (out_challenges) HIP_TRY(hipMemcpyAsync(out_challenges, dc, bc, hipMemcpyDeviceToHost, ctx->stream));
   if (accum) HIP_TRY(hipMemcpyAsync(out_quads, dq, bo, hipMemcpyDeviceToHost, ctx->stream));
   if (accum && out_h_eval) HIP_TRY(hipMemcpyAsync(out_h_eval, dh, bh, hipMemcpyDeviceToHost, ctx->stream));

@@ -181,9 +181,12 @@ __device__ __forceinline__ void mc_n(uint64_t& acc, const uint32_t* x, const uin
   }
 }
 
-// Column-chained forms of f29_mul / f29_sqr (same arithmetic, same result).
+// Column-chained forms of f29_mul / f29_sqr (same arithmetic, same result),
+// generic over the field: up to four multiply-adds per asm statement, the
+// power-of-two limb and p_0 = 1 folded in as 64-bit shift-adds.  The hot
+// paths use the generated per-field forms below (f29_mul_a / f29_sqr_a).
 template <class P>
-__device__ __forceinline__ F29<P> f29_mul_c(const F29<P>& a, const F29<P>& b) {
+__device__ __forceinline__ F29<P> f29_mul_g(const F29<P>& a, const F29<P>& b) {
   using K = F29Consts<P>;
   uint32_t m[9];
   F29<P> r;
@@ -230,7 +233,7 @@ __device__ __forceinline__ F29<P> f29_mul_c(const F29<P>& a, const F29<P>& b) {
 }
 
 template <class P>
-__device__ __forceinline__ F29<P> f29_sqr_c(const F29<P>& a) {
+__device__ __forceinline__ F29<P> f29_sqr_g(const F29<P>& a) {
   using K = F29Consts<P>;
   uint32_t m[9], d[9];
   F29<P> r;
@@ -281,6 +284,24 @@ __device__ __forceinline__ F29<P> f29_sqr_c(const F29<P>& a) {
   }
   r.l[8] = (uint32_t)acc;
   return r;
+}
+
+// One asm statement per product column, generated per field by
+// tools/gen_fp29_asm.py (fp29_asm.hpp, included at the end of this file):
+// every multiply-add of a column in one chain, including the reduction's
+// power-of-two limb and p_0, so no 64-bit shift-adds, no {m, 0} register
+// pairs and one s_nop pad per column.  Mul: 187 VALU instead of 200 (Pasta).
+template <class P>
+__device__ F29<P> f29_mul_a(const F29<P>& a, const F29<P>& b);
+template <class P>
+__device__ F29<P> f29_sqr_a(const F29<P>& a);
+template <class P>
+__device__ __forceinline__ F29<P> f29_mul_c(const F29<P>& a, const F29<P>& b) {
+  return f29_mul_a<P>(a, b);
+}
+template <class P>
+__device__ __forceinline__ F29<P> f29_sqr_c(const F29<P>& a) {
+  return f29_sqr_a<P>(a);
 }
 
 // Montgomery product a * b * 2^-261 mod p (lazy: Norm, < 2p), product scanning
@@ -416,11 +437,21 @@ __device__ __forceinline__ F29<P> f29_canon(const F29<P>& a) {
 // v Norm, < 8p: v == 0 mod p?  Cheap limb-0 filter (v = j p, j < 8, has
 // limb 0 = (j p) mod 2^29); the exact check runs only on a hit.
 template <class P>
+constexpr bool f29_jp0_linear() {  // (j p) mod 2^29 == j: p = 1 mod 2^29 (Pasta)
+  for (int j = 0; j < 8; j++)
+    if (F29Consts<P>::JP0[j] != (uint32_t)j) return false;
+  return true;
+}
+template <class P>
 __device__ __forceinline__ bool f29_is_zero_mod(const F29<P>& v) {
   using K = F29Consts<P>;
   bool hit = false;
+  if constexpr (f29_jp0_linear<P>()) {
+    hit = v.l[0] < 8u;  // one compare instead of eight
+  } else {
 #pragma unroll
-  for (int j = 0; j < 8; j++) hit |= v.l[0] == K::JP0[j];
+    for (int j = 0; j < 8; j++) hit |= v.l[0] == K::JP0[j];
+  }
   if (!hit) return false;
   return f29_is_zero_exact<P>(f29_canon<P>(f29_reduce3<P>(v)));
 }
@@ -463,3 +494,5 @@ __device__ __forceinline__ Fe<P> fe_inv_fast(const Fe<P>& a) {
 }
 
 }  // namespace pm
+
+#include "fp29_asm.hpp"

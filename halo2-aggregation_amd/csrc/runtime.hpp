@@ -108,13 +108,14 @@ struct pm_ctx {
   int prefetch = -1;  // -1 auto, 0 off, 1 on (diagnostics: PM_PREFETCH env)
   int groups = 0;     // window groups, 0 = auto (diagnostics: PM_GROUPS env)
   int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
+  int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)
   bool timed(const char* name) const { return timing && (timing_filter.empty() || timing_filter == name); }
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets, ntt_scratch, bitsQ;
+      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad;
   std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;
@@ -128,7 +129,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ};
+            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad};
   }
   ~pm_ctx();
   int begin_call();
@@ -152,8 +153,9 @@ struct CurveOps {
   int (*point_add)(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
   int (*synth_scalars)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, uint32_t mont, void* d_out);
   int (*synth_bases)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, void* d_out);
+  // vk_repr != nullptr: replay the transcript into d_challenges first (d_status as in transcript)
   int (*accum)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const void* d_points, const void* d_scalars,
-               const void* d_challenges, void* d_out_quads, void* d_out_h);
+               void* d_challenges, void* d_out_quads, void* d_out_h, const uint64_t* vk_repr, void* d_status);
   int (*selftest_field)(Ctx* ctx, uint64_t seed, uint32_t n, uint64_t* mismatches);
   int (*transcript)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4], const void* d_points,
                     const void* d_scalars, void* d_challenges, void* d_status);

@@ -206,6 +206,7 @@ def _load():
         "pm_ctx_set_stream": ([_vp, _vp], ctypes.c_int),
         "pm_ctx_set_window": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_accum_split": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing_filter": ([_vp, ctypes.c_char_p], ctypes.c_int),
         "pm_ctx_kernel_stats": ([_vp, ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
@@ -419,6 +420,10 @@ class Context:
 
     def set_pipeline(self, groups=0, min_chunk=0):
         _check(lib().pm_ctx_set_pipeline(self.h, groups, min_chunk))
+
+    def set_accum_split(self, lg_lanes=-1):
+        """Accumulator lanes per MSM term = 2^lg_lanes (-1 = automatic)."""
+        _check(lib().pm_ctx_set_accum_split(self.h, lg_lanes))
 
     def set_timing(self, on=True, only=None):
         """HIP-event timing; `only` restricts events to one kernel name (each

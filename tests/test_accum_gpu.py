@@ -33,6 +33,26 @@ def test_golden_accumulator(gpu_ctx):
         assert np.array_equal(quads, npz[f"{name}.quads"]), name
 
 
+@pytest.mark.parametrize("lg", [0, 1, 2, 3, 4, 6])
+def test_split_ladder_widths(gpu_ctx, lg):
+    """Every lanes-per-term setting of the term multiplication (2^lg lanes,
+    k_acc_ladder + k_acc_termmul_split; lg = 0 is the one-lane GLV kernel)
+    reproduces the golden vectors, including the identity / W_1 = -W_0 edge
+    case, and random rich-shape proofs on Pallas."""
+    gpu_ctx.set_accum_split(lg)
+    try:
+        test_golden_accumulator(gpu_ctx)
+        C, sh, proofs = U.make_case(0, "rich", 12, 3, 0x5917 + lg)
+        ps = U.to_product_shape(0, sh)
+        pts, scs, chs = A.pack_proofs(C, sh, proofs)
+        quads, h = gpu_ctx.accum_batch(ps, pts, scs, chs)
+        for b, pf in enumerate(proofs):
+            q, hh = A.pack_result(C, A.accumulate_msm(C, sh, pf))
+            assert np.array_equal(h[b], hh) and np.array_equal(quads[b], q), b
+    finally:
+        gpu_ctx.set_accum_split(-1)
+
+
 @pytest.mark.parametrize("cid", [0, 1, 2])
 @pytest.mark.parametrize("shape", ["simple", "rich"])
 def test_random_proofs_vs_oracle(gpu_ctx, cid, shape):

@@ -1,0 +1,118 @@
+"""CPU: the generated per-column asm of csrc/fp29_asm.hpp (tools/gen_fp29_asm.py)
+computes the radix-2^29 Montgomery product a b 2^-261 mod p.
+
+The header is executed here by a small interpreter of exactly the constructs
+the generator emits (v_mad_u64_u32 chains, v_lshrrev_b64, and the C lines that
+derive m_k / the output limbs from the accumulator's low word), with 64-bit
+wrap-around checks, so a generator bug is caught without a GPU.  The device
+self-test (tests/test_msm_gpu.py::test_radix29_field_selftest) checks the same
+functions on the MI355X against the 32-bit arithmetic."""
+import os
+import random
+import re
+
+import pasta as P
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "halo2-aggregation_amd", "csrc", "fp29_asm.hpp")
+M29 = (1 << 29) - 1
+M64 = (1 << 64) - 1
+FIELDS = {"PallasFp": P.PALLAS_P, "VestaFp": P.VESTA_P, "Bn254Fq": P.BN254_P, "Bn254Fr": P.BN254_R}
+
+
+def _functions():
+    src = open(HDR).read()
+    out = {}
+    for m in re.finditer(r"F29<(\w+)> (f29_(?:mul|sqr)_a)<\w+>\((.*?)\) \{\n(.*?)\n\}\n", src, re.S):
+        out[(m.group(2), m.group(1))] = m.group(4)
+    return out
+
+
+def _run(body, a, b=None):
+    env = {"a.l": list(a), "b.l": list(b) if b is not None else None, "m": [0] * 9, "r.l": [0] * 9, "d": [0] * 8}
+    acc = 0
+
+    def val(expr):
+        expr = expr.strip()
+        mm = re.fullmatch(r"([a-z.]+)\[(\d+)\]", expr)
+        if mm:
+            return env[mm.group(1)][int(mm.group(2))]
+        return int(expr.rstrip("u"))
+
+    stmts = re.findall(r'asm\("(.*?)"\s*:\s*"\+v"\(acc\), "=&s"\(c\)\s*:\s*(.*?)\);|^  (?!asm)([^\n]*?);$', body, re.S | re.M)
+    for text, ins, cline in stmts:
+        if text:
+            ops = [val(x.split("(", 1)[1][:-1]) for x in re.findall(r'"[vs]"\([^)]*\)', ins)]
+            for ins_text in text.split("\\n\\t"):
+                f = [x.strip() for x in ins_text.replace(",", " ").split()]
+                if f[0] == "v_mad_u64_u32":
+                    assert f[1] == "%0" and f[2] == "%1" and f[5] == "%0"
+                    x = ops[int(f[3][1:]) - 2] if f[3].startswith("%") else int(f[3])
+                    y = ops[int(f[4][1:]) - 2] if f[4].startswith("%") else int(f[4])
+                    assert x < 2 ** 32 and y < 2 ** 32
+                    acc += x * y
+                    assert acc <= M64, "column overflow"
+                elif f[0] == "v_lshrrev_b64":
+                    assert f[1:] == ["%0", "29", "%0"]
+                    acc >>= 29
+                else:
+                    raise AssertionError(ins_text)
+            continue
+        c = cline
+        if c.startswith("for (int i = 0; i < 8; i++) d[i] = a.l[i] << 1"):
+            env["d"] = [(x << 1) & 0xFFFFFFFF for x in env["a.l"][:8]]
+        elif re.fullmatch(r"m\[\d\] = \(0u - \(uint32_t\)acc\) & kM29", c):
+            env["m"][int(c[2])] = (-(acc & 0xFFFFFFFF)) & M29
+        elif re.fullmatch(r"m\[\d\] = \(\(uint32_t\)acc \* \d+u\) & kM29", c):
+            inv = int(re.search(r"\* (\d+)u", c).group(1))
+            env["m"][int(c[2])] = ((acc & 0xFFFFFFFF) * inv) & M29
+        elif re.fullmatch(r"r\.l\[\d\] = \(uint32_t\)acc & kM29", c):
+            env["r.l"][int(c[4])] = acc & M29
+        elif c == "r.l[8] = (uint32_t)(acc >> 29)":
+            assert acc >> 29 < 2 ** 32
+            env["r.l"][8] = acc >> 29
+        elif not re.fullmatch(r"F29<\w+> r|uint32_t (m|d)\[\d\]|uint64_t acc = 0, c|\(void\)c|return r", c):
+            raise AssertionError("unhandled line: " + c)
+    return env["r.l"]
+
+
+def _limbs(v):
+    return [(v >> (29 * i)) & M29 for i in range(9)]
+
+
+def _value(l):
+    return sum(x << (29 * i) for i, x in enumerate(l))
+
+
+def test_generated_header_is_current():
+    import subprocess
+    import sys
+
+    gen = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_fp29_asm.py")], capture_output=True,
+                         text=True, check=True).stdout
+    assert gen == open(HDR).read(), "fp29_asm.hpp is stale: rerun tools/gen_fp29_asm.py"
+
+
+@pytest.mark.parametrize("field", sorted(FIELDS))
+def test_column_asm_products(field):
+    p = FIELDS[field]
+    fns = _functions()
+    mul, sqr = fns[("f29_mul_a", field)], fns[("f29_sqr_a", field)]
+    rinv = pow(1 << 261, -1, p)
+    rng = random.Random(0xA5A5 + len(field))
+    vals = [0, 1, p - 1, p - 2, 2 * p - 1, 3 * p + 7, 4 * p - 1] + [rng.randrange(4 * p) for _ in range(40)]
+    for i, x in enumerate(vals):
+        y = vals[(7 * i + 3) % len(vals)]
+        r = _run(mul, _limbs(x), _limbs(y))
+        assert all(l <= M29 for l in r[:8])
+        assert _value(r) % p == x * y * rinv % p and _value(r) < 2 * p
+        r = _run(sqr, _limbs(x))
+        assert _value(r) % p == x * x * rinv % p and _value(r) < 2 * p
+    # loose operand limbs (a + 6p limb-wise, the f29_sub form) on the mul path
+    K6 = [l + (1 << 29) - 1 for l in _limbs(0)]  # stands in for a loose limb pattern < 2^30
+    x = rng.randrange(p)
+    lx = [a + b for a, b in zip(_limbs(x), K6)]
+    y = rng.randrange(2 * p)
+    r = _run(mul, lx, _limbs(y))
+    assert _value(r) % p == _value(lx) * y * rinv % p

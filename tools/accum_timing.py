@@ -12,13 +12,15 @@ import torch  # noqa: E402
 import accum_util as U  # noqa: E402
 import halo2_amd as H  # noqa: E402
 
-KERNELS = ["transcript", "acc_scalars", "acc_termmul", "acc_sum"]
+KERNELS = ["transcript", "acc_ladder", "acc_scalars", "acc_termmul", "acc_sum"]
 
 
 def main():
     curve = int(os.environ.get("CURVE", "2"))
     ctx = H.Context(0)
-    for shape, log_n, B in [("simple", 14, 16), ("simple", 17, 256), ("simple", 17, 4096), ("rich", 17, 256)]:
+    splits = [int(x) for x in os.environ.get("SPLITS", "-1").split(",")]
+    for split, shape, log_n, B in [(sp,) + c for sp in splits for c in [("simple", 14, 16), ("simple", 17, 256), ("simple", 17, 4096), ("rich", 17, 256)]]:
+        ctx.set_accum_split(split)
         C, sh, _ = U.make_case(curve, shape, log_n, 0, 0x5EED)
         ps = U.to_product_shape(curve, sh)
         npts, nsc, _ = ps.layout()
@@ -55,7 +57,7 @@ def main():
             run()
         ctx.set_timing(False)
         ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}
-        print(json.dumps({"transcript": fused, "shape": shape, "log_n": log_n, "B": B, "wall_ms": round(wall * 1e3, 3),
+        print(json.dumps({"split": split, "transcript": fused, "shape": shape, "log_n": log_n, "B": B, "wall_ms": round(wall * 1e3, 3),
                           "proofs_per_s": round(B / wall, 1), "kernels_ms": ks}), flush=True)
 
 
