@@ -43,12 +43,15 @@ template <class Cv>
 int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
                            const void* d_scalars, void* d_ch, void* d_status);
 
-// Lanes per term of the split ladder: the largest power of two (<= 16) that
-// keeps B T S within about two waves per SIMD of the 1024 on an MI355X.
+// Lanes per item for the latency-bound accumulator kernels: the largest
+// power of two 2^lg <= 2^maxlg that keeps items * 2^lg within about two
+// waves per SIMD of the 1024 on an MI355X.  Split ladder: maxlg = 3 (8 lanes
+// x 16 bits: 112 ladder doublings; 16 x 8 measured no faster, the wider
+// butterfly and the second wave per SIMD cost what the shorter loop saves).
 constexpr size_t kAccLaneBudget = 1024 * 2 * 64;
-inline uint32_t acc_auto_split(size_t nterm) {
+inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
   uint32_t lg = 0;
-  while (lg < 4 && (nterm << (lg + 1)) <= kAccLaneBudget) lg++;
+  while (lg < maxlg && (items << (lg + 1)) <= kAccLaneBudget) lg++;
   return lg;
 }
 
@@ -201,7 +204,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   uint32_t* dcoef = (uint32_t*)ctx->acc_coef.p;
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
   const size_t nterm = (size_t)B * T;
-  const uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_split(nterm);
+  const uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_lanes(nterm, 3);
   const uint32_t S = 1u << lgS, Lb = (kGlvBits + S - 1) / S;
   hipEvent_t lad_done = nullptr;
   if (lgS > 0) {  // ladder on the reduction stream, after this call's uploads
@@ -232,8 +235,10 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
               (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
                   h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.p, dpart)));
   }
+  const uint32_t lgL = acc_auto_lanes((size_t)B * 4, 5);
   PM_LAUNCH(ctx, "acc_sum",
-            (k_acc_sum<Cv><<<(unsigned)((B * 4 + 63) / 64), 64, 0, st>>>(h, dpart, (uint32_t*)d_out)));
+            (k_acc_sum<Cv><<<(unsigned)((B * 4 * (1u << lgL) + 63) / 64), 64, 0, st>>>(h, dpart, lgL,
+                                                                                      (uint32_t*)d_out)));
   HIP_TRY(hipStreamSynchronize(st));
   ctx->end_call();
   return PM_OK;

@@ -250,7 +250,7 @@ template <> struct Glv<Bn254Curve> {
   static constexpr uint32_t G2[9] = {0x2fafba64u, 0x8fa7d32du, 0x773a6ef2u, 0x6eb9c714u, 0xc7e0b3d7u, 0xd91d232eu, 0x00000002u, 0x00000000u, 0x00000000u};  // round(2^384 (-b1) / r)
 };
 
-constexpr int kGlvBits = 130;  // loop length (|k_i| < 2^128, margin for the floor())
+constexpr int kGlvBits = 128;  // loop length: |k_i| <= (|a1| + |a2|) (1 + 2^-120) < 2^127.8 (tests/test_glv.py)
 
 // x (nx limbs) * y (ny limbs) -> out (nx + ny limbs), schoolbook, plain C.
 template <int NX, int NY>
@@ -412,11 +412,11 @@ __global__ void __launch_bounds__(256) k_acc_ladder(AccumHdr h, const uint32_t* 
     return;
   }
   const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
-  Xyzz29<F> q{px, py, f29_const<F>(F29Consts<F>::ONE), f29_const<F>(F29Consts<F>::ONE)};
-  store_xyzz29<F>(&out[0], q);
+  Jac29<F> q{px, py, f29_const<F>(F29Consts<F>::ONE)};
+  store_xyzz29<F>(&out[0], Xyzz29<F>{px, py, q.Z, q.Z});
   for (uint32_t j = 1; j < nq; j++) {
-    for (uint32_t d = 0; d < L; d++) q = xyzz29_dbl_impl<F, false>(q.X, q.Y, q.ZZ, q.ZZZ);
-    store_xyzz29<F>(&out[j], q);
+    for (uint32_t d = 0; d < L; d++) q = jac29_dbl<F>(q);
+    store_xyzz29<F>(&out[j], jac29_to_xyzz<F>(q));
   }
 }
 
@@ -481,18 +481,24 @@ __global__ void __launch_bounds__(256) k_acc_termmul_split(AccumHdr h, const uin
   if (j == 0) store_xyzz29<F>(&part[g], acc);
 }
 
+// k_acc_sum: 2^lgL lanes per (proof, output) (lgL <= 5): lane l sums terms
+// lo + l, lo + l + 2^lgL, ...; a butterfly of cross-lane shuffles folds the
+// partials and lane 0 converts to the unique affine point (binary-GCD
+// inversion).  Outputs in MultiopenVar order w, zw, f, e.
 template <class Cv>
 __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename Cv::Base>* __restrict__ part,
-                                                uint32_t* __restrict__ out) {
+                                                uint32_t lgL, uint32_t* __restrict__ out) {
   using F = typename Cv::Base;
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= h.B * 4) return;
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t NL = 1u << lgL, g = gl >> lgL, lane = gl & (NL - 1);
+  if (g >= h.B * 4) return;  // whole groups only (a group never straddles a wave)
   const uint32_t b = g >> 2, o = g & 3;
-  // MultiopenVar order: w, zw, f, e
   const uint32_t lo = o == 0 ? h.nslots : o == 1 ? h.nslots + h.nsets : o == 2 ? 0 : h.T - 1;
   const uint32_t hi = o == 0 ? h.nslots + h.nsets : o == 1 ? h.nslots + 2 * h.nsets : o == 2 ? h.nslots : h.T;
   Xyzz29<F> acc = xyzz29_inf<F>();
-  for (uint32_t t = lo; t < hi; t++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
+  for (uint32_t t = lo + lane; t < hi; t += NL) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
+  for (uint32_t m = 1; m < NL; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
+  if (lane != 0) return;
   uint32_t wx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!xyzz29_is_inf<F>(acc)) {
     F29<F> x, y;

@@ -14,6 +14,7 @@
 // group elements regardless of input order.
 #pragma once
 #include "fp256.hpp"
+#include "inv_bgcd.hpp"
 
 namespace pm {
 
@@ -163,7 +164,7 @@ PM_HD Xyzz<F> xyzz_add(const Xyzz<F>& p, const Xyzz<F>& q) {
 template <class F>
 PM_HD Aff<F> xyzz_to_aff(const Xyzz<F>& p) {
   if (xyzz_is_inf<F>(p)) return aff_inf<F>();
-  const Fe<F> inv = fe_inv<F>(fe_mul<F>(p.ZZ, p.ZZZ));  // 1/(ZZ*ZZZ)
+  const Fe<F> inv = fe_inv_bgcd<F>(fe_mul<F>(p.ZZ, p.ZZZ));  // 1/(ZZ*ZZZ), binary GCD
   Aff<F> a;
   a.x = fe_mul<F>(p.X, fe_mul<F>(inv, p.ZZZ));  // X/ZZ
   a.y = fe_mul<F>(p.Y, fe_mul<F>(inv, p.ZZ));   // Y/ZZZ

@@ -86,6 +86,44 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_dbl(const Xyzz29<F>& p) {
   return xyzz29_dbl_impl<F, false>(p.X, p.Y, p.ZZ, p.ZZZ);
 }
 
+// ------------------------------------------------- Jacobian doubling chain
+// dbl-2009-l (a = 0) on Jacobian (X, Y, Z): 2M + 5S instead of XYZZ's 6M + 3S,
+// for pure doubling chains (the accumulator's ladder).  Inputs Norm with
+// X, Y < 3p, Z < 4p; outputs the same.  No identity handling: the chain starts
+// from an affine non-identity point of odd order, so it never reaches O.
+template <class F>
+struct Jac29 {
+  F29<F> X, Y, Z;
+};
+template <class F>
+__device__ __forceinline__ Jac29<F> jac29_dbl(const Jac29<F>& p) {
+  using K = F29Consts<F>;
+  const F29<F> A = f29_sqr_c<F>(p.X);                                     // < 2p
+  const F29<F> B = f29_sqr_c<F>(p.Y);                                     // < 2p
+  const F29<F> C = f29_sqr_c<F>(B);                                       // < 2p
+  const F29<F> s = f29_sqr_c<F>(f29_norm<F>(f29_add<F>(p.X, B)));         // (X + B)^2, X + B < 5p
+  const F29<F> u = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(s, f29_add<F>(A, C), K::K8x3)));  // (4p, 10p) -> < 3p
+  const F29<F> D = f29_reduce3<F>(f29_norm<F>(f29_add<F>(u, u)));         // < 3p
+  const F29<F> E = f29_norm<F>(f29_add<F>(f29_add<F>(A, A), A));          // < 6p
+  Jac29<F> r;
+  r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(E), f29_add<F>(D, D), K::K8x3)));  // (2p, 10p) -> < 3p
+  const F29<F> w = f29_sub<F>(D, r.X, K::K6);                            // loose limbs < 2^31, < 9p
+  F29<F> C8 = C;
+#pragma unroll
+  for (int i = 0; i < 9; i++) C8.l[i] = C.l[i] << 3;
+  C8 = f29_reduce3<F>(f29_norm<F>(C8));                                   // 8C < 16p -> < 3p
+  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_mul_c<F>(E, w), C8, K::K8x3)));  // (5p, 10p) -> < 3p
+  const F29<F> yz = f29_mul_c<F>(p.Y, p.Z);                              // < 2p
+  r.Z = f29_norm<F>(f29_add<F>(yz, yz));                                  // < 4p
+  return r;
+}
+// Jacobian -> XYZZ storage form (ZZ = Z^2, ZZZ = Z^3, both < 2p)
+template <class F>
+__device__ __forceinline__ Xyzz29<F> jac29_to_xyzz(const Jac29<F>& p) {
+  const F29<F> zz = f29_sqr_c<F>(p.Z);
+  return Xyzz29<F>{p.X, p.Y, zz, f29_mul_c<F>(zz, p.Z)};
+}
+
 // ------------------------------------------------------------ mixed add
 // madd-2008-s: acc + (x2, y2) with the base (canonical, R261) negated when
 // `neg`.  The caller tracks the identity of acc (acc_inf) and of the base.

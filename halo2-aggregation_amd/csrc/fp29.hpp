@@ -28,6 +28,7 @@
 // ZZ, ZZZ < 2p), so 3p < 2^256 and the 8 x u32 packed form holds them.
 #pragma once
 #include "fp256.hpp"
+#include "inv_bgcd.hpp"
 
 namespace pm {
 
@@ -48,6 +49,7 @@ template <> struct F29Consts<PallasFp> {
   static constexpr uint32_t K6[9] = {0x20000006u, 0x38792c6fu, 0x3375a964u, 0x2f2bd06eu, 0x20000cd9u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x017fffffu};  // 6p, limbs >= 2^29 - 1
   static constexpr uint32_t K8x3[9] = {0x60000008u, 0x6b4c3b3du, 0x79f2372fu, 0x698fc091u, 0x60001120u, 0x5ffffffdu, 0x5ffffffdu, 0x5ffffffdu, 0x01fffffdu};  // 8p, limbs >= 3 * 2^29 - 3
   static constexpr uint32_t JP0[8] = {0x00000000u, 0x00000001u, 0x00000002u, 0x00000003u, 0x00000004u, 0x00000005u, 0x00000006u, 0x00000007u};  // (j p) mod 2^29, j < 8
+  static constexpr uint32_t R783[9] = {0x087c2a3au, 0x04d0a808u, 0x0a88e396u, 0x0f66ba31u, 0x06fd7543u, 0x0d4ff50bu, 0x1f1a2028u, 0x12d9910du, 0x00049116u};  // 2^783 mod p: inverse fix-up (f29_inv)
   static constexpr uint32_t QMAGIC = 0x0003ffffu;  // floor(2^40 / (p_8 + 1))
 };
 template <> struct F29Consts<VestaFp> {
@@ -60,6 +62,7 @@ template <> struct F29Consts<VestaFp> {
   static constexpr uint32_t K6[9] = {0x20000006u, 0x2d4c162fu, 0x3efd4c51u, 0x2f2bd071u, 0x20000cd9u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x017fffffu};  // 6p, limbs >= 2^29 - 1
   static constexpr uint32_t K8x3[9] = {0x60000008u, 0x71bac83du, 0x6951bb15u, 0x698fc096u, 0x60001120u, 0x5ffffffdu, 0x5ffffffdu, 0x5ffffffdu, 0x01fffffdu};  // 8p, limbs >= 3 * 2^29 - 3
   static constexpr uint32_t JP0[8] = {0x00000000u, 0x00000001u, 0x00000002u, 0x00000003u, 0x00000004u, 0x00000005u, 0x00000006u, 0x00000007u};  // (j p) mod 2^29, j < 8
+  static constexpr uint32_t R783[9] = {0x1725f045u, 0x0bcb119eu, 0x05aace00u, 0x1fd24ea8u, 0x1ee82c09u, 0x038572d8u, 0x11fd9d97u, 0x06792c88u, 0x000bd037u};  // 2^783 mod p: inverse fix-up (f29_inv)
   static constexpr uint32_t QMAGIC = 0x0003ffffu;  // floor(2^40 / (p_8 + 1))
 };
 template <> struct F29Consts<Bn254Fq> {
@@ -72,6 +75,7 @@ template <> struct F29Consts<Bn254Fq> {
   static constexpr uint32_t K6[9] = {0x32edefaau, 0x261a4447u, 0x2aafd3d9u, 0x30fed0e4u, 0x212318cfu, 0x31238483u, 0x23e94785u, 0x3628e537u, 0x012259d5u};  // 6p, limbs >= 2^29 - 1
   static constexpr uint32_t K8x3[9] = {0x63e7ea38u, 0x682305b3u, 0x63951a75u, 0x76a91684u, 0x6c2ecbbdu, 0x76da0602u, 0x65370a05u, 0x72e1319du, 0x01832270u};  // 8p, limbs >= 3 * 2^29 - 3
   static constexpr uint32_t JP0[8] = {0x00000000u, 0x187cfd47u, 0x10f9fa8eu, 0x0976f7d5u, 0x01f3f51cu, 0x1a70f263u, 0x12edefaau, 0x0b6aecf1u};  // (j p) mod 2^29, j < 8
+  static constexpr uint32_t R783[9] = {0x0e2312b2u, 0x16c05ca2u, 0x0bc84389u, 0x1cdf310bu, 0x11adafddu, 0x032e568eu, 0x1d6ae48cu, 0x10d4cd1fu, 0x0026c2d2u};  // 2^783 mod p: inverse fix-up (f29_inv)
   static constexpr uint32_t QMAGIC = 0x00054a47u;  // floor(2^40 / (p_8 + 1))
 };
 
@@ -85,6 +89,7 @@ template <> struct F29Consts<Bn254Fr> {
   static constexpr uint32_t K6[9] = {0x20000006u, 0x3a5e0bbcu, 0x3628d9e4u, 0x2ee365b3u, 0x2122ef12u, 0x31238483u, 0x23e94785u, 0x3628e537u, 0x012259d5u};  // 6p, limbs >= 2^29 - 1
   static constexpr uint32_t K8x3[9] = {0x60000008u, 0x787d64f9u, 0x72e12284u, 0x7e848798u, 0x6c2e9416u, 0x76da0602u, 0x65370a05u, 0x72e1319du, 0x01832270u};  // 8p, limbs >= 3 * 2^29 - 3
   static constexpr uint32_t JP0[8] = {0x00000000u, 0x10000001u, 0x00000002u, 0x10000003u, 0x00000004u, 0x10000005u, 0x00000006u, 0x10000007u};  // (j p) mod 2^29, j < 8
+  static constexpr uint32_t R783[9] = {0x001fddb2u, 0x17d30b63u, 0x1a2600eeu, 0x09507c47u, 0x1496b29bu, 0x0b00a268u, 0x15b645ebu, 0x1f9fcb3du, 0x001baa96u};  // 2^783 mod p: inverse fix-up (f29_inv)
   static constexpr uint32_t QMAGIC = 0x00054a47u;  // floor(2^40 / (p_8 + 1))
 };
 
@@ -458,9 +463,10 @@ __device__ __forceinline__ bool f29_is_zero_mod(const F29<P>& v) {
 
 // a^(p-2) (Fermat inverse; 0 -> 0) by left-to-right square-and-multiply over
 // the constant exponent (lane-uniform control flow).  Input Norm < 4p,
-// output Norm < 2p, both in the R = 2^261 Montgomery form.
+// output Norm < 2p, both in the R = 2^261 Montgomery form.  Kept as the
+// reference for f29_inv (selftest).
 template <class P>
-__device__ F29<P> f29_inv(const F29<P>& a) {
+__device__ F29<P> f29_inv_fermat(const F29<P>& a) {
   uint32_t e[8], br = 0;
   const uint32_t two[8] = {2, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -471,6 +477,17 @@ __device__ F29<P> f29_inv(const F29<P>& a) {
     if ((e[bit >> 5] >> (bit & 31)) & 1u) r = f29_mul_c<P>(r, a);
   }
   return r;
+}
+
+// Inverse by the binary GCD (inv_bgcd.hpp, ~4x lower latency than Fermat):
+// a = y 2^261 (Norm, < 4p) -> canonical packed -> (y 2^261)^-1 -> times
+// 2^783 / 2^261 = y^-1 2^261.  Output Norm, < 2p; 0 -> 0.
+template <class P>
+__device__ F29<P> f29_inv(const F29<P>& a) {
+  uint32_t w[8], v[8];
+  f29_pack<P>(f29_canon<P>(a), w);
+  bg_inverse<P>(w, v);
+  return f29_mul_c<P>(f29_unpack<P>(v), f29_const<P>(F29Consts<P>::R783));
 }
 
 // R256 packed Montgomery (Rust layout, canonical) -> F29 (Norm, < 2p)
@@ -484,13 +501,11 @@ __device__ __forceinline__ void f29_to_r256(const F29<P>& a, uint32_t w[8]) {
   f29_pack<P>(f29_canon<P>(f29_mul_c<P>(a, f29_const<P>(F29Consts<P>::TO256))), w);
 }
 
-// Inverse of an R256 Montgomery element through the radix-2^29 arithmetic
-// (~40% lower latency than the 32-bit chain); same result as fe_inv.
+// Inverse of an R256 Montgomery element (binary GCD, inv_bgcd.hpp); same
+// result as fe_inv.
 template <class P>
 __device__ __forceinline__ Fe<P> fe_inv_fast(const Fe<P>& a) {
-  Fe<P> r;
-  f29_to_r256<P>(f29_inv<P>(f29_from_r256<P>(a.l)), r.l);
-  return r;
+  return fe_inv_bgcd<P>(a);
 }
 
 }  // namespace pm

@@ -81,6 +81,18 @@ __global__ void k_selftest_field(uint64_t seed, uint32_t n, uint32_t* __restrict
   uint32_t w[8];
   f29_pack<F>(f29_canon<F>(A), w);
   nb += !f29_eq_r256<F>(f29_unpack<F>(w), a);
+  // inversions: binary GCD (inv_bgcd.hpp) against Fermat, R256 and R261 forms
+  // (f29_inv takes Norm < 4p: T = 2A reduced below 3p exercises its
+  // canonicalisation)
+  const Fe<F> ia = fe_inv<F>(a);
+  const Fe<F> ib = fe_inv_fast<F>(a);
+  uint32_t d = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) d |= ia.l[k] ^ ib.l[k];
+  nb += d != 0;
+  nb += !f29_eq_r256<F>(f29_inv<F>(A), ia);
+  nb += !f29_eq_r256<F>(f29_inv<F>(T), fe_inv<F>(fe_add<F>(a, a)));
+  nb += !f29_eq_r256<F>(f29_inv_fermat<F>(A), ia);
   if (nb) atomicAdd(bad, nb);
 }
 

@@ -56,3 +56,5 @@ def test_glv_constants(name):
         k2 = c1 * -b1 - c2 * b2
         assert (k1 + k2 * lam - k) % C.r == 0
         assert abs(k1) < 1 << 128 and abs(k2) < 1 << 128
+    # provable bound behind kGlvBits = 128: |k_i| <= (|a1| + |a2|) or (|b1| + |b2|), times (1 + 2^-120)
+    assert max(abs(a1) + abs(a2), abs(b1) + abs(b2)) * (1 + 2.0 ** -100) < 2.0 ** 128

@@ -19,7 +19,9 @@ def main():
     curve = int(os.environ.get("CURVE", "2"))
     ctx = H.Context(0)
     splits = [int(x) for x in os.environ.get("SPLITS", "-1").split(",")]
-    for split, shape, log_n, B in [(sp,) + c for sp in splits for c in [("simple", 14, 16), ("simple", 17, 256), ("simple", 17, 4096), ("rich", 17, 256)]]:
+    for split, shape, log_n, B in [(sp,) + c for sp in splits for c in [("simple", 14, 16), ("simple", 17, 256), ("simple", 17, 4096), ("rich", 17, 256)]
+                                          if os.environ.get("CASES", "all") == "all" or "%s:%d" % (c[0], c[2]) in
+                                          os.environ["CASES"].split(",")]:
         ctx.set_accum_split(split)
         C, sh, _ = U.make_case(curve, shape, log_n, 0, 0x5EED)
         ps = U.to_product_shape(curve, sh)
@@ -46,11 +48,13 @@ def main():
                                        dh.data_ptr())
 
         run()
-        reps = 5
-        t = time.time()
+        reps = int(os.environ.get("REPS", "20"))
+        ts = []
         for _ in range(reps):
+            t = time.time()
             run()
-        wall = (time.time() - t) / reps
+            ts.append(time.time() - t)
+        wall = sorted(ts)[len(ts) // 2]  # median of single calls
         ctx.set_timing(True)
         ctx.reset_stats()
         for _ in range(reps):
