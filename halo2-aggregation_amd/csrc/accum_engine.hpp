@@ -49,6 +49,7 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
 // x 16 bits: 112 ladder doublings; 16 x 8 measured no faster, the wider
 // butterfly and the second wave per SIMD cost what the shorter loop saves).
 constexpr size_t kAccLaneBudget = 1024 * 2 * 64;
+constexpr size_t kAccScalarsLds = 128 * 1024;
 inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
   uint32_t lg = 0;
   while (lg < maxlg && (items << (lg + 1)) <= kAccLaneBudget) lg++;
@@ -192,39 +193,50 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
 
   const hipStream_t st = ctx->stream;
   int rc;
-  if ((rc = ctx->acc_prog.ensure(prog.size() * 4))) return rc;
-  if ((rc = ctx->acc_const.ensure(cst.size() * 4 + 32))) return rc;
-  if ((rc = ctx->acc_vk.ensure(vk.size() * 8))) return rc;
+  if ((rc = ctx->acc_prog.put(prog, st))) return rc;
+  if ((rc = ctx->acc_const.put(cst, st, 32))) return rc;
+  if ((rc = ctx->acc_vk.put(vk, st))) return rc;
   if ((rc = ctx->acc_coef.ensure((size_t)B * T * 32))) return rc;
   if ((rc = ctx->acc_part.ensure((size_t)B * T * sizeof(Xyzz<F>)))) return rc;
-  HIP_TRY(hipMemcpyAsync(ctx->acc_prog.p, prog.data(), prog.size() * 4, hipMemcpyHostToDevice, st));
-  if (!cst.empty()) HIP_TRY(hipMemcpyAsync(ctx->acc_const.p, cst.data(), cst.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->acc_vk.p, vk.data(), vk.size() * 8, hipMemcpyHostToDevice, st));
-  const uint32_t* dprog = (const uint32_t*)ctx->acc_prog.p;
+  const uint32_t* dprog = (const uint32_t*)ctx->acc_prog.buf.p;
   uint32_t* dcoef = (uint32_t*)ctx->acc_coef.p;
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
   const size_t nterm = (size_t)B * T;
   const uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_lanes(nterm, 3);
   const uint32_t S = 1u << lgS, Lb = (kGlvBits + S - 1) / S;
-  hipEvent_t lad_done = nullptr;
-  if (lgS > 0) {  // ladder on the reduction stream, after this call's uploads
+  hipEvent_t lad_done = nullptr, up = nullptr;
+  if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
     if ((rc = ctx->acc_lad.ensure(nterm * S * sizeof(Xyzz<F>)))) return rc;
-    hipEvent_t up = ctx->next_event();
+    up = ctx->next_event();
     lad_done = ctx->next_event();
     if (!up || !lad_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(up, st));
-    HIP_TRY(hipStreamWaitEvent(ctx->red_stream, up, 0));
-    PM_LAUNCH_ST(ctx, ctx->red_stream, "acc_ladder",
-                 (k_acc_ladder<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, ctx->red_stream>>>(
-                     h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.p, S, Lb,
-                     (Xyzz<F>*)ctx->acc_lad.p)));
-    HIP_TRY(hipEventRecord(lad_done, ctx->red_stream));
   }
   if (vk_repr && (rc = transcript_device_impl<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status))) return rc;
+  // k_acc_scalars stages (nsc + T) rows of 32 B per proof in LDS (lane
+  // stride nl + 1): proofs per block nl <= 64 within a 128 KiB budget
+  const size_t row_bytes = (size_t)(L.nsc + T) * 32;
+  const uint32_t nl = (uint32_t)std::min<size_t>(64, kAccScalarsLds / row_bytes - 1);
+  if (nl == 0) return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
+  const size_t lds = row_bytes * (nl + 1);
   PM_LAUNCH(ctx, "acc_scalars",
-            (k_acc_scalars<Fs><<<(unsigned)((B + 63) / 64), 64, 0, st>>>(
-                h, dprog, (const uint32_t*)ctx->acc_const.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
+            (k_acc_scalars<Fs><<<(unsigned)((B + nl - 1) / nl), nl, lds, st>>>(
+                h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
                 dcoef, (uint32_t*)d_hout)));
+  // The ladder (points only) is launched after the transcript replay and
+  // k_acc_scalars (their few blocks are dispatched first); together with the
+  // cached uploads this took B = 256 from ~1.03 to ~0.85 ms.  Partitioning
+  // the CUs between the two streams (hipExtStreamCreateWithCUMask) measured
+  // no better.
+  if (lgS > 0) {  // ladder on the reduction stream, after this call's uploads
+    const hipStream_t sl = ctx->red_stream;
+    HIP_TRY(hipStreamWaitEvent(sl, up, 0));
+    PM_LAUNCH_ST(ctx, sl, "acc_ladder",
+                 (k_acc_ladder<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, sl>>>(
+                     h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, S, Lb,
+                     (Xyzz<F>*)ctx->acc_lad.p)));
+    HIP_TRY(hipEventRecord(lad_done, sl));
+  }
   if (lgS > 0) {
     HIP_TRY(hipStreamWaitEvent(st, lad_done, 0));
     PM_LAUNCH(ctx, "acc_termmul",
@@ -233,7 +245,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   } else {
     PM_LAUNCH(ctx, "acc_termmul",
               (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
-                  h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.p, dpart)));
+                  h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, dpart)));
   }
   const uint32_t lgL = acc_auto_lanes((size_t)B * 4, 5);
   PM_LAUNCH(ctx, "acc_sum",
@@ -290,11 +302,10 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
 
   const hipStream_t st = ctx->stream;
   int rc;
-  if ((rc = ctx->tr_prog.ensure(prog.size() * 4))) return rc;
-  HIP_TRY(hipMemcpyAsync(ctx->tr_prog.p, prog.data(), prog.size() * 4, hipMemcpyHostToDevice, st));
+  if ((rc = ctx->tr_prog.put(prog, st))) return rc;
   PM_LAUNCH(ctx, "transcript",
             (k_transcript<Cv><<<(unsigned)((B + 63) / 64), 64, 0, st>>>(
-                hd, (const uint32_t*)ctx->tr_prog.p, (const uint32_t*)d_points, (const uint32_t*)d_scalars,
+                hd, (const uint32_t*)ctx->tr_prog.buf.p, (const uint32_t*)d_points, (const uint32_t*)d_scalars,
                 (uint32_t*)d_ch, (uint32_t*)d_status)));
   return PM_OK;
 }

@@ -48,11 +48,33 @@ __device__ __forceinline__ void stfe(uint32_t* base, uint32_t idx, const Fe<Fs>&
   store_fe4<Fs>(reinterpret_cast<uint4*>(base + 8ull * idx), v);
 }
 
+// One lane's rows of field elements in LDS, word-major with a padded lane
+// stride (conflict-free when the lanes of a wave read the same row).
+// k_acc_scalars stages each proof's evaluations here once, with coalesced
+// loads, instead of ~60 dependent global loads per lane, and accumulates the
+// MSM coefficients here instead of read-modify-writes to global memory.
+struct LdsRows {
+  uint32_t* base;
+  uint32_t lane, stride;  // stride = lanes per block + 1
+  template <class Fs>
+  __device__ __forceinline__ Fe<Fs> get(uint32_t row) const {
+    Fe<Fs> r;
+#pragma unroll
+    for (int w = 0; w < 8; w++) r.l[w] = base[(row * 8 + w) * stride + lane];
+    return r;
+  }
+  template <class Fs>
+  __device__ __forceinline__ void put(uint32_t row, const Fe<Fs>& v) const {
+#pragma unroll
+    for (int w = 0; w < 8; w++) base[(row * 8 + w) * stride + lane] = v.l[w];
+  }
+};
+
 // Postfix program (compute_expr, verifier.rs:58-151); every END folds the
 // finished expression into acc = acc * mult + value (vanishing Horner in y,
 // or compress_expressions in theta, lookup.rs:214-243).
 template <class Fs>
-__device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const uint32_t* sc, const AccumHdr& h,
+__device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const LdsRows& sc, const AccumHdr& h,
                                 const uint32_t* consts, Fe<Fs> acc, const Fe<Fs>& mult) {
   Fe<Fs> st[kAccStack];
   int sp = 0;
@@ -61,11 +83,12 @@ __device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const uint32
     if (op == PM_EXPR_END) {
       acc = fe_add<Fs>(fe_mul<Fs>(acc, mult), st[--sp]);
     } else if (op <= PM_EXPR_INSTANCE) {
-      const uint32_t* src = op == PM_EXPR_CONST ? consts : sc;
-      const uint32_t base = op == PM_EXPR_CONST ? h.c_user
-                            : op == PM_EXPR_FIXED ? h.sc_fixed
-                            : op == PM_EXPR_ADVICE ? h.sc_adv : h.sc_inst;
-      st[sp++] = ldfe<Fs>(src, base + arg);
+      if (op == PM_EXPR_CONST) {
+        st[sp++] = ldfe<Fs>(consts, h.c_user + arg);
+      } else {
+        const uint32_t base = op == PM_EXPR_FIXED ? h.sc_fixed : op == PM_EXPR_ADVICE ? h.sc_adv : h.sc_inst;
+        st[sp++] = sc.get<Fs>(base + arg);
+      }
     } else if (op == PM_EXPR_NEG) {
       st[sp - 1] = fe_neg<Fs>(st[sp - 1]);
     } else if (op == PM_EXPR_SUM) {
@@ -87,11 +110,23 @@ __global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* 
                                                     const uint32_t* __restrict__ scalars,
                                                     const uint32_t* __restrict__ challenges,
                                                     uint32_t* __restrict__ coef, uint32_t* __restrict__ h_out) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  extern __shared__ uint32_t acc_lds[];  // (nsc + T) rows x 8 words x (blockDim + 1)
+  const uint32_t nl = blockDim.x, b0 = blockIdx.x * nl, b = b0 + threadIdx.x;
+  const uint32_t nv = min(nl, h.B - b0);  // proofs in this block
+  {  // coalesced staging of the block's evaluations (rows [0, nsc))
+    const uint32_t per = 8 * h.nsc;
+    const uint32_t* src = scalars + (size_t)per * b0;
+    for (uint32_t f = threadIdx.x; f < per * nv; f += nl) {
+      const uint32_t pl = f / per, k = f - pl * per;
+      acc_lds[k * (nl + 1) + pl] = src[f];
+    }
+  }
+  __syncthreads();
   if (b >= h.B) return;
-  const uint32_t* sc = scalars + 8ull * h.nsc * b;
+  const LdsRows sc{acc_lds, threadIdx.x, nl + 1};
+  const LdsRows cf{acc_lds + (size_t)8 * h.nsc * (nl + 1), threadIdx.x, nl + 1};  // coefficient rows
   const uint32_t* ch = challenges + 8ull * 7 * b;
-  uint32_t* cf = coef + 8ull * h.T * b;
+  uint32_t* cfg = coef + 8ull * h.T * b;
   const Fe<Fs> theta = ldfe<Fs>(ch, 0), beta = ldfe<Fs>(ch, 1), gamma = ldfe<Fs>(ch, 2), y = ldfe<Fs>(ch, 3),
                x = ldfe<Fs>(ch, 4), v = ldfe<Fs>(ch, 5), u = ldfe<Fs>(ch, 6);
   const Fe<Fs> one = fe_one<Fs>(), zero = fe_zero<Fs>();
@@ -130,10 +165,9 @@ __global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* 
   // expressions in order gates, permutation, lookups; h = h*y + expr
   Fe<Fs> hv = acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, zero, y);
   if (h.n_perm_sets) {
-    const uint32_t* ps = sc + 8ull * h.sc_perm;
-    auto zp = [&](uint32_t i) { return ldfe<Fs>(ps, 3 * i); };
-    auto zpn = [&](uint32_t i) { return ldfe<Fs>(ps, 3 * i + 1); };
-    auto zpl = [&](uint32_t i) { return ldfe<Fs>(ps, 3 * i + 2); };
+    auto zp = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i); };
+    auto zpn = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i + 1); };
+    auto zpl = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i + 2); };
     hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_0, fe_sub<Fs>(one, zp(0))));
     const Fe<Fs> zl = zp(h.n_perm_sets - 1);
     hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_last, fe_sub<Fs>(fe_sqr<Fs>(zl), zl)));
@@ -144,8 +178,8 @@ __global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* 
       Fe<Fs> left = zpn(ci), right = zp(ci);
       const uint32_t k1 = min(h.n_perm_cols, (ci + 1) * h.perm_chunk);
       for (uint32_t k = ci * h.perm_chunk; k < k1; k++) {
-        const Fe<Fs> ev = ldfe<Fs>(sc, prog[h.p_permcol + k]);
-        const Fe<Fs> sg = ldfe<Fs>(sc, h.sc_sigma + k);
+        const Fe<Fs> ev = sc.get<Fs>(prog[h.p_permcol + k]);
+        const Fe<Fs> sg = sc.get<Fs>(h.sc_sigma + k);
         left = fe_mul<Fs>(left, fe_add<Fs>(fe_add<Fs>(fe_mul<Fs>(beta, sg), ev), gamma));
         const Fe<Fs> t = fe_mul<Fs>(bx, ldfe<Fs>(consts, h.c_delta + k));
         right = fe_mul<Fs>(right, fe_add<Fs>(fe_add<Fs>(t, ev), gamma));
@@ -159,8 +193,8 @@ __global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* 
     const Fe<Fs> rfac = fe_mul<Fs>(fe_add<Fs>(cin, beta), fe_add<Fs>(ctab, gamma));
     for (uint32_t i = 0; i < h.num_lookups; i++) {
       const uint32_t e = h.sc_lk + 5 * i;
-      const Fe<Fs> z = ldfe<Fs>(sc, e), zw = ldfe<Fs>(sc, e + 1), a = ldfe<Fs>(sc, e + 2),
-                   ap = ldfe<Fs>(sc, e + 3), s = ldfe<Fs>(sc, e + 4);
+      const Fe<Fs> z = sc.get<Fs>(e), zw = sc.get<Fs>(e + 1), a = sc.get<Fs>(e + 2), ap = sc.get<Fs>(e + 3),
+                   s = sc.get<Fs>(e + 4);
       hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_0, fe_sub<Fs>(one, z)));
       hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_last, fe_sub<Fs>(fe_sqr<Fs>(z), z)));
       const Fe<Fs> left = fe_mul<Fs>(fe_mul<Fs>(fe_add<Fs>(a, beta), fe_add<Fs>(s, gamma)), zw);
@@ -178,7 +212,7 @@ __global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* 
   Fe<Fs> up[kAccMaxSets];
   up[h.nsets - 1] = one;
   for (int j = (int)h.nsets - 2; j >= 0; j--) up[j] = fe_mul<Fs>(up[j + 1], u);
-  for (uint32_t t = 0; t < h.nslots; t++) stfe<Fs>(cf, t, zero);
+  for (uint32_t t = 0; t < h.nslots; t++) cf.put<Fs>(t, zero);
   Fe<Fs> coefH = zero, ev = zero;
   uint32_t qi = 0;
   for (uint32_t j = 0; j < h.nsets; j++) {
@@ -187,23 +221,23 @@ __global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* 
     Fe<Fs> c = up[j];
     for (int i = (int)m - 1; i >= 0; i--) {
       const uint32_t slot = prog[h.p_query + 2 * (qi + i)], eidx = prog[h.p_query + 2 * (qi + i) + 1];
-      const Fe<Fs> e = eidx == kEvalH ? h_eval : ldfe<Fs>(sc, eidx);
+      const Fe<Fs> e = eidx == kEvalH ? h_eval : sc.get<Fs>(eidx);
       ev = fe_add<Fs>(ev, fe_mul<Fs>(c, e));
       if (slot == kSlotH) coefH = fe_add<Fs>(coefH, c);
-      else stfe<Fs>(cf, slot, fe_add<Fs>(ldfe<Fs>(cf, slot), c));
+      else cf.put<Fs>(slot, fe_add<Fs>(cf.get<Fs>(slot), c));
       c = fe_mul<Fs>(c, v);
     }
     qi += m;
-    stfe<Fs>(cf, h.nslots + j, up[j]);
-    stfe<Fs>(cf, h.nslots + h.nsets + j, fe_mul<Fs>(fe_mul<Fs>(up[j], ldfe<Fs>(consts, h.c_omega_eval + j)), x));
+    cf.put<Fs>(h.nslots + j, up[j]);
+    cf.put<Fs>(h.nslots + h.nsets + j, fe_mul<Fs>(fe_mul<Fs>(up[j], ldfe<Fs>(consts, h.c_omega_eval + j)), x));
   }
   Fe<Fs> xp = one;
   for (uint32_t i = 0; i < h.nh; i++) {
-    stfe<Fs>(cf, h.h_slot0 + i, fe_add<Fs>(ldfe<Fs>(cf, h.h_slot0 + i), fe_mul<Fs>(coefH, xp)));
+    cf.put<Fs>(h.h_slot0 + i, fe_add<Fs>(cf.get<Fs>(h.h_slot0 + i), fe_mul<Fs>(coefH, xp)));
     xp = fe_mul<Fs>(xp, xn);
   }
-  stfe<Fs>(cf, h.T - 1, fe_neg<Fs>(ev));
-  for (uint32_t t = 0; t < h.T; t++) stfe<Fs>(cf, t, fe_from_mont<Fs>(ldfe<Fs>(cf, t)));
+  cf.put<Fs>(h.T - 1, fe_neg<Fs>(ev));
+  for (uint32_t t = 0; t < h.T; t++) stfe<Fs>(cfg, t, fe_from_mont<Fs>(cf.get<Fs>(t)));
 }
 
 // ------------------------------------------------------------------- GLV

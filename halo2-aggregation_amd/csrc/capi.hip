@@ -45,6 +45,7 @@ int pm::Buf::ensure(size_t bytes) {
     return set_error(PM_ERR_HIP, std::string("hipMalloc(") + std::to_string(want) + "): " + hipGetErrorString(e));
   }
   cap = want;
+  gen++;
   return PM_OK;
 }
 void pm::Buf::release() {

@@ -9,6 +9,7 @@
 
 #include "../../include/pasta_msm.h"
 
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
@@ -37,8 +38,20 @@ constexpr size_t kPrefetchBytes = ~size_t(0);
 struct Buf {
   void* p = nullptr;
   size_t cap = 0;
+  uint64_t gen = 0;  // bumped on every (re)allocation
   int ensure(size_t bytes);
   void release();
+};
+
+// Device copy of a small host table (accumulator / transcript programs,
+// constants, VK points) that is uploaded only when its bytes change: a batch
+// of proofs against one verifying key re-sends nothing after the first call.
+struct CachedUpload {
+  Buf buf;
+  std::vector<uint8_t> host;
+  uint64_t gen_at_upload = ~0ull;
+  template <class T>
+  int put(const std::vector<T>& v, hipStream_t st, size_t pad = 0);
 };
 
 struct MsmPlan {
@@ -115,7 +128,8 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_prog, acc_const, acc_vk, acc_coef, acc_part, acc_io, bases29, tr_prog, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad;
+      win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad;
+  pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
   std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;
@@ -129,7 +143,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog,   &acc_const, &acc_vk, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad};
   }
   ~pm_ctx();
   int begin_call();
@@ -175,3 +189,18 @@ extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
     if (e_ != hipSuccess)                                                                   \
       return pm::set_error(PM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
+
+namespace pm {
+template <class T>
+int CachedUpload::put(const std::vector<T>& v, hipStream_t st, size_t pad) {
+  const size_t bytes = v.size() * sizeof(T);
+  int rc;
+  if ((rc = buf.ensure(bytes + pad))) return rc;
+  if (buf.gen == gen_at_upload && host.size() == bytes && (bytes == 0 || memcmp(host.data(), v.data(), bytes) == 0))
+    return PM_OK;
+  if (bytes) HIP_TRY(hipMemcpyAsync(buf.p, v.data(), bytes, hipMemcpyHostToDevice, st));
+  host.assign((const uint8_t*)v.data(), (const uint8_t*)v.data() + bytes);
+  gen_at_upload = buf.gen;
+  return PM_OK;
+}
+}  // namespace pm
