@@ -384,7 +384,7 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernels = kernel_breakdown(ctx, step, ("transcript", "acc_scalars", "acc_termmul", "acc_sum"))
+    kernels = kernel_breakdown(ctx, step, ("transcript", "acc_ladder", "acc_scalars", "acc_termmul", "acc_sum"))
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
