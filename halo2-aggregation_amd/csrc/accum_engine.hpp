@@ -213,16 +213,17 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     HIP_TRY(hipEventRecord(up, st));
   }
   if (vk_repr && (rc = transcript_device_impl<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status))) return rc;
-  // k_acc_scalars stages (nsc + T) rows of 32 B per proof in LDS (lane
-  // stride nl + 1): proofs per block nl <= 64 within a 128 KiB budget
-  const size_t row_bytes = (size_t)(L.nsc + T) * 32;
-  const uint32_t nl = (uint32_t)std::min<size_t>(64, kAccScalarsLds / row_bytes - 1);
-  if (nl == 0) return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
-  const size_t lds = row_bytes * (nl + 1);
+  // k_acc_scalars: 4 waves per block of np proofs, (nsc + T + exchange)
+  // rows of 32 B per proof in LDS (proof stride np + 1), np <= 64 within
+  // a 128 KiB budget
+  const size_t row_bytes = (size_t)(L.nsc + T + kAccXVals + acc_num_vals(h)) * 32;
+  const uint32_t np = (uint32_t)std::min<size_t>(64, kAccScalarsLds / row_bytes - 1);
+  if (np == 0) return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
+  const size_t lds = row_bytes * (np + 1);
   PM_LAUNCH(ctx, "acc_scalars",
-            (k_acc_scalars<Fs><<<(unsigned)((B + nl - 1) / nl), nl, lds, st>>>(
+            (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, st>>>(
                 h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
-                dcoef, (uint32_t*)d_hout)));
+                dcoef, (uint32_t*)d_hout, np)));
   // The ladder (points only) is launched after the transcript replay and
   // k_acc_scalars (their few blocks are dispatched first); together with the
   // cached uploads this took B = 256 from ~1.03 to ~0.85 ms.  Partitioning
@@ -232,7 +233,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     const hipStream_t sl = ctx->red_stream;
     HIP_TRY(hipStreamWaitEvent(sl, up, 0));
     PM_LAUNCH_ST(ctx, sl, "acc_ladder",
-                 (k_acc_ladder<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, sl>>>(
+                 (k_acc_ladder<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, 0, sl>>>(
                      h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, S, Lb,
                      (Xyzz<F>*)ctx->acc_lad.p)));
     HIP_TRY(hipEventRecord(lad_done, sl));

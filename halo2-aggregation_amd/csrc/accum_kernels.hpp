@@ -20,6 +20,7 @@
 #include "accum_plan.hpp"
 #include "msm_kernels.hpp"
 #include "curve29.hpp"
+#include "coop29.hpp"
 
 namespace pm {
 
@@ -104,140 +105,200 @@ __device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const LdsRow
   return acc;
 }
 
+// k_acc_scalars: one block of 4 waves per np proofs (np <= 64, lane = proof
+// within the block).  The waves work on independent parts of the same proofs
+// (divergent roles inside one wave would serialise):
+//   wave 0  x^n, the Lagrange denominators' batched inversion, l_0, l_last,
+//           l_blind (the long latency chain);
+//   wave 1  gate expressions (Horner in y -> hv_g) and every permutation /
+//           lookup identity value that does not need the l_i;
+//   wave 2  the calc_witness coefficients (u / v powers, zw, H expansion)
+//           and the e-term sums that do not need h_eval;
+//   then wave 0 folds the identity values into h (h = h y + sel val,
+//   sel in {l_0, l_last, 1 - l_last - l_blind}), h_eval and the e
+//   coefficient; finally all 4 waves convert the T coefficients.
+// LDS rows per proof (word-major, proof stride np + 1): [0, nsc) evaluations,
+// then T coefficients, then the exchange rows (kAccX*).
+constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXVals = 3;  // exchange row offsets
+constexpr int kAccSelL0 = 0, kAccSelLast = 1, kAccSelOmb = 2;
+
+// identity values of the permutation / lookup arguments in h-fold order
+// (permutation.rs:190-324, lookup.rs:173-311) with their selector
+__host__ __device__ inline uint32_t acc_num_vals(const AccumHdr& h) {
+  return (h.n_perm_sets ? 2 * h.n_perm_sets + 1 : 0) + 5 * h.num_lookups;
+}
+
 template <class Fs>
-__global__ void __launch_bounds__(64) k_acc_scalars(AccumHdr h, const uint32_t* __restrict__ prog,
-                                                    const uint32_t* __restrict__ consts,
-                                                    const uint32_t* __restrict__ scalars,
-                                                    const uint32_t* __restrict__ challenges,
-                                                    uint32_t* __restrict__ coef, uint32_t* __restrict__ h_out) {
-  extern __shared__ uint32_t acc_lds[];  // (nsc + T) rows x 8 words x (blockDim + 1)
-  const uint32_t nl = blockDim.x, b0 = blockIdx.x * nl, b = b0 + threadIdx.x;
-  const uint32_t nv = min(nl, h.B - b0);  // proofs in this block
+__global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t* __restrict__ prog,
+                                                     const uint32_t* __restrict__ consts,
+                                                     const uint32_t* __restrict__ scalars,
+                                                     const uint32_t* __restrict__ challenges,
+                                                     uint32_t* __restrict__ coef, uint32_t* __restrict__ h_out,
+                                                     uint32_t np) {
+  extern __shared__ uint32_t acc_lds[];
+  const uint32_t role = threadIdx.x >> 6, pl = threadIdx.x & 63;
+  const uint32_t b0 = blockIdx.x * np, b = b0 + pl;
+  const uint32_t nv = min(np, h.B - b0);  // proofs in this block
   {  // coalesced staging of the block's evaluations (rows [0, nsc))
     const uint32_t per = 8 * h.nsc;
     const uint32_t* src = scalars + (size_t)per * b0;
-    for (uint32_t f = threadIdx.x; f < per * nv; f += nl) {
-      const uint32_t pl = f / per, k = f - pl * per;
-      acc_lds[k * (nl + 1) + pl] = src[f];
+    for (uint32_t f = threadIdx.x; f < per * nv; f += blockDim.x) {
+      const uint32_t q = f / per, k = f - q * per;
+      acc_lds[k * (np + 1) + q] = src[f];
     }
   }
   __syncthreads();
-  if (b >= h.B) return;
-  const LdsRows sc{acc_lds, threadIdx.x, nl + 1};
-  const LdsRows cf{acc_lds + (size_t)8 * h.nsc * (nl + 1), threadIdx.x, nl + 1};  // coefficient rows
-  const uint32_t* ch = challenges + 8ull * 7 * b;
-  uint32_t* cfg = coef + 8ull * h.T * b;
-  const Fe<Fs> theta = ldfe<Fs>(ch, 0), beta = ldfe<Fs>(ch, 1), gamma = ldfe<Fs>(ch, 2), y = ldfe<Fs>(ch, 3),
-               x = ldfe<Fs>(ch, 4), v = ldfe<Fs>(ch, 5), u = ldfe<Fs>(ch, 6);
+  const bool live = pl < nv;
+  const LdsRows sc{acc_lds, pl, np + 1};
+  const LdsRows cf{acc_lds + (size_t)8 * h.nsc * (np + 1), pl, np + 1};
+  const LdsRows xr{acc_lds + (size_t)8 * (h.nsc + h.T) * (np + 1), pl, np + 1};
+  const uint32_t* ch = challenges + 8ull * 7 * (live ? b : b0);
   const Fe<Fs> one = fe_one<Fs>(), zero = fe_zero<Fs>();
+  const Fe<Fs> y = ldfe<Fs>(ch, 3), x = ldfe<Fs>(ch, 4);
+  Fe<Fs> l_0 = zero, l_last = zero, omb = zero, inv_xn1 = zero;
 
-  // x^n (verifier.rs:513-516)
-  Fe<Fs> xn = x;
-  for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
-  const Fe<Fs> xn1 = fe_sub<Fs>(xn, one);
-
-  // l_i = w^i (x^n - 1) / (n (x - w^i)), w = omega^-1, i < bf + 2, plus
-  // 1 / (x^n - 1) for h_eval: one batched inversion (Montgomery's trick).
-  const uint32_t K = h.bf + 3;
-  Fe<Fs> den[kAccMaxBlind + 3], pre[kAccMaxBlind + 3];
-  const Fe<Fs> nfe = ldfe<Fs>(consts, h.c_n);
-  for (uint32_t i = 0; i < K; i++) {
-    den[i] = i + 1 < K ? fe_mul<Fs>(nfe, fe_sub<Fs>(x, ldfe<Fs>(consts, h.c_wpow + i))) : xn1;
-    pre[i] = i ? fe_mul<Fs>(pre[i - 1], den[i]) : den[i];
-  }
-  Fe<Fs> inv = fe_inv_fast<Fs>(pre[K - 1]);
-  for (uint32_t i = K - 1; i > 0; i--) {
-    const Fe<Fs> t = fe_mul<Fs>(inv, pre[i - 1]);
-    inv = fe_mul<Fs>(inv, den[i]);
-    den[i] = t;  // now 1 / den_i
-  }
-  den[0] = inv;
-  Fe<Fs> l_0 = zero, l_last = zero, l_blind = zero;
-  for (uint32_t i = 0; i + 1 < K; i++) {
-    const Fe<Fs> li = fe_mul<Fs>(fe_mul<Fs>(ldfe<Fs>(consts, h.c_wpow + i), xn1), den[i]);
-    if (i == 0) l_0 = li;
-    else if (i == h.bf + 1) l_last = li;
-    else l_blind = fe_add<Fs>(l_blind, li);
-  }
-  const Fe<Fs> inv_xn1 = den[K - 1];
-  const Fe<Fs> omb = fe_sub<Fs>(one, fe_add<Fs>(l_last, l_blind));  // 1 - (l_last + l_blind)
-
-  // expressions in order gates, permutation, lookups; h = h*y + expr
-  Fe<Fs> hv = acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, zero, y);
-  if (h.n_perm_sets) {
-    auto zp = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i); };
-    auto zpn = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i + 1); };
-    auto zpl = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i + 2); };
-    hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_0, fe_sub<Fs>(one, zp(0))));
-    const Fe<Fs> zl = zp(h.n_perm_sets - 1);
-    hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_last, fe_sub<Fs>(fe_sqr<Fs>(zl), zl)));
-    for (uint32_t i = 1; i < h.n_perm_sets; i++)
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_0, fe_sub<Fs>(zp(i), zpl(i - 1))));
-    const Fe<Fs> bx = fe_mul<Fs>(beta, x);
-    for (uint32_t ci = 0; ci < h.n_perm_sets; ci++) {
-      Fe<Fs> left = zpn(ci), right = zp(ci);
-      const uint32_t k1 = min(h.n_perm_cols, (ci + 1) * h.perm_chunk);
-      for (uint32_t k = ci * h.perm_chunk; k < k1; k++) {
-        const Fe<Fs> ev = sc.get<Fs>(prog[h.p_permcol + k]);
-        const Fe<Fs> sg = sc.get<Fs>(h.sc_sigma + k);
-        left = fe_mul<Fs>(left, fe_add<Fs>(fe_add<Fs>(fe_mul<Fs>(beta, sg), ev), gamma));
-        const Fe<Fs> t = fe_mul<Fs>(bx, ldfe<Fs>(consts, h.c_delta + k));
-        right = fe_mul<Fs>(right, fe_add<Fs>(fe_add<Fs>(t, ev), gamma));
+  if (live && role == 0) {
+    // x^n (verifier.rs:513-516)
+    Fe<Fs> xn = x;
+    for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
+    const Fe<Fs> xn1 = fe_sub<Fs>(xn, one);
+    // l_i = w^i (x^n - 1) / (n (x - w^i)), w = omega^-1, i < bf + 2, plus
+    // 1 / (x^n - 1) for h_eval: one batched inversion (Montgomery's trick).
+    const uint32_t K = h.bf + 3;
+    Fe<Fs> den[kAccMaxBlind + 3], pre[kAccMaxBlind + 3];
+    const Fe<Fs> nfe = ldfe<Fs>(consts, h.c_n);
+    for (uint32_t i = 0; i < K; i++) {
+      den[i] = i + 1 < K ? fe_mul<Fs>(nfe, fe_sub<Fs>(x, ldfe<Fs>(consts, h.c_wpow + i))) : xn1;
+      pre[i] = i ? fe_mul<Fs>(pre[i - 1], den[i]) : den[i];
+    }
+    Fe<Fs> inv = fe_inv_fast<Fs>(pre[K - 1]);
+    for (uint32_t i = K - 1; i > 0; i--) {
+      const Fe<Fs> t = fe_mul<Fs>(inv, pre[i - 1]);
+      inv = fe_mul<Fs>(inv, den[i]);
+      den[i] = t;  // now 1 / den_i
+    }
+    den[0] = inv;
+    Fe<Fs> l_blind = zero;
+    for (uint32_t i = 0; i + 1 < K; i++) {
+      const Fe<Fs> li = fe_mul<Fs>(fe_mul<Fs>(ldfe<Fs>(consts, h.c_wpow + i), xn1), den[i]);
+      if (i == 0) l_0 = li;
+      else if (i == h.bf + 1) l_last = li;
+      else l_blind = fe_add<Fs>(l_blind, li);
+    }
+    inv_xn1 = den[K - 1];
+    omb = fe_sub<Fs>(one, fe_add<Fs>(l_last, l_blind));  // 1 - (l_last + l_blind)
+  } else if (live && role == 1) {
+    // gates (verifier.rs:593-605), then the identity values in fold order
+    xr.put<Fs>(kAccXHvg, acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, zero, y));
+    const Fe<Fs> beta = ldfe<Fs>(ch, 1), gamma = ldfe<Fs>(ch, 2);
+    uint32_t vi = kAccXVals;
+    if (h.n_perm_sets) {
+      auto zp = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i); };
+      auto zpn = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i + 1); };
+      auto zpl = [&](uint32_t i) { return sc.get<Fs>(h.sc_perm + 3 * i + 2); };
+      xr.put<Fs>(vi++, fe_sub<Fs>(one, zp(0)));                              // l_0
+      const Fe<Fs> zl = zp(h.n_perm_sets - 1);
+      xr.put<Fs>(vi++, fe_sub<Fs>(fe_sqr<Fs>(zl), zl));                      // l_last
+      for (uint32_t i = 1; i < h.n_perm_sets; i++) xr.put<Fs>(vi++, fe_sub<Fs>(zp(i), zpl(i - 1)));  // l_0
+      const Fe<Fs> bx = fe_mul<Fs>(beta, x);
+      for (uint32_t ci = 0; ci < h.n_perm_sets; ci++) {                      // omb
+        Fe<Fs> left = zpn(ci), right = zp(ci);
+        const uint32_t k1 = min(h.n_perm_cols, (ci + 1) * h.perm_chunk);
+        for (uint32_t k = ci * h.perm_chunk; k < k1; k++) {
+          const Fe<Fs> ev = sc.get<Fs>(prog[h.p_permcol + k]);
+          const Fe<Fs> sg = sc.get<Fs>(h.sc_sigma + k);
+          left = fe_mul<Fs>(left, fe_add<Fs>(fe_add<Fs>(fe_mul<Fs>(beta, sg), ev), gamma));
+          const Fe<Fs> t = fe_mul<Fs>(bx, ldfe<Fs>(consts, h.c_delta + k));
+          right = fe_mul<Fs>(right, fe_add<Fs>(fe_add<Fs>(t, ev), gamma));
+        }
+        xr.put<Fs>(vi++, fe_sub<Fs>(left, right));
       }
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(fe_sub<Fs>(left, right), omb));
     }
+    if (h.num_lookups) {
+      const Fe<Fs> theta = ldfe<Fs>(ch, 0);
+      const Fe<Fs> cin = acc_eval_code<Fs>(prog + h.p_lkin, h.n_lkin, sc, h, consts, zero, theta);
+      const Fe<Fs> ctab = acc_eval_code<Fs>(prog + h.p_lktab, h.n_lktab, sc, h, consts, zero, theta);
+      const Fe<Fs> rfac = fe_mul<Fs>(fe_add<Fs>(cin, beta), fe_add<Fs>(ctab, gamma));
+      for (uint32_t i = 0; i < h.num_lookups; i++) {
+        const uint32_t e = h.sc_lk + 5 * i;
+        const Fe<Fs> z = sc.get<Fs>(e), zw = sc.get<Fs>(e + 1), a = sc.get<Fs>(e + 2), ap = sc.get<Fs>(e + 3),
+                     s = sc.get<Fs>(e + 4);
+        const Fe<Fs> left = fe_mul<Fs>(fe_mul<Fs>(fe_add<Fs>(a, beta), fe_add<Fs>(s, gamma)), zw);
+        const Fe<Fs> as = fe_sub<Fs>(a, s);
+        xr.put<Fs>(vi++, fe_sub<Fs>(one, z));                                     // l_0
+        xr.put<Fs>(vi++, fe_sub<Fs>(fe_sqr<Fs>(z), z));                           // l_last
+        xr.put<Fs>(vi++, fe_sub<Fs>(left, fe_mul<Fs>(rfac, z)));                  // omb
+        xr.put<Fs>(vi++, as);                                                     // l_0
+        xr.put<Fs>(vi++, fe_mul<Fs>(as, fe_sub<Fs>(a, ap)));                      // omb
+      }
+    }
+  } else if (live && role == 2) {
+    // calc_witness coefficients (closed form of the Horner walks); the e term
+    // is -(sum_{non-H} c e + h_eval sum_{H queries} c), finished by wave 0
+    const Fe<Fs> v = ldfe<Fs>(ch, 5), u = ldfe<Fs>(ch, 6);
+    Fe<Fs> xn = x;
+    for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
+    Fe<Fs> up[kAccMaxSets];
+    up[h.nsets - 1] = one;
+    for (int j = (int)h.nsets - 2; j >= 0; j--) up[j] = fe_mul<Fs>(up[j + 1], u);
+    for (uint32_t t = 0; t < h.nslots; t++) cf.put<Fs>(t, zero);
+    Fe<Fs> coefH = zero, ev = zero, ceh = zero;
+    uint32_t qi = 0;
+    for (uint32_t j = 0; j < h.nsets; j++) {
+      const uint32_t m = prog[h.p_setlen + j];
+      // c_i = u^{S-1-j} v^{m-1-i}, walked from the last query of the set
+      Fe<Fs> c = up[j];
+      for (int i = (int)m - 1; i >= 0; i--) {
+        const uint32_t slot = prog[h.p_query + 2 * (qi + i)], eidx = prog[h.p_query + 2 * (qi + i) + 1];
+        if (eidx == kEvalH) ceh = fe_add<Fs>(ceh, c);
+        else ev = fe_add<Fs>(ev, fe_mul<Fs>(c, sc.get<Fs>(eidx)));
+        if (slot == kSlotH) coefH = fe_add<Fs>(coefH, c);
+        else cf.put<Fs>(slot, fe_add<Fs>(cf.get<Fs>(slot), c));
+        c = fe_mul<Fs>(c, v);
+      }
+      qi += m;
+      cf.put<Fs>(h.nslots + j, up[j]);
+      cf.put<Fs>(h.nslots + h.nsets + j, fe_mul<Fs>(fe_mul<Fs>(up[j], ldfe<Fs>(consts, h.c_omega_eval + j)), x));
+    }
+    Fe<Fs> xp = one;
+    for (uint32_t i = 0; i < h.nh; i++) {
+      cf.put<Fs>(h.h_slot0 + i, fe_add<Fs>(cf.get<Fs>(h.h_slot0 + i), fe_mul<Fs>(coefH, xp)));
+      xp = fe_mul<Fs>(xp, xn);
+    }
+    xr.put<Fs>(kAccXEvs, ev);
+    xr.put<Fs>(kAccXCeh, ceh);
   }
-  if (h.num_lookups) {
-    const Fe<Fs> cin = acc_eval_code<Fs>(prog + h.p_lkin, h.n_lkin, sc, h, consts, zero, theta);
-    const Fe<Fs> ctab = acc_eval_code<Fs>(prog + h.p_lktab, h.n_lktab, sc, h, consts, zero, theta);
-    const Fe<Fs> rfac = fe_mul<Fs>(fe_add<Fs>(cin, beta), fe_add<Fs>(ctab, gamma));
+  __syncthreads();
+  if (live && role == 0) {
+    // expressions in order gates, permutation, lookups: h = h y + expr
+    Fe<Fs> hv = xr.get<Fs>(kAccXHvg);
+    uint32_t vi = kAccXVals;
+    auto fold = [&](const Fe<Fs>& sel) {
+      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(sel, xr.get<Fs>(vi++)));
+    };
+    if (h.n_perm_sets) {
+      fold(l_0);
+      fold(l_last);
+      for (uint32_t i = 1; i < h.n_perm_sets; i++) fold(l_0);
+      for (uint32_t ci = 0; ci < h.n_perm_sets; ci++) fold(omb);
+    }
     for (uint32_t i = 0; i < h.num_lookups; i++) {
-      const uint32_t e = h.sc_lk + 5 * i;
-      const Fe<Fs> z = sc.get<Fs>(e), zw = sc.get<Fs>(e + 1), a = sc.get<Fs>(e + 2), ap = sc.get<Fs>(e + 3),
-                   s = sc.get<Fs>(e + 4);
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_0, fe_sub<Fs>(one, z)));
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_last, fe_sub<Fs>(fe_sqr<Fs>(z), z)));
-      const Fe<Fs> left = fe_mul<Fs>(fe_mul<Fs>(fe_add<Fs>(a, beta), fe_add<Fs>(s, gamma)), zw);
-      const Fe<Fs> right = fe_mul<Fs>(rfac, z);
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(omb, fe_sub<Fs>(left, right)));
-      const Fe<Fs> as = fe_sub<Fs>(a, s);
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(l_0, as));
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(omb, fe_mul<Fs>(as, fe_sub<Fs>(a, ap))));
+      fold(l_0);
+      fold(l_last);
+      fold(omb);
+      fold(l_0);
+      fold(omb);
     }
+    const Fe<Fs> h_eval = fe_mul<Fs>(hv, inv_xn1);
+    if (h_out) stfe<Fs>(h_out, b, h_eval);
+    const Fe<Fs> ev = fe_add<Fs>(xr.get<Fs>(kAccXEvs), fe_mul<Fs>(xr.get<Fs>(kAccXCeh), h_eval));
+    cf.put<Fs>(h.T - 1, fe_neg<Fs>(ev));
   }
-  const Fe<Fs> h_eval = fe_mul<Fs>(hv, inv_xn1);
-  if (h_out) stfe<Fs>(h_out, b, h_eval);
-
-  // calc_witness coefficients (closed form of the Horner walks)
-  Fe<Fs> up[kAccMaxSets];
-  up[h.nsets - 1] = one;
-  for (int j = (int)h.nsets - 2; j >= 0; j--) up[j] = fe_mul<Fs>(up[j + 1], u);
-  for (uint32_t t = 0; t < h.nslots; t++) cf.put<Fs>(t, zero);
-  Fe<Fs> coefH = zero, ev = zero;
-  uint32_t qi = 0;
-  for (uint32_t j = 0; j < h.nsets; j++) {
-    const uint32_t m = prog[h.p_setlen + j];
-    // c_i = u^{S-1-j} v^{m-1-i}, walked from the last query of the set
-    Fe<Fs> c = up[j];
-    for (int i = (int)m - 1; i >= 0; i--) {
-      const uint32_t slot = prog[h.p_query + 2 * (qi + i)], eidx = prog[h.p_query + 2 * (qi + i) + 1];
-      const Fe<Fs> e = eidx == kEvalH ? h_eval : sc.get<Fs>(eidx);
-      ev = fe_add<Fs>(ev, fe_mul<Fs>(c, e));
-      if (slot == kSlotH) coefH = fe_add<Fs>(coefH, c);
-      else cf.put<Fs>(slot, fe_add<Fs>(cf.get<Fs>(slot), c));
-      c = fe_mul<Fs>(c, v);
-    }
-    qi += m;
-    cf.put<Fs>(h.nslots + j, up[j]);
-    cf.put<Fs>(h.nslots + h.nsets + j, fe_mul<Fs>(fe_mul<Fs>(up[j], ldfe<Fs>(consts, h.c_omega_eval + j)), x));
+  __syncthreads();
+  if (live) {
+    uint32_t* cfg = coef + 8ull * h.T * b;
+    for (uint32_t t = role; t < h.T; t += 4) stfe<Fs>(cfg, t, fe_from_mont<Fs>(cf.get<Fs>(t)));
   }
-  Fe<Fs> xp = one;
-  for (uint32_t i = 0; i < h.nh; i++) {
-    cf.put<Fs>(h.h_slot0 + i, fe_add<Fs>(cf.get<Fs>(h.h_slot0 + i), fe_mul<Fs>(coefH, xp)));
-    xp = fe_mul<Fs>(xp, xn);
-  }
-  cf.put<Fs>(h.T - 1, fe_neg<Fs>(ev));
-  for (uint32_t t = 0; t < h.T; t++) stfe<Fs>(cfg, t, fe_from_mont<Fs>(cf.get<Fs>(t)));
 }
 
 // ------------------------------------------------------------------- GLV
@@ -424,16 +485,20 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
 // depends only on the points, so it runs on a second stream while the
 // transcript replay and k_acc_scalars derive the coefficients.
 //
-// k_acc_ladder: one lane per (proof, term): Q_0 = P, Q_{j+1} = [2^L] Q_j,
-// stored packed (R261 XYZZ, storage bounds of curve29.hpp) at lad[g S + j].
+// k_acc_ladder: one quad per (proof, term) (coop29.hpp: each Jacobian
+// doubling is 3 product levels split over the 4 lanes): Q_0 = P,
+// Q_{j+1} = [2^L] Q_j, stored packed (R261 XYZZ, storage bounds of
+// curve29.hpp) at lad[g S + j].
 template <class Cv>
 __global__ void __launch_bounds__(256) k_acc_ladder(AccumHdr h, const uint32_t* __restrict__ prog,
                                                     const uint32_t* __restrict__ points,
                                                     const uint32_t* __restrict__ vk, uint32_t S, uint32_t L,
                                                     Xyzz<typename Cv::Base>* __restrict__ lad) {
   using F = typename Cv::Base;
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= h.B * h.T) return;
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = gl >> 2;
+  if (g >= h.B * h.T) return;  // whole quads (4 B T lanes)
+  const bool st = (gl & 3u) == 0;
   const uint32_t b = g / h.T, t = g - b * h.T;
   const uint32_t src = prog[h.p_termsrc + t];
   const uint32_t idx = src & 0x0FFFFFFFu;
@@ -442,15 +507,17 @@ __global__ void __launch_bounds__(256) k_acc_ladder(AccumHdr h, const uint32_t* 
   Xyzz<F>* out = lad + (size_t)g * S;
   const uint32_t nq = (kGlvBits + L - 1) / L;  // Q_j actually used (nq <= S)
   if (aff_is_inf<F>(P)) {
-    for (uint32_t j = 0; j < nq; j++) store_xyzz29<F>(&out[j], xyzz29_inf<F>());
+    if (st)
+      for (uint32_t j = 0; j < nq; j++) store_xyzz29<F>(&out[j], xyzz29_inf<F>());
     return;
   }
   const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
   Jac29<F> q{px, py, f29_const<F>(F29Consts<F>::ONE)};
-  store_xyzz29<F>(&out[0], Xyzz29<F>{px, py, q.Z, q.Z});
+  if (st) store_xyzz29<F>(&out[0], Xyzz29<F>{px, py, q.Z, q.Z});
   for (uint32_t j = 1; j < nq; j++) {
-    for (uint32_t d = 0; d < L; d++) q = jac29_dbl<F>(q);
-    store_xyzz29<F>(&out[j], jac29_to_xyzz<F>(q));
+    for (uint32_t d = 0; d < L; d++) q = jac29_dbl_q<F>(q);
+    const Xyzz29<F> x = jac29_to_xyzz_q<F>(q);
+    if (st) store_xyzz29<F>(&out[j], x);
   }
 }
 
@@ -472,6 +539,9 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_shfl_xor(const Xyzz29<F>& p, int m) 
 // [k1_i 2^{i - j L}] (+-Q_j) + [k2_i 2^{i - j L}] (+-phi(Q_j)), joint
 // double-and-add with full XYZZ additions; then log2(S) butterfly steps and
 // lane 0 stores the term's point.  phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ).
+// (A quad-cooperative form (coop29.hpp) measured slower here: it needs
+// ~260 VGPRs, so only one wave per SIMD fits and the 4x larger grid runs in
+// two rounds.)
 template <class Cv>
 __global__ void __launch_bounds__(256) k_acc_termmul_split(AccumHdr h, const uint32_t* __restrict__ coef,
                                                            const Xyzz<typename Cv::Base>* __restrict__ lad,

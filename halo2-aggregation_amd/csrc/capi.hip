@@ -285,7 +285,7 @@ int pm_ctx_set_stream(pm_ctx* ctx, void* s) {
 
 int pm_ctx_set_accum_split(pm_ctx* ctx, int lg_lanes) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
-  if (lg_lanes < -1 || lg_lanes > 6) return set_error(PM_ERR_ARG, "accum split out of range (-1 auto, 0..6)");
+  if (lg_lanes < -1 || lg_lanes > 5) return set_error(PM_ERR_ARG, "accum split out of range (-1 auto, 0..5)");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->acc_split = lg_lanes;
   return PM_OK;

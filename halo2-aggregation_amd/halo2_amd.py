@@ -422,7 +422,7 @@ class Context:
         _check(lib().pm_ctx_set_pipeline(self.h, groups, min_chunk))
 
     def set_accum_split(self, lg_lanes=-1):
-        """Accumulator lanes per MSM term = 2^lg_lanes (-1 = automatic)."""
+        """Accumulator: 2^lg_lanes lanes (bit segments) per MSM term, 0..5 (-1 = automatic)."""
         _check(lib().pm_ctx_set_accum_split(self.h, lg_lanes))
 
     def set_timing(self, on=True, only=None):

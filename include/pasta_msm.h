@@ -61,9 +61,10 @@ int pm_ctx_set_window(pm_ctx* ctx, int c);
  * the next group's accumulation (0 = automatic, 1 = no pipelining) and the
  * minimum accumulate slice per lane (0 = automatic). */
 int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk);
-/* Batch accumulator: 2^lg_lanes lanes per MSM term (split ladder, 0..6;
- * -1 = automatic: more lanes per term while the batch leaves SIMDs idle).
- * Results do not depend on it. */
+/* Batch accumulator: each MSM term's scalar is split into 2^lg_lanes bit
+ * segments, one lane each (0..5; 0 = one lane per term; -1 = automatic: more
+ * lanes per term while the batch leaves SIMDs idle).  Results do not depend
+ * on it. */
 int pm_ctx_set_accum_split(pm_ctx* ctx, int lg_lanes);
 /* Per-kernel HIP-event timing on the context stream (for bench/profiling).
  * Every event pair costs ~10 us of stream time on MI355X, so a timed region
