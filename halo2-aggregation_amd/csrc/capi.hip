@@ -131,7 +131,10 @@ static int bit_length(uint32_t v) {
 MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk) {
   MsmPlan pl;
   int lg = bit_length((uint32_t)std::max<size_t>(n, 1)) - 1;
-  int c = c_override > 0 ? c_override : std::max(4, std::min(kAutoMaxC, lg - 4));
+  // auto window: lg - 2 from 2^14 up (capped at 16), lg - 4 below; swept on
+  // MI355X (profiles/r01_s3/c_sweep_*.jsonl): 2^16 c = 14, 2^18 c = 16 (was
+  // lg - 4 everywhere: 2^18 0.85 -> 0.77 ms, 2^16 0.68 -> 0.61 ms)
+  int c = c_override > 0 ? c_override : std::max(4, std::min(kAutoMaxC, lg >= 14 ? lg - 2 : lg - 4));
   c = std::max(kMinC, std::min(kMaxC, c));
   pl.c = c;
   pl.W = (256 + c - 1) / c;

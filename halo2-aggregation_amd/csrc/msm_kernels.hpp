@@ -480,7 +480,11 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
       store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc_inf ? xyzz29_inf<F>() : acc);
       acc_inf = true;
       gb++;
-      while (offsets[gb + 1] <= p) gb++;
+      // skip empty buckets by binary search: a window narrower than cmax
+      // leaves half its slots empty, and a linear walk over them (one
+      // dependent load each) stalled the lane crossing into the next window
+      // (W = 18 at 2^20: accumulate 1.06 -> 2.0 ms)
+      if (offsets[gb + 1] <= p) gb = find_bucket(offsets, gb, s1, p);
       bend = offsets[gb + 1];
       owned = true;
     }

@@ -18,7 +18,7 @@ def bit_length(v):
 
 def make_plan(n, c_override=0, chunk_override=0, groups_override=0):
     lg = bit_length(max(n, 1)) - 1
-    c = c_override if c_override > 0 else max(4, min(16, lg - 4))
+    c = c_override if c_override > 0 else max(4, min(16, lg - 2 if lg >= 14 else lg - 4))
     c = max(4, min(20, c))
     W = (256 + c - 1) // c
     base, extra = 256 // W, 256 % W
