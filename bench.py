@@ -36,7 +36,7 @@ METRIC = "Pallas MSM Mscalar/s at 2^20 (1/2/4/8 GPU); aggregated proofs verified
 LOGN = 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_PAIR = 96            # 32 B scalar + 64 B affine base
-MADS_PER_MADD = 8 * 117 + 2 * 81  # v_mad_u64_u32 per XYZZ mixed add, radix-2^29 Pasta (fp29.hpp)
+MADS_PER_MADD = 8 * 135 + 2 * 99  # v_mad_u64_u32 per XYZZ mixed add issued by the per-column asm products (fp29_asm.hpp, Pasta)
 SEED_SCALARS, SEED_BASES = 0x5EED, 0xA11CE
 
 
@@ -172,8 +172,10 @@ def main():
         if vp:
             # The binding roofline is integer VALU: one XYZZ mixed
             # add = 8 products + 2 squares in the radix-2^29 arithmetic
-            # (fp29.hpp): 8 x 117 + 2 x 81 = 1098 v_mad_u64_u32 for the Pasta
-            # moduli; ~n*W adds per launch; peak = measured mad issue rate.
+            # (fp29_asm.hpp): 8 x 135 + 2 x 99 = 1278 v_mad_u64_u32 for the
+            # Pasta moduli (the reduction's p_0 = 1 and p_8 = 2^22 limbs are
+            # multiply-adds too); ~n*W adds per launch; peak = measured mad
+            # issue rate.
             W = windows_for(n, args.window)
             mads = int(n * W * MADS_PER_MADD / acc_launches_per_msm)
             ach = mads / (acc_avg_ms * 1e-3) / 1e12
@@ -457,7 +459,7 @@ def accum_cpu_baseline(curve, log_n, host, vk, B, budget_s):
 def windows_for(n, c_override=0):
     """Window count of the engine's launch plan (capi.hip make_plan)."""
     lg = max(n, 1).bit_length() - 1
-    c = c_override if c_override > 0 else max(4, min(16, lg - 4))
+    c = c_override if c_override > 0 else max(4, min(16, lg - 2 if lg >= 14 else lg - 4))
     c = max(4, min(20, c))
     return (256 + c - 1) // c
 
