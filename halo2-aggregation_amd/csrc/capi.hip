@@ -128,7 +128,7 @@ static int bit_length(uint32_t v) {
   return b;
 }
 
-MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk) {
+MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk, int nbits) {
   MsmPlan pl;
   int lg = bit_length((uint32_t)std::max<size_t>(n, 1)) - 1;
   // auto window: lg - 2 from 2^14 up (capped at 16), lg - 4 below; swept on
@@ -137,9 +137,9 @@ MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk) 
   int c = c_override > 0 ? c_override : std::max(4, std::min(kAutoMaxC, lg >= 14 ? lg - 2 : lg - 4));
   c = std::max(kMinC, std::min(kMaxC, c));
   pl.c = c;
-  pl.W = (256 + c - 1) / c;
-  pl.base = 256 / pl.W;
-  pl.extra = 256 % pl.W;
+  pl.W = (nbits + c - 1) / c;
+  pl.base = nbits / pl.W;
+  pl.extra = nbits % pl.W;
   pl.cmax = pl.base + (pl.extra ? 1 : 0);
   pl.K = 1 << (pl.cmax - 1);
   pl.L1 = std::min(kL1, pl.K);
@@ -270,6 +270,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_GROUPS")) c->groups = std::atoi(e);
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
+  if (const char* e = std::getenv("PM_GLV")) c->glv = std::atoi(e) != 0;
   *out = c.release();
   return PM_OK;
 }
@@ -283,6 +284,13 @@ int pm_ctx_set_stream(pm_ctx* ctx, void* s) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+  return PM_OK;
+}
+
+int pm_ctx_set_glv(pm_ctx* ctx, int enable) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->glv = enable != 0;
   return PM_OK;
 }
 

@@ -65,6 +65,30 @@ int launch_sort(int W, bool d16, const uint32_t* s, uint32_t n, uint32_t canonic
   }
 }
 
+// GLV mode (variable-base MSM, c >= kGlvMinC): W = ceil(128 / c) in {7 .. 11}
+template <class Cv, int W>
+void launch_sort_glv_w(bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* bh,
+                       void* digits, uint32_t stride, hipStream_t st) {
+  const size_t lds = (size_t)W * g.NCB * 4;
+  if (d16)
+    k_sort_hist_glv<Cv, W, true><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint16_t*)digits, bh, stride);
+  else
+    k_sort_hist_glv<Cv, W, false><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint32_t*)digits, bh,
+                                                                       stride);
+}
+template <class Cv>
+int launch_sort_glv(int W, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* bh,
+                    void* digits, uint32_t stride, hipStream_t st) {
+  switch (W) {
+#define PM_WG(k) \
+  case k: launch_sort_glv_w<Cv, k>(d16, s, n, canonical, g, bh, digits, stride, st); return PM_OK;
+    PM_WG(7) PM_WG(8) PM_WG(9) PM_WG(10) PM_WG(11)
+#undef PM_WG
+    default: return set_error(PM_ERR_UNSUPPORTED, "GLV window count out of range");
+  }
+}
+constexpr int kGlvMinC = 12;  // below: the plain 256-bit pipeline (small n)
+
 // Run the device pipeline; result = host XYZZ point (sum over windows).
 //
 // Sort once, then the windows are processed in G groups from the top window
@@ -92,13 +116,19 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   }
   if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "n exceeds 2^26 points per device call");
   const bool fixed = ft != nullptr;
-  const MsmPlan pl = fixed ? make_plan_fixed(ft->npad, ft->c, ctx->min_chunk)
-                           : make_plan(n, ctx->window_c, ctx->groups, ctx->min_chunk);
+  // GLV mode: s_i P_i = k1_i P_i + k2_i phi(P_i) with |k1|, |k2| < 2^127, i.e.
+  // an MSM of 2n points with 128-bit scalars: the same number of bucket
+  // additions, half the windows (bucket reduction and host Horner halve).
+  MsmPlan pl = fixed ? make_plan_fixed(ft->npad, ft->c, ctx->min_chunk)
+                     : make_plan(2 * n, ctx->window_c, ctx->groups, ctx->min_chunk, 128);
+  const bool glv = !fixed && ctx->glv && pl.c >= kGlvMinC;
+  if (!fixed && !glv) pl = make_plan(n, ctx->window_c, ctx->groups, ctx->min_chunk);
+  const size_t npts = glv ? 2 * n : n;  // sort entries per window row
   const hipStream_t st = ctx->stream, st2 = ctx->red_stream;
   const int Wr = fixed ? 1 : pl.W;                  // bucket sets (reduced windows)
   const int wpg = fixed ? 1 : pl.wpg;
-  const size_t stride = fixed ? ft->npad : n;       // digit row length
-  const size_t E = fixed ? (size_t)pl.W * stride : n;  // entries of one sort row
+  const size_t stride = fixed ? ft->npad : npts;    // digit row length
+  const size_t E = fixed ? (size_t)pl.W * stride : npts;  // entries of one sort row
   const size_t TOT = (size_t)Wr * pl.NB + 1;
   const size_t nW = (size_t)stride * pl.W;
   const int NJ = pl.NB2 + kTJobs;                        // bit-sum jobs per window
@@ -157,20 +187,28 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if (fixed) {
     bases29 = (const uint32_t*)ft->d;
   } else {
-    if ((rc = ctx->bases29.ensure((size_t)n * 64))) return rc;
+    if ((rc = ctx->bases29.ensure(npts * 64))) return rc;
     bases29 = (const uint32_t*)ctx->bases29.p;
     hipEvent_t ready = ctx->next_event();
     bases_done = ctx->next_event();
     if (!ready || !bases_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(ready, st));
     HIP_TRY(hipStreamWaitEvent(st2, ready, 0));
-    PM_LAUNCH_ST(ctx, st2, "bases_r261",
-                 (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st2>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
+    if (glv)
+      PM_LAUNCH_ST(ctx, st2, "bases_r261",
+                   (k_bases_glv<Cv><<<(un + 255) / 256, 256, 0, st2>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
+    else
+      PM_LAUNCH_ST(ctx, st2, "bases_r261",
+                   (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st2>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
     HIP_TRY(hipEventRecord(bases_done, st2));
   }
   const uint32_t canon = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
-  PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, bh, ctx->digits.p,
-                                                   (uint32_t)stride, fixed ? 1u : 0u, st));
+  if (glv)
+    PM_LAUNCH(ctx, "sort_hist", rc = launch_sort_glv<Cv>(pl.W, d16, d_scalars, un, canon, g, bh, ctx->digits.p,
+                                                         (uint32_t)stride, st));
+  else
+    PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, bh, ctx->digits.p,
+                                                     (uint32_t)stride, fixed ? 1u : 0u, st));
   if (rc) return rc;
   PM_LAUNCH(ctx, "scan", {
     k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum);

@@ -25,6 +25,7 @@
 // G_b) as one Horner over absolute bit positions.
 #pragma once
 #include "curve29.hpp"
+#include "glv.hpp"
 
 namespace pm {
 
@@ -81,10 +82,10 @@ __device__ __forceinline__ Xyzz<F> load_xyzz(const Xyzz<F>* src) {
 // buckets).  Signed digits: d in [-2^(c_w-1)+1, 2^(c_w-1)], code = |d| |
 // sign<<31, code 0 = skip.  The top window never produces a carry because
 // scalars are < 2^255.
-template <int W>
+template <int W, int NBITS = 256>
 struct WinGeom {
-  static constexpr int base = 256 / W;
-  static constexpr int extra = 256 % W;
+  static constexpr int base = NBITS / W;
+  static constexpr int extra = NBITS % W;
   static constexpr __host__ __device__ int width(int w) { return base + (w < extra ? 1 : 0); }
   static constexpr __host__ __device__ int offset(int w) { return w * base + (w < extra ? w : extra); }
 };
@@ -230,6 +231,32 @@ __device__ __forceinline__ uint32_t signed_digit(const Fe<Fs>& s, int w, uint32_
   return d ? (d | (neg << 31)) : 0u;
 }
 
+// GLV mode: signed digit of window w of a 128-bit magnitude k (4 words,
+// |k| < 2^127 - 2^112 so the top window never carries), negated when `flip`.
+// A flipped scalar is recoded into [-2^(C-1), 2^(C-1) - 1] (negate when
+// d >= 2^(C-1)) so that after the flip every digit is in the usual
+// [-2^(C-1) + 1, 2^(C-1)]: the 2-byte digit code has no room for -2^15.
+template <int W>
+__device__ __forceinline__ uint32_t signed_digit128(const uint32_t k[4], int w, uint32_t& carry, uint32_t flip) {
+  using G = WinGeom<W, 128>;
+  const int C = G::width(w);
+  const int bit = G::offset(w);
+  const int limb = bit >> 5, sh = bit & 31;
+  const uint32_t lo = k[limb] >> sh;
+  const uint32_t hi = (sh != 0 && limb + 1 < 4) ? (k[limb + 1] << (32 - sh)) : 0u;
+  const uint32_t raw = (lo | hi) & ((1u << C) - 1u);
+  uint32_t d = raw + carry;
+  uint32_t neg = 0;
+  if (w != W - 1 && d + flip > (1u << (C - 1))) {
+    d = (1u << C) - d;
+    neg = 1;
+    carry = 1;
+  } else {
+    carry = 0;
+  }
+  return d ? (d | ((neg ^ flip) << 31)) : 0u;
+}
+
 template <class Fs>
 __device__ __forceinline__ Fe<Fs> load_canonical(const uint32_t* scalars, uint32_t i, uint32_t canonical) {
   Fe<Fs> s = load_fe4<Fs>(reinterpret_cast<const uint4*>(scalars + 8ull * i));
@@ -294,6 +321,44 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
     const size_t row = merged ? (size_t)cb * W + w : (size_t)k;
     bh[row * g.nblk + blockIdx.x] = hist[k];
   }
+}
+
+// GLV mode: sort entry v < n is (k1 of scalar v, base P_v), entry n + v is
+// (k2 of scalar v, base phi(P_v)); both scalars < 2^127 in W windows over
+// 128 bits (Babai-rounded split, glv.hpp), the split's signs folded into the
+// digit signs.  stride = 2n.
+template <class Cv, int W, bool D16>
+__global__ void __launch_bounds__(kSortThreads) k_sort_hist_glv(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                                uint32_t canonical, SortGeom g,
+                                                                typename DigitCode<D16>::T* __restrict__ digits,
+                                                                uint32_t* __restrict__ bh, uint32_t stride) {
+  using Fs = typename Cv::Scalar;
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
+  const int nbins = W * g.NCB;
+  for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
+  __syncthreads();
+  for (int r = 0; r < kSortPerThread; r++) {
+    const uint32_t v = blockIdx.x * kSortB + r * kSortThreads + threadIdx.x;
+    if (v >= stride) break;
+    const bool hi = v >= n;
+    const Fe<Fs> s = load_canonical<Fs>(scalars, hi ? v - n : v, canonical);
+    uint32_t k1[6], k2[6];
+    bool n1, n2;
+    glv_split<Cv, true>(s, k1, k2, n1, n2);
+    uint32_t k[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) k[i] = hi ? k2[i] : k1[i];
+    const uint32_t flip = (hi ? n2 : n1) ? 1u : 0u;
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint32_t code = signed_digit128<W>(k, w, carry, flip);
+      digits[(size_t)w * stride + v] = DigitCode<D16>::enc(code);
+      if (code) atomicAdd(&hist[w * g.NCB + ((code & ~kNegBit) >> g.FB)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nbins; k += kSortThreads) bh[(size_t)k * g.nblk + blockIdx.x] = hist[k];
 }
 
 // coarse-segment entry: WIDE = slot << 32 | index | sign << 31;
@@ -523,6 +588,28 @@ __global__ void __launch_bounds__(256) k_bases_to_r261(const uint32_t* __restric
     const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     st29<F>(o + 2 * c, f29_canon<F>(f29_from_r256<F>(w)));
   }
+}
+
+// GLV mode: out[i] = P_i and out[n + i] = phi(P_i) = (beta x, y), R261 canonical
+// ((0, 0) stays (0, 0), which k_accumulate skips).
+template <class Cv>
+__global__ void __launch_bounds__(256) k_bases_glv(const uint32_t* __restrict__ in, uint32_t n,
+                                                   uint32_t* __restrict__ out) {
+  using F = typename Cv::Base;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* q = reinterpret_cast<const uint4*>(in + 16ull * i);
+  uint4* o = reinterpret_cast<uint4*>(out + 16ull * i);
+  uint4* o2 = reinterpret_cast<uint4*>(out + 16ull * ((size_t)n + i));
+  const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+  const F29<F> x = f29_canon<F>(f29_from_r256<F>(wx));
+  const F29<F> y = f29_canon<F>(f29_from_r256<F>(wy));
+  st29<F>(o, x);
+  st29<F>(o + 2, y);
+  st29<F>(o2, f29_canon<F>(f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), x)));
+  st29<F>(o2 + 2, y);
 }
 
 // Fixed-base table (pm_fixed_bases_create): entry (w, i) at w * npad + i is

@@ -74,7 +74,8 @@ struct MsmPlan {
   int width(int w) const { return base + (w < extra ? 1 : 0); }
 };
 
-MsmPlan make_plan(size_t n, int c_override, int groups_override = 0, int min_chunk = 0);
+// nbits: scalar bits covered by the windows (256; 128 in GLV mode, n = 2 x points)
+MsmPlan make_plan(size_t n, int c_override, int groups_override = 0, int min_chunk = 0, int nbits = 256);
 // fixed-base MSM over a table of npad rows per window (one window group,
 // accumulate work = W * npad entries)
 MsmPlan make_plan_fixed(size_t npad, int c, int min_chunk = 0);
@@ -121,6 +122,7 @@ struct pm_ctx {
   int prefetch = -1;  // -1 auto, 0 off, 1 on (diagnostics: PM_PREFETCH env)
   int groups = 0;     // window groups, 0 = auto (diagnostics: PM_GROUPS env)
   int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
+  int glv = 0;        // variable-base MSM in GLV mode (pm_ctx_set_glv, PM_GLV env): measured slower, off
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)

@@ -207,6 +207,7 @@ def _load():
         "pm_ctx_set_window": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_split": ([_vp, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_glv": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing_filter": ([_vp, ctypes.c_char_p], ctypes.c_int),
         "pm_ctx_kernel_stats": ([_vp, ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
@@ -420,6 +421,10 @@ class Context:
 
     def set_pipeline(self, groups=0, min_chunk=0):
         _check(lib().pm_ctx_set_pipeline(self.h, groups, min_chunk))
+
+    def set_glv(self, enable=True):
+        """Variable-base MSM in GLV mode (2n points, 128-bit scalars); results do not depend on it."""
+        _check(lib().pm_ctx_set_glv(self.h, 1 if enable else 0))
 
     def set_accum_split(self, lg_lanes=-1):
         """Accumulator: 2^lg_lanes lanes (bit segments) per MSM term, 0..5 (-1 = automatic)."""

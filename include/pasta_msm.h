@@ -61,6 +61,11 @@ int pm_ctx_set_window(pm_ctx* ctx, int c);
  * the next group's accumulation (0 = automatic, 1 = no pipelining) and the
  * minimum accumulate slice per lane (0 = automatic). */
 int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk);
+/* Variable-base MSM in GLV mode (default off): s P = k1 P + k2 phi(P) with
+ * |k1|, |k2| < 2^127, an MSM of 2n points with 128-bit scalars and half the
+ * windows; used when the chosen window is >= 12 bits.  Measured slower on
+ * MI355X.  Results do not depend on it. */
+int pm_ctx_set_glv(pm_ctx* ctx, int enable);
 /* Batch accumulator: each MSM term's scalar is split into 2^lg_lanes bit
  * segments, one lane each (0..5; 0 = one lane per term; -1 = automatic: more
  * lanes per term while the batch leaves SIMDs idle).  Results do not depend

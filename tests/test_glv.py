@@ -1,9 +1,10 @@
 """CPU checks of the GLV constants compiled into the accumulator kernels
-(halo2-aggregation_amd/csrc/accum_kernels.hpp, Glv<Curve>): beta is a cube
+(halo2-aggregation_amd/csrc/glv.hpp, Glv<Curve>): beta is a cube
 root of unity of the base field with phi(G) = (beta Gx, Gy) = [lambda]G, the
 lattice vectors satisfy a + b lambda = 0 mod r, and the device's decomposition
 (floor with 2^384-scaled g1, g2) gives |k1|, |k2| < 2^128 with
-k = k1 + lambda k2 mod r on random and edge scalars."""
+k = k1 + lambda k2 mod r on random and edge scalars; with Babai rounding (the
+MSM's GLV mode) |k1|, |k2| < 2^127."""
 import os
 import random
 import re
@@ -13,7 +14,7 @@ import pytest
 import pasta as P
 
 HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "halo2-aggregation_amd", "csrc",
-                   "accum_kernels.hpp")
+                   "glv.hpp")
 CURVES = {"PallasCurve": P.PALLAS, "VestaCurve": P.VESTA, "Bn254Curve": P.BN254}
 
 
@@ -58,3 +59,79 @@ def test_glv_constants(name):
         assert abs(k1) < 1 << 128 and abs(k2) < 1 << 128
     # provable bound behind kGlvBits = 128: |k_i| <= (|a1| + |a2|) or (|b1| + |b2|), times (1 + 2^-120)
     assert max(abs(a1) + abs(a2), abs(b1) + abs(b2)) * (1 + 2.0 ** -100) < 2.0 ** 128
+
+
+@pytest.mark.parametrize("name", list(CURVES))
+def test_glv_rounded_split_below_2_127(name):
+    """glv_split<Cv, ROUND=true> (mp_quot384 adds 2^383 before taking the
+    quotient): |k1|, |k2| < 2^127, so the MSM's 8 signed 16-bit windows over
+    128 bits never carry out of the top window."""
+    C = CURVES[name]
+    g = _parse()[name]
+    a1, b1, a2, b2 = g["A1"], -g["NB1"], g["A2"], g["B2"]
+    lam = None
+    beta = g["BETA"] * pow(P.R_MONT, -1, C.p) % C.p
+    for cand in range(2, 50):
+        l0 = pow(cand, (C.r - 1) // 3, C.r)
+        for l in (l0, l0 * l0 % C.r):
+            if l != 1 and C.mul(l, C.gen) == (beta * C.gen[0] % C.p, C.gen[1]):
+                lam = l
+        if lam:
+            break
+    rng = random.Random(11)
+    ks = [0, 1, 2, C.r - 1, C.r - 2, lam, (C.r + 1) // 2, 1 << 253, (1 << 254) % C.r] + [rng.randrange(C.r) for _ in range(5000)]
+    # near the rounding boundaries of c1 / c2
+    for t in range(1, 200):
+        ks.append((t * (1 << 384) // g["G1"]) % C.r)
+        ks.append((t * (1 << 384) // g["G2"] + 1) % C.r)
+    # the provable bound: half the basis sum plus the rounding slack
+    assert max(abs(a1) + abs(a2), abs(b1) + abs(b2)) / 2 + 2 < 2.0 ** 127 - 2.0 ** 112
+    for k in ks:
+        c1 = (k * g["G1"] + (1 << 383)) >> 384
+        c2 = (k * g["G2"] + (1 << 383)) >> 384
+        assert c1 < 1 << 128 and c2 < 1 << 128
+        k1 = k - c1 * a1 - c2 * a2
+        k2 = c1 * -b1 - c2 * b2
+        assert (k1 + k2 * lam - k) % C.r == 0
+        # the top 16-bit window of |k| plus a carry stays below 2^15 (msm_kernels.hpp signed_digit128)
+        assert abs(k1) < (1 << 127) - (1 << 112) and abs(k2) < (1 << 127) - (1 << 112), (name, k)
+
+
+def _digits128(k, W, flip):
+    """Python restatement of msm_kernels.hpp signed_digit128 (GLV mode)."""
+    base, extra = 128 // W, 128 % W
+    out, carry, off = [], 0, 0
+    for w in range(W):
+        C = base + (1 if w < extra else 0)
+        d = ((k >> off) & ((1 << C) - 1)) + carry
+        off += C
+        neg = 0
+        if w != W - 1 and d + flip > (1 << (C - 1)):
+            d, neg, carry = (1 << C) - d, 1, 1
+        else:
+            carry = 0
+        out.append((C, -d if (neg ^ flip) else d))
+    return out
+
+
+@pytest.mark.parametrize("W", [7, 8, 9, 10, 11])
+def test_glv_signed_digits(W):
+    """The GLV-mode recoding of a 128-bit magnitude with the split's sign:
+    digits sum to (-1)^flip k, the non-top windows stay within
+    [-2^(C-1)+1, 2^(C-1)], every |d| <= 2^(cmax-1) (the bucket count) and, at
+    cmax = 16, no digit is -2^15 (the 2-byte digit code has no room for it)."""
+    rng = random.Random(W)
+    top = (1 << 127) - (1 << 112) - 1
+    ks = [0, 1, top, top - 1, (1 << 112) - 1, 1 << 111] + [rng.randrange(top) for _ in range(3000)]
+    for k in ks:
+        for flip in (0, 1):
+            ds = _digits128(k, W, flip)
+            cmax = max(C for C, _ in ds)
+            val, off = 0, 0
+            for i, (C, d) in enumerate(ds):
+                if i < W - 1:
+                    assert -(1 << (C - 1)) < d <= 1 << (C - 1), (k, flip, C, d)
+                assert abs(d) <= 1 << (cmax - 1) and not (cmax == 16 and d == -(1 << 15)), (k, flip, C, d)
+                val += d << off
+                off += C
+            assert val == (-k if flip else k)

@@ -34,6 +34,23 @@ def test_every_window_width(golden, gpu_ctx, c):
         gpu_ctx.set_window(0)
 
 
+@pytest.mark.parametrize("c", [0, 12, 13, 16, 18, 20])
+def test_glv_off_matches(golden, gpu_ctx, c):
+    """GLV mode (2n points, 128-bit Babai-rounded halves) gives the same
+    points as the default plain 256-bit pipeline."""
+    try:
+        for name, case in golden.items():
+            gpu_ctx.set_window(c)
+            gpu_ctx.set_glv(True)
+            a = gpu_ctx.msm(case["curve"], case["scalars"], case["bases"])
+            gpu_ctx.set_glv(False)
+            b = gpu_ctx.msm(case["curve"], case["scalars"], case["bases"])
+            assert np.array_equal(a, case["expected"]) and np.array_equal(b, case["expected"]), name
+    finally:
+        gpu_ctx.set_glv(False)
+        gpu_ctx.set_window(0)
+
+
 @pytest.mark.parametrize("groups,min_chunk", [(1, 0), (2, 1), (3, 7), (5, 0), (16, 64), (64, 2)])
 def test_pipeline_groups(golden, gpu_ctx, groups, min_chunk):
     """Window-group pipelining (reduction of group g overlapping accumulation
