@@ -304,10 +304,15 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
   const hipStream_t st = ctx->stream;
   int rc;
   if ((rc = ctx->tr_prog.put(prog, st))) return rc;
+  const size_t ncoord = B * 2 * (size_t)L.npts, nall = ncoord + B * (size_t)L.nsc;
+  if ((rc = ctx->tr_canon.ensure(nall * 32))) return rc;
+  uint32_t* cpts = (uint32_t*)ctx->tr_canon.p;
+  uint32_t* cscs = cpts + 8 * ncoord;
   PM_LAUNCH(ctx, "transcript",
-            (k_transcript<Cv><<<(unsigned)((B + 63) / 64), 64, 0, st>>>(
-                hd, (const uint32_t*)ctx->tr_prog.buf.p, (const uint32_t*)d_points, (const uint32_t*)d_scalars,
-                (uint32_t*)d_ch, (uint32_t*)d_status)));
+            (k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
+                 (uint32_t)B, L.npts, L.nsc, (const uint32_t*)d_points, (const uint32_t*)d_scalars, cpts, cscs),
+             k_transcript<Cv><<<(unsigned)((B + 63) / 64), 64, 0, st>>>(
+                 hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status)));
   return PM_OK;
 }
 

@@ -144,12 +144,37 @@ __device__ __forceinline__ void tr_settle(TrLane& s, uint32_t (*buf)[64], uint32
   }
 }
 
+// Montgomery -> canonical for every point coordinate and scalar of the batch,
+// one lane per field element (B (2 npts + nsc) lanes), so the transcript's
+// serial chain only hashes: pts_out / scs_out have the layout of the inputs.
+template <class Cv>
+__global__ void __launch_bounds__(256) k_tr_canon(uint32_t B, uint32_t npts, uint32_t nsc,
+                                                  const uint32_t* __restrict__ points,
+                                                  const uint32_t* __restrict__ scalars,
+                                                  uint32_t* __restrict__ pts_out, uint32_t* __restrict__ scs_out) {
+  using F = typename Cv::Base;
+  using Fs = typename Cv::Scalar;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t ncoord = (size_t)B * 2 * npts, nall = ncoord + (size_t)B * nsc;
+  if (e >= nall) return;
+  if (e < ncoord) {
+    const Fe<F> v = load_fe4<F>(reinterpret_cast<const uint4*>(points + 8 * e));
+    store_fe4<F>(reinterpret_cast<uint4*>(pts_out + 8 * e), fe_from_mont<F>(v));
+  } else {
+    const size_t k = e - ncoord;
+    const Fe<Fs> v = load_fe4<Fs>(reinterpret_cast<const uint4*>(scalars + 8 * k));
+    store_fe4<Fs>(reinterpret_cast<uint4*>(scs_out + 8 * k), fe_from_mont<Fs>(v));
+  }
+}
+
+// points / scalars: canonical (k_tr_canon).  The next record's words are
+// loaded one record ahead (the record index comes from the uniform program,
+// so the address is known early) to hide the global-load latency.
 template <class Cv>
 __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint32_t* __restrict__ prog,
                                                    const uint32_t* __restrict__ points,
                                                    const uint32_t* __restrict__ scalars,
                                                    uint32_t* __restrict__ challenges, uint32_t* __restrict__ status) {
-  using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   __shared__ uint32_t buf[64][64];
   const uint32_t lane = threadIdx.x;
@@ -165,43 +190,35 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
   const uint32_t* pts = points + 16ull * hd.npts * b;
   const uint32_t* scs = scalars + 8ull * hd.nsc * b;
   uint32_t d[16];
+  auto fetch = [&](uint32_t k, uint32_t w[16]) {
+    const uint32_t op = k < hd.nprog ? prog[k] : 0u;
+    const uint32_t kind = op >> 24, idx = op & 0xffffffu;
+    const uint32_t* src = kind == kTrPoint ? pts + 16 * idx : kind == kTrScalar ? scs + 8 * idx : pts;
+    const uint32_t nw = kind == kTrPoint ? 16 : kind == kTrScalar ? 8 : 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = (uint32_t)i < nw ? src[i] : 0u;
+  };
+  uint32_t cur[16], nxt[16];
+  fetch(0, cur);
   for (uint32_t k = 0; k < hd.nprog; k++) {
     const uint32_t op = prog[k];
     const uint32_t kind = op >> 24, idx = op & 0xffffffu;
+    fetch(k + 1, nxt);
     if (kind == kTrPoint) {
-      Fe<F> x, y;
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        x.l[i] = pts[16 * idx + i];
-        y.l[i] = pts[16 * idx + 8 + i];
-      }
       uint32_t z = 0;
 #pragma unroll
-      for (int i = 0; i < 8; i++) z |= x.l[i] | y.l[i];
+      for (int i = 0; i < 16; i++) z |= cur[i];
       if (z == 0) {
         st |= kTrStatusIdentity;
-        continue;
-      }
-      x = fe_from_mont<F>(x);
-      y = fe_from_mont<F>(y);
-      tr_put_byte(s, buf, lane, 1);
-#pragma unroll
-      for (int i = 0; i < 8; i++) tr_put_word(s, buf, lane, x.l[i]);
-#pragma unroll
-      for (int i = 0; i < 8; i++) tr_put_word(s, buf, lane, y.l[i]);
-    } else if (kind == kTrScalar || kind == kTrVk) {
-      Fe<Fs> v;
-      if (kind == kTrVk) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) v.l[i] = hd.vk[i];
       } else {
+        tr_put_byte(s, buf, lane, 1);
 #pragma unroll
-        for (int i = 0; i < 8; i++) v.l[i] = scs[8 * idx + i];
-        v = fe_from_mont<Fs>(v);
+        for (int i = 0; i < 16; i++) tr_put_word(s, buf, lane, cur[i]);
       }
+    } else if (kind == kTrScalar || kind == kTrVk) {
       tr_put_byte(s, buf, lane, 2);
 #pragma unroll
-      for (int i = 0; i < 8; i++) tr_put_word(s, buf, lane, v.l[i]);
+      for (int i = 0; i < 8; i++) tr_put_word(s, buf, lane, kind == kTrVk ? hd.vk[i] : cur[i]);
     } else {
       tr_put_byte(s, buf, lane, 0);
     }
@@ -214,6 +231,8 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
 #pragma unroll
       for (int i = 0; i < 8; i++) out[i] = c.l[i];
     }
+#pragma unroll
+    for (int i = 0; i < 16; i++) cur[i] = nxt[i];
   }
   if (status) status[b] = st;
 }
