@@ -59,7 +59,7 @@ int main() {
     run<8>("f29_inv_bgcd", buf, blocks);
     run<9>("f29_inv_fermat", buf, blocks);
   }
-  for (int blocks : {256, 1024}) {
+  for (int blocks : {256, 1024, 2048, 4096}) {
     run<4>("f29_mul_chain", buf, blocks);
     run<5>("f29_sqr_chain", buf, blocks);
     run<0>("jac29_dbl", buf, blocks);
