@@ -50,6 +50,13 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
 // butterfly and the second wave per SIMD cost what the shorter loop saves).
 constexpr size_t kAccLaneBudget = 1024 * 2 * 64;
 constexpr size_t kAccScalarsLds = 128 * 1024;
+// LDS fence: the transcript and k_acc_scalars blocks request kAccScalarsLds
+// and every ladder block kAccLadderFence (unused), so the two can never share
+// a CU (160 KiB per CU).  Both sides are single-wave latency chains; sharing
+// a SIMD with a ladder wave doubled k_acc_scalars (0.14 -> 0.27 ms at
+// B = 256).
+constexpr size_t kAccLadderFence = 40 * 1024;
+static_assert(kAccScalarsLds + kAccLadderFence > 160 * 1024, "the fence must not fit beside k_acc_scalars");
 inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
   uint32_t lg = 0;
   while (lg < maxlg && (items << (lg + 1)) <= kAccLaneBudget) lg++;
@@ -213,13 +220,13 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     HIP_TRY(hipEventRecord(up, st));
   }
   if (vk_repr && (rc = transcript_device_impl<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status))) return rc;
-  // k_acc_scalars: 4 waves per block of np proofs, (nsc + T + exchange)
-  // rows of 32 B per proof in LDS (proof stride np + 1), np <= 64 within
-  // a 128 KiB budget
-  const size_t row_bytes = (size_t)(L.nsc + T + kAccXVals + acc_num_vals(h)) * 32;
+  // k_acc_scalars: 4 waves per block of np proofs, (nsc + T + exchange +
+  // work) rows of 32 B per proof in LDS (proof stride np + 1), np <= 64
+  // within a 128 KiB budget
+  const size_t row_bytes = (size_t)(L.nsc + T + kAccXVals + acc_num_vals(h) + 2 * (h.bf + 3) + kAccStack) * 32;
   const uint32_t np = (uint32_t)std::min<size_t>(64, kAccScalarsLds / row_bytes - 1);
   if (np == 0) return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
-  const size_t lds = row_bytes * (np + 1);
+  const size_t lds = std::max(row_bytes * (np + 1), lgS > 0 ? kAccScalarsLds : 0);
   PM_LAUNCH(ctx, "acc_scalars",
             (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, st>>>(
                 h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
@@ -233,7 +240,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     const hipStream_t sl = ctx->red_stream;
     HIP_TRY(hipStreamWaitEvent(sl, up, 0));
     PM_LAUNCH_ST(ctx, sl, "acc_ladder",
-                 (k_acc_ladder<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, 0, sl>>>(
+                 (k_acc_ladder<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, kAccLadderFence, sl>>>(
                      h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, S, Lb,
                      (Xyzz<F>*)ctx->acc_lad.p)));
     HIP_TRY(hipEventRecord(lad_done, sl));
@@ -258,7 +265,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
 }
 
 // Batched Blake2b transcript replay (transcript_kernels.hpp): absorb program
-// in verifier read order, one lane per proof, challenges written in the
+// in verifier read order, four lanes per proof, challenges written in the
 // (B, 7, 4) layout pm_accum_batch reads.
 template <class Cv>
 int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
@@ -308,10 +315,14 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
   if ((rc = ctx->tr_canon.ensure(nall * 32))) return rc;
   uint32_t* cpts = (uint32_t*)ctx->tr_canon.p;
   uint32_t* cscs = cpts + 8 * ncoord;
+  // LDS fence against the accumulator's ladder (kAccLadderFence) while the
+  // blocks fit one per CU; larger batches run without the ladder anyway
+  const size_t tblocks = (B + kTrSlots - 1) / kTrSlots;
+  const bool fence = tblocks <= 256;
   PM_LAUNCH(ctx, "transcript",
             (k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
                  (uint32_t)B, L.npts, L.nsc, (const uint32_t*)d_points, (const uint32_t*)d_scalars, cpts, cscs),
-             k_transcript<Cv><<<(unsigned)((B + 63) / 64), 64, 0, st>>>(
+             k_transcript<Cv><<<(unsigned)tblocks, 64, fence ? kAccScalarsLds : 0, st>>>(
                  hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status)));
   return PM_OK;
 }

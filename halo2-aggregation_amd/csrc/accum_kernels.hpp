@@ -77,30 +77,35 @@ struct LdsRows {
 // or compress_expressions in theta, lookup.rs:214-243).
 template <class Fs>
 __device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const LdsRows& sc, const AccumHdr& h,
-                                const uint32_t* consts, Fe<Fs> acc, const Fe<Fs>& mult) {
-  Fe<Fs> st[kAccStack];
-  int sp = 0;
+                                const uint32_t* consts, const LdsRows& stk, Fe<Fs> acc, const Fe<Fs>& mult) {
+  // top of stack in registers, the entries below it in the lane's LDS rows
+  // (a private array indexed by the runtime depth lived in scratch memory)
+  Fe<Fs> top;
+  int sp = 0;  // entries, including top
   for (uint32_t i = 0; i < len; i++) {
     const uint32_t op = code[i] & 0xffu, arg = code[i] >> 8;
     if (op == PM_EXPR_END) {
-      acc = fe_add<Fs>(fe_mul<Fs>(acc, mult), st[--sp]);
+      acc = fe_add<Fs>(fe_mul<Fs>(acc, mult), top);
+      sp = 0;
     } else if (op <= PM_EXPR_INSTANCE) {
+      if (sp) stk.put<Fs>(sp - 1, top);
       if (op == PM_EXPR_CONST) {
-        st[sp++] = ldfe<Fs>(consts, h.c_user + arg);
+        top = ldfe<Fs>(consts, h.c_user + arg);
       } else {
         const uint32_t base = op == PM_EXPR_FIXED ? h.sc_fixed : op == PM_EXPR_ADVICE ? h.sc_adv : h.sc_inst;
-        st[sp++] = sc.get<Fs>(base + arg);
+        top = sc.get<Fs>(base + arg);
       }
+      sp++;
     } else if (op == PM_EXPR_NEG) {
-      st[sp - 1] = fe_neg<Fs>(st[sp - 1]);
+      top = fe_neg<Fs>(top);
     } else if (op == PM_EXPR_SUM) {
-      st[sp - 2] = fe_add<Fs>(st[sp - 2], st[sp - 1]);
+      top = fe_add<Fs>(stk.get<Fs>(sp - 2), top);
       sp--;
-    } else {  // PROD, SCALED
-      const Fe<Fs> b = op == PM_EXPR_PROD ? st[sp - 1] : ldfe<Fs>(consts, h.c_user + arg);
-      const int dst = op == PM_EXPR_PROD ? sp - 2 : sp - 1;
-      st[dst] = fe_mul<Fs>(st[dst], b);
-      if (op == PM_EXPR_PROD) sp--;
+    } else if (op == PM_EXPR_PROD) {
+      top = fe_mul<Fs>(stk.get<Fs>(sp - 2), top);
+      sp--;
+    } else {  // SCALED
+      top = fe_mul<Fs>(top, ldfe<Fs>(consts, h.c_user + arg));
     }
   }
   return acc;
@@ -119,7 +124,11 @@ __device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const LdsRow
 //   sel in {l_0, l_last, 1 - l_last - l_blind}), h_eval and the e
 //   coefficient; finally all 4 waves convert the T coefficients.
 // LDS rows per proof (word-major, proof stride np + 1): [0, nsc) evaluations,
-// then T coefficients, then the exchange rows (kAccX*).
+// then T coefficients, then the exchange rows (kAccX*), then the work rows of
+// wave 0 (2 (bf + 3): Montgomery's-trick denominators and prefix products)
+// and of wave 1 (kAccStack: the expression stack).  Nothing is indexed at
+// run time in private arrays: those live in scratch memory, whose latency
+// sat on every chain (4 KiB of scratch per lane, ~0.23 ms per call).
 constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXVals = 3;  // exchange row offsets
 constexpr int kAccSelL0 = 0, kAccSelLast = 1, kAccSelOmb = 2;
 
@@ -153,6 +162,9 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const LdsRows sc{acc_lds, pl, np + 1};
   const LdsRows cf{acc_lds + (size_t)8 * h.nsc * (np + 1), pl, np + 1};
   const LdsRows xr{acc_lds + (size_t)8 * (h.nsc + h.T) * (np + 1), pl, np + 1};
+  const uint32_t r_wk = h.nsc + h.T + kAccXVals + acc_num_vals(h);
+  const LdsRows wk{acc_lds + (size_t)8 * r_wk * (np + 1), pl, np + 1};                      // wave 0
+  const LdsRows stk{acc_lds + (size_t)8 * (r_wk + 2 * (h.bf + 3)) * (np + 1), pl, np + 1};  // wave 1
   const uint32_t* ch = challenges + 8ull * 7 * (live ? b : b0);
   const Fe<Fs> one = fe_one<Fs>(), zero = fe_zero<Fs>();
   const Fe<Fs> y = ldfe<Fs>(ch, 3), x = ldfe<Fs>(ch, 4);
@@ -165,32 +177,35 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     const Fe<Fs> xn1 = fe_sub<Fs>(xn, one);
     // l_i = w^i (x^n - 1) / (n (x - w^i)), w = omega^-1, i < bf + 2, plus
     // 1 / (x^n - 1) for h_eval: one batched inversion (Montgomery's trick).
+    // rows: den_i at wk[i], prefix products at wk[K + i]
     const uint32_t K = h.bf + 3;
-    Fe<Fs> den[kAccMaxBlind + 3], pre[kAccMaxBlind + 3];
     const Fe<Fs> nfe = ldfe<Fs>(consts, h.c_n);
+    Fe<Fs> pre = zero;
     for (uint32_t i = 0; i < K; i++) {
-      den[i] = i + 1 < K ? fe_mul<Fs>(nfe, fe_sub<Fs>(x, ldfe<Fs>(consts, h.c_wpow + i))) : xn1;
-      pre[i] = i ? fe_mul<Fs>(pre[i - 1], den[i]) : den[i];
+      const Fe<Fs> den = i + 1 < K ? fe_mul<Fs>(nfe, fe_sub<Fs>(x, ldfe<Fs>(consts, h.c_wpow + i))) : xn1;
+      pre = i ? fe_mul<Fs>(pre, den) : den;
+      wk.put<Fs>(i, den);
+      wk.put<Fs>(K + i, pre);
     }
-    Fe<Fs> inv = fe_inv_fast<Fs>(pre[K - 1]);
+    Fe<Fs> inv = fe_inv_fast<Fs>(pre);
     for (uint32_t i = K - 1; i > 0; i--) {
-      const Fe<Fs> t = fe_mul<Fs>(inv, pre[i - 1]);
-      inv = fe_mul<Fs>(inv, den[i]);
-      den[i] = t;  // now 1 / den_i
+      const Fe<Fs> t = fe_mul<Fs>(inv, wk.get<Fs>(K + i - 1));
+      inv = fe_mul<Fs>(inv, wk.get<Fs>(i));
+      wk.put<Fs>(i, t);  // now 1 / den_i
     }
-    den[0] = inv;
+    wk.put<Fs>(0, inv);
     Fe<Fs> l_blind = zero;
     for (uint32_t i = 0; i + 1 < K; i++) {
-      const Fe<Fs> li = fe_mul<Fs>(fe_mul<Fs>(ldfe<Fs>(consts, h.c_wpow + i), xn1), den[i]);
+      const Fe<Fs> li = fe_mul<Fs>(fe_mul<Fs>(ldfe<Fs>(consts, h.c_wpow + i), xn1), wk.get<Fs>(i));
       if (i == 0) l_0 = li;
       else if (i == h.bf + 1) l_last = li;
       else l_blind = fe_add<Fs>(l_blind, li);
     }
-    inv_xn1 = den[K - 1];
+    inv_xn1 = wk.get<Fs>(K - 1);
     omb = fe_sub<Fs>(one, fe_add<Fs>(l_last, l_blind));  // 1 - (l_last + l_blind)
   } else if (live && role == 1) {
     // gates (verifier.rs:593-605), then the identity values in fold order
-    xr.put<Fs>(kAccXHvg, acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, zero, y));
+    xr.put<Fs>(kAccXHvg, acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, stk, zero, y));
     const Fe<Fs> beta = ldfe<Fs>(ch, 1), gamma = ldfe<Fs>(ch, 2);
     uint32_t vi = kAccXVals;
     if (h.n_perm_sets) {
@@ -217,8 +232,8 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     }
     if (h.num_lookups) {
       const Fe<Fs> theta = ldfe<Fs>(ch, 0);
-      const Fe<Fs> cin = acc_eval_code<Fs>(prog + h.p_lkin, h.n_lkin, sc, h, consts, zero, theta);
-      const Fe<Fs> ctab = acc_eval_code<Fs>(prog + h.p_lktab, h.n_lktab, sc, h, consts, zero, theta);
+      const Fe<Fs> cin = acc_eval_code<Fs>(prog + h.p_lkin, h.n_lkin, sc, h, consts, stk, zero, theta);
+      const Fe<Fs> ctab = acc_eval_code<Fs>(prog + h.p_lktab, h.n_lktab, sc, h, consts, stk, zero, theta);
       const Fe<Fs> rfac = fe_mul<Fs>(fe_add<Fs>(cin, beta), fe_add<Fs>(ctab, gamma));
       for (uint32_t i = 0; i < h.num_lookups; i++) {
         const uint32_t e = h.sc_lk + 5 * i;
@@ -239,16 +254,18 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     const Fe<Fs> v = ldfe<Fs>(ch, 5), u = ldfe<Fs>(ch, 6);
     Fe<Fs> xn = x;
     for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
-    Fe<Fs> up[kAccMaxSets];
-    up[h.nsets - 1] = one;
-    for (int j = (int)h.nsets - 2; j >= 0; j--) up[j] = fe_mul<Fs>(up[j + 1], u);
     for (uint32_t t = 0; t < h.nslots; t++) cf.put<Fs>(t, zero);
     Fe<Fs> coefH = zero, ev = zero, ceh = zero;
     uint32_t qi = 0;
-    for (uint32_t j = 0; j < h.nsets; j++) {
+    for (uint32_t j = 0; j < h.nsets; j++) qi += prog[h.p_setlen + j];
+    // sets from the last, so u^{S-1-j} is a running product (every
+    // coefficient is a sum, so the order of the additions does not matter)
+    Fe<Fs> upj = one;
+    for (int j = (int)h.nsets - 1; j >= 0; j--) {
       const uint32_t m = prog[h.p_setlen + j];
+      qi -= m;
       // c_i = u^{S-1-j} v^{m-1-i}, walked from the last query of the set
-      Fe<Fs> c = up[j];
+      Fe<Fs> c = upj;
       for (int i = (int)m - 1; i >= 0; i--) {
         const uint32_t slot = prog[h.p_query + 2 * (qi + i)], eidx = prog[h.p_query + 2 * (qi + i) + 1];
         if (eidx == kEvalH) ceh = fe_add<Fs>(ceh, c);
@@ -257,9 +274,9 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
         else cf.put<Fs>(slot, fe_add<Fs>(cf.get<Fs>(slot), c));
         c = fe_mul<Fs>(c, v);
       }
-      qi += m;
-      cf.put<Fs>(h.nslots + j, up[j]);
-      cf.put<Fs>(h.nslots + h.nsets + j, fe_mul<Fs>(fe_mul<Fs>(up[j], ldfe<Fs>(consts, h.c_omega_eval + j)), x));
+      cf.put<Fs>(h.nslots + j, upj);
+      cf.put<Fs>(h.nslots + h.nsets + j, fe_mul<Fs>(fe_mul<Fs>(upj, ldfe<Fs>(consts, h.c_omega_eval + j)), x));
+      upj = fe_mul<Fs>(upj, u);
     }
     Fe<Fs> xp = one;
     for (uint32_t i = 0; i < h.nh; i++) {

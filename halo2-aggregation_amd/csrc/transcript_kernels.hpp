@@ -31,9 +31,8 @@
 // rejects the identity before touching the hash (C::from_xy(0, 0) fails,
 // transcript.rs:101-110): such a point is skipped and flagged in `status`.
 //
-// One lane per proof; each lane's message buffer lives in LDS word-major
-// ([word][lane]) so the compression's 32 word reads are conflict-free.  All
-// lanes run the same absorb program, so block boundaries (and the
+// Four lanes per proof (see TrLane); each proof's message buffer lives in
+// LDS.  All proofs run the same absorb program, so block boundaries (and the
 // compressions) stay wave-uniform unless a proof has an identity point.
 #pragma once
 #include "blake2b.hpp"
@@ -65,80 +64,188 @@ PM_HD Fe<Fs> fe_from_bytes_wide(const uint32_t d[16]) {
   return fe_add<Fs>(fe_mul<Fs>(lo, r2), fe_mul<Fs>(hi, r3));
 }
 
-// Per-lane absorb state.  The message stream lives in a 256-byte circular
-// buffer in LDS (two blocks, word-major [word][lane]); bytes are packed into
-// whole words in a register first, so LDS sees only 32-bit stores.  The
-// invariant between records is pos <= 128: a full block stays buffered until
-// more data arrives (blake2b_simd's lazy compression), and the compression
-// has a single call site in tr_settle().
-struct TrLane {
-  uint64_t h[8];
-  uint64_t t;    // bytes compressed so far (multiple of 128)
-  uint32_t pos;  // bytes buffered after t
-  uint32_t acc;  // pending partial word (low `pos & 3` bytes valid)
-};
+// Each proof's transcript is run by the 4 lanes of a quad (16 proofs per
+// 64-lane block).  The absorb bookkeeping is repeated by all 4 lanes; the
+// compression is split by column: lane q holds column q of the working state
+// (v[q], v[4+q], v[8+q], v[12+q]) and of the chaining value (h[q], h[4+q]),
+// runs one G per half round, and the diagonal half round is reached by
+// rotating b, c, d by 1, 2, 3 lanes inside the quad (DPP quad_perm, no LDS).
+// A compression is then 12 x 2 G steps per lane instead of 12 x 8: the
+// single-lane form was bound by its ~2 K dependent VALU instructions.
+//
+// The message stream lives in a 256-byte circular buffer in LDS (two blocks,
+// 64-bit-word-major [w64][slot]); bytes are packed into whole 32-bit words in
+// a register first.  The invariant between records is pos <= 128: a full
+// block stays buffered until more data arrives (blake2b_simd's lazy
+// compression), and the compression has a single call site in tr_settle().
+constexpr uint32_t kTrSlots = 16;  // proofs per 64-lane block
 
-__device__ __forceinline__ void tr_store(uint32_t (*buf)[64], uint32_t lane, uint32_t widx, uint32_t w) {
-  buf[widx & 63][lane] = w;
+struct TrLane {
+  uint64_t h0, h1;  // h[q], h[4 + q]
+  uint64_t t;       // bytes compressed so far (multiple of 128)
+  uint32_t pos;     // bytes buffered after t
+  uint32_t acc;     // pending partial word (low `pos & 3` bytes valid)
+};
+typedef uint64_t TrBuf[32][kTrSlots];
+
+// all 4 lanes of the quad store the same word to the same address
+__device__ __forceinline__ void tr_store(TrBuf& buf, uint32_t slot, uint32_t widx, uint32_t w) {
+  reinterpret_cast<uint32_t*>(&buf[(widx >> 1) & 31][slot])[widx & 1] = w;
 }
 
-__device__ __forceinline__ void tr_put_byte(TrLane& s, uint32_t (*buf)[64], uint32_t lane, uint32_t b) {
+__device__ __forceinline__ void tr_put_byte(TrLane& s, TrBuf& buf, uint32_t slot, uint32_t b) {
   const uint32_t a = (uint32_t)s.t + s.pos;
   const uint32_t k = a & 3;
   s.acc |= b << (8 * k);
   if (k == 3) {
-    tr_store(buf, lane, a >> 2, s.acc);
+    tr_store(buf, slot, a >> 2, s.acc);
     s.acc = 0;
   }
   s.pos++;
 }
 
-__device__ __forceinline__ void tr_put_word(TrLane& s, uint32_t (*buf)[64], uint32_t lane, uint32_t w) {
+__device__ __forceinline__ void tr_put_word(TrLane& s, TrBuf& buf, uint32_t slot, uint32_t w) {
   const uint32_t a = (uint32_t)s.t + s.pos;
   const uint32_t k = a & 3;
   if (k == 0) {
-    tr_store(buf, lane, a >> 2, w);
+    tr_store(buf, slot, a >> 2, w);
   } else {
-    tr_store(buf, lane, a >> 2, s.acc | (w << (8 * k)));
+    tr_store(buf, slot, a >> 2, s.acc | (w << (8 * k)));
     s.acc = w >> (32 - 8 * k);
   }
   s.pos += 4;
 }
 
+// lane i of the quad receives x from lane P[i]
+template <int CTRL>
+__device__ __forceinline__ uint64_t tr_qperm(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+constexpr int kQRot1 = 1 | 2 << 2 | 3 << 4 | 0 << 6;  // from lane q + 1
+constexpr int kQRot2 = 2 | 3 << 2 | 0 << 4 | 1 << 6;  // from lane q + 2
+constexpr int kQRot3 = 3 | 0 << 2 | 1 << 4 | 2 << 6;  // from lane q + 3
+
+// sigma rows of RFC 7693 §2.7, packed per half round: nibble q of COL is
+// sigma[2q] (the x word of column G q), of COLY sigma[2q+1]; DIAG / DIAGY the
+// same for the diagonal G's (sigma[8 + 2q], sigma[9 + 2q]).
+struct TrSigma {
+  uint16_t colx, coly, diagx, diagy;
+};
+__host__ __device__ constexpr TrSigma tr_sigma_pack(const int (&r)[16]) {
+  return TrSigma{(uint16_t)(r[0] | r[2] << 4 | r[4] << 8 | r[6] << 12),
+                 (uint16_t)(r[1] | r[3] << 4 | r[5] << 8 | r[7] << 12),
+                 (uint16_t)(r[8] | r[10] << 4 | r[12] << 8 | r[14] << 12),
+                 (uint16_t)(r[9] | r[11] << 4 | r[13] << 8 | r[15] << 12)};
+}
+constexpr int kB2Sigma[10][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+                                  {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+                                  {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+                                  {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+                                  {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+                                  {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+                                  {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+                                  {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+                                  {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+                                  {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+
+#define PM_B2_GQ(a, b, c, d, x, y) \
+  do {                             \
+    a = a + b + (x);               \
+    d = PM_B2_ROT(d ^ a, 32);         \
+    c = c + d;                     \
+    b = PM_B2_ROT(b ^ c, 24);         \
+    a = a + b + (y);               \
+    d = PM_B2_ROT(d ^ a, 16);         \
+    c = c + d;                     \
+    b = PM_B2_ROT(b ^ c, 63);         \
+  } while (0)
+
+// F(h, m, t, f) of RFC 7693 §3.2 by the quad: m = the 16 words of the block
+// starting at 64-bit word w0 of the slot's buffer; lane q updates h[q] and
+// h[4 + q].
+template <int R>
+__device__ __forceinline__ void tr_round_q(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, const TrBuf& buf,
+                                           uint32_t slot, uint32_t w0, uint32_t q4) {
+  constexpr TrSigma S = tr_sigma_pack(kB2Sigma[R % 10]);
+  const uint64_t x0 = buf[(w0 + ((S.colx >> q4) & 15)) & 31][slot];
+  const uint64_t y0 = buf[(w0 + ((S.coly >> q4) & 15)) & 31][slot];
+  const uint64_t x1 = buf[(w0 + ((S.diagx >> q4) & 15)) & 31][slot];
+  const uint64_t y1 = buf[(w0 + ((S.diagy >> q4) & 15)) & 31][slot];
+  PM_B2_GQ(a, b, c, d, x0, y0);
+  b = tr_qperm<kQRot1>(b);
+  c = tr_qperm<kQRot2>(c);
+  d = tr_qperm<kQRot3>(d);
+  PM_B2_GQ(a, b, c, d, x1, y1);
+  b = tr_qperm<kQRot3>(b);
+  c = tr_qperm<kQRot2>(c);
+  d = tr_qperm<kQRot1>(d);
+}
+#undef PM_B2_GQ
+
+__device__ __forceinline__ void tr_compress_q(TrLane& s, const TrBuf& buf, uint32_t slot, uint32_t q, uint32_t w0,
+                                              uint64_t tcount, bool last) {
+  const uint64_t iv_c = q == 0 ? Blake2bIV::v[0] : q == 1 ? Blake2bIV::v[1] : q == 2 ? Blake2bIV::v[2]
+                                                                                      : Blake2bIV::v[3];
+  const uint64_t iv_d = q == 0 ? Blake2bIV::v[4] : q == 1 ? Blake2bIV::v[5] : q == 2 ? Blake2bIV::v[6]
+                                                                                      : Blake2bIV::v[7];
+  uint64_t a = s.h0, b = s.h1, c = iv_c, d = iv_d;
+  if (q == 0) d ^= tcount;    // v12 ^= t
+  if (q == 2 && last) d = ~d;  // v14 = ~v14
+  const uint32_t q4 = 4 * q;
+  tr_round_q<0>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<1>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<2>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<3>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<4>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<5>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<6>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<7>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<8>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<9>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<10>(a, b, c, d, buf, slot, w0, q4);
+  tr_round_q<11>(a, b, c, d, buf, slot, w0, q4);
+  s.h0 ^= a ^ c;
+  s.h1 ^= b ^ d;
+}
+
 // Compress every full block that more data has arrived after; with `squeeze`
-// also finalise a copy of the state and return the digest in d.
-__device__ __forceinline__ void tr_settle(TrLane& s, uint32_t (*buf)[64], uint32_t lane, bool squeeze, uint32_t d[16]) {
+// finalise (the buffered tail zero-padded) and return the digest in d (all
+// 4 lanes) without advancing the state.
+__device__ __forceinline__ void tr_settle(TrLane& s, TrBuf& buf, uint32_t slot, uint32_t q, bool squeeze,
+                                          uint32_t d[16]) {
   for (;;) {
     const bool flush = s.pos > 128;
     const bool fin = !flush && squeeze;
     if (!flush && !fin) return;
     const uint32_t a = (uint32_t)s.t + s.pos;
-    if (fin && (a & 3)) tr_store(buf, lane, a >> 2, s.acc);  // partial word, zero above pos
-    const uint32_t w0 = ((uint32_t)s.t & 255) >> 2;
-    uint64_t m[16], hh[8];
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-      m[i] = (uint64_t)buf[(w0 + 2 * i) & 63][lane] | ((uint64_t)buf[(w0 + 2 * i + 1) & 63][lane] << 32);
+    const uint32_t wd0 = ((uint32_t)s.t & 255) >> 2;  // first 32-bit word of the block
     if (fin) {
+      if (a & 3) tr_store(buf, slot, a >> 2, s.acc);  // partial word, zero above pos
+      const uint32_t z0 = (s.pos + 3) >> 2;
 #pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const uint32_t lo = 8u * i;
-        m[i] &= s.pos >= lo + 8 ? ~0ull : s.pos <= lo ? 0ull : ((1ull << (8 * (s.pos - lo))) - 1);
-      }
+      for (uint32_t j = 0; j < 32; j++)
+        if (j >= z0) tr_store(buf, slot, wd0 + j, 0u);
     }
-#pragma unroll
-    for (int i = 0; i < 8; i++) hh[i] = s.h[i];
-    blake2b_compress(hh, m, fin ? s.t + s.pos : s.t + 128, fin);
+    TrLane n = s;
+    tr_compress_q(n, buf, slot, q, wd0 >> 1, fin ? s.t + s.pos : s.t + 128, fin);
     if (fin) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        d[2 * i] = (uint32_t)hh[i];
-        d[2 * i + 1] = (uint32_t)(hh[i] >> 32);
-      }
+// digest word 2i, 2i + 1 = h[i]: h[K] is lane K's h0, h[4 + K] its h1
+#define PM_TR_BC(K)                                                                                            \
+  d[2 * K] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)n.h0, K * 0x55, 0xF, 0xF, false);               \
+  d[2 * K + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(n.h0 >> 32), K * 0x55, 0xF, 0xF, false);   \
+  d[2 * K + 8] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)n.h1, K * 0x55, 0xF, 0xF, false);           \
+  d[2 * K + 9] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(n.h1 >> 32), K * 0x55, 0xF, 0xF, false);
+      PM_TR_BC(0)
+      PM_TR_BC(1)
+      PM_TR_BC(2)
+      PM_TR_BC(3)
+#undef PM_TR_BC
       return;
     }
-#pragma unroll
-    for (int i = 0; i < 8; i++) s.h[i] = hh[i];
+    s.h0 = n.h0;
+    s.h1 = n.h1;
     s.t += 128;
     s.pos -= 128;
   }
@@ -169,23 +276,35 @@ __global__ void __launch_bounds__(256) k_tr_canon(uint32_t B, uint32_t npts, uin
 
 // points / scalars: canonical (k_tr_canon).  The next record's words are
 // loaded one record ahead (the record index comes from the uniform program,
-// so the address is known early) to hide the global-load latency.
+// so the address is known early) to hide the global-load latency.  64 lanes
+// = 16 proofs x 4 lanes; a quad always runs (and exits) together, as the
+// DPP exchanges in the compression require.
 template <class Cv>
 __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint32_t* __restrict__ prog,
                                                    const uint32_t* __restrict__ points,
                                                    const uint32_t* __restrict__ scalars,
                                                    uint32_t* __restrict__ challenges, uint32_t* __restrict__ status) {
   using Fs = typename Cv::Scalar;
-  __shared__ uint32_t buf[64][64];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t b = blockIdx.x * 64 + lane;
+  __shared__ TrBuf buf;
+  const uint32_t slot = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const uint32_t b = blockIdx.x * kTrSlots + slot;
   if (b >= hd.B) return;
   TrLane s;
-#pragma unroll
-  for (int i = 0; i < 8; i++) s.h[i] = hd.h0[i];
+  s.h0 = q == 0 ? hd.h0[0] : q == 1 ? hd.h0[1] : q == 2 ? hd.h0[2] : hd.h0[3];
+  s.h1 = q == 0 ? hd.h0[4] : q == 1 ? hd.h0[5] : q == 2 ? hd.h0[6] : hd.h0[7];
   s.t = 0;
   s.pos = 0;
   s.acc = 0;
+  // from_bytes_wide split over the quad: lane 0 computes lo R^2, lane 1 hi R^3
+  Fe<Fs> kq;
+  {
+    Fe<Fs> r2;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r2.l[i] = Fs::R2[i];
+    const Fe<Fs> r3 = fe_mul<Fs>(r2, r2);
+#pragma unroll
+    for (int i = 0; i < 8; i++) kq.l[i] = (q & 1) ? r3.l[i] : r2.l[i];
+  }
   uint32_t st = 0;
   const uint32_t* pts = points + 16ull * hd.npts * b;
   const uint32_t* scs = scalars + 8ull * hd.nsc * b;
@@ -211,30 +330,42 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
       if (z == 0) {
         st |= kTrStatusIdentity;
       } else {
-        tr_put_byte(s, buf, lane, 1);
+        tr_put_byte(s, buf, slot, 1);
 #pragma unroll
-        for (int i = 0; i < 16; i++) tr_put_word(s, buf, lane, cur[i]);
+        for (int i = 0; i < 16; i++) tr_put_word(s, buf, slot, cur[i]);
       }
     } else if (kind == kTrScalar || kind == kTrVk) {
-      tr_put_byte(s, buf, lane, 2);
+      tr_put_byte(s, buf, slot, 2);
 #pragma unroll
-      for (int i = 0; i < 8; i++) tr_put_word(s, buf, lane, kind == kTrVk ? hd.vk[i] : cur[i]);
+      for (int i = 0; i < 8; i++) tr_put_word(s, buf, slot, kind == kTrVk ? hd.vk[i] : cur[i]);
     } else {
-      tr_put_byte(s, buf, lane, 0);
+      tr_put_byte(s, buf, slot, 0);
     }
     // one compression site for every record kind
     const bool squeeze = kind == kTrSqueeze;
-    tr_settle(s, buf, lane, squeeze, d);
+    tr_settle(s, buf, slot, q, squeeze, d);
     if (squeeze) {
-      const Fe<Fs> c = fe_from_bytes_wide<Fs>(d);
-      uint32_t* out = challenges + 8ull * (kTrChallenges * b + idx);
+      Fe<Fs> x;  // lo (even lanes) or hi (odd lanes); a bitwise select, since a
+                 // conditional select of the array halves became a scratch access
+      const uint32_t mq = 0u - (q & 1u);
 #pragma unroll
-      for (int i = 0; i < 8; i++) out[i] = c.l[i];
+      for (int i = 0; i < 8; i++) x.l[i] = (d[8 + i] & mq) | (d[i] & ~mq);
+      const Fe<Fs> pr = fe_mul<Fs>(x, kq);
+      Fe<Fs> p0, p1;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        p0.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pr.l[i], 0x00, 0xF, 0xF, false);
+        p1.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pr.l[i], 0x55, 0xF, 0xF, false);
+      }
+      const Fe<Fs> c = fe_add<Fs>(p0, p1);  // = fe_from_bytes_wide(d)
+      uint2* out = reinterpret_cast<uint2*>(challenges + 8ull * (kTrChallenges * b + idx));
+      out[q] = make_uint2(q == 0 ? c.l[0] : q == 1 ? c.l[2] : q == 2 ? c.l[4] : c.l[6],
+                          q == 0 ? c.l[1] : q == 1 ? c.l[3] : q == 2 ? c.l[5] : c.l[7]);
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) cur[i] = nxt[i];
   }
-  if (status) status[b] = st;
+  if (status && q == 0) status[b] = st;
 }
 
 }  // namespace pm
