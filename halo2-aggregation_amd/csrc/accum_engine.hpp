@@ -49,6 +49,7 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
 // x 16 bits: 112 ladder doublings; 16 x 8 measured no faster, the wider
 // butterfly and the second wave per SIMD cost what the shorter loop saves).
 constexpr size_t kAccLaneBudget = 1024 * 2 * 64;
+constexpr size_t kAccSumLanes = 16384;
 constexpr size_t kAccScalarsLds = 128 * 1024;
 // LDS fence: the transcript and k_acc_scalars blocks request kAccScalarsLds
 // and every ladder block kAccLadderFence (unused), so the two can never share
@@ -209,7 +210,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   uint32_t* dcoef = (uint32_t*)ctx->acc_coef.p;
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
   const size_t nterm = (size_t)B * T;
-  const uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_lanes(nterm, 3);
+  uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_lanes(nterm, 3);
+  // 16 / 32 lanes per term only while the term products still fit one wave
+  // per SIMD (B = 16: 0.65 -> 0.58 ms; B = 256 stays at 8 lanes, 16 measured
+  // 0.71 -> 0.75 ms: profiles/r01_s4/accum_split_sweep.jsonl)
+  if (ctx->acc_split < 0 && lgS == 3)
+    while (lgS < 5 && (nterm << (lgS + 1)) <= kAccLaneBudget / 2) lgS++;
   const uint32_t S = 1u << lgS, Lb = (kGlvBits + S - 1) / S;
   hipEvent_t lad_done = nullptr, up = nullptr;
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
@@ -255,7 +261,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
               (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
                   h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, dpart)));
   }
-  const uint32_t lgL = acc_auto_lanes((size_t)B * 4, 5);
+  // lanes per output: at most ~16 K in total.  The affine conversion runs on
+  // lane 0 of each group, and it slowed from ~0.08 to ~0.14 ms when 32
+  // lanes per output spread the 1024 outputs of B = 256 over 512 waves
+  // (profiles/r01_s4/accum_sum_lanes.jsonl).
+  uint32_t lgL = 0;
+  while (lgL < 5 && ((size_t)B * 4 << (lgL + 1)) <= kAccSumLanes) lgL++;
   PM_LAUNCH(ctx, "acc_sum",
             (k_acc_sum<Cv><<<(unsigned)((B * 4 * (1u << lgL) + 63) / 64), 64, 0, st>>>(h, dpart, lgL,
                                                                                       (uint32_t*)d_out)));
