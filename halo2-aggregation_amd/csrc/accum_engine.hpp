@@ -42,6 +42,9 @@ void push_fe(std::vector<uint32_t>& v, const Fe<Fs>& a) {
 template <class Cv>
 int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
                            const void* d_scalars, void* d_ch, void* d_status);
+template <class Cv>
+int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
+                      const void* d_scalars, void* d_ch, void* d_status, hipStream_t st);
 
 // Lanes per item for the latency-bound accumulator kernels: the largest
 // power of two 2^lg <= 2^maxlg that keeps items * 2^lg within about two
@@ -217,15 +220,28 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   if (ctx->acc_split < 0 && lgS == 3)
     while (lgS < 5 && (nterm << (lgS + 1)) <= kAccLaneBudget / 2) lgS++;
   const uint32_t S = 1u << lgS, Lb = (kGlvBits + S - 1) / S;
-  hipEvent_t lad_done = nullptr, up = nullptr;
+  // Streams: with the split ladder (points only, the critical chain) it goes
+  // first on the main stream, and the transcript replay + k_acc_scalars run
+  // beside it on the reduction stream (kept off the ladder's CUs by the LDS
+  // fence); the term products wait for both.  Launching the ladder after the
+  // other two on the side stream cost ~20 us of start-up and ~20 us of
+  // cross-stream wake-up on the critical path (profiles/r01_s4/ktrace_*).
+  hipStream_t side = st;
+  hipEvent_t up = nullptr, sc_done = nullptr;
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
     if ((rc = ctx->acc_lad.ensure(nterm * S * sizeof(Xyzz<F>)))) return rc;
     up = ctx->next_event();
-    lad_done = ctx->next_event();
-    if (!up || !lad_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+    sc_done = ctx->next_event();
+    if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(up, st));
+    PM_LAUNCH(ctx, "acc_ladder",
+              (k_acc_ladder<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, kAccLadderFence, st>>>(
+                  h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, S, Lb,
+                  (Xyzz<F>*)ctx->acc_lad.p)));
+    side = ctx->red_stream;
+    HIP_TRY(hipStreamWaitEvent(side, up, 0));
   }
-  if (vk_repr && (rc = transcript_device_impl<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status))) return rc;
+  if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side))) return rc;
   // k_acc_scalars: 4 waves per block of np proofs, (nsc + T + exchange +
   // work) rows of 32 B per proof in LDS (proof stride np + 1), np <= 64
   // within a 128 KiB budget
@@ -233,26 +249,13 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   const uint32_t np = (uint32_t)std::min<size_t>(64, kAccScalarsLds / row_bytes - 1);
   if (np == 0) return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
   const size_t lds = std::max(row_bytes * (np + 1), lgS > 0 ? kAccScalarsLds : 0);
-  PM_LAUNCH(ctx, "acc_scalars",
-            (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, st>>>(
-                h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
-                dcoef, (uint32_t*)d_hout, np)));
-  // The ladder (points only) is launched after the transcript replay and
-  // k_acc_scalars (their few blocks are dispatched first); together with the
-  // cached uploads this took B = 256 from ~1.03 to ~0.85 ms.  Partitioning
-  // the CUs between the two streams (hipExtStreamCreateWithCUMask) measured
-  // no better.
-  if (lgS > 0) {  // ladder on the reduction stream, after this call's uploads
-    const hipStream_t sl = ctx->red_stream;
-    HIP_TRY(hipStreamWaitEvent(sl, up, 0));
-    PM_LAUNCH_ST(ctx, sl, "acc_ladder",
-                 (k_acc_ladder<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, kAccLadderFence, sl>>>(
-                     h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, S, Lb,
-                     (Xyzz<F>*)ctx->acc_lad.p)));
-    HIP_TRY(hipEventRecord(lad_done, sl));
-  }
+  PM_LAUNCH_ST(ctx, side, "acc_scalars",
+               (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, side>>>(
+                   h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
+                   dcoef, (uint32_t*)d_hout, np)));
   if (lgS > 0) {
-    HIP_TRY(hipStreamWaitEvent(st, lad_done, 0));
+    HIP_TRY(hipEventRecord(sc_done, side));
+    HIP_TRY(hipStreamWaitEvent(st, sc_done, 0));
     PM_LAUNCH(ctx, "acc_termmul",
               (k_acc_termmul_split<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
                   h, dcoef, (const Xyzz<F>*)ctx->acc_lad.p, lgS, Lb, dpart)));
@@ -279,8 +282,8 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
 // in verifier read order, four lanes per proof, challenges written in the
 // (B, 7, 4) layout pm_accum_batch reads.
 template <class Cv>
-int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
-                           const void* d_scalars, void* d_ch, void* d_status) {
+int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
+                      const void* d_scalars, void* d_ch, void* d_status, hipStream_t st) {
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
   AccLayout L;
@@ -319,7 +322,6 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
   const Fe<Fs> vk = fe_from_mont<Fs>(fe_from_u64<Fs>(vk_repr));
   for (int i = 0; i < 8; i++) hd.vk[i] = vk.l[i];
 
-  const hipStream_t st = ctx->stream;
   int rc;
   if ((rc = ctx->tr_prog.put(prog, st))) return rc;
   const size_t ncoord = B * 2 * (size_t)L.npts, nall = ncoord + B * (size_t)L.nsc;
@@ -330,12 +332,18 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
   // blocks fit one per CU; larger batches run without the ladder anyway
   const size_t tblocks = (B + kTrSlots - 1) / kTrSlots;
   const bool fence = tblocks <= 256;
-  PM_LAUNCH(ctx, "transcript",
+  PM_LAUNCH_ST(ctx, st, "transcript",
             (k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
                  (uint32_t)B, L.npts, L.nsc, (const uint32_t*)d_points, (const uint32_t*)d_scalars, cpts, cscs),
              k_transcript<Cv><<<(unsigned)tblocks, 64, fence ? kAccScalarsLds : 0, st>>>(
                  hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status)));
   return PM_OK;
+}
+
+template <class Cv>
+int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
+                           const void* d_scalars, void* d_ch, void* d_status) {
+  return transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, ctx->stream);
 }
 
 // vk_repr = from_bytes_wide(Blake2b("Halo2-Verify-Key", ...)) (verifier.rs:347-354)
