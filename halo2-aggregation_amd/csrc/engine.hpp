@@ -124,7 +124,9 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const bool glv = !fixed && ctx->glv && pl.c >= kGlvMinC;
   if (!fixed && !glv) pl = make_plan(n, ctx->window_c, ctx->groups, ctx->min_chunk);
   const size_t npts = glv ? 2 * n : n;  // sort entries per window row
-  const hipStream_t st = ctx->stream, st2 = ctx->red_stream;
+  // reduction stream only when window groups overlap; with one group the
+  // cross-stream wake-up cost ~12 us between k_accumulate and the fixup
+  const hipStream_t st = ctx->stream, st2 = pl.G > 1 ? ctx->red_stream : st;
   const int Wr = fixed ? 1 : pl.W;                  // bucket sets (reduced windows)
   const int wpg = fixed ? 1 : pl.wpg;
   const size_t stride = fixed ? ft->npad : npts;    // digit row length
@@ -268,8 +270,10 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     else
       PM_LAUNCH(ctx, "accumulate",
                 (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg)));
-    HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi], st));
-    HIP_TRY(hipStreamWaitEvent(st2, ctx->grp_ev[2 * gi], 0));
+    if (st2 != st) {
+      HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi], st));
+      HIP_TRY(hipStreamWaitEvent(st2, ctx->grp_ev[2 * gi], 0));
+    }
     PM_LAUNCH_ST(ctx, st2, "fixup", {
       if (fixed)  // merged buckets span ~W*n/2^(c-1)/chunk slices each: one lane per bucket
         k_fixup<F><<<(s1 - s0 + 255) / 256, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg,
