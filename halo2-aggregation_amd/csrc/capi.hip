@@ -271,6 +271,10 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_GLV")) c->glv = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PM_SORT_PPT")) {
+    const int v = std::atoi(e);
+    c->sort_ppt = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+  }
   *out = c.release();
   return PM_OK;
 }

@@ -39,6 +39,21 @@
 namespace pm {
 // ---------------------------------------------------------- MSM pipeline
 
+template <bool D16, bool WIDE>
+void launch_coarse(const void* dg, uint32_t ue, SortGeom gm, const uint32_t* bofs, void* mid, dim3 grid, size_t lds,
+                   hipStream_t st) {
+  using DT = typename DigitCode<D16>::T;
+  using MT = typename SortEntry<WIDE>::T;
+  const DT* d = (const DT*)dg;
+  MT* m = (MT*)mid;
+  switch (gm.ppt) {
+    case 1: k_sort_coarse<D16, WIDE, 1><<<grid, kSortThreads, lds, st>>>(d, ue, gm, bofs, m); break;
+    case 2: k_sort_coarse<D16, WIDE, 2><<<grid, kSortThreads, lds, st>>>(d, ue, gm, bofs, m); break;
+    case 4: k_sort_coarse<D16, WIDE, 4><<<grid, kSortThreads, lds, st>>>(d, ue, gm, bofs, m); break;
+    default: k_sort_coarse<D16, WIDE, 8><<<grid, kSortThreads, lds, st>>>(d, ue, gm, bofs, m); break;
+  }
+}
+
 template <class Fs, int W>
 void launch_sort_w(bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* bh,
                    void* digits, uint32_t stride, uint32_t merged, hipStream_t st) {
@@ -138,7 +153,15 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   SortGeom g;  // histogram geometry (blocks of scalars)
   g.FB = std::max(0, pl.cmax - 1 - 8);
   g.NCB = (pl.K >> g.FB) + 1;
-  g.nblk = (int)((stride + kSortB - 1) / kSortB);
+  // points per thread: blocks of 1024 threads x ppt points, ppt the largest
+  // power of two <= 8 that still gives >= 128 blocks (2^20: 8192 points per
+  // block; larger blocks give longer contiguous runs per coarse bin in
+  // k_sort_coarse and a 4x smaller block histogram to scan: sort 0.19 ->
+  // 0.16 ms at 2^20; small n keeps enough blocks)
+  g.ppt = 1;
+  while (g.ppt < kSortPerThread && stride >= (size_t)256 * g.ppt * kSortThreads) g.ppt *= 2;
+  if (ctx->sort_ppt > 0 && !fixed) g.ppt = ctx->sort_ppt;  // PM_SORT_PPT (1, 2, 4, 8): tuning experiments
+  g.nblk = (int)((stride + (size_t)g.ppt * kSortThreads - 1) / ((size_t)g.ppt * kSortThreads));
   SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
   if (fixed) gm.nblk = g.nblk * pl.W;
   const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
@@ -212,29 +235,25 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum, bofs, nullptr);
   });
   {
-    const size_t lds = (size_t)kSortB * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
+    const size_t lds = (size_t)g.ppt * kSortThreads * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
     const dim3 grid(gm.nblk, Wr);
     void* dg = ctx->digits.p;
     const uint32_t ue = (uint32_t)E;
     if (d16 && !wide)
-      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<true, false><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint16_t*)dg, ue, gm, bofs, (uint32_t*)mid)));
+      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<true, false>(dg, ue, gm, bofs, mid, grid, lds, st));
     else if (d16)
-      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<true, true><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint16_t*)dg, ue, gm, bofs, (uint64_t*)mid)));
+      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<true, true>(dg, ue, gm, bofs, mid, grid, lds, st));
     else if (!wide)
-      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<false, false><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint32_t*)dg, ue, gm, bofs, (uint32_t*)mid)));
+      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<false, false>(dg, ue, gm, bofs, mid, grid, lds, st));
     else
-      PM_LAUNCH(ctx, "sort_coarse", (k_sort_coarse<false, true><<<grid, kSortThreads, lds, st>>>(
-                                        (const uint32_t*)dg, ue, gm, bofs, (uint64_t*)mid)));
+      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<false, true>(dg, ue, gm, bofs, mid, grid, lds, st));
   }
   // LDS cache: room for 1.5x the mean segment (random digits fill segments
   // evenly; a skewed segment falls back to re-reading mid), capped at 64 KiB
   const size_t esz = wide ? 8 : 4;
   const size_t mean_seg = E / std::max(1, g.NCB - 1) + 1;
   const uint32_t cache_n = (uint32_t)std::min<size_t>(kFineCacheBytes / esz, (mean_seg * 3 / 2 + 63) & ~size_t(63));
-  const size_t lds_fine = (size_t)cache_n * esz + ((size_t)(1 << g.FB) + kFineThreads / 64 + 1) * 4;
+  const size_t lds_fine = (size_t)cache_n * (esz + 4) + ((size_t)(1 << g.FB) + kFineThreads / 64 + 1) * 4;
   if (wide)
     PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<true><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
                                     (const uint64_t*)mid, bofs, gm, Wr, pl.NB, cache_n, offsets, sorted)));

@@ -122,6 +122,7 @@ struct pm_ctx {
   int prefetch = -1;  // -1 auto, 0 off, 1 on (diagnostics: PM_PREFETCH env)
   int groups = 0;     // window groups, 0 = auto (diagnostics: PM_GROUPS env)
   int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
+  int sort_ppt = 0;   // sort points per thread, 0 = auto (diagnostics: PM_SORT_PPT env, 1/2/4/8)
   int glv = 0;        // variable-base MSM in GLV mode (pm_ctx_set_glv, PM_GLV env): measured slower, off
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;

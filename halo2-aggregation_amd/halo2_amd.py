@@ -21,7 +21,7 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpasta_msm.so")
+LIB_PATH = os.environ.get("PM_LIB") or os.path.join(_HERE, "lib", "libpasta_msm.so")  # PM_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "pasta_msm.h")
 
 PALLAS, VESTA, BN254 = 0, 1, 2
