@@ -168,7 +168,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // 4-B coarse entries when the entry index fits beside the fine bits and the sign
   const bool wide = E > (size_t(1) << (31 - g.FB));
   const bool d16 = pl.cmax <= 16;
-  const size_t longs_stride = 16 + (size_t)pl.maxlong * sizeof(LongChain);
+  // per group: [nlong, nshort, pad] [maxlong long chains] [nthreads short chains]
+  const size_t longs_stride = (16 + ((size_t)pl.maxlong + pl.nthreads) * sizeof(LongChain) + 15) & ~size_t(15);
   int rc;
   if ((rc = ctx->digits.ensure(nW * (d16 ? 2 : 4)))) return rc;
   if ((rc = ctx->sorted.ensure(nW * 4))) return rc;
@@ -283,12 +284,16 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     Xyzz<F>* hg = head + (size_t)gi * pl.nthreads;
     uint32_t* nlong = (uint32_t*)((char*)ctx->longs.p + gi * longs_stride);
     LongChain* longs = (LongChain*)((char*)nlong + 16);
+    uint32_t* nshort = nlong + 1;
+    LongChain* shorts = longs + pl.maxlong;
     if (prefetch)
       PM_LAUNCH(ctx, "accumulate",
-                (k_accumulate<F, true><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg)));
+                (k_accumulate<F, true><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg,
+                                                                 pl.nthreads, fixed ? nullptr : longs, nlong, shorts, nshort)));
     else
       PM_LAUNCH(ctx, "accumulate",
-                (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg)));
+                (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg,
+                                                                  pl.nthreads, fixed ? nullptr : longs, nlong, shorts, nshort)));
     if (st2 != st) {
       HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi], st));
       HIP_TRY(hipStreamWaitEvent(st2, ctx->grp_ev[2 * gi], 0));
@@ -298,9 +303,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
         k_fixup<F><<<(s1 - s0 + 255) / 256, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg,
                                                            longs, nlong);
       else
-        k_fixup_slice<F><<<ablocks, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg, longs,
-                                                   nlong);
-      k_fixup_long<F><<<pl.maxlong, 256, 0, st2>>>(longs, nlong, buckets, hg);
+        k_fixup_short<F><<<ablocks, 256, 0, st2>>>(shorts, nshort, buckets, hg);
+      k_fixup_long<F><<<std::min<uint32_t>(pl.maxlong, 256), 256, 0, st2>>>(longs, nlong, buckets, hg);
     });
     PM_LAUNCH_ST(ctx, st2, "bucket_seg",
                  (k_bucket_seg<F><<<(nw * pl.M1 + 255) / 256, 256, 0, st2>>>(offsets, buckets, w0, nw, pl.NB, pl.L1,

@@ -24,6 +24,7 @@
 // The host (host_ec.hpp) then evaluates sum_w 2^{o_w} (sum T + L1 * sum_b 2^b
 // G_b) as one Horner over absolute bit positions.
 #pragma once
+#include "coop29.hpp"
 #include "curve29.hpp"
 #include "glv.hpp"
 
@@ -533,6 +534,17 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ off
   return lo;
 }
 
+// A bucket whose sorted run crosses slice boundaries is started by slice
+// t_first (which stores its partial in buckets[gb]); every later slice it
+// reaches stores its first partial in head[].  Chains up to kMaxChain slices
+// are folded serially (k_bucket_seg, or k_fixup for the fixed-base MSM);
+// longer ones (giant buckets: adversarial or highly repetitive scalars) are
+// queued for k_fixup_long, one workgroup per bucket with an LDS tree.
+constexpr uint32_t kMaxChain = 32;
+struct LongChain {
+  uint32_t gb, t_first, t_last;
+};
+
 // PREFETCH: issue the next entry's index + base loads before this entry's
 // addition (hides the dependent HBM gather when the bases exceed the
 // Infinity Cache, at the cost of 16+ VGPRs).
@@ -541,7 +553,9 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
                                                     const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
                                                     const uint32_t* __restrict__ bases, uint32_t chunk,
                                                     Xyzz<F>* __restrict__ buckets,
-                                                    Xyzz<F>* __restrict__ head) {
+                                                    Xyzz<F>* __restrict__ head, uint32_t nthreads,
+                                                    LongChain* __restrict__ longs, uint32_t* __restrict__ nlong,
+                                                    LongChain* __restrict__ shorts, uint32_t* __restrict__ nshort) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t base = offsets[s0], total = offsets[s1];
   const uint32_t start = base + t * chunk;
@@ -586,6 +600,22 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
     acc = xyzz29_madd<F>(acc, x, y, acc_inf);
   }
   store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc_inf ? xyzz29_inf<F>() : acc);
+  // owner of a bucket that runs on past this slice: queue the chain for
+  // k_fixup_short / k_fixup_long (longs == nullptr: k_fixup walks buckets).
+  // The short list is compacted (one atomic per wave), so the fixup's lanes
+  // are dense: a per-slice fixup lane idled or diverged (~55 us at 2^20).
+  if (!longs) return;
+  uint32_t t_last = t;
+  if (owned && bend > end) t_last = min((bend - 1 - base) / chunk, nthreads - 1);
+  if (t_last - t > kMaxChain) longs[atomicAdd(nlong, 1u)] = LongChain{gb, t + 1, t_last};
+  const bool sh = t_last > t && t_last - t <= kMaxChain;
+  const uint64_t m = __ballot(sh);
+  if (!m) return;
+  const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+  uint32_t k0 = 0;
+  if (lane == leader) k0 = atomicAdd(nshort, (uint32_t)__popcll(m));
+  k0 = __shfl(k0, (int)leader, 64);
+  if (sh) shorts[k0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = LongChain{gb, t + 1, t_last};
 }
 
 // Base conversion (once per MSM): Rust-layout R = 2^256 Montgomery -> the
@@ -678,43 +708,23 @@ __global__ void __launch_bounds__(256) k_fixed_table(const uint32_t* __restrict_
 }
 
 // --------------------------------------------------------------- 5. fixup
-// The owner of a bucket that runs past its slice adds the head partials of
-// the following slices.  Chains up to kMaxChain are walked serially; longer
-// ones (giant buckets: adversarial or highly repetitive scalars) are queued
-// for k_fixup_long, one workgroup per bucket with an LDS tree.
-constexpr uint32_t kMaxChain = 32;
-struct LongChain {
-  uint32_t gb, t_first, t_last;
-};
+// Slice-boundary partials (see kMaxChain).  Variable-base MSM: k_accumulate
+// queued every chain (short list: k_fixup_short; long list: k_fixup_long).
+// Fixed-base MSM (merged buckets span ~8 slices each): k_fixup, one lane per
+// bucket, queues the long ones.  Then k_fixup_long.
 
-// One lane per accumulate slice t: the slice holding the end of a bucket's
-// first partial walks the following slices' head partials (variable-base
-// MSM: buckets average ~2 slices or fewer, so chains are short and rare).
+// One lane per queued short chain (k_accumulate's compacted list).
 template <class F>
-__global__ void __launch_bounds__(256) k_fixup_slice(const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
-                                                     uint32_t chunk, uint32_t nthreads,
+__global__ void __launch_bounds__(256) k_fixup_short(const LongChain* __restrict__ shorts,
+                                                     const uint32_t* __restrict__ nshort,
                                                      Xyzz<F>* __restrict__ buckets,
-                                                     const Xyzz<F>* __restrict__ head,
-                                                     LongChain* __restrict__ longs,
-                                                     uint32_t* __restrict__ nlong) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nthreads) return;
-  const uint32_t base = offsets[s0], total = offsets[s1];
-  const uint32_t start = base + t * chunk;
-  if (start >= total) return;
-  const uint32_t end = min(start + chunk, total);
-  const uint32_t gb = find_bucket(offsets, s0, s1, end - 1);
-  const uint32_t bstart = offsets[gb], bend = offsets[gb + 1];
-  if (bstart < start || bend <= end) return;  // not owned, or fully inside
-  const uint32_t t_last = min((bend - 1 - base) / chunk, nthreads - 1);
-  if (t_last - t > kMaxChain) {
-    const uint32_t k = atomicAdd(nlong, 1u);
-    longs[k] = LongChain{gb, t + 1, t_last};
-    return;
-  }
-  Xyzz29<F> acc = load_xyzz29<F>(&buckets[gb]);
-  for (uint32_t t2 = t + 1; t2 <= t_last; t2++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
-  store_xyzz29<F>(&buckets[gb], acc);
+                                                     const Xyzz<F>* __restrict__ head) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= *nshort) return;
+  const LongChain lc = shorts[k];
+  Xyzz29<F> acc = load_xyzz29<F>(&buckets[lc.gb]);
+  for (uint32_t t2 = lc.t_first; t2 <= lc.t_last; t2++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
+  store_xyzz29<F>(&buckets[lc.gb], acc);
 }
 
 // One lane per bucket gb in [s0, s1): a bucket whose sorted run crosses
@@ -753,22 +763,25 @@ __global__ void __launch_bounds__(256) k_fixup_long(const LongChain* __restrict_
                                                     Xyzz<F>* __restrict__ buckets,
                                                     const Xyzz<F>* __restrict__ head) {
   __shared__ Xyzz29<F> lds[256];
-  if (blockIdx.x >= *nlong) return;
-  const LongChain lc = longs[blockIdx.x];
+  const uint32_t nl = *nlong;
   const int tid = threadIdx.x;
-  Xyzz29<F> acc = xyzz29_inf<F>();
-  for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256)
-    acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
-  lds[tid] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s) {
-      acc = xyzz29_add<F>(acc, lds[tid + s]);
-      lds[tid] = acc;
+  for (uint32_t k = blockIdx.x; k < nl; k += gridDim.x) {  // grid-stride: usually nl = 0
+    const LongChain lc = longs[k];
+    Xyzz29<F> acc = xyzz29_inf<F>();
+    for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256)
+      acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
+    lds[tid] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) {
+        acc = xyzz29_add<F>(acc, lds[tid + s]);
+        lds[tid] = acc;
+      }
+      __syncthreads();
     }
+    if (tid == 0) store_xyzz29<F>(&buckets[lc.gb], xyzz29_add<F>(load_xyzz29<F>(&buckets[lc.gb]), acc));
     __syncthreads();
   }
-  if (tid == 0) store_xyzz29<F>(&buckets[lc.gb], xyzz29_add<F>(load_xyzz29<F>(&buckets[lc.gb]), acc));
 }
 
 // ------------------------------------------------------ 6. segment sums
@@ -831,13 +844,22 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
   }
   lds[tid] = acc;
   __syncthreads();
+  // tree: once 4 s lanes are free, each addition is quad-cooperative
+  // (coop29.hpp: ~2x lower latency; the tree levels run one wave per SIMD)
   for (int s = kRedThreads / 2; s > 0; s >>= 1) {
-    if (tid < s) {
+    if (4 * s <= kRedThreads) {
+      const int v = tid >> 2;
+      if (v < s) {
+        const Xyzz29<F> r = xyzz29_add_q<F>(lds[v], lds[v + s]);
+        if ((tid & 3) == 0) lds[v] = r;  // the quad read lds[v] in this same wave
+      }
+    } else if (tid < s) {
       acc = xyzz29_add<F>(acc, lds[tid + s]);
       lds[tid] = acc;
     }
     __syncthreads();
   }
+  acc = lds[0];
   const size_t out = (size_t)w * (NB2 + kTJobs) + job;
   if (nsplit > 1) {
     if (tid == 0) {

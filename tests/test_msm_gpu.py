@@ -152,6 +152,23 @@ def test_all_equal_scalars_large(gpu_ctx):
                                                      b.cpu().numpy().view(np.uint64)))
 
 
+@pytest.mark.parametrize("distinct", [3, 40, 700])
+def test_few_distinct_scalars(gpu_ctx, distinct):
+    """Scalars from a small set: buckets of ~n/distinct points whose runs
+    cross several accumulate slices (the short chains folded inside
+    k_bucket_seg) or more than kMaxChain of them (k_fixup_long)."""
+    import torch
+
+    n = 1 << 16
+    s, b = _torch_inputs(gpu_ctx, 0, n)
+    idx = torch.arange(n, device=s.device) % distinct
+    s[:] = s[idx]
+    torch.cuda.synchronize()
+    got = gpu_ctx.msm_device(0, s.data_ptr(), b.data_ptr(), n)
+    assert np.array_equal(got, msm_ref.best_multiexp(0, s.cpu().numpy().view(np.uint64),
+                                                     b.cpu().numpy().view(np.uint64)))
+
+
 def test_resident_bases_window(golden, gpu_ctx):
     case = golden["pallas_n4096"]
     rb = gpu_ctx.upload_bases(0, case["bases"])
