@@ -208,6 +208,13 @@ struct SortGeom {
   int NCB;   // coarse bins per window
   int nblk;  // point blocks of ppt * kSortThreads points
   int ppt;   // points per thread, <= kSortPerThread
+  // words the histogram kernel zeroes for later stages (instead of two
+  // hipMemsetAsync fills per call): the scan sentinel, and the chain-list
+  // counters (4 words) of each window group
+  uint32_t* clr_bh;
+  uint32_t* clr_longs;
+  uint32_t clr_stride;  // words between group headers
+  int clr_groups;
 };
 
 // signed digit of window w (WinGeom), carry in/out; returns |d| | neg << 31
@@ -265,6 +272,12 @@ __device__ __forceinline__ Fe<Fs> load_canonical(const uint32_t* scalars, uint32
   return canonical ? s : fe_from_mont<Fs>(s);
 }
 
+__device__ __forceinline__ void sort_clear(const SortGeom& g) {
+  if (threadIdx.x == 0 && g.clr_bh) *g.clr_bh = 0u;
+  if (threadIdx.x < 4u * (uint32_t)g.clr_groups)
+    g.clr_longs[(threadIdx.x >> 2) * g.clr_stride + (threadIdx.x & 3u)] = 0u;
+}
+
 // stored digit: D16 (cmax <= 16): (|d| - 1) | neg << 15, 0xFFFF = zero
 // (|d| = 2^15 only occurs positive, so that code is free); else |d| | neg << 31
 template <bool D16>
@@ -298,6 +311,7 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
                                                             uint32_t merged) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
   const int nbins = W * g.NCB;
+  if (blockIdx.x == 0) sort_clear(g);
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
   __syncthreads();
   for (int r = 0; r < g.ppt; r++) {
@@ -337,6 +351,7 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist_glv(const uint32_t* 
   using Fs = typename Cv::Scalar;
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
   const int nbins = W * g.NCB;
+  if (blockIdx.x == 0) sort_clear(g);
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
   __syncthreads();
   for (int r = 0; r < g.ppt; r++) {
