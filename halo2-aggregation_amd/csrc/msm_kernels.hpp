@@ -814,11 +814,25 @@ __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__
   const int w = gid / M1, j = gid - w * M1;
   const size_t base = (size_t)w * NB + (size_t)j * L1;
   Xyzz29<F> s = xyzz29_inf<F>(), t = xyzz29_inf<F>();
-  for (int i = L1 - 1; i >= 1; i--) {
-    if (offsets[base + i] != offsets[base + i + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base + i]));
-    t = xyzz29_add<F>(t, s);
+  if (L1 == 4) {
+    // S = B0 + B1 + B2 + B3 and T = B1 + 2 B2 + 3 B3 in 5 additions (the
+    // running-sum walk below needs 7): P23 = B2 + B3, P123 = B1 + P23,
+    // S = B0 + P123, T = (P123 + P23) + B3
+    Xyzz29<F> B[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      B[i] = offsets[base + i] != offsets[base + i + 1] ? load_xyzz29<F>(&buckets[base + i]) : xyzz29_inf<F>();
+    const Xyzz29<F> p23 = xyzz29_add<F>(B[2], B[3]);
+    const Xyzz29<F> p123 = xyzz29_add<F>(B[1], p23);
+    s = xyzz29_add<F>(B[0], p123);
+    t = xyzz29_add<F>(xyzz29_add<F>(p123, p23), B[3]);
+  } else {
+    for (int i = L1 - 1; i >= 1; i--) {
+      if (offsets[base + i] != offsets[base + i + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base + i]));
+      t = xyzz29_add<F>(t, s);
+    }
+    if (offsets[base] != offsets[base + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base]));
   }
-  if (offsets[base] != offsets[base + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base]));
   store_xyzz29<F>(&S[gid], s);
   store_xyzz29<F>(&T[gid], t);
 }
