@@ -489,7 +489,8 @@ __global__ void __launch_bounds__(256) k_acc_termmul_split(AccumHdr h, const uin
 // k_acc_sum: 2^lgL lanes per (proof, output) (lgL <= 5): lane l sums terms
 // lo + l, lo + l + 2^lgL, ...; a butterfly of cross-lane shuffles folds the
 // partials and lane 0 converts to the unique affine point (binary-GCD
-// inversion).  Outputs in MultiopenVar order w, zw, f, e.
+// inversion).  With >= 4 lanes the lanes work in quads (quad-cooperative
+// additions).  Outputs in MultiopenVar order w, zw, f, e.
 template <class Cv>
 __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename Cv::Base>* __restrict__ part,
                                                 uint32_t lgL, uint32_t* __restrict__ out) {
@@ -501,8 +502,17 @@ __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename 
   const uint32_t lo = o == 0 ? h.nslots : o == 1 ? h.nslots + h.nsets : o == 2 ? 0 : h.T - 1;
   const uint32_t hi = o == 0 ? h.nslots + h.nsets : o == 1 ? h.nslots + 2 * h.nsets : o == 2 ? h.nslots : h.T;
   Xyzz29<F> acc = xyzz29_inf<F>();
-  for (uint32_t t = lo + lane; t < hi; t += NL) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
-  for (uint32_t m = 1; m < NL; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
+  if (NL >= 4) {
+    // quads of lanes act as one lane (coop29.hpp: each addition at ~half the
+    // latency); all 4 lanes of a quad see the same terms
+    const uint32_t v = lane >> 2, NV = NL >> 2;
+    for (uint32_t t = lo + v; t < hi; t += NV)
+      acc = xyzz29_add_q<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
+    for (uint32_t m = 4; m < NL; m <<= 1) acc = xyzz29_add_q<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
+  } else {
+    for (uint32_t t = lo + lane; t < hi; t += NL) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
+    for (uint32_t m = 1; m < NL; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
+  }
   if (lane != 0) return;
   uint32_t wx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!xyzz29_is_inf<F>(acc)) {
