@@ -109,7 +109,10 @@ def test_synth_on_device_matches_oracle(gpu_ctx, curve):
     assert np.array_equal(B, msm_ref.synth_bases(curve, P.SEED_BASES, 12345, n))
 
 
-@pytest.mark.parametrize("curve,n", [(0, 5000), (0, (1 << 16) + 123), (1, 1 << 16), (2, 40000), (0, 1 << 18)])
+# sizes cover every sort block shape (1024 threads x ppt points: ppt 1 below
+# 2^18, 2 from 2^18, 4 from 2^19, 8 from 2^20), ragged tails included
+@pytest.mark.parametrize("curve,n", [(0, 5000), (0, (1 << 16) + 123), (1, 1 << 16), (2, 40000), (0, 1 << 18),
+                                     (1, (1 << 19) + 777), (2, (1 << 20) + 5)])
 def test_vs_c_oracle(gpu_ctx, curve, n):
     s, b = _torch_inputs(gpu_ctx, curve, n)
     got = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
