@@ -513,19 +513,22 @@ __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename 
     for (uint32_t t = lo + lane; t < hi; t += NL) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
     for (uint32_t m = 1; m < NL; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
   }
-  if (lane != 0) return;
+  // affine conversion: by the group's first quad (quad-cooperative inversion,
+  // each lane then stores one 16-B quarter), or by lane 0 alone
+  const bool quad = NL >= 4;
+  if (lane >= (quad ? 4u : 1u)) return;
   uint32_t wx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (!xyzz29_is_inf<F>(acc)) {
-    F29<F> x, y;
-    xyzz29_to_aff<F>(acc, x, y);
-    f29_to_r256<F>(x, wx);
-    f29_to_r256<F>(y, wy);
+  if (!xyzz29_is_inf<F>(acc)) {  // uniform over the quad (equal acc)
+    const F29<F> zz = f29_mul_c<F>(acc.ZZ, acc.ZZZ);
+    const F29<F> inv = quad ? f29_inv_q<F>(zz) : f29_inv<F>(zz);  // 1 / (ZZ ZZZ)
+    f29_to_r256<F>(f29_canon<F>(f29_mul_c<F>(acc.X, f29_mul_c<F>(inv, acc.ZZZ))), wx);
+    f29_to_r256<F>(f29_canon<F>(f29_mul_c<F>(acc.Y, f29_mul_c<F>(inv, acc.ZZ))), wy);
   }
   uint4* q = reinterpret_cast<uint4*>(out + 16ull * g);
-  q[0] = make_uint4(wx[0], wx[1], wx[2], wx[3]);
-  q[1] = make_uint4(wx[4], wx[5], wx[6], wx[7]);
-  q[2] = make_uint4(wy[0], wy[1], wy[2], wy[3]);
-  q[3] = make_uint4(wy[4], wy[5], wy[6], wy[7]);
+  if (!quad || lane == 0) q[0] = make_uint4(wx[0], wx[1], wx[2], wx[3]);
+  if (!quad || lane == 1) q[1] = make_uint4(wx[4], wx[5], wx[6], wx[7]);
+  if (!quad || lane == 2) q[2] = make_uint4(wy[0], wy[1], wy[2], wy[3]);
+  if (!quad || lane == 3) q[3] = make_uint4(wy[4], wy[5], wy[6], wy[7]);
 }
 
 }  // namespace pm

@@ -490,6 +490,15 @@ __device__ F29<P> f29_inv(const F29<P>& a) {
   return f29_mul_c<P>(f29_unpack<P>(v), f29_const<P>(F29Consts<P>::R783));
 }
 
+// Quad-cooperative f29_inv (bg_inverse_q): all 4 lanes of a quad, same input.
+template <class P>
+__device__ F29<P> f29_inv_q(const F29<P>& a) {
+  uint32_t w[8], v[8];
+  f29_pack<P>(f29_canon<P>(a), w);
+  bg_inverse_q<P>(w, v);
+  return f29_mul_c<P>(f29_unpack<P>(v), f29_const<P>(F29Consts<P>::R783));
+}
+
 // R256 packed Montgomery (Rust layout, canonical) -> F29 (Norm, < 2p)
 template <class P>
 __device__ __forceinline__ F29<P> f29_from_r256(const uint32_t w[8]) {

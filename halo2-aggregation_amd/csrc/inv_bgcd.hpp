@@ -204,6 +204,143 @@ PM_HD void bg_inverse(const uint32_t y[8], uint32_t out[8]) {
   bg_join(v, out);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// lane K's value of x, for every lane of the quad (DPP quad_perm [K,K,K,K])
+template <int K>
+__device__ __forceinline__ uint32_t bg_qbc(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, K * 0x55, 0xF, 0xF, false);
+}
+#endif
+
+// Quad-cooperative bg_inverse: the 4 lanes of a quad call it with the same y
+// (all 4 active) and all receive y^-1.  Each batch's approximation and 30
+// inner steps run redundantly; its four 9-limb linear combinations run one per
+// lane (a' on lane 0, b' on 1, u' on 2, v' on 3) with the same uniform code,
+// then the quad exchanges them with DPP moves.  The sign of a' (b') negates
+// u' (v') afterwards instead of negating (f, g) before: -x mod p is the same
+// number, so the result equals bg_inverse's bit for bit.
+template <class P>
+__device__ void bg_inverse_q(const uint32_t y[8], uint32_t out[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const BgConsts<P> K = bg_consts<P>();
+  const uint32_t q = threadIdx.x & 3u;
+  const bool ab = q < 2u, odd = (q & 1u) != 0u;
+  const uint32_t m_ab = ab ? ~0u : 0u;
+  uint32_t a[9], b[9], u[9], v[9];
+  bg_split(y, a);
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    b[i] = K.p[i];
+    u[i] = i == 0 ? 1u : 0u;
+    v[i] = 0u;
+  }
+  for (int it = 0; it < K.batches; it++) {
+    int n = 62;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const uint32_t x = a[i] | b[i];
+      const int li = 30 * i + 32 - bg_clz32(x);
+      n = (x != 0u && li > n) ? li : n;
+    }
+    const int sh = n - 32, qq = sh / 30, off = sh - 30 * qq;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      a0 = i == qq ? a[i] : a0;
+      a1 = i == qq + 1 ? a[i] : a1;
+      a2 = i == qq + 2 ? a[i] : a2;
+      b0 = i == qq ? b[i] : b0;
+      b1 = i == qq + 1 ? b[i] : b1;
+      b2 = i == qq + 2 ? b[i] : b2;
+    }
+    const uint64_t wa = (uint64_t)a0 | ((uint64_t)a1 << 30) | ((uint64_t)a2 << 60);
+    const uint64_t wb = (uint64_t)b0 | ((uint64_t)b1 << 30) | ((uint64_t)b2 << 60);
+    uint64_t A = (uint64_t)a[0] | ((uint64_t)(uint32_t)(wa >> off) << 30);
+    uint64_t B = (uint64_t)b[0] | ((uint64_t)(uint32_t)(wb >> off) << 30);
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+    for (int j = 0; j < kBgIter; j++) {
+      const bool oddA = (A & 1u) != 0;
+      const bool sw = oddA && A < B;
+      const uint64_t tA = sw ? B : A, tB = sw ? A : B;
+      const int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      A = (oddA ? tA - tB : tA) >> 1;
+      B = tB;
+      f0 = oddA ? tf0 - tf1 : tf0;
+      g0 = oddA ? tg0 - tg1 : tg0;
+      f1 = (int32_t)((uint32_t)tf1 << 1);
+      g1 = (int32_t)((uint32_t)tg1 << 1);
+    }
+    // this lane's combination: (x f + y g [+ k p]) / 2^30
+    const int32_t f = odd ? f1 : f0, g = odd ? g1 : g0;
+    uint32_t x[9], z[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      x[i] = (a[i] & m_ab) | (u[i] & ~m_ab);
+      z[i] = (b[i] & m_ab) | (v[i] & ~m_ab);
+    }
+    int64_t c = (int64_t)x[0] * f + (int64_t)z[0] * g;
+    const uint32_t k = ab ? 0u : (((uint32_t)c * K.pinv) & kBgM);
+    c += (int64_t)k * K.p[0];
+    c >>= 30;
+    uint32_t o[9];
+#pragma unroll
+    for (int i = 1; i < 9; i++) {
+      c += (int64_t)x[i] * f + (int64_t)z[i] * g + (int64_t)k * K.p[i];
+      o[i - 1] = (uint32_t)c & kBgM;
+      c >>= 30;
+    }
+    const int64_t top = c;
+    o[8] = (uint32_t)c;
+    const bool neg = top < 0;
+    // candidates: -o (a / b lanes), o + p and o - p (u / v lanes)
+    uint32_t rn[9], rs[9], rt[9];
+    int64_t dn = 0, cs = 0, ct = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int64_t oi = i < 8 ? (int64_t)o[i] : top;
+      dn -= oi;
+      cs += oi + K.p[i];
+      ct += oi - (int64_t)K.p[i];
+      rn[i] = i < 8 ? ((uint32_t)dn & kBgM) : (uint32_t)dn;
+      rs[i] = i < 8 ? ((uint32_t)cs & kBgM) : (uint32_t)cs;
+      rt[i] = i < 8 ? ((uint32_t)ct & kBgM) : (uint32_t)ct;
+      dn >>= 30;
+      cs >>= 30;
+      ct >>= 30;
+    }
+    const bool ge = !neg && (int32_t)rt[8] >= 0;
+    uint32_t r[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) r[i] = ab ? (neg ? rn[i] : o[i]) : (neg ? rs[i] : ge ? rt[i] : o[i]);
+    // u' (v') is negated mod p when a' (b') was negative
+    const uint32_t nb = neg ? 1u : 0u;
+    const uint32_t n0 = bg_qbc<0>(nb), n1 = bg_qbc<1>(nb);
+    const bool flip = !ab && (odd ? n1 : n0) != 0u;
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) nz |= r[i];
+    int64_t dp = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      dp += (int64_t)K.p[i] - (int64_t)r[i];
+      const uint32_t pi = i < 8 ? ((uint32_t)dp & kBgM) : (uint32_t)dp;
+      dp >>= 30;
+      r[i] = (flip && nz != 0u) ? pi : r[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      a[i] = bg_qbc<0>(r[i]);
+      b[i] = bg_qbc<1>(r[i]);
+      u[i] = bg_qbc<2>(r[i]);
+      v[i] = bg_qbc<3>(r[i]);
+    }
+  }
+  bg_join(v, out);
+#else
+  bg_inverse<P>(y, out);
+#endif
+}
+
 // Montgomery-form inverse (R = 2^256): a = x R -> x^-1 R.  bg_inverse gives
 // (x R)^-1 = x^-1 R^-1; two products by R^2 restore x^-1 R.
 template <class P>

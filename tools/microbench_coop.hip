@@ -11,7 +11,7 @@ using F = Bn254Fq;
 
 template <int V>
 __global__ void __launch_bounds__(64) k_chain(uint32_t* out, int iters) {
-  const uint32_t t = (V == 1 || V == 3) ? (threadIdx.x >> 2) : threadIdx.x;
+  const uint32_t t = (V == 1 || V == 3 || V == 10) ? (threadIdx.x >> 2) : threadIdx.x;
   F29<F> x, y;
   for (int i = 0; i < 9; i++) { x.l[i] = (t * 7 + i * 977 + blockIdx.x) & kM29; y.l[i] = (t * 3 + i * 131) & kM29; }
   x.l[8] &= 0x3ffff; y.l[8] &= 0x3ffff;
@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(64) k_chain(uint32_t* out, int iters) {
     if (V == 7) a = xyzz29_dbl_q<F>(a);
     if (V == 8) x = f29_inv<F>(f29_add<F>(x, y));
     if (V == 9) x = f29_inv_fermat<F>(f29_add<F>(x, y));
+    if (V == 10) x = f29_inv_q<F>(f29_add<F>(x, y));
   }
   uint32_t s = 0;
   for (int i = 0; i < 9; i++) s ^= j.X.l[i] ^ a.X.l[i] ^ x.l[i];
@@ -58,6 +59,7 @@ int main() {
   for (int blocks : {256}) {
     run<8>("f29_inv_bgcd", buf, blocks);
     run<9>("f29_inv_fermat", buf, blocks);
+    run<10>("f29_inv_bgcd_quad", buf, blocks);
   }
   for (int blocks : {256, 1024, 2048, 4096}) {
     run<4>("f29_mul_chain", buf, blocks);
