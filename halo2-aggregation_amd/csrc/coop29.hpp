@@ -59,13 +59,21 @@ template <class F>
 __device__ __forceinline__ Jac29<F> jac29_dbl_q(const Jac29<F>& p) {
   using K = F29Consts<F>;
   const uint32_t q = quad_id();
-  // L1: A = X^2, B = Y^2, YZ = Y Z
-  const F29<F> r1 = qmul<F>(q, p.X, p.X, p.Y, p.Y, p.Y, p.Z, p.X, p.X);
+  // L1: A = X^2, B = Y^2, YZ = Y Z (operands: lane 0 (X, X), 1 (Y, Y),
+  // 2 (Y, Z), 3 (X, X) -- one or two selects per limb instead of qsel's three)
+  const uint32_t m12 = (q == 1u || q == 2u) ? ~0u : 0u, m2 = q == 2u ? ~0u : 0u;
+  F29<F> o1a, o1b;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    o1a.l[i] = bsel(m12, p.Y.l[i], p.X.l[i]);
+    o1b.l[i] = bsel(m2, p.Z.l[i], o1a.l[i]);
+  }
+  const F29<F> r1 = f29_mul_c<F>(o1a, o1b);
   const F29<F> A = qbc<0, F>(r1), B = qbc<1, F>(r1), YZ = qbc<2, F>(r1);
-  // L2: C = B^2, s = (X + B)^2, F = E^2 (E = 3A)
+  // L2: C = B^2, s = (X + B)^2, F = E^2 (E = 3A): three squarings
   const F29<F> t = f29_norm<F>(f29_add<F>(p.X, B));                       // < 5p
   const F29<F> E = f29_norm<F>(f29_add<F>(f29_add<F>(A, A), A));          // < 6p
-  const F29<F> r2 = qmul<F>(q, B, B, t, t, E, E, B, B);
+  const F29<F> r2 = f29_sqr_c<F>(qsel<F>(q, B, t, E, B));
   const F29<F> C = qbc<0, F>(r2), s = qbc<1, F>(r2), FF = qbc<2, F>(r2);
   const F29<F> u = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(s, f29_add<F>(A, C), K::K8x3)));
   const F29<F> D = f29_reduce3<F>(f29_norm<F>(f29_add<F>(u, u)));
