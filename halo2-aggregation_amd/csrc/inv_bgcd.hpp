@@ -204,6 +204,7 @@ PM_HD void bg_inverse(const uint32_t y[8], uint32_t out[8]) {
   bg_join(v, out);
 }
 
+#if defined(__HIPCC__) || defined(__HIP__)  // device code (the host-only test build skips it)
 #if defined(__HIP_DEVICE_COMPILE__)
 // lane K's value of x, for every lane of the quad (DPP quad_perm [K,K,K,K])
 template <int K>
@@ -340,6 +341,7 @@ __device__ void bg_inverse_q(const uint32_t y[8], uint32_t out[8]) {
   bg_inverse<P>(y, out);
 #endif
 }
+#endif  // __HIPCC__ || __HIP__
 
 // Montgomery-form inverse (R = 2^256): a = x R -> x^-1 R.  bg_inverse gives
 // (x R)^-1 = x^-1 R^-1; two products by R^2 restore x^-1 R.
