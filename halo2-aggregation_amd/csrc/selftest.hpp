@@ -93,6 +93,13 @@ __global__ void k_selftest_field(uint64_t seed, uint32_t n, uint32_t* __restrict
   nb += !f29_eq_r256<F>(f29_inv<F>(A), ia);
   nb += !f29_eq_r256<F>(f29_inv<F>(T), fe_inv<F>(fe_add<F>(a, a)));
   nb += !f29_eq_r256<F>(f29_inv_fermat<F>(A), ia);
+  // quad-cooperative inversion: the 4 lanes of a quad share one input (edge
+  // case (i / 4) % 32), checked only for whole quads
+  if ((i | 3u) < n) {
+    const uint32_t i4 = i >> 2;
+    const Fe<F> c = st_edge<F>(i4 % 32, synth_scalar<F>(seed ^ 0x9E37ull, i4));
+    nb += !f29_eq_r256<F>(f29_inv_q<F>(f29_from_r256<F>(c.l)), fe_inv<F>(c));
+  }
   if (nb) atomicAdd(bad, nb);
 }
 
