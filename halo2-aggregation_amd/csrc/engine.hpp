@@ -315,7 +315,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
                  (k_bucket_bits<F><<<dim3(NJ, nw, nsplit), kRedThreads, 0, st2>>>(S, T, w0, pl.M1, pl.NB2, G, nsplit,
                                                                                       bitsP, tickets)));
     PM_LAUNCH_ST(ctx, st2, "bits_combine",
-                 (k_bits_combine<F><<<(nw * NQ + 63) / 64, 64, 0, st2>>>(G, w0, nw, pl.NB2, Qb)));
+                 (k_bits_combine<F><<<(4 * nw * NQ + 63) / 64, 64, 0, st2>>>(G, w0, nw, pl.NB2, Qb)));
     HIP_TRY(hipMemcpyAsync((Xyzz<F>*)ctx->h_pinned + (size_t)w0 * NQ, Qb + (size_t)w0 * NQ,
                            (size_t)nw * NQ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st2));
     HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi + 1], st2));

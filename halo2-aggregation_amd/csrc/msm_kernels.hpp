@@ -924,29 +924,28 @@ constexpr int kBitsFold = 2;
 template <class F>
 __global__ void __launch_bounds__(64) k_bits_combine(const Xyzz<F>* __restrict__ G, int w0, int nw, int NB2,
                                                      Xyzz<F>* __restrict__ Q) {
+  // a quad per output: quad-cooperative doubling / addition (coop29.hpp),
+  // then lane k converts coordinate k
   const int NJ = NB2 + kTJobs, NQ = (NB2 + kBitsFold - 1) / kBitsFold + 1;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nw * NQ) return;
-  const int w = w0 + g / NQ, j = g % NQ;
+  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2, lk = threadIdx.x & 3;
+  if (gq >= nw * NQ) return;  // whole quads (blocks of 64 lanes hold 16 quads)
+  const int w = w0 + gq / NQ, j = gq % NQ;
   const Xyzz<F>* gw = G + (size_t)w * NJ;
   Xyzz29<F> acc;
   if (j == NQ - 1) {
     acc = load_xyzz29<F>(&gw[NB2]);
-    for (int t = 1; t < kTJobs; t++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&gw[NB2 + t]));
+    for (int t = 1; t < kTJobs; t++) acc = xyzz29_add_q<F>(acc, load_xyzz29<F>(&gw[NB2 + t]));
   } else {
     const int b0 = j * kBitsFold, b1 = min(NB2, b0 + kBitsFold);
     acc = load_xyzz29<F>(&gw[b1 - 1]);
-    for (int b = b1 - 2; b >= b0; b--) acc = xyzz29_add<F>(xyzz29_dbl<F>(acc), load_xyzz29<F>(&gw[b]));
+    for (int b = b1 - 2; b >= b0; b--) acc = xyzz29_add_q<F>(xyzz29_dbl_q<F>(acc), load_xyzz29<F>(&gw[b]));
   }
+  const F29<F> c = qsel<F>((uint32_t)lk, acc.X, acc.Y, acc.ZZ, acc.ZZZ);
+  uint32_t o[8];
+  f29_to_r256<F>(c, o);
   uint4* q = reinterpret_cast<uint4*>(&Q[(size_t)w * NQ + j]);
-  const F29<F>* c[4] = {&acc.X, &acc.Y, &acc.ZZ, &acc.ZZZ};
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t o[8];
-    f29_to_r256<F>(*c[k], o);
-    q[2 * k] = make_uint4(o[0], o[1], o[2], o[3]);
-    q[2 * k + 1] = make_uint4(o[4], o[5], o[6], o[7]);
-  }
+  q[2 * lk] = make_uint4(o[0], o[1], o[2], o[3]);
+  q[2 * lk + 1] = make_uint4(o[4], o[5], o[6], o[7]);
 }
 
 // ------------------------------------------------------ synthetic inputs
