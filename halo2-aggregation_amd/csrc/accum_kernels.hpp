@@ -388,8 +388,8 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
 //
 // k_acc_ladder: one quad per (proof, term) (coop29.hpp: each Jacobian
 // doubling is 3 product levels split over the 4 lanes): Q_0 = P,
-// Q_{j+1} = [2^L] Q_j, stored packed (R261 XYZZ, storage bounds of
-// curve29.hpp) at lad[g S + j].
+// Q_{j+1} = [2^L] Q_j, stored packed (R261 Jacobian X, Y, Z in the X, Y, ZZ
+// slots of an Xyzz) at lad[g S + j].
 template <class Cv>
 __global__ void __launch_bounds__(256) k_acc_ladder(AccumHdr h, const uint32_t* __restrict__ prog,
                                                     const uint32_t* __restrict__ points,
@@ -414,11 +414,16 @@ __global__ void __launch_bounds__(256) k_acc_ladder(AccumHdr h, const uint32_t* 
   }
   const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
   Jac29<F> q{px, py, f29_const<F>(F29Consts<F>::ONE)};
-  if (st) store_xyzz29<F>(&out[0], Xyzz29<F>{px, py, q.Z, q.Z});
+  // stored as Jacobian (X, Y, Z in the X, Y, ZZ slots): the term products
+  // derive ZZ, ZZZ in parallel, off this chain
+  if (st) store_xyzz29<F>(&out[0], Xyzz29<F>{q.X, q.Y, q.Z, q.Z});
   for (uint32_t j = 1; j < nq; j++) {
     for (uint32_t d = 0; d < L; d++) q = jac29_dbl_q<F>(q);
-    const Xyzz29<F> x = jac29_to_xyzz_q<F>(q);
-    if (st) store_xyzz29<F>(&out[j], x);
+    // Z < 4p can exceed the 2^256 of the packed store (Pasta): canonical
+    if (st) {
+      const F29<F> z = f29_canon<F>(q.Z);
+      store_xyzz29<F>(&out[j], Xyzz29<F>{q.X, q.Y, z, z});
+    }
   }
 }
 
@@ -460,7 +465,8 @@ __global__ void __launch_bounds__(256) k_acc_termmul_split(AccumHdr h, const uin
   const uint32_t lo = j * L, hi = min(lo + L, (uint32_t)kGlvBits);
   Xyzz29<F> acc = xyzz29_inf<F>();
   if (lo < hi) {
-    const Xyzz29<F> Q = load_xyzz29<F>(&lad[(size_t)g * S + j]);
+    const Xyzz29<F> QJ = load_xyzz29<F>(&lad[(size_t)g * S + j]);  // Jacobian X, Y, Z (k_acc_ladder)
+    const Xyzz29<F> Q = jac29_to_xyzz<F>(Jac29<F>{QJ.X, QJ.Y, QJ.ZZ});
     // Y < 3p -> 6p - Y reduced below 3p (dbl needs Y < 4p)
     const F29<F> yneg = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), Q.Y, K::K6)));
     const Xyzz29<F> T1{Q.X, n1 ? yneg : Q.Y, Q.ZZ, Q.ZZZ};
