@@ -172,7 +172,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   h.c_user = 0;
   for (uint32_t i = 0; i < s->n_constants; i++) push_fe<Fs>(cst, fe_from_u64<Fs>(s->constants + 4 * i));
   const Fe<Fs> omega = fe_from_u64<Fs>(s->omega), delta = fe_from_u64<Fs>(s->delta);
-  const Fe<Fs> omega_inv = fe_inv<Fs>(omega);
+  const Fe<Fs> omega_inv = fe_inv_bgcd<Fs>(omega);  // host binary GCD: ~10x faster than Fermat, same value
   h.c_delta = (uint32_t)(cst.size() / 8);
   Fe<Fs> acc = fe_one<Fs>();
   for (uint32_t k = 0; k < s->n_perm_columns; k++) {
