@@ -36,7 +36,6 @@ METRIC = "Pallas MSM Mscalar/s at 2^20 (1/2/4/8 GPU); aggregated proofs verified
 LOGN = 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_PAIR = 96            # 32 B scalar + 64 B affine base
-MADS_PER_MADD = 8 * 135 + 2 * 99  # v_mad_u64_u32 per XYZZ mixed add issued by the per-column asm products (fp29_asm.hpp, Pasta)
 SEED_SCALARS, SEED_BASES = 0x5EED, 0xA11CE
 
 
@@ -53,14 +52,73 @@ def parse():
     ap.add_argument("--ntt-logn", type=int, default=20, help="NTT leg size (0 = skip)")
     ap.add_argument("--accum-batch", type=int, default=256, help="proofs per GPU for the accumulator leg (0 = skip)")
     ap.add_argument("--accum-logn", type=int, default=17)
+    ap.add_argument("--logn22", type=int, default=1,
+                    help="also time the 2^22 Pallas MSM per GPU (north-star size, weak scaling) (1) or skip it (0)")
+    ap.add_argument("--strong-logn", type=int, default=22,
+                    help="strong-scaling leg: a fixed 2^k Vesta MSM split over the ranks (SURVEY config 4); 0 = skip")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous check only: no GPU work (gloo), prints the JSON skeleton")
     return ap.parse_args()
 
 
-def load_valu_peak():
-    p = os.path.join(ROOT, "profiles", "valu_peak.json")
-    if os.path.exists(p):
-        return json.load(open(p))
-    return None
+def cpu_threads():
+    """Host threads for the CPU baselines: the CPUs this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when the box sets it (the
+    GPU pool gives each 1-GPU job a 16-CPU share while os.cpu_count() reports
+    the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_info():
+    return {"threads_used": cpu_threads(), "os_cpu_count": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a torch.distributed environment: start N ranks
+    through torch.distributed.run as a CHILD process (nothing in this process
+    has touched the GPU or imported torch yet) and exit with its code.  The
+    JSON line is printed by the child's rank 0 on the inherited stdout."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def load_valu_counters(workload, avg_ms):
+    """Integer-VALU roofline of k_accumulate from rocprofv3 SQ counters of the
+    same kernel on the same workload (profiles/pmc_valu.json, written by
+    tools/pmc_valu.py from the committed CSV): v_mad_u64_u32-class (INT64)
+    lane-ops per second against the measured 64-bit multiply-add issue peak,
+    and the fraction of SIMD issue cycles the counted VALU mix occupies."""
+    p = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if not os.path.exists(p):
+        return None
+    d = json.load(open(p)).get(workload)
+    if not d:
+        return None
+    s = avg_ms * 1e-3
+    mad_rate = d["int64_insts_per_launch"] * 64 / s / 1e12
+    return {"achieved": round(mad_rate, 3), "peak": d["int64_peak_Tops"], "unit": "T lane-mad64/s",
+            "frac": round(mad_rate / d["int64_peak_Tops"], 4),
+            "issue_frac": d.get("issue_frac"), "valu_insts_per_launch": d["valu_insts_per_launch"],
+            "int64_insts_per_launch": d["int64_insts_per_launch"], "source": d["source"]}
 
 
 def load_pmc_traffic(workload, launches_per_msm):
@@ -85,14 +143,20 @@ def load_ntt_traffic(workload):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, rank, world)
     import numpy as np
     import torch
 
     import halo2_amd as H
-    from sharded import combine_partials, shard_range
+    from sharded import shard_range, split_range
 
     torch.cuda.set_device(local)
     dist = None
@@ -106,94 +170,56 @@ def main():
     if args.window:
         ctx.set_window(args.window)
     dev = torch.device("cuda", local)
-    d_s = torch.empty((n, 4), dtype=torch.int64, device=dev)
-    d_b = torch.empty((n, 8), dtype=torch.int64, device=dev)
     i0, _ = shard_range(rank, world, n)
-    ctx.synth_scalars(curve, SEED_SCALARS, i0, n, d_s.data_ptr())
-    ctx.synth_bases(curve, SEED_BASES, i0, n, d_b.data_ptr())
-    torch.cuda.synchronize()
-
+    leg = run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline=True, breakdown=True)
+    d_s, d_b, result = leg.pop("_d_s"), leg.pop("_d_b"), leg.pop("_result")
     gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
 
     def padd(a, b):
         return H.point_add(curve, a, b)
 
-    def step():
-        part = ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n)
-        return combine_partials(part, dist, dev, padd, world, gathered)
-
-    for _ in range(args.warmup):
-        step()
-    # timed region: HIP events only around the roofline kernel (every event
-    # pair costs ~10 us of stream time on MI355X)
-    ctx.set_timing(True, only="accumulate")
-    ctx.reset_stats()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        result = step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
-    launches, acc_ms = ctx.kernel_stats("accumulate")
-    acc_launches_per_msm = max(1, launches) / args.steps
-    # per-MSM kernel breakdown from a separate, untimed diagnostic run with
-    # events around every launch (the pipelined engine launches accumulate /
-    # fixup / bucket_* once per window group)
-    kernels = kernel_breakdown(ctx, step, ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate",
-                                           "fixup", "bucket_seg", "bucket_bits", "bits_combine", "host_tail"])
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     fixed = run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, result) if args.fixed else None
+    cpu = cpu_baseline(d_s, d_b, n, result, args.cpu_seconds) if (rank == 0 and world == 1 and not args.no_cpu) \
+        else None
+    del d_s, d_b
+    big = None
+    if args.logn22:
+        # the north-star size: a 2^22 Pallas MSM per GPU (weak scaling)
+        n22 = 1 << 22
+        big = run_msm_leg(args, ctx, dist, dev, world, curve, n22, shard_range(rank, world, n22)[0], roofline=True,
+                          breakdown=True, check_port=(rank == 0 and world == 1 and not args.no_cpu))
+        for k in ("_d_s", "_d_b", "_result"):
+            big.pop(k)
+    strong = None
+    if args.strong_logn:
+        # SURVEY config 4: ONE fixed 2^k Vesta MSM split over the ranks
+        # (strong scaling; sharded.split_range), partials all-gathered + folded
+        nt = 1 << args.strong_logn
+        lo, cnt = split_range(rank, world, nt)
+        strong = run_msm_leg(args, ctx, dist, dev, world, H.VESTA, cnt, lo, roofline=False, breakdown=False,
+                             n_total=nt, check_port=(rank == 0 and world == 1 and not args.no_cpu))
+        for k in ("_d_s", "_d_b", "_result"):
+            strong.pop(k)
+    torch.cuda.empty_cache()
     ntt = run_ntt(args, ctx, dist, dev, world) if args.ntt_logn > 0 else None
     accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
 
     if rank == 0:
-        ms_per_step = elapsed * 1e3 / args.steps
-        value = world * n / (elapsed / args.steps) / 1e6
-        acc_avg_ms = acc_ms / max(1, launches)
-        # algorithmic bytes of one accumulate launch: the MSM consumes all n
-        # (scalar, base) pairs -> 96 B x n; one launch covers one
-        # window group, i.e. 1 / (launches per MSM) of it
-        alg_bytes = BYTES_PER_PAIR * n / acc_launches_per_msm
-        achieved = alg_bytes / (acc_avg_ms * 1e-3) / 1e9
-        workload = f"pallas_msm_2^{args.logn}_per_gpu"
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc_traffic(workload, acc_launches_per_msm),
-                "kernel": "k_accumulate", "avg_launch_ms": round(acc_avg_ms, 4),
-                "launches_per_msm": acc_launches_per_msm, "alg_bytes_per_launch": int(alg_bytes)}
-        vp = load_valu_peak()
-        if vp:
-            # The binding roofline is integer VALU: one XYZZ mixed
-            # add = 8 products + 2 squares in the radix-2^29 arithmetic
-            # (fp29_asm.hpp): 8 x 135 + 2 x 99 = 1278 v_mad_u64_u32 for the
-            # Pasta moduli (the reduction's p_0 = 1 and p_8 = 2^22 limbs are
-            # multiply-adds too); ~n*W adds per launch; peak = measured mad
-            # issue rate.
-            W = windows_for(n, args.window)
-            mads = int(n * W * MADS_PER_MADD / acc_launches_per_msm)
-            ach = mads / (acc_avg_ms * 1e-3) / 1e12
-            roof["valu_int"] = {"achieved": round(ach, 3), "peak": vp["v_mad_u64_u32_Tops"], "unit": "T v_mad_u64_u32/s",
-                                "frac": round(ach / vp["v_mad_u64_u32_Tops"], 4), "mads_per_launch": mads}
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mscalar/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "metric": METRIC, "value": leg["value"], "unit": "Mscalar/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": leg["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (SplitMix64 scalars in [0,r), bases [a_i]G generated on device)",
-            "config": {"workload": workload, "curve": "pallas", "n_per_gpu": n, "n_total": world * n,
-                       "scalars": "montgomery", "bases": "affine montgomery, HBM-resident",
-                       "parallelism": f"point-slice x{world} + RCCL all-gather of partial points"},
-            "kernels_ms": kernels,
-            "roofline": roof,
+            "config": leg["config"],
+            "kernels_ms": leg["kernels_ms"],
+            "roofline": leg["roofline"],
         }
-        if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(d_s, d_b, n, result, args.cpu_seconds)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
+        if big is not None:
+            out["logn22"] = big
+        if strong is not None:
+            out["strong_vesta"] = strong
         if fixed is not None:
             out["fixed_base"] = fixed
         if ntt is not None:
@@ -210,6 +236,136 @@ def main():
             out["accumulator"] = accum
         print(json.dumps(out), flush=True)
     if dist:
+        dist.destroy_process_group()
+
+
+def timed_steps(step, steps, warmup, dist, dev):
+    """W untimed steps, then K steps between barrier + synchronize on both
+    sides; returns (max-over-ranks seconds, last step's result)."""
+    import torch
+
+    for _ in range(warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    result = None
+    for _ in range(steps):
+        result = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, result
+
+
+MSM_KERNELS = ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg",
+               "bucket_bits", "bits_combine", "host_tail"]
+
+
+def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, n_total=None, check_port=False):
+    """One MSM leg: this rank's n pairs [i0, i0 + n) generated on the device,
+    one step = pm_msm_device + all-gather of the partials + host fold.
+    n_total None: weak scaling (world * n pairs); else strong (n_total split)."""
+    import numpy as np
+    import torch
+
+    import halo2_amd as H
+    from sharded import combine_partials
+
+    d_s = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
+    d_b = torch.empty((max(n, 1), 8), dtype=torch.int64, device=dev)
+    ctx.synth_scalars(curve, SEED_SCALARS, i0, n, d_s.data_ptr())
+    ctx.synth_bases(curve, SEED_BASES, i0, n, d_b.data_ptr())
+    torch.cuda.synchronize()
+    gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
+
+    def padd(a, b):
+        return H.point_add(curve, a, b)
+
+    def step():
+        part = ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n) if n else np.zeros(8, np.uint64)
+        return combine_partials(part, dist, dev, padd, world, gathered)
+
+    # timed region: HIP events only around the roofline kernel (every event
+    # pair costs ~10 us of stream time on MI355X)
+    if roofline:
+        for _ in range(args.warmup):
+            step()
+        ctx.set_timing(True, only="accumulate")
+        ctx.reset_stats()
+    elapsed, result = timed_steps(step, args.steps, 0 if roofline else args.warmup, dist, dev)
+    launches, acc_ms = ctx.kernel_stats("accumulate") if roofline else (0, 0.0)
+    ctx.set_timing(False)
+    lg = (n_total or n).bit_length() - 1
+    name = H.CURVE_NAMES[curve] if hasattr(H, "CURVE_NAMES") else ("pallas", "vesta", "bn254")[curve]
+    total = n_total if n_total is not None else world * n
+    out = {"value": round(total / (elapsed / args.steps) / 1e6, 3), "unit": "Mscalar/s",
+           "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+           "scaling": "strong" if n_total is not None else "weak",
+           "config": {"workload": f"{name}_msm_2^{lg}" + ("_total" if n_total is not None else "_per_gpu"),
+                      "curve": name, "n_per_gpu": n, "n_total": total, "scalars": "montgomery",
+                      "bases": "affine montgomery, HBM-resident",
+                      "parallelism": f"point-slice x{world} + RCCL all-gather of partial points"}}
+    if breakdown:
+        # per-MSM kernel breakdown from a separate, untimed diagnostic run with
+        # events around every launch
+        out["kernels_ms"] = kernel_breakdown(ctx, step, MSM_KERNELS)
+    if roofline and launches:
+        acc_launches_per_msm = launches / args.steps
+        acc_avg_ms = acc_ms / launches
+        # algorithmic bytes of one accumulate launch: the MSM consumes all n
+        # (scalar, base) pairs -> 96 B x n (SURVEY §8d); one launch covers one
+        # window group, i.e. 1 / (launches per MSM) of it
+        alg_bytes = BYTES_PER_PAIR * n / acc_launches_per_msm
+        achieved = alg_bytes / (acc_avg_ms * 1e-3) / 1e9
+        workload = f"{name}_msm_2^{lg}_per_gpu"
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc_traffic(workload, acc_launches_per_msm),
+                "kernel": "k_accumulate", "avg_launch_ms": round(acc_avg_ms, 4),
+                "launches_per_msm": acc_launches_per_msm, "alg_bytes_per_launch": int(alg_bytes)}
+        valu = load_valu_counters(workload, acc_avg_ms)
+        if valu:
+            roof["valu_int"] = valu
+        out["roofline"] = roof
+    if check_port and n:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import msm_ref
+
+        out["matches_c_port"] = bool(np.array_equal(
+            np.asarray(result), msm_ref.best_multiexp(curve, d_s.cpu().numpy().view(np.uint64),
+                                                      d_b.cpu().numpy().view(np.uint64), threads=cpu_threads())))
+    out.update(_d_s=d_s, _d_b=d_b, _result=result)
+    return out
+
+
+def dry_run(args, rank, world):
+    """Launcher check without a GPU: gloo rendezvous, the same barrier /
+    max-over-ranks timing as the real legs, and the JSON skeleton."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mscalar/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "dry run (no GPU work)",
+                          "config": {"workload": f"pallas_msm_2^{args.logn}_per_gpu"}}), flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 
@@ -339,7 +495,7 @@ def ntt_cpu_baseline(curve, k, src, w, first, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import msm_ref
 
-    threads = int(os.environ.get("BENCH_CPU_THREADS", "16"))
+    threads = cpu_threads()
     reps, t0 = 0, time.perf_counter()
     match = None
     while True:
@@ -351,6 +507,7 @@ def ntt_cpu_baseline(curve, k, src, w, first, budget_s):
             break
     dt = (time.perf_counter() - t0) / reps
     return {"value": round((1 << k) / dt / 1e6, 3), "unit": "Melem/s", "cores": threads, "kind": "port",
+            "host": cpu_info(),
             "sample": f"{reps} x best_fft(2^{k}) in oracle/msm_ref.c ({dt * 1e3:.1f} ms each)",
             "matches_gpu": match}
 
@@ -456,14 +613,6 @@ def accum_cpu_baseline(curve, log_n, host, vk, B, budget_s):
             "matches_gpu": match}
 
 
-def windows_for(n, c_override=0):
-    """Window count of the engine's launch plan (capi.hip make_plan)."""
-    lg = max(n, 1).bit_length() - 1
-    c = c_override if c_override > 0 else max(4, min(16, lg - 2 if lg >= 14 else lg - 4))
-    c = max(4, min(20, c))
-    return (256 + c - 1) // c
-
-
 def cpu_baseline(d_s, d_b, n, gpu_result, budget_s):
     """C restatement of halo2 best_multiexp on the host, same inputs."""
     import numpy as np
@@ -473,7 +622,7 @@ def cpu_baseline(d_s, d_b, n, gpu_result, budget_s):
 
     S = d_s.cpu().numpy().view(np.uint64)
     B = d_b.cpu().numpy().view(np.uint64)
-    threads = int(os.environ.get("BENCH_CPU_THREADS", "16"))
+    threads = cpu_threads()
     reps, t0 = 0, time.perf_counter()
     match = None
     while True:
@@ -485,6 +634,7 @@ def cpu_baseline(d_s, d_b, n, gpu_result, budget_s):
             break
     dt = time.perf_counter() - t0
     return {"value": round(reps * n / dt / 1e6, 4), "unit": "Mscalar/s", "cores": threads, "kind": "port",
+            "host": cpu_info(),
             "sample": f"{reps} x Pallas best_multiexp of the same 2^{n.bit_length() - 1} inputs "
                       f"({dt:.1f} s, oracle/msm_ref.c, {threads} threads)",
             "matches_gpu": match}

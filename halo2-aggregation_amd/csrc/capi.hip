@@ -263,7 +263,11 @@ int pm_ctx_create(int device, pm_ctx** out) {
   std::unique_ptr<Ctx> c(new Ctx());
   c->device = device;
   HIP_TRY(hipSetDevice(device));
-  HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  // the context's own stream is a BLOCKING stream: it is ordered after work
+  // the caller queued on the legacy null stream (torch's default stream), so
+  // a *_device entry sees inputs the caller has just written there.  The
+  // internal reduction stream is ordered by events only.
+  HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault));
   c->stream = c->own_stream;
   HIP_TRY(hipStreamCreateWithFlags(&c->red_stream, hipStreamNonBlocking));
   if (const char* e = std::getenv("PM_PREFETCH")) c->prefetch = std::atoi(e);
@@ -287,7 +291,14 @@ int pm_ctx_destroy(pm_ctx* ctx) {
 int pm_ctx_set_stream(pm_ctx* ctx, void* s) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+  ctx->stream = (hipStream_t)s;  // NULL = the legacy null stream itself
+  return PM_OK;
+}
+
+int pm_ctx_use_own_stream(pm_ctx* ctx) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->stream = ctx->own_stream;
   return PM_OK;
 }
 

@@ -204,6 +204,7 @@ def _load():
         "pm_ctx_create": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
         "pm_ctx_destroy": ([_vp], ctypes.c_int),
         "pm_ctx_set_stream": ([_vp, _vp], ctypes.c_int),
+        "pm_ctx_use_own_stream": ([_vp], ctypes.c_int),
         "pm_ctx_set_window": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_split": ([_vp, ctypes.c_int], ctypes.c_int),
@@ -414,7 +415,12 @@ class Context:
             pass
 
     def set_stream(self, stream_handle):
+        """Run on the caller's HIP stream (0 = the legacy null stream);
+        use_own_stream() restores the context's own (blocking) stream."""
         _check(lib().pm_ctx_set_stream(self.h, _vp(stream_handle or 0)))
+
+    def use_own_stream(self):
+        _check(lib().pm_ctx_use_own_stream(self.h))
 
     def set_window(self, c):
         _check(lib().pm_ctx_set_window(self.h, c))

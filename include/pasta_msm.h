@@ -52,9 +52,21 @@ int pm_device_count(int* count);
 /* ------------------------------------------------------------- context */
 int pm_ctx_create(int device, pm_ctx** out);
 int pm_ctx_destroy(pm_ctx* ctx);
-/* Run on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+/* Stream ordering contract.  Every entry point is synchronous: it returns
+ * after its own work has finished.  Its device work is queued on the
+ * context's current stream, so inputs the caller wrote on the device must be
+ * ordered before it:
+ *   - by default the context runs on its own BLOCKING stream, which is
+ *     ordered after everything queued on the legacy null stream (torch's
+ *     default stream, the hipMemcpy / hipMemset default);
+ *   - pm_ctx_set_stream(ctx, s) runs on the caller's stream s instead
+ *     (e.g. torch.cuda.current_stream().cuda_stream); s == NULL is the legacy
+ *     null stream itself, not "the context's own stream";
+ *   - pm_ctx_use_own_stream(ctx) goes back to the context's own stream.
+ * Work the caller queues on any other non-blocking stream must be
+ * synchronised by the caller before the call. */
 int pm_ctx_set_stream(pm_ctx* ctx, void* hip_stream);
+int pm_ctx_use_own_stream(pm_ctx* ctx);
 /* Force the window width c (0 = automatic). */
 int pm_ctx_set_window(pm_ctx* ctx, int c);
 /* Pipeline tuning: number of window groups whose bucket reduction overlaps

@@ -37,6 +37,14 @@ def lib():
     return _lib
 
 
+def default_threads():
+    """CPUs this process may use (affinity mask), capped by OMP_NUM_THREADS:
+    on the GPU pool os.cpu_count() reports the whole machine, not the job's share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(cap)) if cap.isdigit() and int(cap) > 0 else n)
+
+
 def _p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
 
@@ -46,7 +54,7 @@ def best_multiexp(curve: int, scalars: np.ndarray, bases: np.ndarray, canonical=
     bases = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, 8)
     assert scalars.shape[0] == bases.shape[0]
     out = np.zeros(8, dtype=np.uint64)
-    threads = threads or os.cpu_count() or 1
+    threads = threads or default_threads()
     rc = lib().msm_ref_best_multiexp(curve, _p(scalars), _p(bases), scalars.shape[0], int(bool(canonical)),
                                      int(threads), _p(out))
     assert rc == 0
@@ -55,14 +63,14 @@ def best_multiexp(curve: int, scalars: np.ndarray, bases: np.ndarray, canonical=
 
 def synth_scalars(curve: int, seed: int, i0: int, n: int, threads=None):
     out = np.zeros((n, 4), dtype=np.uint64)
-    rc = lib().msm_ref_synth_scalars(curve, seed, i0, n, int(threads or os.cpu_count() or 1), _p(out))
+    rc = lib().msm_ref_synth_scalars(curve, seed, i0, n, int(threads or default_threads()), _p(out))
     assert rc == 0
     return out
 
 
 def synth_bases(curve: int, seed: int, i0: int, n: int, threads=None):
     out = np.zeros((n, 8), dtype=np.uint64)
-    rc = lib().msm_ref_synth_bases(curve, seed, i0, n, int(threads or os.cpu_count() or 1), _p(out))
+    rc = lib().msm_ref_synth_bases(curve, seed, i0, n, int(threads or default_threads()), _p(out))
     assert rc == 0
     return out
 

@@ -31,6 +31,9 @@ CASES = [
     ("vesta_rich_k10", 1, "rich", 10, 2, 0xACC3, None),
     ("bn254_rich_k17", 2, "rich", 17, 2, 0xACC4, None),
     ("bn254_simple_edge", 2, "simple", 14, 3, 0xACC5, "edge"),
+    # the reference's only real configuration: ONE inner simple-example proof
+    # at k = 9 (examples/simple-example.rs:561,620-626), B = 1
+    ("bn254_simple_k9_single", 2, "simple", 9, 1, 0xACC6, None),
 ]
 
 

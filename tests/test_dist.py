@@ -136,3 +136,33 @@ def test_sharded_accumulator_gloo():
     want = np.stack([A.pack_result(C, A.accumulate_msm(C, sh, pf))[0] for pf in proofs])
     for r in range(world):
         assert np.array_equal(np.array(res[r], dtype=np.uint64), want), r
+
+
+def test_bench_launcher_world2():
+    """bench.py --gpus 2 without a torch.distributed environment starts 2
+    ranks through torch.distributed.run (child process), the ranks check
+    WORLD_SIZE == --gpus, rendezvous over gloo (--dry-run: no GPU work) and
+    rank 0 prints ONE JSON line with n_gpus == 2."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3
+
+
+def test_bench_world_mismatch_refused():
+    """A rank whose WORLD_SIZE differs from --gpus refuses to report."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd="/tmp")
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)

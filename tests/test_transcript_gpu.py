@@ -114,3 +114,20 @@ def test_empty_batch_and_errors(gpu_ctx):
     import ctypes
     assert H.lib().pm_transcript_batch(gpu_ctx.h, 9, ctypes.byref(ps.c), 0, vk.ctypes.data_as(H._u64p), None, None,
                                        None, None) == -1   # unknown curve
+
+
+@pytest.mark.parametrize("cid", [2, 0])
+def test_single_proof_k9_fused(gpu_ctx, cid):
+    """The reference's only real configuration: ONE simple-example proof at
+    k = 9 (examples/simple-example.rs:561,620-626) -- B = 1 through the fused
+    transcript replay + accumulator, against the oracle."""
+    C, sh, proofs = U.make_case(cid, "simple", 9, 1, 0x9009 + cid)
+    ps = U.to_product_shape(cid, sh)
+    vkr = T.vk_repr(C.r, b"simple-example k=9")
+    vk = np.array(A.to_limbs_mont(C.r, vkr), dtype=np.uint64)
+    T.with_replayed_challenges(C, sh, proofs, vkr)
+    pts, scs, chs = A.pack_proofs(C, sh, proofs)
+    quads, h, ch, st = gpu_ctx.accum_batch_transcript(ps, pts, scs, vk)
+    assert np.array_equal(ch, chs) and not st.any()
+    q, hh = A.pack_result(C, A.accumulate_msm(C, sh, proofs[0]))
+    assert np.array_equal(quads[0], q) and np.array_equal(h[0], hh)
