@@ -126,8 +126,8 @@ def load_pmc_traffic(workload, launches_per_msm):
     were taken on this workload with the same launch structure."""
     p = os.path.join(ROOT, "profiles", "pmc_accumulate.json")
     if os.path.exists(p):
-        d = json.load(open(p))
-        if d.get("workload") == workload and d.get("launches_per_msm", 1) == launches_per_msm:
+        d = json.load(open(p)).get("workloads", {}).get(workload)
+        if d and d.get("launches_per_msm", 1) == launches_per_msm:
             return d.get("hbm_bytes_per_launch")
     return None
 

@@ -59,6 +59,11 @@ pm_ctx::~pm_ctx() {
   for (pm::Buf* b : all_bufs()) b->release();
   for (auto& t : ntt_tw) t.buf.release();
   if (h_pinned) (void)hipHostFree(h_pinned);
+  for (int t = 0; t < pm::kMaxStageThreads; t++) {
+    if (stage_pending[t]) (void)hipEventSynchronize(stage_ev[t]);
+    if (h_stage[t]) (void)hipHostFree(h_stage[t]);
+    if (stage_ev[t]) (void)hipEventDestroy(stage_ev[t]);
+  }
   for (auto& e : ev_pool) (void)hipEventDestroy(e);
   for (auto& e : grp_ev) (void)hipEventDestroy(e);
   if (red_stream) (void)hipStreamDestroy(red_stream);
@@ -109,10 +114,72 @@ int pm_ctx::ensure_group_events(int n) {
 int pm_ctx::ensure_pinned(size_t bytes) {
   if (bytes <= h_pinned_cap) return PM_OK;
   if (h_pinned) (void)hipHostFree(h_pinned);
+  for (int t = 0; t < pm::kMaxStageThreads; t++) {
+    if (stage_pending[t]) (void)hipEventSynchronize(stage_ev[t]);
+    if (h_stage[t]) (void)hipHostFree(h_stage[t]);
+    if (stage_ev[t]) (void)hipEventDestroy(stage_ev[t]);
+  }
   h_pinned = nullptr;
   h_pinned_cap = 0;
   HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocDefault));
   h_pinned_cap = bytes;
+  return PM_OK;
+}
+
+int pm_ctx::upload_h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
+  hipEvent_t ta = nullptr, tb = nullptr;
+  if (timed("h2d")) {
+    ta = next_event();
+    tb = next_event();
+    HIP_TRY(hipEventRecord(ta, st));
+  }
+  const int T = std::max(0, std::min(pm::kMaxStageThreads, h2d_threads));
+  if (T == 0 || bytes < (size_t(1) << 20)) {
+    HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+  } else {
+    for (int t = 0; t < T; t++) {
+      if (!h_stage[t]) HIP_TRY(hipHostMalloc(&h_stage[t], pm::kStageChunk, hipHostMallocDefault));
+      if (!stage_ev[t]) HIP_TRY(hipEventCreateWithFlags(&stage_ev[t], hipEventDisableTiming));
+    }
+    const size_t nchunks = (bytes + pm::kStageChunk - 1) / pm::kStageChunk;
+    const int nt = (int)std::min<size_t>((size_t)T, nchunks);
+    std::vector<int> rcs(nt, PM_OK);
+    std::vector<std::string> errs(nt);
+    // thread t owns pinned buffer t and copies chunks t, t + nt, ...: refill
+    // after the DMA of its previous chunk (event), host memcpy, async DMA
+    auto worker = [&](int t) {
+      for (size_t k = t; k < nchunks; k += nt) {
+        const size_t off = k * pm::kStageChunk, len = std::min(pm::kStageChunk, bytes - off);
+        hipError_t e = hipSuccess;
+        if (stage_pending[t]) e = hipEventSynchronize(stage_ev[t]);
+        stage_pending[t] = false;
+        if (e == hipSuccess) {
+          std::memcpy(h_stage[t], (const char*)h + off, len);
+          e = hipMemcpyAsync((char*)d + off, h_stage[t], len, hipMemcpyHostToDevice, st);
+        }
+        if (e == hipSuccess) e = hipEventRecord(stage_ev[t], st);
+        if (e != hipSuccess) {
+          rcs[t] = PM_ERR_HIP;
+          errs[t] = std::string("staged H2D: ") + hipGetErrorString(e);
+          return;
+        }
+        stage_pending[t] = true;
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back([&, t] {
+      (void)hipSetDevice(device);
+      worker(t);
+    });
+    worker(0);
+    for (auto& x : th) x.join();
+    for (int t = 0; t < nt; t++)
+      if (rcs[t]) return pm::set_error(rcs[t], errs[t]);
+  }
+  if (ta) {
+    HIP_TRY(hipEventRecord(tb, st));
+    mark("h2d", ta, tb);
+  }
   return PM_OK;
 }
 
@@ -192,11 +259,13 @@ const CurveOps* curve_ops(int curve) {
   }
 }
 
+// pre29: d_b holds resident bases already in the R = 2^261 form (pm_bases)
 int dispatch_msm_device(Ctx* ctx, int curve, const void* d_s, const void* d_b, size_t n, uint32_t flags,
-                        uint64_t out[8]) {
+                        uint64_t out[8], bool pre29 = false) {
   const CurveOps* ops = curve_ops(curve);
   if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
-  return ops->msm(ctx, d_s, d_b, n, flags, out);
+  flags &= ~kBasesR261;  // internal bit: never taken from the caller
+  return ops->msm(ctx, d_s, d_b, n, flags | (pre29 ? kBasesR261 : 0u), out);
 }
 
 int msm_host_inputs(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
@@ -209,8 +278,8 @@ int msm_host_inputs(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t
   if ((rc = ctx->begin_call())) return rc;
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
   if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
-  HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(hipMemcpyAsync(ctx->in_bases.p, bases, n * 64, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
+  if ((rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) return rc;
   return dispatch_msm_device(ctx, curve, ctx->in_scalars.p, ctx->in_bases.p, n, flags, out);
 }
 
@@ -275,6 +344,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_GLV")) c->glv = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PM_H2D_THREADS")) c->h2d_threads = std::max(0, std::min(kMaxStageThreads, std::atoi(e)));
   if (const char* e = std::getenv("PM_SORT_PPT")) {
     const int v = std::atoi(e);
     c->sort_ppt = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
@@ -425,6 +495,9 @@ int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size
   return PM_OK;
 }
 
+// Resident SRS bases: stored in the pipeline's R = 2^261 canonical form
+// (converted once here), so pm_msm_resident* skips the per-call conversion and
+// holds one copy (64 B per point) instead of two.
 struct pm_bases {
   int curve;
   int device;
@@ -432,17 +505,39 @@ struct pm_bases {
   void* d;
 };
 
-int pm_bases_upload(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, pm_bases** out) {
+static int bases_upload(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, pm_bases** out) {
   if (!ctx || !out || (n && !bases)) return set_error(PM_ERR_ARG, "null argument");
-  if (!valid_curve(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
+  *out = nullptr;
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "more than 2^26 resident bases");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  HIP_TRY(hipSetDevice(ctx->device));
+  int rc = ctx->begin_call();
+  if (rc) return rc;
   std::unique_ptr<pm_bases> b(new pm_bases{curve, ctx->device, n, nullptr});
   HIP_TRY(hipMalloc(&b->d, std::max<size_t>(64, n * 64)));
-  HIP_TRY(hipMemcpyAsync(b->d, bases, n * 64, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  const void* src = bases;
+  if (host && n) {
+    if ((rc = ctx->in_bases.ensure(n * 64)) || (rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) {
+      (void)hipFree(b->d);
+      return rc;
+    }
+    src = ctx->in_bases.p;
+  }
+  if ((rc = ops->bases_to29(ctx, src, n, b->d))) {
+    (void)hipFree(b->d);
+    return rc;
+  }
   *out = b.release();
   return PM_OK;
+}
+
+int pm_bases_upload(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, pm_bases** out) {
+  return bases_upload(ctx, curve, bases, true, n, out);
+}
+
+int pm_bases_upload_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, pm_bases** out) {
+  return bases_upload(ctx, curve, d_bases, false, n, out);
 }
 
 int pm_bases_release(pm_bases* b) {
@@ -453,8 +548,8 @@ int pm_bases_release(pm_bases* b) {
   return PM_OK;
 }
 
-int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* scalars, size_t n,
-                    uint32_t flags, uint64_t out[8]) {
+static int msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const void* scalars, bool host, size_t n,
+                        uint32_t flags, uint64_t out[8]) {
   if (!ctx || !b || !out || (n && !scalars)) return set_error(PM_ERR_ARG, "null argument");
   if (b->device != ctx->device) return set_error(PM_ERR_ARG, "bases live on another device");
   if (offset > b->n || n > b->n - offset) return set_error(PM_ERR_ARG, "window exceeds resident bases");
@@ -465,9 +560,31 @@ int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_
   }
   int rc = ctx->begin_call();
   if (rc) return rc;
-  if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
-  HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
-  return dispatch_msm_device(ctx, b->curve, ctx->in_scalars.p, (const char*)b->d + offset * 64, n, flags, out);
+  const void* d_s = scalars;
+  if (host) {
+    if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
+    if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
+    d_s = ctx->in_scalars.p;
+  }
+  return dispatch_msm_device(ctx, b->curve, d_s, (const char*)b->d + offset * 64, n, flags, out, true);
+}
+
+int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* scalars, size_t n,
+                    uint32_t flags, uint64_t out[8]) {
+  return msm_resident(ctx, b, offset, scalars, true, n, flags, out);
+}
+
+int pm_msm_resident_device(pm_ctx* ctx, const pm_bases* b, size_t offset, const void* d_scalars, size_t n,
+                           uint32_t flags, uint64_t out[8]) {
+  return msm_resident(ctx, b, offset, d_scalars, false, n, flags, out);
+}
+
+int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  if (threads < 0 || threads > kMaxStageThreads) return set_error(PM_ERR_ARG, "h2d threads out of range (0..8)");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->h2d_threads = threads;
+  return PM_OK;
 }
 
 // ------------------------------------------------- NTT (§8f-4)
@@ -518,7 +635,7 @@ static int fixed_create(pm_ctx* ctx, int curve, const void* bases, bool host, si
   const void* d = bases;
   if (host) {
     if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->in_bases.p, bases, n * 64, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) return rc;
     d = ctx->in_bases.p;
   }
   if ((rc = ops->fixed_table(ctx, d, ft.get()))) {
@@ -567,7 +684,7 @@ int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_sca
   }
   int rc = ctx->begin_call();
   if (rc) return rc;
-  return curve_ops(fb->curve)->msm_fixed(ctx, fb, d_scalars, n, flags, out);
+  return curve_ops(fb->curve)->msm_fixed(ctx, fb, d_scalars, n, flags & ~kBasesR261, out);
 }
 
 int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars, size_t n, uint32_t flags,
@@ -583,8 +700,8 @@ int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars,
   int rc = ctx->begin_call();
   if (rc) return rc;
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
-  HIP_TRY(hipMemcpyAsync(ctx->in_scalars.p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
-  return curve_ops(fb->curve)->msm_fixed(ctx, fb, ctx->in_scalars.p, n, flags, out);
+  if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
+  return curve_ops(fb->curve)->msm_fixed(ctx, fb, ctx->in_scalars.p, n, flags & ~kBasesR261, out);
 }
 
 int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {

@@ -134,9 +134,11 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // GLV mode: s_i P_i = k1_i P_i + k2_i phi(P_i) with |k1|, |k2| < 2^127, i.e.
   // an MSM of 2n points with 128-bit scalars: the same number of bucket
   // additions, half the windows (bucket reduction and host Horner halve).
+  // pre29: resident bases already in the pipeline's R = 2^261 form (pm_bases)
+  const bool pre29 = !fixed && (flags & kBasesR261) != 0;
   MsmPlan pl = fixed ? make_plan_fixed(ft->npad, ft->c, ctx->min_chunk)
                      : make_plan(2 * n, ctx->window_c, ctx->groups, ctx->min_chunk, 128);
-  const bool glv = !fixed && ctx->glv && pl.c >= kGlvMinC;
+  const bool glv = !fixed && !pre29 && ctx->glv && pl.c >= kGlvMinC;
   if (!fixed && !glv) pl = make_plan(n, ctx->window_c, ctx->groups, ctx->min_chunk);
   const size_t npts = glv ? 2 * n : n;  // sort entries per window row
   // reduction stream only when window groups overlap; with one group the
@@ -214,6 +216,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const uint32_t* bases29;
   if (fixed) {
     bases29 = (const uint32_t*)ft->d;
+  } else if (pre29) {
+    bases29 = d_bases;
   } else {
     if ((rc = ctx->bases29.ensure(npts * 64))) return rc;
     bases29 = (const uint32_t*)ctx->bases29.p;
@@ -421,6 +425,20 @@ int msm_fixed_to_aff(Ctx* ctx, const pm_fixed_bases* ft, const void* d_s, size_t
   int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, nullptr, n, flags, &r, ft);
   if (rc) return rc;
   aff_to_u64<F>(xyzz_to_aff<F>(r), out);
+  return PM_OK;
+}
+
+// Resident bases (pm_bases_upload*): convert once at upload so every
+// pm_msm_resident* call skips k_bases_to_r261 and the bases29 copy.
+template <class Cv>
+int bases_to29_impl(Ctx* ctx, const void* d_in, size_t n, void* d_out) {
+  using F = typename Cv::Base;
+  if (n == 0) return PM_OK;
+  if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "more than 2^26 resident bases");
+  k_bases_to_r261<F><<<(unsigned)((n + 255) / 256), 256, 0, ctx->stream>>>((const uint32_t*)d_in, (uint32_t)n,
+                                                                          (uint32_t*)d_out);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
   return PM_OK;
 }
 

@@ -34,6 +34,14 @@ constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg (serial chain: 
 // (2^22: 4.91 vs 5.30 ms, profiles/r01_s2), so auto-prefetch is off; PM_PREFETCH=1
 // still selects it.
 constexpr size_t kPrefetchBytes = ~size_t(0);
+// internal msm flag (never in the public header; the C-ABI strips it from
+// caller flags): d_bases already hold the pipeline's R = 2^261 canonical
+// form (resident pm_bases converted at upload), so no per-call conversion
+constexpr uint32_t kBasesR261 = 1u << 30;
+// host -> device staging of large host inputs (pm_msm, pm_msm_resident):
+// chunks of this size through pinned buffers, one per copy thread
+constexpr size_t kStageChunk = size_t(4) << 20;
+constexpr int kMaxStageThreads = 8;
 
 struct Buf {
   void* p = nullptr;
@@ -137,6 +145,12 @@ struct pm_ctx {
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
+  // pinned staging for host inputs (upload_h2d): one chunk buffer + one
+  // event per copy thread; h2d_threads = 0 -> plain pageable hipMemcpyAsync
+  int h2d_threads = 4;
+  void* h_stage[pm::kMaxStageThreads] = {};
+  hipEvent_t stage_ev[pm::kMaxStageThreads] = {};
+  bool stage_pending[pm::kMaxStageThreads] = {};
   // timing
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -152,6 +166,10 @@ struct pm_ctx {
   int begin_call();
   int end_call();
   int ensure_pinned(size_t bytes);
+  // host -> device copy of a large caller buffer on `st`: chunks are copied
+  // by h2d_threads host threads into pinned buffers and DMA'd from there
+  // (pageable hipMemcpyAsync stages through the runtime's own small buffer)
+  int upload_h2d(void* d, const void* h, size_t bytes, hipStream_t st);
   int ensure_group_events(int n);
   hipEvent_t next_event();
   void mark(const char* name, hipEvent_t a, hipEvent_t b);
@@ -181,6 +199,8 @@ struct CurveOps {
   int (*ntt)(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint64_t omega[4], const uint64_t* scale);
   int (*msm_fixed)(Ctx* ctx, const pm_fixed_bases* ft, const void* d_scalars, size_t n, uint32_t flags,
                    uint64_t out[8]);
+  // resident bases: Rust-layout affine (R = 2^256) -> the pipeline's R = 2^261 canonical form
+  int (*bases_to29)(Ctx* ctx, const void* d_in, size_t n, void* d_out);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

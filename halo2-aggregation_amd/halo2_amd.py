@@ -219,7 +219,11 @@ def _load():
         "pm_msm_multi": ([ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int, _u64p],
                          ctypes.c_int),
         "pm_bases_upload": ([_vp, ctypes.c_int, _u64p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
+        "pm_bases_upload_device": ([_vp, ctypes.c_int, _vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
         "pm_bases_release": ([_vp], ctypes.c_int),
+        "pm_msm_resident_device": ([_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_uint32, _u64p],
+                                   ctypes.c_int),
+        "pm_ctx_set_h2d_threads": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_msm_resident": ([_vp, _vp, ctypes.c_size_t, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p],
                             ctypes.c_int),
         "pm_point_add": ([ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
@@ -332,11 +336,19 @@ def device_count():
 
 
 class Bases:
-    def __init__(self, ctx, curve, bases):
-        b = _as_u64(bases, 8)
-        self.ctx, self.n = ctx, b.shape[0]
+    """Device-resident SRS bases (pm_bases_upload / pm_bases_upload_device):
+    host `bases` (n x 8 u64), or `d_bases` (device pointer) with `n`."""
+
+    def __init__(self, ctx, curve, bases=None, d_bases=None, n=None):
+        self.ctx, self.curve = ctx, curve
         h = _vp()
-        _check(lib().pm_bases_upload(ctx.h, curve, _p(b), self.n, ctypes.byref(h)))
+        if d_bases is not None:
+            self.n = int(n)
+            _check(lib().pm_bases_upload_device(ctx.h, curve, _vp(d_bases), self.n, ctypes.byref(h)))
+        else:
+            b = _as_u64(bases, 8)
+            self.n = b.shape[0]
+            _check(lib().pm_bases_upload(ctx.h, curve, _p(b), self.n, ctypes.byref(h)))
         self.h = h
 
     def release(self):
@@ -464,8 +476,17 @@ class Context:
                                    SCALARS_CANONICAL if canonical else 0, _p(out)))
         return out
 
-    def upload_bases(self, curve, bases):
-        return Bases(self, curve, bases)
+    def upload_bases(self, curve, bases=None, d_bases=None, n=None):
+        return Bases(self, curve, bases, d_bases, n)
+
+    def msm_resident_device(self, bases: Bases, offset, d_scalars, n, canonical=False):
+        out = np.zeros(8, dtype=np.uint64)
+        _check(lib().pm_msm_resident_device(self.h, bases.h, offset, _vp(d_scalars), n,
+                                            SCALARS_CANONICAL if canonical else 0, _p(out)))
+        return out
+
+    def set_h2d_threads(self, threads):
+        _check(lib().pm_ctx_set_h2d_threads(self.h, threads))
 
     def fixed_bases(self, curve, bases=None, c=0, d_bases=None, n=None):
         return FixedBases(self, curve, bases, c, d_bases, n)

@@ -114,12 +114,29 @@ int pm_msm_device(pm_ctx* ctx, int curve, const void* d_scalars, const void* d_b
 int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
                  int ngpu, uint64_t out[8]);
 
-/* Device-resident base cache: the SRS bases of halo2 Params are fixed, so a
- * caller uploads them once and runs many MSMs against a window of them. */
+/* Device-resident base cache: the SRS bases of halo2 Params (`params.g`,
+ * `params.g_lagrange`, replacing the `bases` argument of best_multiexp at
+ * examples/simple-example.rs:638-640) are fixed, so a caller uploads them once
+ * and runs many MSMs against a window [offset, offset + n) of them.  The
+ * library converts them once, at upload, to the pipeline's internal form
+ * (64 B per point on the device, no per-call conversion).
+ * _upload takes host bases (Rust layout, as pm_msm), _upload_device bases
+ * already in device memory of ctx's device (copied; the caller keeps its
+ * buffer).  pm_msm_resident takes host scalars (staged through pinned
+ * memory, see pm_ctx_set_h2d_threads), pm_msm_resident_device device
+ * scalars. */
 int pm_bases_upload(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, pm_bases** out);
+int pm_bases_upload_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, pm_bases** out);
 int pm_bases_release(pm_bases* b);
 int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* scalars,
                     size_t n, uint32_t flags, uint64_t out[8]);
+int pm_msm_resident_device(pm_ctx* ctx, const pm_bases* b, size_t offset, const void* d_scalars,
+                           size_t n, uint32_t flags, uint64_t out[8]);
+/* Host inputs of pm_msm / pm_msm_ctx / pm_msm_resident / pm_msm_fixed /
+ * pm_bases_upload are copied to the device in 4 MiB chunks through pinned
+ * buffers by `threads` host threads (0..8, default 4, env PM_H2D_THREADS);
+ * 0 = one plain pageable hipMemcpyAsync.  Results never depend on it. */
+int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads);
 
 /* Device self-test of the MSM pipeline's radix-2^29 lazy field arithmetic
  * against the 32-bit Montgomery arithmetic (n random + edge operand pairs of
