@@ -171,7 +171,8 @@ def main():
         ctx.set_window(args.window)
     dev = torch.device("cuda", local)
     i0, _ = shard_range(rank, world, n)
-    leg = run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline=True, breakdown=True)
+    leg = run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline=True, breakdown=True,
+                      host_leg=(world == 1))
     d_s, d_b, result = leg.pop("_d_s"), leg.pop("_d_b"), leg.pop("_result")
     gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
 
@@ -214,6 +215,9 @@ def main():
             "kernels_ms": leg["kernels_ms"],
             "roofline": leg["roofline"],
         }
+        for k in ("raw_device_bases_ms_per_step", "raw_device_bases_matches", "host_scalars"):
+            if k in leg:
+                out[k] = leg[k]
         if cpu is not None:
             out["cpu_baseline"] = cpu
         if big is not None:
@@ -268,10 +272,14 @@ MSM_KERNELS = ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "a
                "bucket_bits", "bits_combine", "host_tail"]
 
 
-def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, n_total=None, check_port=False):
+def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, n_total=None, check_port=False,
+                host_leg=False):
     """One MSM leg: this rank's n pairs [i0, i0 + n) generated on the device,
-    one step = pm_msm_device + all-gather of the partials + host fold.
-    n_total None: weak scaling (world * n pairs); else strong (n_total split)."""
+    one step = pm_msm_resident_device against the rank's resident bases
+    (pm_bases_upload_device: the SRS bases are uploaded and converted to the
+    pipeline form once, untimed, like params.g in halo2) + all-gather of the
+    partials + host fold.  n_total None: weak scaling (world * n pairs); else
+    strong (n_total split over the ranks)."""
     import numpy as np
     import torch
 
@@ -283,13 +291,16 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     ctx.synth_scalars(curve, SEED_SCALARS, i0, n, d_s.data_ptr())
     ctx.synth_bases(curve, SEED_BASES, i0, n, d_b.data_ptr())
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rb = ctx.upload_bases(curve, d_bases=d_b.data_ptr(), n=n) if n else None
+    upload_ms = (time.perf_counter() - t0) * 1e3
     gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
 
     def padd(a, b):
         return H.point_add(curve, a, b)
 
     def step():
-        part = ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n) if n else np.zeros(8, np.uint64)
+        part = ctx.msm_resident_device(rb, 0, d_s.data_ptr(), n) if n else np.zeros(8, np.uint64)
         return combine_partials(part, dist, dev, padd, world, gathered)
 
     # timed region: HIP events only around the roofline kernel (every event
@@ -303,14 +314,15 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     launches, acc_ms = ctx.kernel_stats("accumulate") if roofline else (0, 0.0)
     ctx.set_timing(False)
     lg = (n_total or n).bit_length() - 1
-    name = H.CURVE_NAMES[curve] if hasattr(H, "CURVE_NAMES") else ("pallas", "vesta", "bn254")[curve]
+    name = ("pallas", "vesta", "bn254")[curve]
     total = n_total if n_total is not None else world * n
     out = {"value": round(total / (elapsed / args.steps) / 1e6, 3), "unit": "Mscalar/s",
            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
            "scaling": "strong" if n_total is not None else "weak",
            "config": {"workload": f"{name}_msm_2^{lg}" + ("_total" if n_total is not None else "_per_gpu"),
-                      "curve": name, "n_per_gpu": n, "n_total": total, "scalars": "montgomery",
-                      "bases": "affine montgomery, HBM-resident",
+                      "curve": name, "n_per_gpu": n, "n_total": total, "scalars": "montgomery, HBM-resident",
+                      "bases": "affine, HBM-resident SRS (pm_bases_upload_device, converted once at upload, "
+                               f"{upload_ms:.1f} ms untimed)",
                       "parallelism": f"point-slice x{world} + RCCL all-gather of partial points"}}
     if breakdown:
         # per-MSM kernel breakdown from a separate, untimed diagnostic run with
@@ -333,6 +345,17 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
         if valu:
             roof["valu_int"] = valu
         out["roofline"] = roof
+    if roofline:
+        # the same MSM from raw device bases (R = 2^256 layout converted on
+        # every call, pm_msm_device), for comparison
+        def raw():
+            return ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n)
+        raw_s, raw_res = timed_steps(raw, max(3, args.steps // 4), 1, dist, dev)
+        out["raw_device_bases_ms_per_step"] = round(raw_s * 1e3 / max(3, args.steps // 4), 4)
+        if world == 1:
+            out["raw_device_bases_matches"] = bool(np.array_equal(np.asarray(raw_res), np.asarray(result)))
+    if host_leg and n:
+        out["host_scalars"] = run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, result)
     if check_port and n:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import msm_ref
@@ -340,8 +363,38 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
         out["matches_c_port"] = bool(np.array_equal(
             np.asarray(result), msm_ref.best_multiexp(curve, d_s.cpu().numpy().view(np.uint64),
                                                       d_b.cpu().numpy().view(np.uint64), threads=cpu_threads())))
+    if rb is not None:
+        rb.release()
     out.update(_d_s=d_s, _d_b=d_b, _result=result)
     return out
+
+
+def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
+    """The drop-in path a Rust best_multiexp shim takes:
+    scalars in (pageable) host memory, bases resident -> pm_msm_resident.
+    Reports the PCIe-inclusive rate and the scalar H2D time on its own
+    (HIP events around the copy), for the default plain pageable
+    hipMemcpyAsync and for the pinned staging through 4 copy threads."""
+    import numpy as np
+
+    S = d_s.cpu().numpy().view(np.uint64).copy()
+    res = {}
+    for label, threads in (("pageable", 0), ("staged_4_threads", 4)):
+        ctx.set_h2d_threads(threads)
+        k = max(3, args.steps // 2)
+        el, got = timed_steps(lambda: ctx.msm_resident(rb, 0, S), k, 1, None, dev)
+        ctx.set_timing(True, only="h2d")
+        ctx.reset_stats()
+        for _ in range(3):
+            ctx.msm_resident(rb, 0, S)
+        ctx.set_timing(False)
+        cnt, h2d_ms = ctx.kernel_stats("h2d")
+        h2d = h2d_ms / max(1, cnt)
+        res[label] = {"ms_per_msm": round(el * 1e3 / k, 4), "Mscalar_s": round(n / (el / k) / 1e6, 3),
+                      "scalar_h2d_ms": round(h2d, 4), "scalar_h2d_GBps": round(32 * n / (h2d * 1e-3) / 1e9, 2),
+                      "matches": bool(np.array_equal(np.asarray(got), np.asarray(want)))}
+    ctx.set_h2d_threads(0)
+    return res
 
 
 def dry_run(args, rank, world):

@@ -146,8 +146,11 @@ struct pm_ctx {
   void* h_pinned = nullptr;
   size_t h_pinned_cap = 0;
   // pinned staging for host inputs (upload_h2d): one chunk buffer + one
-  // event per copy thread; h2d_threads = 0 -> plain pageable hipMemcpyAsync
-  int h2d_threads = 4;
+  // event per copy thread; h2d_threads = 0 -> plain pageable hipMemcpyAsync.
+  // Default 0: on MI355X the runtime's pageable copy of 32 MB already runs at
+  // ~52 GB/s (82 % of PCIe 5 x16) vs ~38 GB/s through 4 staging threads
+  // (profiles/r02/b/bench.json host_scalars)
+  int h2d_threads = 0;
   void* h_stage[pm::kMaxStageThreads] = {};
   hipEvent_t stage_ev[pm::kMaxStageThreads] = {};
   bool stage_pending[pm::kMaxStageThreads] = {};

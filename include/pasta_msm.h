@@ -133,9 +133,11 @@ int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_
 int pm_msm_resident_device(pm_ctx* ctx, const pm_bases* b, size_t offset, const void* d_scalars,
                            size_t n, uint32_t flags, uint64_t out[8]);
 /* Host inputs of pm_msm / pm_msm_ctx / pm_msm_resident / pm_msm_fixed /
- * pm_bases_upload are copied to the device in 4 MiB chunks through pinned
- * buffers by `threads` host threads (0..8, default 4, env PM_H2D_THREADS);
- * 0 = one plain pageable hipMemcpyAsync.  Results never depend on it. */
+ * pm_bases_upload: threads = 0 (default) copies them with one pageable
+ * hipMemcpyAsync; 1..8 stages them in 4 MiB chunks through pinned buffers,
+ * `threads` host threads each (env PM_H2D_THREADS).  Measured on MI355X the
+ * pageable copy is the faster one (~52 vs ~38 GB/s for 32 MB).  Results never
+ * depend on it. */
 int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads);
 
 /* Device self-test of the MSM pipeline's radix-2^29 lazy field arithmetic

@@ -117,6 +117,35 @@ def test_fixed_known_dlog_2_20(gpu_ctx):
         fb.release()
 
 
+@pytest.mark.parametrize("curve", [0, 2])
+def test_fixed_known_dlog_2_23(gpu_ctx, curve):
+    """The outer prover's commit size (k = 23, examples/simple-example.rs:663,702):
+    a 2^23 fixed-base table (auto c = 20: 13 windows, ~7 GB) on Pallas and
+    BN254 == [sum s_i a_i]G, and == the variable-base MSM of the same inputs."""
+    import torch
+
+    from dlog_util import known_dlog_point
+
+    n = 1 << 23
+    dev = torch.device("cuda", gpu_ctx.device)
+    s = torch.empty((n, 4), dtype=torch.int64, device=dev)
+    b = torch.empty((n, 8), dtype=torch.int64, device=dev)
+    gpu_ctx.synth_scalars(curve, P.SEED_SCALARS, 0, n, s.data_ptr())
+    gpu_ctx.synth_bases(curve, P.SEED_BASES, 0, n, b.data_ptr())
+    torch.cuda.synchronize()
+    fb = gpu_ctx.fixed_bases(curve, d_bases=b.data_ptr(), n=n)
+    try:
+        assert fb.c == 20 and fb.windows == 13
+        got = fb.msm_device(s.data_ptr(), n)
+    finally:
+        fb.release()
+    assert np.array_equal(got, gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n))
+    del s, b
+    torch.cuda.empty_cache()
+    C = P.CURVES[curve]
+    assert P.limbs_to_point(C, [int(x) for x in got]) == known_dlog_point(curve, n)
+
+
 def test_fixed_errors(gpu_ctx):
     with pytest.raises(H.PmError):
         gpu_ctx.fixed_bases(0, np.zeros((0, 8), np.uint64))

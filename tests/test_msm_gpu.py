@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import halo2_amd as H
+from dlog_util import known_dlog_point
 import msm_ref
 import pasta as P
 
@@ -131,26 +132,11 @@ def test_known_dlog(gpu_ctx, curve, logn):
     s, b = _torch_inputs(gpu_ctx, curve, n)
     got = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
     C = P.CURVES[curve]
-    S = msm_ref.synth_scalars(curve, P.SEED_SCALARS, 0, n)       # Montgomery form
-    A = msm_ref.synth_scalars(curve, P.SEED_BASES, 0, n)         # dlogs a_i (Montgomery)
-    rinv = pow(P.R_MONT, -1, C.r)
-    tot = 0
-    for k in range(0, n, 1 << 16):  # sum s_i a_i in R^2-scaled Montgomery domain
-        ss = [int(x) for x in _to_int(S[k:k + (1 << 16)])]
-        aa = [int(x) for x in _to_int(A[k:k + (1 << 16)])]
-        tot += sum(x * y for x, y in zip(ss, aa))
-    tot = tot * rinv * rinv % C.r
-    # a_i == 0 maps to 1 in the generator; never happens for these seeds (checked)
-    assert P.limbs_to_point(C, [int(x) for x in got]) == C.mul(tot, C.gen)
+    assert P.limbs_to_point(C, [int(x) for x in got]) == known_dlog_point(curve, n)
     if logn >= 22:
         # and bit for bit against the C restatement of best_multiexp
         assert np.array_equal(got, msm_ref.best_multiexp(curve, s.cpu().numpy().view(np.uint64),
                                                          b.cpu().numpy().view(np.uint64)))
-
-
-def _to_int(L):
-    L = L.astype(object)
-    return L[:, 0] + (L[:, 1] << 64) + (L[:, 2] << 128) + (L[:, 3] << 192)
 
 
 def test_all_equal_scalars_large(gpu_ctx):
@@ -211,3 +197,45 @@ def test_errors():
         H.best_multiexp(0, np.zeros((2, 4), np.uint64), np.zeros((1, 8), np.uint64))
     assert np.array_equal(H.best_multiexp(0, np.zeros((0, 4), np.uint64), np.zeros((0, 8), np.uint64)),
                           np.zeros(8, np.uint64))
+
+
+@pytest.mark.parametrize("curve,n", [(0, (1 << 20) + 3), (1, 70001), (2, 5000)])
+def test_resident_device_and_staged_host_paths(gpu_ctx, curve, n):
+    """Resident bases (converted to the pipeline form at upload, from device
+    or host memory) give the raw-bases result, with device scalars, host
+    scalars staged through pinned buffers by 0 (pageable), 1, 3 and 8 copy
+    threads (4 MiB chunks, ragged tail), windows at an offset, and GLV on
+    (ignored for pre-converted bases)."""
+    s, b = _torch_inputs(gpu_ctx, curve, n)
+    want = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+    S = s.cpu().numpy().view(np.uint64)
+    B = b.cpu().numpy().view(np.uint64)
+    rb = gpu_ctx.upload_bases(curve, d_bases=b.data_ptr(), n=n)
+    rh = gpu_ctx.upload_bases(curve, B)
+    try:
+        assert np.array_equal(gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), n), want)
+        assert np.array_equal(gpu_ctx.msm_resident_device(rh, 0, s.data_ptr(), n), want)
+        for t in (0, 1, 3, 8):
+            gpu_ctx.set_h2d_threads(t)
+            assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S), want), t
+            assert np.array_equal(gpu_ctx.msm(curve, S, B), want), t
+        gpu_ctx.set_h2d_threads(0)
+        k = n // 3
+        part = gpu_ctx.msm_device(curve, s[k:].data_ptr(), b[k:].data_ptr(), n - k)
+        assert np.array_equal(gpu_ctx.msm_resident(rb, k, S[k:]), part)
+        gpu_ctx.set_glv(True)
+        assert np.array_equal(gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), n), want)
+    finally:
+        gpu_ctx.set_glv(False)
+        gpu_ctx.set_h2d_threads(0)
+        rb.release()
+        rh.release()
+    if n < (1 << 20):
+        assert np.array_equal(want, msm_ref.best_multiexp(curve, S, B))
+
+
+def test_h2d_threads_argument_checked(gpu_ctx):
+    with pytest.raises(H.PmError):
+        gpu_ctx.set_h2d_threads(9)
+    with pytest.raises(H.PmError):
+        gpu_ctx.set_h2d_threads(-1)
