@@ -242,6 +242,9 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     HIP_TRY(hipStreamWaitEvent(side, up, 0));
   }
   if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side))) return rc;
+  // status: the replay stores bits 0-1 per proof, k_acc_scalars ORs in the
+  // denominator bit; without a replay the words start at zero
+  if (d_status && !vk_repr) HIP_TRY(hipMemsetAsync(d_status, 0, B * sizeof(uint32_t), side));
   // k_acc_scalars: 4 waves per block of np proofs, (nsc + T + exchange +
   // work) rows of 32 B per proof in LDS (proof stride np + 1), np <= 64
   // within a 128 KiB budget
@@ -252,7 +255,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   PM_LAUNCH_ST(ctx, side, "acc_scalars",
                (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, side>>>(
                    h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
-                   dcoef, (uint32_t*)d_hout, np)));
+                   dcoef, (uint32_t*)d_hout, np, (uint32_t*)d_status)));
   if (lgS > 0) {
     HIP_TRY(hipEventRecord(sc_done, side));
     HIP_TRY(hipStreamWaitEvent(st, sc_done, 0));
@@ -304,7 +307,8 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
   squeeze(1);                                              // beta :390
   squeeze(2);                                              // gamma :393
   pts(L.p_permz, L.n_perm_sets);                           // :402-409
-  pts(L.p_lkz, s->num_lookups);                            // :411-417
+  for (uint32_t i = 0; i < s->num_lookups; i++)            // :411-417 (lookup.rs:100: an
+    prog.push_back((kTrPoint << 24) | kTrLookupZFlag | (L.p_lkz + i));  // identity Z aborts)
   pts(L.p_rand, 1);                                        // :419-421
   squeeze(3);                                              // y :423
   pts(L.p_h, s->quotient_degree);                          // :425-434

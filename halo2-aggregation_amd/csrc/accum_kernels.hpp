@@ -55,6 +55,10 @@ __device__ __forceinline__ void stfe(uint32_t* base, uint32_t idx, const Fe<Fs>&
 // k_acc_scalars stages each proof's evaluations here once, with coalesced
 // loads, instead of ~60 dependent global loads per lane, and accumulates the
 // MSM coefficients here instead of read-modify-writes to global memory.
+// per-proof status bit set by k_acc_scalars (include/pasta_msm.h
+// PM_ACCUM_DENOM_ZERO); bits 0-1 come from the transcript replay
+static constexpr uint32_t kAccStatusDenomZero = 4;
+
 struct LdsRows {
   uint32_t* base;
   uint32_t lane, stride;  // stride = lanes per block + 1
@@ -144,7 +148,7 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
                                                      const uint32_t* __restrict__ scalars,
                                                      const uint32_t* __restrict__ challenges,
                                                      uint32_t* __restrict__ coef, uint32_t* __restrict__ h_out,
-                                                     uint32_t np) {
+                                                     uint32_t np, uint32_t* __restrict__ status) {
   extern __shared__ uint32_t acc_lds[];
   const uint32_t role = threadIdx.x >> 6, pl = threadIdx.x & 63;
   const uint32_t b0 = blockIdx.x * np, b = b0 + pl;
@@ -187,6 +191,10 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
       wk.put<Fs>(i, den);
       wk.put<Fs>(K + i, pre);
     }
+    // a zero denominator (x^n = 1, or x = omega^-i for a Lagrange basis
+    // point) is where the reference's main_gate.div fails (vanishing.rs:175,
+    // verifier.rs:580): flag the proof; its outputs are then unspecified
+    if (status && fe_is_zero<Fs>(fe_from_mont<Fs>(pre))) status[b] |= kAccStatusDenomZero;
     Fe<Fs> inv = fe_inv_fast<Fs>(pre);
     for (uint32_t i = K - 1; i > 0; i--) {
       const Fe<Fs> t = fe_mul<Fs>(inv, wk.get<Fs>(K + i - 1));

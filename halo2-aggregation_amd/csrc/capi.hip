@@ -760,7 +760,8 @@ int pm_shape_layout(const pm_proof_shape* shape, uint32_t* points_per_proof, uin
 }
 
 int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_points,
-                          const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval) {
+                          const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval,
+                          void* d_out_status) {
   if (!ctx || !shape || (B && (!d_points || !d_scalars || !d_challenges || !d_out_quads)))
     return set_error(PM_ERR_ARG, "null argument");
   const CurveOps* ops = curve_ops(curve);
@@ -769,11 +770,12 @@ int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, s
   int rc = ctx->begin_call();
   if (rc) return rc;
   return ops->accum(ctx, shape, B, d_points, d_scalars, const_cast<void*>(d_challenges), d_out_quads, d_out_h_eval, nullptr,
-                    nullptr);
+                    d_out_status);
 }
 
 int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t* points,
-                   const uint64_t* scalars, const uint64_t* challenges, uint64_t* out_quads, uint64_t* out_h_eval) {
+                   const uint64_t* scalars, const uint64_t* challenges, uint64_t* out_quads, uint64_t* out_h_eval,
+                   uint32_t* out_status) {
   if (!ctx || !shape || (B && (!points || !scalars || !challenges || !out_quads)))
     return set_error(PM_ERR_ARG, "null argument");
   const CurveOps* ops = curve_ops(curve);
@@ -784,17 +786,20 @@ int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (B == 0) return PM_OK;
   if ((rc = ctx->begin_call())) return rc;
-  const size_t bp = B * npts * 64, bs = B * nsc * 32, bc = B * 7 * 32, bo = B * 4 * 64, bh = B * 32;
-  if ((rc = ctx->acc_io.ensure(bp + bs + bc + bo + bh))) return rc;
+  const size_t bp = B * npts * 64, bs = B * nsc * 32, bc = B * 7 * 32, bo = B * 4 * 64, bh = B * 32, bst = B * 4;
+  if ((rc = ctx->acc_io.ensure(bp + bs + bc + bo + bh + bst))) return rc;
   char* base = (char*)ctx->acc_io.p;
   HIP_TRY(hipMemcpyAsync(base, points, bp, hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipMemcpyAsync(base + bp, scalars, bs, hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipMemcpyAsync(base + bp + bs, challenges, bc, hipMemcpyHostToDevice, ctx->stream));
   char* dq = base + bp + bs + bc;
   char* dh = dq + bo;
-  if ((rc = ops->accum(ctx, shape, B, base, base + bp, base + bp + bs, dq, dh, nullptr, nullptr))) return rc;
+  char* dst = dh + bh;
+  if ((rc = ops->accum(ctx, shape, B, base, base + bp, base + bp + bs, dq, dh, nullptr, out_status ? dst : nullptr)))
+    return rc;
   HIP_TRY(hipMemcpyAsync(out_quads, dq, bo, hipMemcpyDeviceToHost, ctx->stream));
   if (out_h_eval) HIP_TRY(hipMemcpyAsync(out_h_eval, dh, bh, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_status) HIP_TRY(hipMemcpyAsync(out_status, dst, bst, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return PM_OK;
 }
@@ -897,6 +902,54 @@ int pm_accum_batch_transcript(pm_ctx* ctx, int curve, const pm_proof_shape* shap
                               uint32_t* out_status) {
   return transcript_host(ctx, curve, shape, B, vk_repr, points, scalars, out_challenges, out_quads, out_h_eval,
                          out_status, true);
+}
+
+// Proof batch sharded over several contexts (devices) in one process: proofs
+// are independent, so context k takes the contiguous range
+// [k*per, (k+1)*per) and runs the single-context host entry on it in its own
+// thread; the outputs land in place.  challenges == NULL replays the
+// transcript (vk_repr required), else vk_repr is ignored.
+int pm_accum_batch_multi(pm_ctx* const* ctxs, int nctx, int curve, const pm_proof_shape* shape, size_t B,
+                         const uint64_t* points, const uint64_t* scalars, const uint64_t* challenges,
+                         const uint64_t vk_repr[4], uint64_t* out_challenges, uint64_t* out_quads,
+                         uint64_t* out_h_eval, uint32_t* out_status) {
+  if (!ctxs || nctx < 1 || !shape || (B && (!points || !scalars || !out_quads)) || (!challenges && !vk_repr))
+    return set_error(PM_ERR_ARG, "null argument");
+  for (int k = 0; k < nctx; k++)
+    if (!ctxs[k]) return set_error(PM_ERR_ARG, "null context");
+  if (!valid_curve(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
+  uint32_t npts = 0, nsc = 0, ns = 0;
+  int rc = pm_shape_layout(shape, &npts, &nsc, &ns);
+  if (rc) return rc;
+  if (B == 0) return PM_OK;
+  const size_t per = (B + nctx - 1) / nctx;
+  std::vector<int> rcs(nctx, PM_OK);
+  std::vector<std::string> errs(nctx);
+  std::vector<std::thread> th;
+  for (int k = 0; k < nctx; k++) {
+    const size_t lo = std::min(B, per * k), cnt = std::min(B, lo + per) - lo;
+    if (cnt == 0) continue;
+    th.emplace_back([&, k, lo, cnt] {
+      const uint64_t* p = points + lo * npts * 8;
+      const uint64_t* sc = scalars + lo * nsc * 4;
+      uint64_t* q = out_quads + lo * 32;
+      uint64_t* h = out_h_eval ? out_h_eval + lo * 4 : nullptr;
+      uint32_t* st = out_status ? out_status + lo : nullptr;
+      int r;
+      if (challenges)
+        r = pm_accum_batch(ctxs[k], curve, shape, cnt, p, sc, challenges + lo * 28, q, h, st);
+      else
+        r = pm_accum_batch_transcript(ctxs[k], curve, shape, cnt, vk_repr, p, sc,
+                                      out_challenges ? out_challenges + lo * 28 : nullptr, q, h, st);
+      rcs[k] = r;
+      if (r) errs[k] = pm::g_last_error;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int k = 0; k < nctx; k++)
+    if (rcs[k]) return set_error(rcs[k], "context " + std::to_string(k) + ": " + errs[k]);
+  if (challenges && out_challenges) std::memcpy(out_challenges, challenges, B * 7 * 32);
+  return PM_OK;
 }
 
 }  // extern "C"

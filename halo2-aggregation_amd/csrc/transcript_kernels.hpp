@@ -43,6 +43,12 @@ namespace pm {
 enum : uint32_t { kTrSqueeze = 0, kTrPoint = 1, kTrScalar = 2, kTrVk = 3 };
 static constexpr uint32_t kTrChallenges = 7;
 static constexpr uint32_t kTrStatusIdentity = 1;  // an identity point was skipped
+// the skipped identity was a lookup product commitment Z: the reference's
+// common_point error propagates there (lookup.rs:100 `?`), so the in-circuit
+// verifier aborts; elsewhere the error is dropped (lookup.rs:72-73, ...)
+static constexpr uint32_t kTrStatusLookupZIdentity = 2;
+// point-op flag (bit 23 of the op's index field): this point is a lookup Z
+static constexpr uint32_t kTrLookupZFlag = 1u << 23;
 
 struct TranscriptHdr {
   uint32_t B, npts, nsc, nprog;
@@ -311,7 +317,7 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
   uint32_t d[16];
   auto fetch = [&](uint32_t k, uint32_t w[16]) {
     const uint32_t op = k < hd.nprog ? prog[k] : 0u;
-    const uint32_t kind = op >> 24, idx = op & 0xffffffu;
+    const uint32_t kind = op >> 24, idx = op & (kTrLookupZFlag - 1u);
     const uint32_t* src = kind == kTrPoint ? pts + 16 * idx : kind == kTrScalar ? scs + 8 * idx : pts;
     const uint32_t nw = kind == kTrPoint ? 16 : kind == kTrScalar ? 8 : 0;
 #pragma unroll
@@ -328,7 +334,7 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
 #pragma unroll
       for (int i = 0; i < 16; i++) z |= cur[i];
       if (z == 0) {
-        st |= kTrStatusIdentity;
+        st |= kTrStatusIdentity | ((op & kTrLookupZFlag) ? kTrStatusLookupZIdentity : 0u);
       } else {
         tr_put_byte(s, buf, slot, 1);
 #pragma unroll

@@ -235,9 +235,12 @@ def _load():
         "pm_shape_layout": ([ctypes.POINTER(PmProofShape), ctypes.POINTER(ctypes.c_uint32),
                              ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
         "pm_accum_batch": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p, _u64p, _u64p,
-                            _u64p, _u64p], ctypes.c_int),
+                            _u64p, _u64p, _u32p], ctypes.c_int),
         "pm_accum_batch_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _vp, _vp, _vp,
-                                   _vp, _vp], ctypes.c_int),
+                                   _vp, _vp, _vp], ctypes.c_int),
+        "pm_accum_batch_multi": ([ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, ctypes.POINTER(PmProofShape),
+                                  ctypes.c_size_t, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p, _u32p],
+                                 ctypes.c_int),
         "pm_fixed_bases_create": ([_vp, ctypes.c_int, _u64p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_vp)],
                                   ctypes.c_int),
         "pm_fixed_bases_create_device": ([_vp, ctypes.c_int, _vp, ctypes.c_size_t, ctypes.c_int,
@@ -319,6 +322,27 @@ def point_add(curve, a, b):
     out = np.zeros(8, dtype=np.uint64)
     _check(lib().pm_point_add(curve, _p(a), _p(b), _p(out)))
     return out
+
+
+def accum_batch_multi(contexts, shape, points, scalars, challenges=None, vk_repr=None):
+    """pm_accum_batch_multi: the proof batch sharded over `contexts` (one per
+    device).  challenges None -> replay the transcript from vk_repr.
+    Returns (challenges (B,7,4), quads (B,4,8), h_eval (B,4), status (B,))."""
+    npts, nsc, _ = shape.layout()
+    p = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1, npts, 8)
+    B = p.shape[0]
+    s = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(B, nsc, 4)
+    ch_in = None if challenges is None else np.ascontiguousarray(challenges, dtype=np.uint64).reshape(B, 7, 4)
+    vk = None if vk_repr is None else np.ascontiguousarray(vk_repr, dtype=np.uint64).reshape(4)
+    ch = np.zeros((B, 7, 4), dtype=np.uint64)
+    quads = np.zeros((B, 4, 8), dtype=np.uint64)
+    hev = np.zeros((B, 4), dtype=np.uint64)
+    st = np.zeros(B, dtype=np.uint32)
+    arr = (_vp * len(contexts))(*[c.h for c in contexts])
+    _check(lib().pm_accum_batch_multi(arr, len(contexts), shape.curve, ctypes.byref(shape.c), B, _p(p), _p(s),
+                                      _p(ch_in) if ch_in is not None else None, _p(vk) if vk is not None else None,
+                                      _p(ch), _p(quads), _p(hev), st.ctypes.data_as(_u32p)))
+    return ch, quads, hev, st
 
 
 def vk_transcript_repr(curve, pinned: bytes):
@@ -513,13 +537,22 @@ class Context:
         c = np.ascontiguousarray(challenges, dtype=np.uint64).reshape(B, 7, 4)
         quads = np.zeros((B, 4, 8), dtype=np.uint64)
         hev = np.zeros((B, 4), dtype=np.uint64)
+        st = np.zeros(B, dtype=np.uint32)
         _check(lib().pm_accum_batch(self.h, shape.curve, ctypes.byref(shape.c), B, _p(p), _p(s), _p(c), _p(quads),
-                                    _p(hev)))
+                                    _p(hev), st.ctypes.data_as(_u32p)))
+        self.last_status = st
         return quads, hev
 
-    def accum_batch_device(self, shape: ProofShape, B, d_points, d_scalars, d_challenges, d_quads, d_h=0):
+    def accum_batch_status(self, shape: ProofShape, points, scalars, challenges):
+        """pm_accum_batch -> (quads, h_eval, status (B,) u32: PM_ACCUM_DENOM_ZERO)."""
+        q, h = self.accum_batch(shape, points, scalars, challenges)
+        return q, h, self.last_status
+
+    def accum_batch_device(self, shape: ProofShape, B, d_points, d_scalars, d_challenges, d_quads, d_h=0,
+                           d_status=0):
         _check(lib().pm_accum_batch_device(self.h, shape.curve, ctypes.byref(shape.c), B, _vp(d_points),
-                                           _vp(d_scalars), _vp(d_challenges), _vp(d_quads), _vp(d_h or None)))
+                                           _vp(d_scalars), _vp(d_challenges), _vp(d_quads), _vp(d_h or None),
+                                           _vp(d_status or None)))
 
     def _proof_buffers(self, shape, points, scalars):
         npts, nsc, _ = shape.layout()

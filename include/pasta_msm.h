@@ -244,10 +244,35 @@ int pm_shape_layout(const pm_proof_shape* shape, uint32_t* points_per_proof, uin
  * (may be NULL).  curve selects the group (PM_CURVE_*); its scalar field is
  * the field of every scalar above. */
 int pm_accum_batch(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t* points,
-                   const uint64_t* scalars, const uint64_t* challenges, uint64_t* out_quads, uint64_t* out_h_eval);
+                   const uint64_t* scalars, const uint64_t* challenges, uint64_t* out_quads, uint64_t* out_h_eval,
+                   uint32_t* out_status);
 /* Same with every buffer in device memory of ctx's device. */
 int pm_accum_batch_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_points,
-                          const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval);
+                          const void* d_scalars, const void* d_challenges, void* d_out_quads, void* d_out_h_eval,
+                          void* d_out_status);
+/* Per-proof status words (out_status: B x uint32, may be NULL) of every
+ * accumulator entry point.  A nonzero word means the reference verifier
+ * would not have produced an accumulator for that proof; its quad and h_eval
+ * are then unspecified and the caller must reject the proof:
+ *   PM_TRANSCRIPT_IDENTITY_SKIPPED (1)  an identity commitment was skipped by
+ *       the transcript (transcript.rs:101-110), transcript entries only;
+ *   PM_TRANSCRIPT_LOOKUP_Z_IDENTITY (2) that commitment was a lookup product
+ *       Z, where the reference propagates the error and aborts (lookup.rs:100);
+ *   PM_ACCUM_DENOM_ZERO (4)  x^n = 1 or x = omega^-i for a Lagrange basis
+ *       point: the reference's main_gate.div fails (vanishing.rs:175,
+ *       verifier.rs:580). */
+#define PM_ACCUM_DENOM_ZERO 4u
+/* A batch sharded over nctx contexts (one per device) in one process: proofs
+ * are independent, context k takes the contiguous range [k*ceil(B/nctx), ...)
+ * in its own host thread (the multi-GPU form of VerifierChip::verify_proof
+ * over many proofs, src/verifier.rs:227-285).  challenges == NULL replays
+ * the Blake2b transcript from vk_repr (as pm_accum_batch_transcript);
+ * otherwise the given challenges are used and vk_repr may be NULL.
+ * out_challenges, out_h_eval and out_status may be NULL. */
+int pm_accum_batch_multi(pm_ctx* const* ctxs, int nctx, int curve, const pm_proof_shape* shape, size_t B,
+                         const uint64_t* points, const uint64_t* scalars, const uint64_t* challenges,
+                         const uint64_t vk_repr[4], uint64_t* out_challenges, uint64_t* out_quads,
+                         uint64_t* out_h_eval, uint32_t* out_status);
 
 /* ---- Fixed-base MSM ----------------------------------------
  * The prover's commitments (Params::commit / commit_lagrange,
@@ -296,8 +321,11 @@ int pm_fft_device(pm_ctx* ctx, int curve, void* d_data, uint32_t log_n, const ui
  * out_status (may be NULL): B x uint32; bit 0 = an identity point was
  *   skipped (TranscriptChip::common_point rejects the identity before hashing,
  *   transcript.rs:101-110).  Such a proof's challenges differ from an honest
- *   prover's; the caller should reject it. */
+ *   prover's; the caller should reject it.  Bit 1 = that point was a lookup
+ *   product commitment Z (the reference aborts there, lookup.rs:100).  The
+ *   fused accumulator entries add PM_ACCUM_DENOM_ZERO (see pm_accum_batch). */
 #define PM_TRANSCRIPT_IDENTITY_SKIPPED 1u
+#define PM_TRANSCRIPT_LOOKUP_Z_IDENTITY 2u
 
 /* vk_repr = from_bytes_wide(Blake2b-512(personal "Halo2-Verify-Key",
  *   le_u64(len) || pinned[0..len))) in Montgomery form (verifier.rs:341-358).

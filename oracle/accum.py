@@ -354,6 +354,29 @@ def lookup_expressions(r, shape, lk, d, l_0, l_last, l_blind, theta, beta, gamma
     return [e1, e2, e3, e4, e5]
 
 
+STATUS_DENOM_ZERO = 4  # PM_ACCUM_DENOM_ZERO
+
+
+def proof_status(curve, shape, ch):
+    """Status bit of the scalar block: a zero denominator, i.e. x^n = 1 or
+    x = omega^-i for i < bf + 2 (both mean x is an n-th root of unity), where
+    the reference's main_gate.div fails (vanishing.rs:175, verifier.rs:580)."""
+    r = curve.r
+    x = ch[4] % r
+    xn = x
+    for _ in range(shape.log_n):
+        xn = xn * xn % r
+    if xn == 1:
+        return STATUS_DENOM_ZERO
+    omega_inv = pow(shape.omega, -1, r)
+    w = 1
+    for _ in range(2 + shape.blinding_factors):
+        if x == w:
+            return STATUS_DENOM_ZERO
+        w = w * omega_inv % r
+    return 0
+
+
 def scalar_block(curve, shape, d, ch):
     """verifier.rs:512-652 -> (expressions, xn, h_eval)."""
     r = curve.r

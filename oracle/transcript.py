@@ -13,8 +13,13 @@ What it restates:
     0x02 || s (canonical little-endian 32-byte reprs); squeeze = absorb 0x00,
     finalise a copy, read the digest as a little-endian 512-bit integer mod r
     (Challenge255 / from_bytes_wide).  TranscriptChip::common_point returns
-    early for the identity (C::from_xy(0, 0) fails, transcript.rs:101-110), so
-    the identity is never hashed.
+    Err(Error::Synthesis) for the identity (C::from_xy(0, 0) fails,
+    transcript.rs:101-110) before hashing, so the identity is never hashed.
+    Every call site drops that error (lookup.rs:72-73, vanishing.rs:71,98,
+    verifier.rs:362,375, permutation.rs:74) except the lookup product
+    commitment Z (lookup.rs:100 propagates it with `?`: the verifier circuit
+    aborts).  The replay reports both as status bits (STATUS_IDENTITY_SKIPPED,
+    STATUS_LOOKUP_Z_IDENTITY; include/pasta_msm.h).
   * ``vk_repr``            src/verifier.rs:341-358: BLAKE2b-512 with
     personalisation ``Halo2-Verify-Key`` over le_u64(len) || debug string,
     reduced with from_bytes_wide.
@@ -36,17 +41,21 @@ TRANSCRIPT_PERSONAL = b"Halo2-Transcript"
 VERIFY_KEY_PERSONAL = b"Halo2-Verify-Key"
 PREFIX_CHALLENGE, PREFIX_POINT, PREFIX_SCALAR = 0, 1, 2
 CHALLENGE_NAMES = ("theta", "beta", "gamma", "y", "x", "v", "u")
+STATUS_IDENTITY_SKIPPED = 1     # PM_TRANSCRIPT_IDENTITY_SKIPPED
+STATUS_LOOKUP_Z_IDENTITY = 2    # PM_TRANSCRIPT_LOOKUP_Z_IDENTITY
 
 
 class Blake2bTranscript:
     def __init__(self, r):
         self.r = r
         self.state = hashlib.blake2b(digest_size=64, person=TRANSCRIPT_PERSONAL)
-        self.skipped_identity = False
+        self.status = 0
 
-    def common_point(self, pt):
-        if pt is None:                      # transcript.rs:101-110
-            self.skipped_identity = True
+    def common_point(self, pt, lookup_z=False):
+        if pt is None:                      # transcript.rs:101-110: Err(Synthesis)
+            self.status |= STATUS_IDENTITY_SKIPPED
+            if lookup_z:                    # lookup.rs:100 propagates it
+                self.status |= STATUS_LOOKUP_Z_IDENTITY
             return
         x, y = pt
         self.state.update(bytes([PREFIX_POINT]) + x.to_bytes(32, "little") + y.to_bytes(32, "little"))
@@ -68,15 +77,15 @@ def vk_repr(r, pinned: bytes):
 
 
 def replay_challenges(curve, shape, pf, vkr):
-    """-> ([theta, beta, gamma, y, x, v, u], skipped_identity) for one proof in
-    the accumulator layout (oracle/accum.py docstring)."""
+    """-> ([theta, beta, gamma, y, x, v, u], status bits) for one proof in
+    the accumulator layout (oracle/accum.py docstring); status 0 = clean."""
     t = Blake2bTranscript(curve.r)
     po = shape.point_offsets()
 
     def pts(name):
         k, n = po[name]
         for q in pf.points[k:k + n]:
-            t.common_point(q)
+            t.common_point(q, lookup_z=(name == "lk_z"))
 
     t.common_scalar(vkr)                    # verifier.rs:341-358
     pts("inst")                             # :360-363
@@ -95,7 +104,7 @@ def replay_challenges(curve, shape, pf, vkr):
         t.common_scalar(s)
     v = t.squeeze_challenge()               # :718
     u = t.squeeze_challenge()               # :719
-    return [theta, beta, gamma, y, x, v, u], t.skipped_identity
+    return [theta, beta, gamma, y, x, v, u], t.status
 
 
 def with_replayed_challenges(curve, shape, proofs, vkr):

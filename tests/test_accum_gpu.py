@@ -113,3 +113,82 @@ def test_empty_batch_and_bad_shape(gpu_ctx):
         bad = U.to_product_shape(2, sh)
         gpu_ctx.accum_batch(bad, np.zeros((1, npts, 8), np.uint64), np.zeros((1, nsc, 4), np.uint64),
                             np.zeros((1, 7, 4), np.uint64))
+
+
+@pytest.mark.parametrize("cid", [2, 0])
+def test_zero_denominator_status(gpu_ctx, cid):
+    """x an n-th root of unity (x = 1, x = omega^-3; then x^n = 1 and a
+    Lagrange denominator x - omega^-i vanishes): the reference's
+    main_gate.div fails there (vanishing.rs:175, verifier.rs:580), so the
+    proof is flagged PM_ACCUM_DENOM_ZERO and the rest of the batch is
+    untouched (bit-exact vs the oracle)."""
+    C, sh, proofs = U.make_case(cid, "simple", 11, 5, 0xDE0 + cid)
+    w_inv = pow(sh.omega, -1, C.r)
+    proofs[1].challenges[4] = 1
+    proofs[3].challenges[4] = pow(w_inv, 3, C.r)
+    ps = U.to_product_shape(cid, sh)
+    pts, scs, chs = A.pack_proofs(C, sh, proofs)
+    quads, h, st = gpu_ctx.accum_batch_status(ps, pts, scs, chs)
+    want = [A.proof_status(C, sh, pf.challenges) for pf in proofs]
+    assert want == [0, A.STATUS_DENOM_ZERO, 0, A.STATUS_DENOM_ZERO, 0]
+    assert [int(x) for x in st] == want
+    for b in (0, 2, 4):
+        q, hh = A.pack_result(C, A.accumulate_msm(C, sh, proofs[b]))
+        assert np.array_equal(quads[b], q) and np.array_equal(h[b], hh), b
+    # the same through the fused transcript entry (x is then the replayed
+    # challenge, so only the status OR of the clean proofs is checked)
+    vk = np.array(A.to_limbs_mont(C.r, 77), dtype=np.uint64)
+    _, _, _, st2 = gpu_ctx.accum_batch_transcript(ps, pts, scs, vk)
+    assert not st2.any()
+
+
+def test_lookup_z_identity_status(gpu_ctx):
+    """An identity lookup-Z commitment: the reference aborts (lookup.rs:100
+    propagates common_point's error), status = IDENTITY_SKIPPED |
+    LOOKUP_Z_IDENTITY; an identity advice commitment only skips (status 1)."""
+    import transcript as T
+
+    C, sh, proofs = U.make_case(2, "rich", 10, 3, 0x12C)
+    po = sh.point_offsets()
+    proofs[0].points[po["lk_z"][0]] = None
+    proofs[2].points[po["adv"][0]] = None
+    ps = U.to_product_shape(2, sh)
+    vkr = T.vk_repr(C.r, b"lkz")
+    vk = np.array(A.to_limbs_mont(C.r, vkr), dtype=np.uint64)
+    pts, scs, _ = A.pack_proofs(C, sh, proofs)
+    _, _, ch, st = gpu_ctx.accum_batch_transcript(ps, pts, scs, vk)
+    want = [T.replay_challenges(C, sh, pf, vkr)[1] for pf in proofs]
+    assert want == [T.STATUS_IDENTITY_SKIPPED | T.STATUS_LOOKUP_Z_IDENTITY, 0, T.STATUS_IDENTITY_SKIPPED]
+    assert [int(x) for x in st] == want
+    ch2, st2 = gpu_ctx.transcript_batch(ps, pts, scs, vk)
+    assert np.array_equal(ch, ch2) and np.array_equal(st, st2)
+
+
+def test_accum_batch_multi(gpu_ctx):
+    """pm_accum_batch_multi shards the proofs over contexts (here: several
+    contexts on the one device of the box, ragged split) and equals the
+    single-context calls, with caller challenges and with the replay."""
+    import transcript as T
+
+    C, sh, proofs = U.make_case(2, "simple", 12, 11, 0x3417)
+    ps = U.to_product_shape(2, sh)
+    pts, scs, chs = A.pack_proofs(C, sh, proofs)
+    q1, h1, s1 = gpu_ctx.accum_batch_status(ps, pts, scs, chs)
+    vkr = T.vk_repr(C.r, b"multi")
+    vk = np.array(A.to_limbs_mont(C.r, vkr), dtype=np.uint64)
+    qt, ht, cht, stt = gpu_ctx.accum_batch_transcript(ps, pts, scs, vk)
+    extra = [H.Context(0) for _ in range(2)]
+    try:
+        for ctxs in ([gpu_ctx], [gpu_ctx] + extra, extra + [gpu_ctx, extra[0]]):
+            ch, q, h, st = H.accum_batch_multi(ctxs, ps, pts, scs, challenges=chs)
+            assert np.array_equal(q, q1) and np.array_equal(h, h1) and np.array_equal(st, s1)
+            assert np.array_equal(ch, chs)
+            ch, q, h, st = H.accum_batch_multi(ctxs, ps, pts, scs, vk_repr=vk)
+            assert np.array_equal(q, qt) and np.array_equal(h, ht) and np.array_equal(ch, cht)
+            assert np.array_equal(st, stt)
+    finally:
+        for c in extra:
+            c.close()
+    for b in (0, 10):
+        q, hh = A.pack_result(C, A.accumulate_msm(C, sh, proofs[b]))
+        assert np.array_equal(q1[b], q) and np.array_equal(h1[b], hh)
