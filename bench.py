@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--accum-logn", type=int, default=17)
     ap.add_argument("--logn22", type=int, default=1,
                     help="also time the 2^22 Pallas MSM per GPU (north-star size, weak scaling) (1) or skip it (0)")
+    ap.add_argument("--fixed23", type=int, default=1,
+                    help="also time the fixed-base MSM at 2^23 per GPU (the outer prover's k = 23 commit) (1) or skip (0)")
     ap.add_argument("--strong-logn", type=int, default=22,
                     help="strong-scaling leg: a fixed 2^k Vesta MSM split over the ranks (SURVEY config 4); 0 = skip")
     ap.add_argument("--dry-run", action="store_true",
@@ -156,7 +158,7 @@ def main():
     import torch
 
     import halo2_amd as H
-    from sharded import shard_range, split_range
+    from sharded import combine_partials, shard_range, split_range
 
     torch.cuda.set_device(local)
     dist = None
@@ -201,6 +203,21 @@ def main():
                              n_total=nt, check_port=(rank == 0 and world == 1 and not args.no_cpu))
         for k in ("_d_s", "_d_b", "_result"):
             strong.pop(k)
+    fixed23 = None
+    if args.fixed and args.fixed23:
+        # the outer prover's commit size (k = 23, examples/simple-example.rs:663,702):
+        # 2^23 Pallas pairs per GPU against a 2^23 table (auto c = 20, ~7 GB)
+        n23 = 1 << 23
+        i23 = shard_range(rank, world, n23)[0]
+        s23 = torch.empty((n23, 4), dtype=torch.int64, device=dev)
+        b23 = torch.empty((n23, 8), dtype=torch.int64, device=dev)
+        ctx.synth_scalars(curve, SEED_SCALARS, i23, n23, s23.data_ptr())
+        ctx.synth_bases(curve, SEED_BASES, i23, n23, b23.data_ptr())
+        torch.cuda.synchronize()
+        want23 = combine_partials(ctx.msm_device(curve, s23.data_ptr(), b23.data_ptr(), n23), dist, dev, padd,
+                                  world, gathered)
+        fixed23 = run_fixed_base(args, ctx, dist, dev, world, s23, b23, n23, gathered, padd, want23, lg=23)
+        del s23, b23
     torch.cuda.empty_cache()
     ntt = run_ntt(args, ctx, dist, dev, world) if args.ntt_logn > 0 else None
     accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
@@ -226,6 +243,8 @@ def main():
             out["strong_vesta"] = strong
         if fixed is not None:
             out["fixed_base"] = fixed
+        if fixed23 is not None:
+            out["fixed_base_2^23"] = fixed23
         if ntt is not None:
             if world == 1 and not args.no_cpu:
                 ntt["cpu_baseline"] = ntt_cpu_baseline(*ntt.pop("_state"), budget_s=6.0)
@@ -433,7 +452,7 @@ def kernel_breakdown(ctx, step, names, reps=5):
     return {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in names}
 
 
-def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, want):
+def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, want, lg=None):
     """Fixed-base MSM over the same scalars and bases: the
     SRS table [2^{o_w}] P_i is built once (untimed, reported as build_ms),
     then each step is pm_msm_fixed_device + the same all-gather / fold."""
@@ -468,7 +487,8 @@ def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, wan
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    out = {"metric": f"Pallas fixed-base MSM Mscalar/s at 2^{args.logn} (precomputed SRS table)",
+    lg = lg or args.logn
+    out = {"metric": f"Pallas fixed-base MSM Mscalar/s at 2^{lg} (precomputed SRS table)",
            "value": round(world * n / (elapsed / args.steps) / 1e6, 3), "unit": "Mscalar/s",
            "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "c": fb.c, "windows": fb.windows,
            "table_GiB_per_gpu": round(fb.table_bytes / 2**30, 3), "build_ms": round(build_ms, 2),

@@ -51,6 +51,22 @@ __global__ void k_madd(uint32_t* out, int iters) {
   }
 }
 
+// field inversion throughput (binary GCD, f29_inv): the cost a batch-affine
+// bucket accumulation would amortise over the independent additions of a batch
+__global__ void k_inv(uint32_t* out, int iters) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  F29<F> a;
+  for (int i = 0; i < 9; i++) a.l[i] = (t * 7 + i * 977 + 1) & kM29;
+  a.l[8] &= 0x3fffff;
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int k = 0; k < iters; k++) {
+    a = f29_inv<F>(a);
+    a.l[0] += 1;  // keep it nonzero and varying
+  }
+#endif
+  for (int i = 0; i < 8; i++) out[8 * t + i] = a.l[i];
+}
+
 template <class Kern>
 void run(const char* name, Kern k, void* buf, int iters, double ops_per_iter) {
   hipEvent_t e0, e1;
@@ -81,5 +97,6 @@ int main() {
   run("f29_sqr_c", k_mul<5>, buf, 1024, 1);
   run("xyzz_madd_32", k_madd<0>, buf, 128, 1);
   run("xyzz_madd_29", k_madd<1>, buf, 128, 1);
+  run("f29_inv_bgcd", k_inv, buf, 16, 1);
   return 0;
 }
