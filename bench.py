@@ -413,6 +413,16 @@ def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
                       "scalar_h2d_ms": round(h2d, 4), "scalar_h2d_GBps": round(32 * n / (h2d * 1e-3) / 1e9, 2),
                       "matches": bool(np.array_equal(np.asarray(got), np.asarray(want)))}
     ctx.set_h2d_threads(0)
+    # the prover's commit of many polynomials: K MSMs per call
+    # (pm_msm_resident_batch), the scalar copy of MSM j+1 and the host tail of
+    # MSM j-1 overlapping MSM j's kernels
+    K = 8
+    lists = [S] + [np.roll(S, 1 + j, axis=0) for j in range(K - 1)]
+    el, got = timed_steps(lambda: ctx.msm_resident_batch(rb, 0, lists), max(2, args.steps // 8), 1, None, dev)
+    steps = max(2, args.steps // 8)
+    res["batch_8_pipelined"] = {"ms_per_msm": round(el * 1e3 / steps / K, 4),
+                                "Mscalar_s": round(K * n / (el / steps) / 1e6, 3),
+                                "matches": bool(np.array_equal(np.asarray(got[0]), np.asarray(want)))}
     return res
 
 

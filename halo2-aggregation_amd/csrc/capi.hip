@@ -66,6 +66,9 @@ pm_ctx::~pm_ctx() {
   }
   for (auto& e : ev_pool) (void)hipEventDestroy(e);
   for (auto& e : grp_ev) (void)hipEventDestroy(e);
+  for (auto& e : batch_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (copy_stream) (void)hipStreamDestroy(copy_stream);
   if (red_stream) (void)hipStreamDestroy(red_stream);
   if (own_stream) (void)hipStreamDestroy(own_stream);
 }
@@ -344,6 +347,8 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_GLV")) c->glv = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("PM_FINE_CACHE")) c->fine_cache = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("PM_H2D_THREADS")) c->h2d_threads = std::max(0, std::min(kMaxStageThreads, std::atoi(e)));
   if (const char* e = std::getenv("PM_SORT_PPT")) {
     const int v = std::atoi(e);
@@ -577,6 +582,20 @@ int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_
 int pm_msm_resident_device(pm_ctx* ctx, const pm_bases* b, size_t offset, const void* d_scalars, size_t n,
                            uint32_t flags, uint64_t out[8]) {
   return msm_resident(ctx, b, offset, d_scalars, false, n, flags, out);
+}
+
+int pm_msm_resident_batch(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* const* scalars, size_t k,
+                          size_t n, uint32_t flags, uint64_t* out) {
+  if (!ctx || !b || (k && (!scalars || !out))) return set_error(PM_ERR_ARG, "null argument");
+  for (size_t j = 0; j < k && n; j++)
+    if (!scalars[j]) return set_error(PM_ERR_ARG, "null scalar array");
+  if (b->device != ctx->device) return set_error(PM_ERR_ARG, "bases live on another device");
+  if (offset > b->n || n > b->n - offset) return set_error(PM_ERR_ARG, "window exceeds resident bases");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return curve_ops(b->curve)->msm_resident_batch(ctx, (const char*)b->d + offset * 64, scalars, k, n,
+                                                 flags & ~kBasesR261, out);
 }
 
 int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads) {

@@ -120,13 +120,34 @@ constexpr int kGlvMinC = 12;  // below: the plain 256-bit pipeline (small n)
 // entries as a single window (merged histogram rows), and the bucket
 // reduction and host tail handle one window at offset 0 -- no per-window
 // reduction and no cross-window doublings.
+// What the host Horner tail of one enqueued MSM needs (msm_tail): the plan's
+// window geometry, the pinned slot its bit sums land in and its events.
+template <class F>
+struct MsmTail {
+  int G = 0, Wr = 0, NQ = 0, wpg = 1, base = 0, extra = 0, log2L1 = 0;
+  bool fixed = false, empty = true;
+  const Xyzz<F>* hG = nullptr;  // pinned host slot
+  std::vector<hipEvent_t> ev;    // 2 per window group
+  hipStream_t st = nullptr, st2 = nullptr;
+};
+
+template <class F>
+int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result);
+
+// Enqueue the device pipeline of one MSM (everything up to the D2H copy of
+// the folded bit sums into pinned slot `slot`) and describe its host tail in
+// *tail; msm_tail then waits for it and runs the Horner.  Two MSMs can be in
+// flight (slots 0 and 1): the tail of one overlaps the kernels of the next
+// (pm_msm_resident_batch).  tail == nullptr: run the tail here.
 template <class Cv>
 int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases, size_t n, uint32_t flags,
-                    Xyzz<typename Cv::Base>* result, const pm_fixed_bases* ft = nullptr) {
+                    Xyzz<typename Cv::Base>* result, const pm_fixed_bases* ft = nullptr,
+                    MsmTail<typename Cv::Base>* tail = nullptr, int slot = 0) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   if (n == 0) {
-    *result = xyzz_inf<F>();
+    if (tail) *tail = MsmTail<F>{};
+    else *result = xyzz_inf<F>();
     return PM_OK;
   }
   if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "n exceeds 2^26 points per device call");
@@ -154,6 +175,10 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const int NQ = (pl.NB2 + kBitsFold - 1) / kBitsFold + 1;  // folded terms per window (host Horner)
   SortGeom g{};  // histogram geometry (blocks of scalars)
   g.FB = std::max(0, pl.cmax - 1 - 8);
+  // the fixed-base MSM's merged sort rows are W x longer: 4x more coarse bins
+  // once they exceed 2^24 entries (2^23, c = 20: FB 11 -> 9, sort 3.4 -> 2.3 ms)
+  if (fixed && (size_t)pl.W * ft->npad > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
+  if (ctx->sort_fb > 0) g.FB = std::min(pl.cmax - 1, ctx->sort_fb);  // PM_SORT_FB: tuning experiments
   g.NCB = (pl.K >> g.FB) + 1;
   // points per thread: blocks of 1024 threads x ppt points, ppt the largest
   // power of two <= 8 that still gives >= 128 blocks (2^20: 8192 points per
@@ -189,8 +214,10 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->bitsQ.ensure((size_t)Wr * NQ * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->longs.ensure((size_t)pl.G * longs_stride))) return rc;
   const size_t nG = (size_t)Wr * NJ;
-  if ((rc = ctx->ensure_pinned(nG * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->ensure_group_events(2 * pl.G))) return rc;
+  if ((rc = ctx->ensure_pinned(2 * nG * sizeof(Xyzz<F>)))) return rc;  // two slots (batch pipelining)
+  if ((rc = ctx->ensure_group_events(4 * pl.G))) return rc;
+  Xyzz<F>* hslot = (Xyzz<F>*)ctx->h_pinned + (size_t)slot * nG;
+  hipEvent_t* gev = ctx->grp_ev.data() + (size_t)2 * pl.G * slot;
 
   uint32_t* sorted = (uint32_t*)ctx->sorted.p;
   void* mid = ctx->mid.p;
@@ -259,8 +286,18 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // evenly; a skewed segment falls back to re-reading mid), capped at 64 KiB
   const size_t esz = wide ? 8 : 4;
   const size_t mean_seg = E / std::max(1, g.NCB - 1) + 1;
-  const uint32_t cache_n = (uint32_t)std::min<size_t>(kFineCacheBytes / esz, (mean_seg * 3 / 2 + 63) & ~size_t(63));
-  const size_t lds_fine = (size_t)cache_n * (esz + 4) + ((size_t)(1 << g.FB) + kFineThreads / 64 + 1) * 4;
+  // A mean segment that fits 24 KiB is cached whole (1.5x its size); larger
+  // ones go through the chunked path in 16 KiB chunks, which keeps 3 blocks
+  // per CU instead of one (2^22: sort_fine 0.48 -> 0.27 ms, fixed-base 2^23:
+  // 2.5 -> 1.06 ms; profiles/r02/sort/fb_sweep.jsonl)
+  size_t cache_cap = (mean_seg * 3 / 2 + 63) & ~size_t(63);
+  if (cache_cap > kFineCacheSmall / esz) cache_cap = kFineChunkBytes / esz;
+  if (ctx->fine_cache > 0) cache_cap = (size_t)ctx->fine_cache;  // PM_FINE_CACHE: tuning experiments
+  uint32_t cache_n = (uint32_t)std::min<size_t>(cache_cap, kFineCacheBytes / esz);
+  const size_t fine_fixed = ((size_t)3 * (1 << g.FB) + kFineThreads / 64 + 1) * 4;  // hist, lcur, lst, scan
+  if (fine_fixed + 64 * (esz + 4) > kMaxLds) return set_error(PM_ERR_UNSUPPORTED, "sort: fine bits too wide");
+  while (cache_n > 64 && (size_t)cache_n * (esz + 4) + fine_fixed > kMaxLds) cache_n /= 2;
+  const size_t lds_fine = (size_t)cache_n * (esz + 4) + fine_fixed;
   if (wide)
     PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<true><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
                                     (const uint64_t*)mid, bofs, gm, Wr, pl.NB, cache_n, offsets, sorted)));
@@ -301,8 +338,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
                 (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg,
                                                                   pl.nthreads, fixed ? nullptr : longs, nlong, shorts, nshort)));
     if (st2 != st) {
-      HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi], st));
-      HIP_TRY(hipStreamWaitEvent(st2, ctx->grp_ev[2 * gi], 0));
+      HIP_TRY(hipEventRecord(gev[2 * gi], st));
+      HIP_TRY(hipStreamWaitEvent(st2, gev[2 * gi], 0));
     }
     PM_LAUNCH_ST(ctx, st2, "fixup", {
       if (fixed)  // merged buckets span ~W*n/2^(c-1)/chunk slices each: one lane per bucket
@@ -320,14 +357,50 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
                                                                                       bitsP, tickets)));
     PM_LAUNCH_ST(ctx, st2, "bits_combine",
                  (k_bits_combine<F><<<(4 * nw * NQ + 63) / 64, 64, 0, st2>>>(G, w0, nw, pl.NB2, Qb)));
-    HIP_TRY(hipMemcpyAsync((Xyzz<F>*)ctx->h_pinned + (size_t)w0 * NQ, Qb + (size_t)w0 * NQ,
+    HIP_TRY(hipMemcpyAsync(hslot + (size_t)w0 * NQ, Qb + (size_t)w0 * NQ,
                            (size_t)nw * NQ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st2));
-    HIP_TRY(hipEventRecord(ctx->grp_ev[2 * gi + 1], st2));
+    HIP_TRY(hipEventRecord(gev[2 * gi + 1], st2));
   }
+  MsmTail<F> t;
+  t.G = pl.G;
+  t.Wr = Wr;
+  t.NQ = NQ;
+  t.wpg = wpg;
+  t.base = pl.base;
+  t.extra = pl.extra;
+  t.log2L1 = pl.log2L1;
+  t.fixed = fixed;
+  t.empty = false;
+  t.hG = hslot;
+  t.ev.assign(gev, gev + 2 * pl.G);
+  t.st = st;
+  t.st2 = st2;
+  if (tail) {
+    *tail = t;
+    return PM_OK;
+  }
+  if ((rc = msm_tail<F>(ctx, t, result))) return rc;
+  HIP_TRY(hipStreamSynchronize(st2));
+  HIP_TRY(hipStreamSynchronize(st));
+  ctx->end_call();
+  return PM_OK;
+}
 
-  // Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b}) as one
-  // Horner over absolute bit positions q (host_ec.hpp), consumed group by group.
-  const Xyzz<F>* hG = (const Xyzz<F>*)ctx->h_pinned;
+// Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b}) as one
+// Horner over absolute bit positions q (host_ec.hpp), consumed group by group.
+template <class F>
+int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
+  if (t.empty) {
+    *result = xyzz_inf<F>();
+    return PM_OK;
+  }
+  const int Wr = t.Wr, NQ = t.NQ, wpg = t.wpg;
+  const bool fixed = t.fixed;
+  struct {
+    int G, base, extra, log2L1;
+  } pl{t.G, t.base, t.extra, t.log2L1};
+  const hipStream_t st = t.st, st2 = t.st2;
+  const Xyzz<F>* hG = t.hG;
   // the terms as (position, index) sorted by descending position: one flat
   // array (the former vector per position cost ~270 allocations per call)
   std::vector<std::pair<int, int>> terms;
@@ -349,7 +422,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   size_t ti = 0;
   double tail_ms = 0.0;
   for (int gi = pl.G - 1; gi >= 0; gi--) {
-    HIP_TRY(hipEventSynchronize(ctx->grp_ev[2 * gi + 1]));
+    HIP_TRY(hipEventSynchronize(t.ev[2 * gi + 1]));
     const auto t0 = std::chrono::steady_clock::now();
     int low = 0;  // positions above every lower group's terms are final now
     for (int gj = 0; gj < gi; gj++) low = std::max(low, gmax[gj] + 1);
@@ -365,9 +438,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     stt.first += 1;
     stt.second += tail_ms;
   }
-  HIP_TRY(hipStreamSynchronize(st2));
-  HIP_TRY(hipStreamSynchronize(st));
-  ctx->end_call();
+  (void)st;
+  (void)st2;
   *result = host::to_dev<F>(hacc);
   return PM_OK;
 }
@@ -398,6 +470,72 @@ int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint
   int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, (const uint32_t*)d_b, n, flags, &r);
   if (rc) return rc;
   aff_to_u64<F>(xyzz_to_aff<F>(r), out);
+  return PM_OK;
+}
+
+// pm_msm_resident_batch: k MSMs of n host scalars each against resident
+// bases (halo2's commit of many polynomials against params.g).  Scalars of
+// MSM j+1 are copied on the context's copy stream into the second device
+// buffer while MSM j's kernels run, and the host Horner of MSM j-1 runs
+// while the GPU works on MSM j: in steady state the GPU never waits for
+// PCIe or for the host.
+template <class Cv>
+int msm_resident_batch_impl(Ctx* ctx, const void* d_bases29, const uint64_t* const* scalars, size_t k, size_t n,
+                            uint32_t flags, uint64_t* out) {
+  using F = typename Cv::Base;
+  if (k == 0) return PM_OK;
+  if (n == 0) {
+    std::memset(out, 0, k * 64);
+    return PM_OK;
+  }
+  int rc;
+  if ((rc = ctx->in_scalars.ensure(n * 32)) || (rc = ctx->in_scalars2.ensure(n * 32))) return rc;
+  if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  for (int i = 0; i < 4; i++)
+    if (!ctx->batch_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ctx->batch_ev[i], hipEventDisableTiming));
+  hipEvent_t* copied = ctx->batch_ev;      // [slot]: scalars of the slot's MSM are on the device
+  hipEvent_t* consumed = ctx->batch_ev + 2;  // [slot]: the slot's MSM no longer reads its buffer
+  void* dbuf[2] = {ctx->in_scalars.p, ctx->in_scalars2.p};
+  const hipStream_t st = ctx->stream, cs = ctx->copy_stream;
+  auto copy = [&](size_t j) -> int {
+    const int sl = (int)(j & 1);
+    if (j >= 2) HIP_TRY(hipStreamWaitEvent(cs, consumed[sl], 0));
+    HIP_TRY(hipMemcpyAsync(dbuf[sl], scalars[j], n * 32, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipEventRecord(copied[sl], cs));
+    return PM_OK;
+  };
+  MsmTail<F> tails[2];
+  const bool overlap = ctx->groups <= 1;
+  size_t tailed = 0;
+  if ((rc = copy(0))) return rc;
+  for (size_t j = 0; j < k; j++) {
+    const int sl = (int)(j & 1);
+    HIP_TRY(hipStreamWaitEvent(st, copied[sl], 0));
+    if ((rc = msm_device_impl<Cv>(ctx, (const uint32_t*)dbuf[sl], (const uint32_t*)d_bases29, n,
+                                  flags | kBasesR261, nullptr, nullptr, &tails[sl], sl)))
+      return rc;
+    HIP_TRY(hipEventRecord(consumed[sl], st));
+    if (j + 1 < k && (rc = copy(j + 1))) return rc;
+    // with window groups (pm_ctx_set_pipeline) the reduction runs on the
+    // second stream and would race the next MSM's kernels over the shared
+    // workspace: no overlap then, each tail completes before the next MSM
+    const size_t done = overlap ? j : j + 1;  // MSMs whose tail can run now
+    for (; tailed < done; tailed++) {
+      Xyzz<F> r;
+      if ((rc = msm_tail<F>(ctx, tails[tailed & 1], &r))) return rc;
+      if (!overlap) HIP_TRY(hipStreamSynchronize(ctx->red_stream));
+      aff_to_u64<F>(xyzz_to_aff<F>(r), out + 8 * tailed);
+    }
+  }
+  for (; tailed < k; tailed++) {
+    Xyzz<F> r;
+    if ((rc = msm_tail<F>(ctx, tails[tailed & 1], &r))) return rc;
+    aff_to_u64<F>(xyzz_to_aff<F>(r), out + 8 * tailed);
+  }
+  HIP_TRY(hipStreamSynchronize(cs));
+  HIP_TRY(hipStreamSynchronize(ctx->red_stream));
+  HIP_TRY(hipStreamSynchronize(st));
+  ctx->end_call();
   return PM_OK;
 }
 

@@ -125,12 +125,16 @@ struct pm_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t red_stream = nullptr;  // bucket reduction of window group g overlaps accumulation of g-1
+  hipStream_t copy_stream = nullptr; // H2D of the next MSM's scalars (pm_msm_resident_batch)
+  hipEvent_t batch_ev[4] = {};       // batch pipelining: copied[2], consumed[2]
   std::vector<hipEvent_t> grp_ev;    // 2 per window group (accumulated, reduced+copied)
   int window_c = 0;
   int prefetch = -1;  // -1 auto, 0 off, 1 on (diagnostics: PM_PREFETCH env)
   int groups = 0;     // window groups, 0 = auto (diagnostics: PM_GROUPS env)
   int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
   int sort_ppt = 0;   // sort points per thread, 0 = auto (diagnostics: PM_SORT_PPT env, 1/2/4/8)
+  int sort_fb = 0;    // fine bits of the two-level sort, 0 = auto (diagnostics: PM_SORT_FB env)
+  int fine_cache = 0; // entries of the fine pass's LDS segment cache, 0 = auto (diagnostics: PM_FINE_CACHE env)
   int glv = 0;        // variable-base MSM in GLV mode (pm_ctx_set_glv, PM_GLV env): measured slower, off
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;
@@ -138,7 +142,7 @@ struct pm_ctx {
   bool timed(const char* name) const { return timing && (timing_filter.empty() || timing_filter == name); }
   std::mutex mu;
   // workspace
-  pm::Buf in_scalars, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
+  pm::Buf in_scalars, in_scalars2, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
       win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, tr_canon;
   pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
   std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
@@ -161,7 +165,7 @@ struct pm_ctx {
   std::map<std::string, std::pair<uint64_t, double>> stats;
 
   std::vector<pm::Buf*> all_bufs() {
-    return {&in_scalars, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
+    return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
             &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon};
   }
@@ -204,6 +208,9 @@ struct CurveOps {
                    uint64_t out[8]);
   // resident bases: Rust-layout affine (R = 2^256) -> the pipeline's R = 2^261 canonical form
   int (*bases_to29)(Ctx* ctx, const void* d_in, size_t n, void* d_out);
+  // k MSMs of n host scalars against resident (R = 2^261) bases, pipelined
+  int (*msm_resident_batch)(Ctx* ctx, const void* d_bases29, const uint64_t* const* scalars, size_t k, size_t n,
+                            uint32_t flags, uint64_t* out);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

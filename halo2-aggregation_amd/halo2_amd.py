@@ -224,6 +224,8 @@ def _load():
         "pm_msm_resident_device": ([_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_uint32, _u64p],
                                    ctypes.c_int),
         "pm_ctx_set_h2d_threads": ([_vp, ctypes.c_int], ctypes.c_int),
+        "pm_msm_resident_batch": ([_vp, _vp, ctypes.c_size_t, ctypes.POINTER(_u64p), ctypes.c_size_t,
+                                   ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_msm_resident": ([_vp, _vp, ctypes.c_size_t, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p],
                             ctypes.c_int),
         "pm_point_add": ([ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
@@ -507,6 +509,19 @@ class Context:
         out = np.zeros(8, dtype=np.uint64)
         _check(lib().pm_msm_resident_device(self.h, bases.h, offset, _vp(d_scalars), n,
                                             SCALARS_CANONICAL if canonical else 0, _p(out)))
+        return out
+
+    def msm_resident_batch(self, bases: Bases, offset, coeff_list, canonical=False):
+        """pm_msm_resident_batch: one MSM per host scalar array (all of the
+        same length) against resident bases; returns (k, 8) u64."""
+        arrs = [_as_u64(c, 4) for c in coeff_list]
+        n = arrs[0].shape[0] if arrs else 0
+        if any(a.shape[0] != n for a in arrs):
+            raise ValueError("all scalar arrays of a batch must have the same length")
+        ptrs = (_u64p * len(arrs))(*[_p(a) for a in arrs])
+        out = np.zeros((len(arrs), 8), dtype=np.uint64)
+        _check(lib().pm_msm_resident_batch(self.h, bases.h, offset, ptrs, len(arrs), n,
+                                           SCALARS_CANONICAL if canonical else 0, _p(out)))
         return out
 
     def set_h2d_threads(self, threads):

@@ -132,6 +132,14 @@ int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_
                     size_t n, uint32_t flags, uint64_t out[8]);
 int pm_msm_resident_device(pm_ctx* ctx, const pm_bases* b, size_t offset, const void* d_scalars,
                            size_t n, uint32_t flags, uint64_t out[8]);
+/* k MSMs over the same window of resident bases, one per host scalar array
+ * (scalars[j]: n x 4 u64), out: k x 8 u64 -- the prover's commit of many
+ * polynomials against params.g / g_lagrange (create_proof,
+ * examples/simple-example.rs:606,702).  Pipelined: the H2D copy of MSM j+1's
+ * scalars overlaps MSM j's kernels on a second stream, and MSM j-1's host
+ * tail overlaps them too.  Same results as k pm_msm_resident calls. */
+int pm_msm_resident_batch(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* const* scalars,
+                          size_t k, size_t n, uint32_t flags, uint64_t* out);
 /* Host inputs of pm_msm / pm_msm_ctx / pm_msm_resident / pm_msm_fixed /
  * pm_bases_upload: threads = 0 (default) copies them with one pageable
  * hipMemcpyAsync; 1..8 stages them in 4 MiB chunks through pinned buffers,

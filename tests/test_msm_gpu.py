@@ -239,3 +239,42 @@ def test_h2d_threads_argument_checked(gpu_ctx):
         gpu_ctx.set_h2d_threads(9)
     with pytest.raises(H.PmError):
         gpu_ctx.set_h2d_threads(-1)
+
+
+@pytest.mark.parametrize("k,groups", [(1, 0), (2, 0), (5, 0), (3, 2)])
+def test_resident_batch(gpu_ctx, k, groups):
+    """pm_msm_resident_batch (copies of MSM j+1 and the host tail of MSM j-1
+    overlapping MSM j's kernels) == k single pm_msm_resident calls, also with
+    window groups (no overlap then), canonical scalars and an offset window."""
+    import torch
+
+    n = (1 << 16) + 7
+    s, b = _torch_inputs(gpu_ctx, 0, n + 100)
+    B = b.cpu().numpy().view(np.uint64)
+    rb = gpu_ctx.upload_bases(0, B)
+    gpu_ctx.set_pipeline(groups, 0)
+    try:
+        lists = []
+        for j in range(k):
+            sj = torch.empty((n, 4), dtype=torch.int64, device=s.device)
+            gpu_ctx.synth_scalars(0, 0x5EED + 17 * j, 0, n, sj.data_ptr())
+            torch.cuda.synchronize()
+            lists.append(sj.cpu().numpy().view(np.uint64).copy())
+        got = gpu_ctx.msm_resident_batch(rb, 50, lists)
+        for j in range(k):
+            assert np.array_equal(got[j], gpu_ctx.msm_resident(rb, 50, lists[j])), j
+        assert np.array_equal(got[0], msm_ref.best_multiexp(0, lists[0], B[50:50 + n]))
+        C = P.PALLAS
+        rinv = pow(P.R_MONT, -1, C.r)
+        canon = [np.array([P.to_limbs(P.from_limbs([int(x) for x in row]) * rinv % C.r) for row in L[:300]],
+                          dtype=np.uint64) for L in lists[:2]]
+        got_c = gpu_ctx.msm_resident_batch(rb, 0, canon, canonical=True)
+        for j in range(len(canon)):
+            assert np.array_equal(got_c[j], gpu_ctx.msm_resident(rb, 0, lists[j][:300])), j
+        with pytest.raises(ValueError):
+            gpu_ctx.msm_resident_batch(rb, 0, [lists[0], lists[0][:5]])
+        with pytest.raises(H.PmError):
+            gpu_ctx.msm_resident_batch(rb, 200, lists[:1])   # window past the resident bases
+    finally:
+        gpu_ctx.set_pipeline(0, 0)
+        rb.release()
