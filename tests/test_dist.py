@@ -166,3 +166,36 @@ def test_bench_world_mismatch_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env, cwd="/tmp")
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_accum_multi_shard_math_cpu():
+    """pm_accum_batch_multi's split (context k takes [k*ceil(B/n), ...), the
+    same ranges as sharded.split_range) on a ragged batch: running the C
+    accumulator port (oracle/accum_ref.c) per range and concatenating equals
+    the whole batch, challenges, quads, h_eval and status included."""
+    import sys
+
+    for p in (os.path.join(ROOT, "halo2-aggregation_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import accum as A
+    import accum_ref as R
+    import accum_util as U
+    from sharded import split_range
+
+    C, sh, proofs = U.make_case(2, "simple", 10, 7, 0xA77)
+    ps = U.to_product_shape(2, sh)
+    pts, scs, _ = A.pack_proofs(C, sh, proofs)
+    vk = np.array(A.to_limbs_mont(C.r, 99), dtype=np.uint64)
+    whole = R.accum_batch(2, ps.c, pts, scs, vk_repr=vk, threads=2)
+    for nctx in (1, 2, 3, 4, 8):
+        parts = [split_range(k, nctx, 7) for k in range(nctx)]
+        got = [[], [], [], []]
+        for lo, cnt in parts:
+            if cnt == 0:
+                continue
+            out = R.accum_batch(2, ps.c, pts[lo:lo + cnt], scs[lo:lo + cnt], vk_repr=vk, threads=1)
+            for i in range(4):
+                got[i].append(out[i])
+        for i in range(4):
+            assert np.array_equal(np.concatenate(got[i]), whole[i]), (nctx, i)
