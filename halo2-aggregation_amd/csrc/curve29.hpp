@@ -74,8 +74,9 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_dbl_impl(const F29<F>& X, const F29<
   const F29<F> M = f29_norm<F>(f29_add<F>(f29_add<F>(XX, XX), XX));  // < 6p
   Xyzz29<F> r;
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(M), f29_add<F>(S, S), K::K8x3)));  // < 3p
-  const F29<F> D = f29_sub<F>(S, r.X, K::K6);                  // loose, < 8p
-  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_mul_c<F>(M, D), f29_mul_c<F>(W, Y), K::K6)));
+  const F29<F> D = f29_norm<F>(f29_sub<F>(S, r.X, K::K6));     // < 8p
+  const F29<F> nW = f29_norm<F>(f29_sub<F>(f29_zero<F>(), W, K::K2));  // -W, < 2p
+  r.Y = f29_mul2_c<F>(M, D, nW, Y);                              // M D - W Y: 48p^2 + 8p^2, < 2p
   r.ZZ = AFF ? V : f29_mul_c<F>(V, ZZ);
   r.ZZZ = AFF ? W : f29_mul_c<F>(W, ZZZ);
   return r;
@@ -149,8 +150,9 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_madd(const Xyzz29<F>& acc, const F29
   const F29<F> Q = f29_mul_c<F>(acc.X, PP);
   Xyzz29<F> r;
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
-  const F29<F> D = f29_sub<F>(Q, r.X, K::K6);                  // loose limbs < 2^31, < 8p
-  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_mul_c<F>(R, D), f29_mul_c<F>(acc.Y, PPP), K::K6)));
+  const F29<F> D = f29_norm<F>(f29_sub<F>(Q, r.X, K::K6));     // < 8p
+  const F29<F> nY = f29_norm<F>(f29_sub<F>(f29_zero<F>(), acc.Y, K::K6));  // -Y1, < 6p
+  r.Y = f29_mul2_c<F>(R, D, nY, PPP);                            // R D - Y1 PPP: 64p^2 + 12p^2, < 2p
   r.ZZ = f29_mul_c<F>(acc.ZZ, PP);
   r.ZZZ = f29_mul_c<F>(acc.ZZZ, PPP);
   return r;
@@ -178,8 +180,9 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_add(const Xyzz29<F>& p, const Xyzz29
   const F29<F> Q = f29_mul_c<F>(U1, PP);
   Xyzz29<F> r;
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
-  const F29<F> D = f29_sub<F>(Q, r.X, K::K6);
-  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_mul_c<F>(R, D), f29_mul_c<F>(S1, PPP), K::K6)));
+  const F29<F> D = f29_norm<F>(f29_sub<F>(Q, r.X, K::K6));     // < 8p
+  const F29<F> nS1 = f29_norm<F>(f29_sub<F>(f29_zero<F>(), S1, K::K2));  // -S1, < 2p
+  r.Y = f29_mul2_c<F>(R, D, nS1, PPP);                           // 64p^2 + 4p^2, < 2p
   r.ZZ = f29_mul_c<F>(f29_mul_c<F>(p.ZZ, q.ZZ), PP);
   r.ZZZ = f29_mul_c<F>(f29_mul_c<F>(p.ZZZ, q.ZZZ), PPP);
   return r;

@@ -301,8 +301,20 @@ __device__ F29<P> f29_mul_a(const F29<P>& a, const F29<P>& b);
 template <class P>
 __device__ F29<P> f29_sqr_a(const F29<P>& a);
 template <class P>
+__device__ F29<P> f29_mul2_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, const F29<P>& v);
+template <class P>
 __device__ __forceinline__ F29<P> f29_mul_c(const F29<P>& a, const F29<P>& b) {
   return f29_mul_a<P>(a, b);
+}
+// Sum of two products with one Montgomery reduction: (a b + u v) 2^-261.
+// All four operands Norm (limbs < 2^29: a column holds 18 operand products +
+// 6 reduction products < 2^58, < 2^63) and a b + u v < 2^261 p / 1.7 (e.g.
+// a, b < 8p, u < 6p, v < 2p: 76 p^2) -> Norm, < 2p.  Saves a whole reduction
+// (54 multiply-adds on Pasta) and the subtract / normalise / reduce3 of the
+// difference form a b - u' v.
+template <class P>
+__device__ __forceinline__ F29<P> f29_mul2_c(const F29<P>& a, const F29<P>& b, const F29<P>& u, const F29<P>& v) {
+  return f29_mul2_a<P>(a, b, u, v);
 }
 template <class P>
 __device__ __forceinline__ F29<P> f29_sqr_c(const F29<P>& a) {

@@ -24,13 +24,14 @@ FIELDS = {"PallasFp": P.PALLAS_P, "VestaFp": P.VESTA_P, "Bn254Fq": P.BN254_P, "B
 def _functions():
     src = open(HDR).read()
     out = {}
-    for m in re.finditer(r"F29<(\w+)> (f29_(?:mul|sqr)_a)<\w+>\((.*?)\) \{\n(.*?)\n\}\n", src, re.S):
+    for m in re.finditer(r"F29<(\w+)> (f29_(?:mul|sqr|mul2)_a)<\w+>\((.*?)\) \{\n(.*?)\n\}\n", src, re.S):
         out[(m.group(2), m.group(1))] = m.group(4)
     return out
 
 
-def _run(body, a, b=None):
-    env = {"a.l": list(a), "b.l": list(b) if b is not None else None, "m": [0] * 9, "r.l": [0] * 9, "d": [0] * 8}
+def _run(body, a, b=None, u=None, v=None):
+    env = {"a.l": list(a), "b.l": list(b) if b is not None else None, "m": [0] * 9, "r.l": [0] * 9, "d": [0] * 8,
+           "u.l": list(u) if u is not None else None, "v.l": list(v) if v is not None else None}
     acc = 0
 
     def val(expr):
@@ -116,3 +117,23 @@ def test_column_asm_products(field):
     y = rng.randrange(2 * p)
     r = _run(mul, lx, _limbs(y))
     assert _value(r) % p == _value(lx) * y * rinv % p
+
+
+@pytest.mark.parametrize("field", sorted(FIELDS))
+def test_column_asm_sum_of_products(field):
+    """f29_mul2_a: (a b + u v) 2^-261 with one reduction, Norm operands up to
+    the bounds the curve routines use (R, D < 8p; -Y < 6p; PPP < 2p)."""
+    p = FIELDS[field]
+    mul2 = _functions()[("f29_mul2_a", field)]
+    rinv = pow(1 << 261, -1, p)
+    rng = random.Random(0x5A5A + len(field))
+    edge = [0, 1, p - 1, 2 * p - 1, 8 * p - 1, 6 * p - 1]
+    for t in range(60):
+        a = edge[t % len(edge)] if t < 12 else rng.randrange(8 * p)
+        b = rng.randrange(8 * p) if t % 3 else 8 * p - 1
+        u = rng.randrange(6 * p) if t % 5 else 6 * p - 1
+        v = rng.randrange(2 * p) if t % 7 else 2 * p - 1
+        r = _run(mul2, _limbs(a), _limbs(b), _limbs(u), _limbs(v))
+        assert all(l <= M29 for l in r[:8])
+        assert _value(r) % p == (a * b + u * v) * rinv % p
+        assert _value(r) < 2 * p + p // 4  # < 2p for p < 2^254.7 (Pasta, BN254)

@@ -80,6 +80,61 @@ def statement(k, sq, P):
     return body, ins
 
 
+def statement2(k, P):
+    """f29_mul2_a, column k: statement A = carry-in + the a b terms, statement B
+    = the u v terms + the reduction terms (one statement would exceed the
+    inline-asm operand limit)."""
+    insA, bodyA, insB, bodyB = [], [], [], []
+
+    def mad(body, x, y):
+        body.append("v_mad_u64_u32 %%0, %%1, %s, %s, %%0" % (x, y))
+
+    if k >= 10:
+        opnd(insA, "v", "r.l[%d]" % (k - 10))
+    if k > 0:
+        if k - 1 < 9:
+            mad(bodyA, opnd(insA, "v", "m[%d]" % (k - 1)), const(insA, P[0]))
+        bodyA.append("v_lshrrev_b64 %0, 29, %0")
+    if k < 17:
+        for i in range(9):
+            j = k - i
+            if 0 <= j < 9:
+                mad(bodyA, opnd(insA, "v", "a.l[%d]" % i), opnd(insA, "v", "b.l[%d]" % j))
+                mad(bodyB, opnd(insB, "v", "u.l[%d]" % i), opnd(insB, "v", "v.l[%d]" % j))
+        for i in range(9):
+            j = k - i
+            if i < k and 1 <= j < 9 and P[j] != 0:
+                mad(bodyB, opnd(insB, "v", "m[%d]" % i), const(insB, P[j]))
+    return [(bodyA, insA), (bodyB, insB)]
+
+
+def gen_fn2(field):
+    """(a b + u v) 2^-261 mod p with ONE Montgomery reduction (sum of products)."""
+    p = FIELDS[field]
+    P = limbs(p)
+    inv = (-pow(p, -1, 1 << 29)) % (1 << 29)
+    L = []
+    L.append("template <>\n__device__ __forceinline__ F29<%s> f29_mul2_a<%s>(const F29<%s>& a, const F29<%s>& b, "
+             "const F29<%s>& u, const F29<%s>& v) {" % ((field,) * 6))
+    L.append("  F29<%s> r;\n  uint32_t m[9];\n  uint64_t acc = 0, c;" % field)
+    for k in range(17):
+        for body, ins in statement2(k, P):
+            if not body:
+                continue
+            text = "\\n\\t".join(body)
+            L.append('  asm("%s"\n      : "+v"(acc), "=&s"(c)\n      : %s);'
+                     % (text, ", ".join('"%s"(%s)' % ce for ce in ins)))
+        if k < 9:
+            if inv == M29:
+                L.append("  m[%d] = (0u - (uint32_t)acc) & kM29;" % k)
+            else:
+                L.append("  m[%d] = ((uint32_t)acc * %du) & kM29;" % (k, inv))
+        else:
+            L.append("  r.l[%d] = (uint32_t)acc & kM29;" % (k - 9))
+    L.append("  r.l[8] = (uint32_t)(acc >> 29);\n  (void)c;\n  return r;\n}\n")
+    return "\n".join(L)
+
+
 def gen_fn(name, field, sq):
     p = FIELDS[field]
     P = limbs(p)
@@ -111,10 +166,13 @@ def main():
     out = [doc, "//", "// GENERATED by tools/gen_fp29_asm.py -- do not edit.", "#pragma once", '#include "fp29.hpp"', "",
            "namespace pm {", "",
            "template <class P>\n__device__ F29<P> f29_mul_a(const F29<P>& a, const F29<P>& b);",
-           "template <class P>\n__device__ F29<P> f29_sqr_a(const F29<P>& a);", ""]
+           "template <class P>\n__device__ F29<P> f29_sqr_a(const F29<P>& a);",
+           "template <class P>\n__device__ F29<P> f29_mul2_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, "
+           "const F29<P>& v);", ""]
     for f in FIELDS:
         out.append(gen_fn("f29_mul_a", f, False))
         out.append(gen_fn("f29_sqr_a", f, True))
+        out.append(gen_fn2(f))
     out.append("}  // namespace pm")
     print("\n".join(out))
 
