@@ -8,7 +8,8 @@
 //   1. k_sort_hist  one lane per scalar: Montgomery -> canonical, signed
 //                   digits for all W windows (halves the bucket count), LDS
 //                   histogram of (window, coarse bin) per block.   [HBM]
-//   2. k_scan_*     exclusive scan of the block histograms.
+//   2. k_scan_*     exclusive scan of the block histograms (block sums, then
+//                   each block adds the sums before it).
 //   3. k_sort_coarse / k_sort_fine: two-level LDS bucket sort -> per window,
 //                   point indices grouped by bucket (sign in bit 31) and the
 //                   bucket offsets.                                [HBM]
@@ -143,20 +144,6 @@ static __global__ void __launch_bounds__(kScanThreads) k_scan_reduce(const uint3
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// single block: exclusive scan of nb block sums in place
-static __global__ void __launch_bounds__(1024) k_scan_top(uint32_t* __restrict__ bsum, uint32_t nb) {
-  __shared__ uint32_t lds[1024 / 64 + 1];
-  uint32_t carry = 0;
-  for (uint32_t off = 0; off < nb; off += blockDim.x) {
-    const uint32_t i = off + threadIdx.x;
-    const uint32_t v = i < nb ? bsum[i] : 0u;
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(v, lds, total);
-    if (i < nb) bsum[i] = ex + carry;
-    carry += total;
-  }
-}
-
 static __global__ void __launch_bounds__(kScanThreads) k_scan_down(const uint32_t* __restrict__ in, uint32_t N,
                                                            const uint32_t* __restrict__ bsum,
                                                            uint32_t* __restrict__ offsets,
@@ -170,8 +157,14 @@ static __global__ void __launch_bounds__(kScanThreads) k_scan_down(const uint32_
     v[k] = (base + k < N) ? in[base + k] : 0u;
     s += v[k];
   }
+  // this block's offset = sum of the block sums before it (replaces a
+  // single-block scan launch of bsum: nb is a few hundred at 2^20 - 2^23)
+  uint32_t pre = 0;
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kScanThreads) pre += bsum[i];
   uint32_t total;
-  uint32_t run = block_excl_scan(s, lds, total) + bsum[blockIdx.x];
+  block_excl_scan(pre, lds, total);
+  const uint32_t bpre = total;
+  uint32_t run = block_excl_scan(s, lds, total) + bpre;
 #pragma unroll
   for (int k = 0; k < kScanPerThread; k++) {
     if (base + k < N) {
@@ -612,9 +605,16 @@ struct LongChain {
   uint32_t gb, t_first, t_last;
 };
 
-// PREFETCH: issue the next entry's index + base loads before this entry's
-// addition (hides the dependent HBM gather when the bases exceed the
-// Infinity Cache, at the cost of 16+ VGPRs).
+// Base gather by LDS-DMA one entry ahead (PREFETCH): global_load_lds writes
+// the next entry's 64-B base straight into LDS (no VGPRs held across the
+// addition), so its L2 / Infinity Cache latency hides behind this entry's
+// mixed addition.  Per wave 4 KiB: [16-B chunk][lane].
+__device__ __forceinline__ void glds_base(const uint32_t* g, uint4* lds_wave) {
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 4 * k),
+                                     (__attribute__((address_space(3))) void*)(lds_wave + 64 * k), 16, 0, 0);
+}
 template <class F, bool PREFETCH>
 __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
@@ -623,6 +623,7 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
                                                     Xyzz<F>* __restrict__ head, uint32_t nthreads,
                                                     LongChain* __restrict__ longs, uint32_t* __restrict__ nlong,
                                                     LongChain* __restrict__ shorts, uint32_t* __restrict__ nshort) {
+  __shared__ uint4 sb[PREFETCH ? 4 * 4 * 64 : 1];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t base = offsets[s0], total = offsets[s1];
   const uint32_t start = base + t * chunk;
@@ -633,30 +634,51 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
   bool owned = offsets[gb] == start;
   Xyzz29<F> acc = xyzz29_inf<F>();
   bool acc_inf = true;
-  uint32_t code = sorted[start];
-  F29<F> px, py;
-  if (PREFETCH) load_aff29<F>(bases + 16ull * (code & ~kNegBit), px, py);
+  uint32_t code = sorted[start], nxt = 0;  // PREFETCH: code = entry p (base in LDS), nxt = entry p + 1
+  uint4* sw = sb + (PREFETCH ? 256 * (threadIdx.x >> 6) : 0);
+  const uint32_t ln = threadIdx.x & 63;
+  if (PREFETCH) {
+    glds_base(bases + 16ull * (code & ~kNegBit), sw);
+    if (start + 1 < end) nxt = sorted[start + 1];
+  }
   for (uint32_t p = start; p < end; p++) {
+    F29<F> x, y;
+    const uint32_t ccode = code;
+    if (PREFETCH) {
+      // this entry's base landed in LDS (vmcnt covers LDS-DMA; everything
+      // outstanding was issued before the previous addition); read it, and
+      // only then (lgkmcnt) let the next entry's DMA overwrite the slots
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      const uint4 a = sw[ln], b = sw[64 + ln], c = sw[128 + ln], d = sw[192 + ln];
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+      x = f29_unpack<F>(wx);
+      y = f29_unpack<F>(wy);
+    }
     if (p == bend) {
+      // the next bucket's end is loaded before the store, so its use waits
+      // for the load only (vmcnt counts stores too)
+      const uint32_t nb = offsets[gb + 2];
       store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc_inf ? xyzz29_inf<F>() : acc);
       acc_inf = true;
       gb++;
+      bend = nb;
       // skip empty buckets by binary search: a window narrower than cmax
       // leaves half its slots empty, and a linear walk over them (one
       // dependent load each) stalled the lane crossing into the next window
       // (W = 18 at 2^20: accumulate 1.06 -> 2.0 ms)
-      if (offsets[gb + 1] <= p) gb = find_bucket(offsets, gb, s1, p);
-      bend = offsets[gb + 1];
+      if (bend <= p) {
+        gb = find_bucket(offsets, gb, s1, p);
+        bend = offsets[gb + 1];
+      }
       owned = true;
     }
-    F29<F> x, y;
-    const uint32_t ccode = code;
     if (PREFETCH) {
-      x = px;
-      y = py;
       if (p + 1 < end) {
-        code = sorted[p + 1];
-        load_aff29<F>(bases + 16ull * (code & ~kNegBit), px, py);
+        glds_base(bases + 16ull * (nxt & ~kNegBit), sw);
+        code = nxt;
+        if (p + 2 < end) nxt = sorted[p + 2];
       }
     } else {
       load_aff29<F>(bases + 16ull * (ccode & ~kNegBit), x, y);
@@ -780,12 +802,48 @@ __global__ void __launch_bounds__(256) k_fixed_table(const uint32_t* __restrict_
 // Fixed-base MSM (merged buckets span ~8 slices each): k_fixup, one lane per
 // bucket, queues the long ones.  Then k_fixup_long.
 
-// One lane per queued short chain (k_accumulate's compacted list).
+// Long chains (> kMaxChain slices): one workgroup per bucket, grid-stride
+// over the list (usually empty), strided partial sums then an LDS tree.
+template <class F>
+__device__ __forceinline__ void fixup_long_blocks(const LongChain* __restrict__ longs, uint32_t nl,
+                                                  Xyzz<F>* __restrict__ buckets, const Xyzz<F>* __restrict__ head,
+                                                  uint32_t blk, uint32_t nblk) {
+  __shared__ Xyzz29<F> lds[256];
+  const int tid = threadIdx.x;
+  for (uint32_t k = blk; k < nl; k += nblk) {
+    const LongChain lc = longs[k];
+    Xyzz29<F> acc = xyzz29_inf<F>();
+    for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256)
+      acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
+    lds[tid] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) {
+        acc = xyzz29_add<F>(acc, lds[tid + s]);
+        lds[tid] = acc;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) store_xyzz29<F>(&buckets[lc.gb], xyzz29_add<F>(load_xyzz29<F>(&buckets[lc.gb]), acc));
+    __syncthreads();
+  }
+}
+
+// Blocks [0, nsb): one lane per queued short chain (k_accumulate's compacted
+// list).  Blocks [nsb, grid): the long chains (fixup_long_blocks), in the
+// same launch (a separate, almost always empty launch cost ~5 us per MSM).
+// Short and long chains belong to different buckets.
 template <class F>
 __global__ void __launch_bounds__(256) k_fixup_short(const LongChain* __restrict__ shorts,
                                                      const uint32_t* __restrict__ nshort,
                                                      Xyzz<F>* __restrict__ buckets,
-                                                     const Xyzz<F>* __restrict__ head) {
+                                                     const Xyzz<F>* __restrict__ head, uint32_t nsb,
+                                                     const LongChain* __restrict__ longs,
+                                                     const uint32_t* __restrict__ nlong) {
+  if (blockIdx.x >= nsb) {
+    fixup_long_blocks<F>(longs, *nlong, buckets, head, blockIdx.x - nsb, gridDim.x - nsb);
+    return;
+  }
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= *nshort) return;
   const LongChain lc = shorts[k];
@@ -829,26 +887,7 @@ __global__ void __launch_bounds__(256) k_fixup_long(const LongChain* __restrict_
                                                     const uint32_t* __restrict__ nlong,
                                                     Xyzz<F>* __restrict__ buckets,
                                                     const Xyzz<F>* __restrict__ head) {
-  __shared__ Xyzz29<F> lds[256];
-  const uint32_t nl = *nlong;
-  const int tid = threadIdx.x;
-  for (uint32_t k = blockIdx.x; k < nl; k += gridDim.x) {  // grid-stride: usually nl = 0
-    const LongChain lc = longs[k];
-    Xyzz29<F> acc = xyzz29_inf<F>();
-    for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256)
-      acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
-    lds[tid] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (tid < s) {
-        acc = xyzz29_add<F>(acc, lds[tid + s]);
-        lds[tid] = acc;
-      }
-      __syncthreads();
-    }
-    if (tid == 0) store_xyzz29<F>(&buckets[lc.gb], xyzz29_add<F>(load_xyzz29<F>(&buckets[lc.gb]), acc));
-    __syncthreads();
-  }
+  fixup_long_blocks<F>(longs, *nlong, buckets, head, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------ 6. segment sums

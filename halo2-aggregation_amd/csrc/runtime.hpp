@@ -29,11 +29,13 @@ constexpr int kMaxC = 20;
 constexpr int kAutoMaxC = 16;
 constexpr size_t kMaxPoints = size_t(1) << 26;
 constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg (serial chain: 2*L1-1 adds)
-// bases larger than this (bytes) use the prefetching accumulate kernel.  With
-// the radix-2^29 arithmetic the plain kernel is faster at every size measured
-// (2^22: 4.91 vs 5.30 ms, profiles/r01_s2), so auto-prefetch is off; PM_PREFETCH=1
-// still selects it.
-constexpr size_t kPrefetchBytes = ~size_t(0);
+// bases larger than this (bytes) use the prefetching accumulate kernel: the
+// next entry's base arrives by LDS-DMA (global_load_lds) during this entry's
+// addition.  Round 2, same box A/B (profiles/r02/xp/): 2^20 1.04-1.05 ->
+// 1.027 ms, 2^22 4.29-4.30 -> 4.12 ms, so it is on at every size (the
+// round-1 register-prefetch form measured slower and is gone); PM_PREFETCH=0
+// selects the plain kernel.
+constexpr size_t kPrefetchBytes = 0;
 // internal msm flag (never in the public header; the C-ABI strips it from
 // caller flags): d_bases already hold the pipeline's R = 2^261 canonical
 // form (resident pm_bases converted at upload), so no per-call conversion

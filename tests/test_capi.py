@@ -59,5 +59,5 @@ def test_device_code_has_every_launched_kernel():
         assert count(stem) == 3, stem
     assert count("13k_sort_coarse") == 4 * 4  # {2-B, 4-B digits} x {4-B, 8-B entries} x points per thread 1..8
     assert count("11k_sort_fine") == 2
-    for stem in ("13k_scan_reduce", "10k_scan_top", "11k_scan_down"):
+    for stem in ("13k_scan_reduce", "11k_scan_down"):
         assert count(stem) == 1, stem
