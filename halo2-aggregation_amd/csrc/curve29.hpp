@@ -158,6 +158,53 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_madd(const Xyzz29<F>& acc, const F29
   return r;
 }
 
+// ----------------------------------------- signed mixed add, bucket loop
+// k_accumulate's step: acc + (x2, (-1)^s y2) for a canonical base, with the
+// digit's sign folded into R instead of negating y2:
+//   R = 8p + (-1)^s S2 - Y1   (limbs: K8x3 >= 3 * 2^29 - 3 covers the
+//   -S2 - Y1 case, value in (3p, 10p)), the rest as madd-2008-s.
+// No branches: the caller overwrites the result of a lane whose acc is empty,
+// and detects the exceptional P = 0 (acc = +-point) from the output: then
+// ZZ3 = ZZ1 P^2 = 0 and X3 = R^2, so X3 = 0 iff acc = point (double it),
+// else the sum is O (xyzz29_madd_fix).
+// Bounds: R^2 < 100 p^2 < 2^261 p; Y3 = R D + (-Y1) PPP < 80 p^2 + 12 p^2,
+// both fine for p < 2^254.3 (Pasta, BN254): outputs X < 3p, Y, ZZ, ZZZ < 2p.
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_madd_signed(const Xyzz29<F>& acc, const F29<F>& x2, const F29<F>& y2,
+                                                        uint32_t negm) {
+  using K = F29Consts<F>;
+  const F29<F> U2 = f29_mul_c<F>(x2, acc.ZZ);                    // < 2p
+  const F29<F> S2 = f29_mul_c<F>(y2, acc.ZZZ);                   // < 2p
+  const F29<F> P = f29_norm<F>(f29_sub<F>(U2, acc.X, K::K6));  // < 8p
+  F29<F> R;
+#pragma unroll
+  for (int i = 0; i < 9; i++) R.l[i] = K::K8x3[i] + ((S2.l[i] ^ negm) - negm) - acc.Y.l[i];
+  R = f29_norm<F>(R);                                            // < 10p
+  const F29<F> PP = f29_sqr_c<F>(P);
+  const F29<F> PPP = f29_mul_c<F>(P, PP);
+  const F29<F> Q = f29_mul_c<F>(acc.X, PP);
+  Xyzz29<F> r;
+  r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
+  const F29<F> D = f29_norm<F>(f29_sub<F>(Q, r.X, K::K6));     // < 8p
+  const F29<F> nY = f29_norm<F>(f29_sub<F>(f29_zero<F>(), acc.Y, K::K6));  // -Y1, < 6p
+  r.Y = f29_mul2_c<F>(R, D, nY, PPP);
+  r.ZZ = f29_mul_c<F>(acc.ZZ, PP);
+  r.ZZZ = f29_mul_c<F>(acc.ZZZ, PPP);
+  return r;
+}
+// The exceptional cases of xyzz29_madd_signed (r = its output for a
+// non-empty acc).  Returns true when the sum is O.
+template <class F>
+__device__ __forceinline__ bool xyzz29_madd_fix(Xyzz29<F>& r, const F29<F>& x2, const F29<F>& y2, uint32_t negm) {
+  if (!f29_is_zero_mod<F>(r.ZZ)) return false;
+  if (!f29_is_zero_mod<F>(r.X)) {
+    r.ZZ = f29_zero<F>();
+    return true;
+  }
+  r = xyzz29_dbl_impl<F, true>(x2, negm ? f29_neg_canon<F>(y2) : y2, x2, x2);
+  return false;
+}
+
 // ------------------------------------------------------------ full add
 // add-2008-s: p + q, both packed-storage points (identity = ZZ exactly 0).
 template <class F>

@@ -459,8 +459,9 @@ constexpr bool f29_jp0_linear() {  // (j p) mod 2^29 == j: p = 1 mod 2^29 (Pasta
     if (F29Consts<P>::JP0[j] != (uint32_t)j) return false;
   return true;
 }
+// the cheap filter alone: false => v != 0 mod p
 template <class P>
-__device__ __forceinline__ bool f29_is_zero_mod(const F29<P>& v) {
+__device__ __forceinline__ bool f29_zero_filter(const F29<P>& v) {
   using K = F29Consts<P>;
   bool hit = false;
   if constexpr (f29_jp0_linear<P>()) {
@@ -469,7 +470,11 @@ __device__ __forceinline__ bool f29_is_zero_mod(const F29<P>& v) {
 #pragma unroll
     for (int j = 0; j < 8; j++) hit |= v.l[0] == K::JP0[j];
   }
-  if (!hit) return false;
+  return hit;
+}
+template <class P>
+__device__ __forceinline__ bool f29_is_zero_mod(const F29<P>& v) {
+  if (!f29_zero_filter<P>(v)) return false;
   return f29_is_zero_exact<P>(f29_canon<P>(f29_reduce3<P>(v)));
 }
 

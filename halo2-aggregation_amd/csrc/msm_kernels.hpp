@@ -632,8 +632,10 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
   uint32_t gb = find_bucket(offsets, s0, s1, start);
   uint32_t bend = offsets[gb + 1];
   bool owned = offsets[gb] == start;
+  // acc is empty ("fresh") at a bucket start and after a cancellation; an
+  // empty acc has ZZ = 0, so it stores as the identity
   Xyzz29<F> acc = xyzz29_inf<F>();
-  bool acc_inf = true;
+  bool fresh = true;
   uint32_t code = sorted[start], nxt = 0;  // PREFETCH: code = entry p (base in LDS), nxt = entry p + 1
   uint4* sw = sb + (PREFETCH ? 256 * (threadIdx.x >> 6) : 0);
   const uint32_t ln = threadIdx.x & 63;
@@ -660,8 +662,9 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
       // the next bucket's end is loaded before the store, so its use waits
       // for the load only (vmcnt counts stores too)
       const uint32_t nb = offsets[gb + 2];
-      store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc_inf ? xyzz29_inf<F>() : acc);
-      acc_inf = true;
+      store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc);
+      fresh = true;
+      acc.ZZ = f29_zero<F>();
       gb++;
       bend = nb;
       // skip empty buckets by binary search: a window narrower than cmax
@@ -684,11 +687,26 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
       load_aff29<F>(bases + 16ull * (ccode & ~kNegBit), x, y);
       if (p + 1 < end) code = sorted[p + 1];
     }
-    if (f29_is_zero_exact<F>(x) && f29_is_zero_exact<F>(y)) continue;  // identity base (0, 0)
-    if (ccode & kNegBit) y = f29_neg_canon<F>(y);
-    acc = xyzz29_madd<F>(acc, x, y, acc_inf);
+    // identity base (0, 0): y = 0 holds for no point of odd order
+    if (f29_is_zero_exact<F>(y)) continue;
+    const uint32_t negm = 0u - (ccode >> 31);  // kNegBit
+    Xyzz29<F> r = xyzz29_madd_signed<F>(acc, x, y, negm);
+    // ZZ3 = 0 mod p only when acc = +-point: the filter almost never hits,
+    // and the wave-uniform branch keeps the exact check off the hot path
+    const bool hit = !fresh && f29_zero_filter<F>(r.ZZ);
+    if (fresh) {  // first point of the bucket (divergent, every few entries)
+      r.X = x;
+      r.Y = negm ? f29_neg_canon<F>(y) : y;
+      r.ZZ = f29_const<F>(F29Consts<F>::ONE);
+      r.ZZZ = r.ZZ;
+      fresh = false;
+    }
+    if (__builtin_amdgcn_ballot_w64(hit)) {
+      if (hit) fresh = xyzz29_madd_fix<F>(r, x, y, negm);
+    }
+    acc = r;
   }
-  store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc_inf ? xyzz29_inf<F>() : acc);
+  store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc);
   // owner of a bucket that runs on past this slice: queue the chain for
   // k_fixup_short / k_fixup_long (longs == nullptr: k_fixup walks buckets).
   // The short list is compacted (one atomic per wave), so the fixup's lanes
