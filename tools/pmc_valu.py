@@ -26,6 +26,14 @@ INT64_PEAK_T = 33.944
 SIMPLE_PEAK_T = 61.164
 
 
+def kernel_label(path):
+    """'k_accumulate<PallasFp,true>' from the CSV's kernel name"""
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].replace("void ", "").replace("pm::", "").split("(")[0]
+        return name.replace(", ", ",")
+    return "k_accumulate"
+
+
 def per_dispatch(path):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
@@ -57,7 +65,7 @@ def main():
         v, i64 = c["SQ_INSTS_VALU"], c["SQ_INSTS_VALU_INT64"]
         need = i64 * 64 / (INT64_PEAK_T * 1e12) + (v - i64) * 64 / (SIMPLE_PEAK_T * 1e12)
         adds = (1 << lg) * 16  # n x W bucket additions (W = 16 windows at c = 16)
-        valu[wl] = {"kernel": "k_accumulate<PallasFp,false>",
+        valu[wl] = {"kernel": kernel_label(f1),
                     "valu_insts_per_launch": int(v), "int64_insts_per_launch": int(i64),
                     "int32_insts_per_launch": int(c["SQ_INSTS_VALU_INT32"]),
                     "salu_insts_per_launch": int(c.get("SQ_INSTS_SALU", 0)),
@@ -72,7 +80,7 @@ def main():
         wr, _ = per_dispatch(os.path.join(src, f"n{lg}_p3.csv"))
         fkb = median([fe[d]["FETCH_SIZE"] for d in fe])
         wkb = median([wr[d]["WRITE_SIZE"] for d in wr])
-        traffic[wl] = {"kernel": "k_accumulate<PallasFp,false>", "fetch_size_kb_median": fkb,
+        traffic[wl] = {"kernel": kernel_label(f1), "fetch_size_kb_median": fkb,
                        "write_size_kb_median": wkb, "hbm_bytes_per_launch": int((fkb + wkb) * 1024),
                        "launches_per_msm": 1,
                        "source": f"{rel}/n{lg}_p2.csv, n{lg}_p3.csv (separate --pmc FETCH_SIZE / WRITE_SIZE passes)",
