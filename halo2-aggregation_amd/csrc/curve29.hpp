@@ -158,6 +158,9 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_madd(const Xyzz29<F>& acc, const F29
   return r;
 }
 
+template <class F>
+__device__ __forceinline__ F29<F> f29_neg_canon(const F29<F>& y);
+
 // ----------------------------------------- signed mixed add, bucket loop
 // k_accumulate's step: acc + (x2, (-1)^s y2) for a canonical base, with the
 // digit's sign folded into R instead of negating y2:
