@@ -17,6 +17,7 @@
 
 #include "../../include/pasta_msm.h"
 #include "accum_plan.hpp"
+#include "host_ec.hpp"
 #include "msm_kernels.hpp"
 #include "runtime.hpp"
 #include "blake2b.hpp"
@@ -763,6 +764,60 @@ int pm_selftest_field(pm_ctx* ctx, int curve, uint64_t seed, size_t n, uint64_t*
   int rc = ctx->begin_call();
   if (rc) return rc;
   return ops->selftest_field(ctx, seed, (uint32_t)n, mismatches);
+}
+
+extern "C++" {
+namespace {
+template <class P>
+uint64_t selftest_host_field(uint64_t seed, size_t n) {
+  using namespace pm::host;
+  uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1, bad = 0;
+  auto rnd = [&]() {
+    st ^= st << 13;
+    st ^= st >> 7;
+    st ^= st << 17;
+    return st;
+  };
+  auto fe = [&]() {  // uniform-ish below p, plus the edges 0, 1, p - 1
+    E<P> e;
+    const uint64_t k = rnd() % 16;
+    for (int i = 0; i < 4; i++) e.v[i] = k == 0 ? 0 : k == 1 ? (i == 0) : k == 2 ? F64<P>::mod(i) - (i == 0) : rnd();
+    if (k > 2) {
+      e.v[3] %= F64<P>::mod(3);
+    }
+    return e;
+  };
+  for (size_t i = 0; i < n; i++) {
+    const E<P> a = fe(), b = fe();
+    const E<P> x = mul<P>(a, b), y = mul_adx<P>(a, b);
+    bad += memcmp(x.v, y.v, 32) != 0;
+  }
+  Pt<P> h0{fe(), fe(), fe(), fe()}, h1 = h0, g{fe(), fe(), fe(), fe()};
+  for (size_t i = 0; i < 64; i++) {
+    h0 = dbl<P, false>(h0);
+    h1 = dbl<P, true>(h1);
+    if (i & 1) {
+      h0 = addp<P, false>(h0, g);
+      h1 = addp<P, true>(h1, g);
+    }
+  }
+  bad += memcmp(&h0, &h1, sizeof(h0)) != 0;
+  return bad;
+}
+}  // namespace
+}  // extern "C++"
+
+int pm_selftest_host(int curve, uint64_t seed, size_t n, uint64_t* mismatches) {
+  if (!mismatches) return set_error(PM_ERR_ARG, "null argument");
+  if (n > (1u << 24)) return set_error(PM_ERR_ARG, "n too large");
+  if (!pm::host_has_bmi2()) return set_error(PM_ERR_UNSUPPORTED, "CPU without BMI2/ADX");
+  switch (curve) {
+    case PM_CURVE_PALLAS: *mismatches = selftest_host_field<pm::PallasFp>(seed, n); break;
+    case PM_CURVE_VESTA: *mismatches = selftest_host_field<pm::VestaFp>(seed, n); break;
+    case PM_CURVE_BN254: *mismatches = selftest_host_field<pm::Bn254Fq>(seed, n); break;
+    default: return set_error(PM_ERR_ARG, "unknown curve id");
+  }
+  return PM_OK;
 }
 
 // ------------------------------------------------- multiopen accumulator

@@ -388,9 +388,9 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
 }
 
 // The Horner steps q = hi .. lo (hi >= lo): one doubling per position, then
-// the terms at that position.  Two builds of the same code: with BMI2 / ADX
-// the compiler emits mulx / adcx chains for the 64 x 64 products (host tail
-// 166 -> 110 us on this container's Xeon); the dispatch checks the CPU once.
+// the terms at that position.  Two builds: on a CPU with BMI2 / ADX the field
+// products are host::mul_adx (mulx with two carry chains); the dispatch
+// checks the CPU once.
 template <class F>
 inline void horner_steps(host::Pt<F>& hacc, int& q, int low, size_t& ti, const std::pair<int, int>* terms,
                          size_t nterms, const Xyzz<F>* hG) {
@@ -404,13 +404,10 @@ __attribute__((target("bmi2,adx"))) void horner_steps_bmi2(host::Pt<F>& hacc, in
                                                            const std::pair<int, int>* terms, size_t nterms,
                                                            const Xyzz<F>* hG) {
   for (; q >= low; q--) {
-    hacc = host::dbl<F>(hacc);
-    for (; ti < nterms && terms[ti].first == q; ti++) hacc = host::addp<F>(hacc, host::from_dev<F>(hG[terms[ti].second]));
+    hacc = host::dbl<F, true>(hacc);
+    for (; ti < nterms && terms[ti].first == q; ti++)
+      hacc = host::addp<F, true>(hacc, host::from_dev<F>(hG[terms[ti].second]));
   }
-}
-inline bool host_has_bmi2() {
-  static const bool has = __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("adx");
-  return has;
 }
 
 // Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b}) as one

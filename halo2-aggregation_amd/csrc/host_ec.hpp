@@ -125,6 +125,62 @@ inline E<P> mul(const E<P>& a, const E<P>& b) {
   return sub_p_if<P>(t, 0);
 }
 
+// The same product with BMI2 / ADX: CIOS, every round one mulx row of a b_i
+// (lows on the OF chain, highs on the CF chain) and one of m p, m = t_0
+// (-p^-1) mod 2^64, ~25 instructions per round instead of ~55 with
+// mul / adc (the compiler's form keeps rax / rdx busy and spills).  Same
+// no-carry bound as mul().  Only reached through horner_steps_bmi2 (engine.hpp),
+// which runs after a CPU check.
+template <class P>
+inline E<P> mul_adx(const E<P>& a, const E<P>& b) {
+  static constexpr uint64_t INV = F64<P>::inv();
+  static constexpr uint64_t PM[4] = {F64<P>::mod(0), F64<P>::mod(1), F64<P>::mod(2), F64<P>::mod(3)};
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4, hi;
+  for (int i = 0; i < 4; i++) {
+    asm("movq %[bi], %%rdx\n\t"
+        "xorl %%eax, %%eax\n\t"
+        "mulxq %[a0], %%rax, %[hi]\n\t"
+        "adoxq %%rax, %[t0]\n\t"
+        "adcxq %[hi], %[t1]\n\t"
+        "mulxq %[a1], %%rax, %[hi]\n\t"
+        "adoxq %%rax, %[t1]\n\t"
+        "adcxq %[hi], %[t2]\n\t"
+        "mulxq %[a2], %%rax, %[hi]\n\t"
+        "adoxq %%rax, %[t2]\n\t"
+        "adcxq %[hi], %[t3]\n\t"
+        "mulxq %[a3], %%rax, %[t4]\n\t"
+        "adoxq %%rax, %[t3]\n\t"
+        "movl $0, %%eax\n\t"
+        "adcxq %%rax, %[t4]\n\t"
+        "adoxq %%rax, %[t4]\n\t"
+        // m = t0 * INV; t = (t + m p) / 2^64
+        "movq %[t0], %%rdx\n\t"
+        "imulq %[inv], %%rdx\n\t"
+        "xorl %%eax, %%eax\n\t"
+        "mulxq %[p0], %%rax, %[hi]\n\t"
+        "adcxq %[t0], %%rax\n\t"
+        "movq %[hi], %[t0]\n\t"
+        "adcxq %[t1], %[t0]\n\t"
+        "mulxq %[p1], %%rax, %[t1]\n\t"
+        "adoxq %%rax, %[t0]\n\t"
+        "adcxq %[t2], %[t1]\n\t"
+        "mulxq %[p2], %%rax, %[t2]\n\t"
+        "adoxq %%rax, %[t1]\n\t"
+        "adcxq %[t3], %[t2]\n\t"
+        "mulxq %[p3], %%rax, %[t3]\n\t"
+        "adoxq %%rax, %[t2]\n\t"
+        "movl $0, %%eax\n\t"
+        "adcxq %%rax, %[t3]\n\t"
+        "adoxq %[t4], %[t3]"
+        : [t0] "+&r"(t0), [t1] "+&r"(t1), [t2] "+&r"(t2), [t3] "+&r"(t3), [t4] "=&r"(t4), [hi] "=&r"(hi)
+        : [bi] "m"(b.v[i]), [a0] "m"(a.v[0]), [a1] "m"(a.v[1]), [a2] "m"(a.v[2]), [a3] "m"(a.v[3]),
+          [p0] "m"(PM[0]), [p1] "m"(PM[1]), [p2] "m"(PM[2]), [p3] "m"(PM[3]), [inv] "m"(INV)
+        : "rax", "rdx", "cc");
+  }
+  const uint64_t t[4] = {t0, t1, t2, t3};
+  return sub_p_if<P>(t, 0);
+}
+
 template <class P>
 struct Pt {  // XYZZ, ZZ == 0 is the identity
   E<P> X, Y, ZZ, ZZZ;
@@ -137,45 +193,51 @@ inline Pt<P> inf() {
   return r;
 }
 
-template <class P>
+template <class P, bool ADX>
+inline E<P> mulv(const E<P>& a, const E<P>& b) {
+  if constexpr (ADX) return mul_adx<P>(a, b);
+  else return mul<P>(a, b);
+}
+
+template <class P, bool ADX = false>
 inline Pt<P> dbl(const Pt<P>& p) {
   if (is_zero(p.ZZ) || is_zero(p.Y)) return inf<P>();
   const E<P> U = add(p.Y, p.Y);
-  const E<P> V = mul(U, U);
-  const E<P> W = mul(U, V);
-  const E<P> S = mul(p.X, V);
-  const E<P> XX = mul(p.X, p.X);
+  const E<P> V = mulv<P, ADX>(U, U);
+  const E<P> W = mulv<P, ADX>(U, V);
+  const E<P> S = mulv<P, ADX>(p.X, V);
+  const E<P> XX = mulv<P, ADX>(p.X, p.X);
   const E<P> M = add(add(XX, XX), XX);
   Pt<P> r;
-  r.X = sub(mul(M, M), add(S, S));
-  r.Y = sub(mul(M, sub(S, r.X)), mul(W, p.Y));
-  r.ZZ = mul(V, p.ZZ);
-  r.ZZZ = mul(W, p.ZZZ);
+  r.X = sub(mulv<P, ADX>(M, M), add(S, S));
+  r.Y = sub(mulv<P, ADX>(M, sub(S, r.X)), mulv<P, ADX>(W, p.Y));
+  r.ZZ = mulv<P, ADX>(V, p.ZZ);
+  r.ZZZ = mulv<P, ADX>(W, p.ZZZ);
   return r;
 }
 
-template <class P>
+template <class P, bool ADX = false>
 inline Pt<P> addp(const Pt<P>& p, const Pt<P>& q) {
   if (is_zero(q.ZZ)) return p;
   if (is_zero(p.ZZ)) return q;
-  const E<P> U1 = mul(p.X, q.ZZ);
-  const E<P> U2 = mul(q.X, p.ZZ);
-  const E<P> S1 = mul(p.Y, q.ZZZ);
-  const E<P> S2 = mul(q.Y, p.ZZZ);
+  const E<P> U1 = mulv<P, ADX>(p.X, q.ZZ);
+  const E<P> U2 = mulv<P, ADX>(q.X, p.ZZ);
+  const E<P> S1 = mulv<P, ADX>(p.Y, q.ZZZ);
+  const E<P> S2 = mulv<P, ADX>(q.Y, p.ZZZ);
   const E<P> Pd = sub(U2, U1);
   const E<P> R = sub(S2, S1);
   if (is_zero(Pd)) {
-    if (is_zero(R)) return dbl(p);
+    if (is_zero(R)) return dbl<P, ADX>(p);
     return inf<P>();
   }
-  const E<P> PP = mul(Pd, Pd);
-  const E<P> PPP = mul(Pd, PP);
-  const E<P> Q = mul(U1, PP);
+  const E<P> PP = mulv<P, ADX>(Pd, Pd);
+  const E<P> PPP = mulv<P, ADX>(Pd, PP);
+  const E<P> Q = mulv<P, ADX>(U1, PP);
   Pt<P> r;
-  r.X = sub(sub(mul(R, R), PPP), add(Q, Q));
-  r.Y = sub(mul(R, sub(Q, r.X)), mul(S1, PPP));
-  r.ZZ = mul(mul(p.ZZ, q.ZZ), PP);
-  r.ZZZ = mul(mul(p.ZZZ, q.ZZZ), PPP);
+  r.X = sub(sub(mulv<P, ADX>(R, R), PPP), add(Q, Q));
+  r.Y = sub(mulv<P, ADX>(R, sub(Q, r.X)), mulv<P, ADX>(S1, PPP));
+  r.ZZ = mulv<P, ADX>(mulv<P, ADX>(p.ZZ, q.ZZ), PP);
+  r.ZZZ = mulv<P, ADX>(mulv<P, ADX>(p.ZZZ, q.ZZZ), PPP);
   return r;
 }
 
@@ -195,4 +257,10 @@ inline Xyzz<P> to_dev(const Pt<P>& h) {
 }
 
 }  // namespace host
+
+// the host tail's BMI2 / ADX product (host::mul_adx) may run on this CPU
+inline bool host_has_bmi2() {
+  static const bool has = __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("adx");
+  return has;
+}
 }  // namespace pm

@@ -230,6 +230,7 @@ def _load():
                             ctypes.c_int),
         "pm_point_add": ([ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
         "pm_selftest_field": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, _u64p], ctypes.c_int),
+        "pm_selftest_host": ([ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_synth_scalars": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
                               _vp], ctypes.c_int),
         "pm_synth_bases": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, _vp],
@@ -345,6 +346,18 @@ def accum_batch_multi(contexts, shape, points, scalars, challenges=None, vk_repr
                                       _p(ch_in) if ch_in is not None else None, _p(vk) if vk is not None else None,
                                       _p(ch), _p(quads), _p(hev), st.ctypes.data_as(_u32p)))
     return ch, quads, hev, st
+
+
+def selftest_host(curve, seed=1, n=4096):
+    """pm_selftest_host: the host tail's BMI2/ADX Montgomery product and its
+    doubling / addition chain against the portable code (CPU only).  None when
+    the CPU lacks BMI2/ADX."""
+    m = ctypes.c_uint64(0)
+    rc = lib().pm_selftest_host(curve, seed, n, ctypes.byref(m))
+    if rc == -4:  # PM_ERR_UNSUPPORTED
+        return None
+    _check(rc)
+    return m.value
 
 
 def vk_transcript_repr(curve, pinned: bytes):

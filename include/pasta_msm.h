@@ -153,6 +153,13 @@ int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads);
  * the curve's base field); *mismatches = number of failed checks. */
 int pm_selftest_field(pm_ctx* ctx, int curve, uint64_t seed, size_t n, uint64_t* mismatches);
 
+/* Host self-test of the MSM's host tail arithmetic (no GPU): n random
+ * products and a random Horner chain of doublings / additions of the curve's
+ * base field through the BMI2/ADX Montgomery product against the portable
+ * one; *mismatches = failed checks.  PM_ERR_UNSUPPORTED when the CPU lacks
+ * BMI2/ADX (the tail then runs the portable code). */
+int pm_selftest_host(int curve, uint64_t seed, size_t n, uint64_t* mismatches);
+
 /* Affine helpers (host) for combining partial results: out = a + b. */
 int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
 

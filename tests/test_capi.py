@@ -5,6 +5,7 @@ import os
 import re
 
 import halo2_amd as H
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -61,3 +62,13 @@ def test_device_code_has_every_launched_kernel():
     assert count("11k_sort_fine") == 2
     for stem in ("13k_scan_reduce", "11k_scan_down"):
         assert count(stem) == 1, stem
+
+
+@pytest.mark.parametrize("curve", [0, 1, 2])
+def test_host_tail_adx_product(curve):
+    """CPU: the host Horner tail's mulx/adcx/adox Montgomery product (and the
+    doubling / addition chain built on it) equals the portable product."""
+    got = H.selftest_host(curve, seed=0xC0FFEE + curve, n=20000)
+    if got is None:
+        pytest.skip("CPU without BMI2/ADX")
+    assert got == 0
