@@ -340,8 +340,10 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
            "scaling": "strong" if n_total is not None else "weak",
            "config": {"workload": f"{name}_msm_2^{lg}" + ("_total" if n_total is not None else "_per_gpu"),
                       "curve": name, "n_per_gpu": n, "n_total": total, "scalars": "montgomery, HBM-resident",
-                      "bases": "affine, HBM-resident SRS (pm_bases_upload_device, converted once at upload, "
-                               f"{upload_ms:.1f} ms untimed)",
+                      "bases": "affine, HBM-resident SRS (pm_bases_upload_device: converted once at upload"
+                               + (f" and kept as {rb.rows} rows [2^(256 j/{rb.rows})] P, "
+                                  f"{rb.device_bytes / 2**20:.0f} MiB" if rb is not None and rb.rows > 1 else "")
+                               + f"; {upload_ms:.1f} ms, untimed)",
                       "parallelism": f"point-slice x{world} + RCCL all-gather of partial points"}}
     if breakdown:
         # per-MSM kernel breakdown from a separate, untimed diagnostic run with

@@ -392,8 +392,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
   template int ntt_device_impl<Cv>(Ctx*, int, void*, uint32_t, const uint64_t*, const uint64_t*);  \
   template int msm_fixed_to_aff<Cv>(Ctx*, const pm_fixed_bases*, const void*, size_t, uint32_t, uint64_t*); \
   template int bases_to29_impl<Cv>(Ctx*, const void*, size_t, void*);                            \
-  template int msm_resident_batch_impl<Cv>(Ctx*, const void*, const uint64_t* const*, size_t, size_t, uint32_t, \
-                                           uint64_t*);                                               \
+  template int msm_resident_batch_impl<Cv>(Ctx*, const void*, const pm_fixed_bases*, const uint64_t* const*, size_t, \
+                                           size_t, uint32_t, uint64_t*);                             \
   template int transcript_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const uint64_t*, const void*, \
                                           const void*, void*, void*);                            \
   PM_OPS_TABLE(Cv, name)                                                                       \

@@ -502,14 +502,34 @@ int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size
 }
 
 // Resident SRS bases: stored in the pipeline's R = 2^261 canonical form
-// (converted once here), so pm_msm_resident* skips the per-call conversion and
-// holds one copy (64 B per point) instead of two.
+// (converted once here), so pm_msm_resident* skips the per-call conversion.
+// From 2^18 points on the upload also keeps [2^{64 j}] P (4 rows up to 2^21
+// points, [2^128] P beside P above): a full-length resident MSM then runs as a
+// 4-row (2-row) table MSM (pm_fixed_bases_create_rows), whose bucket
+// reduction and host Horner are 4x (2x) shorter (2^20: 1.61 -> 1.40 ms,
+// profiles/r02/rows/).  Row 0 is the bases themselves, so windows with an
+// offset still run the plain pipeline on it.
 struct pm_bases {
   int curve;
   int device;
   size_t n;
-  void* d;
+  void* d;                 // row 0 (64 B per point)
+  pm_fixed_bases* table;   // rows > 1: the same memory as a row table, or nullptr
 };
+
+namespace {
+constexpr size_t kResidentRowsMinN = size_t(1) << 18;
+int resident_rows(size_t n) {
+  if (const char* e = std::getenv("PM_RESIDENT_ROWS")) return std::max(1, std::atoi(e));  // A/B experiments
+  if (n < kResidentRowsMinN) return 1;
+  return n <= (size_t(1) << 21) ? 4 : 2;
+}
+// a resident MSM takes the row-table path when it starts at the first base
+// and covers at least half of the table (rows past n are zero digits)
+bool resident_use_table(const pm_bases* b, size_t offset, size_t n) {
+  return b->table && offset == 0 && n >= kResidentRowsMinN && 2 * n >= b->table->npad;
+}
+}  // namespace
 
 static int bases_upload(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, pm_bases** out) {
   if (!ctx || !out || (n && !bases)) return set_error(PM_ERR_ARG, "null argument");
@@ -520,19 +540,28 @@ static int bases_upload(pm_ctx* ctx, int curve, const void* bases, bool host, si
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();
   if (rc) return rc;
-  std::unique_ptr<pm_bases> b(new pm_bases{curve, ctx->device, n, nullptr});
-  HIP_TRY(hipMalloc(&b->d, std::max<size_t>(64, n * 64)));
+  std::unique_ptr<pm_bases> b(new pm_bases{curve, ctx->device, n, nullptr, nullptr});
   const void* src = bases;
   if (host && n) {
-    if ((rc = ctx->in_bases.ensure(n * 64)) || (rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) {
+    if ((rc = ctx->in_bases.ensure(n * 64)) || (rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream)))
+      return rc;
+    src = ctx->in_bases.p;
+  }
+  const int rows = resident_rows(n);
+  if (rows > 1) {
+    std::unique_ptr<pm_fixed_bases> ft(new pm_fixed_bases{curve, ctx->device, 16, 0, rows, n, 0, nullptr});
+    if ((rc = ops->fixed_table(ctx, src, ft.get()))) {
+      if (ft->d) (void)hipFree(ft->d);
+      return rc;
+    }
+    b->d = ft->d;
+    b->table = ft.release();
+  } else {
+    HIP_TRY(hipMalloc(&b->d, std::max<size_t>(64, n * 64)));
+    if ((rc = ops->bases_to29(ctx, src, n, b->d))) {
       (void)hipFree(b->d);
       return rc;
     }
-    src = ctx->in_bases.p;
-  }
-  if ((rc = ops->bases_to29(ctx, src, n, b->d))) {
-    (void)hipFree(b->d);
-    return rc;
   }
   *out = b.release();
   return PM_OK;
@@ -546,10 +575,20 @@ int pm_bases_upload_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n
   return bases_upload(ctx, curve, d_bases, false, n, out);
 }
 
+int pm_bases_info(const pm_bases* b, size_t* n, int* rows, size_t* device_bytes) {
+  if (!b) return set_error(PM_ERR_ARG, "null argument");
+  if (n) *n = b->n;
+  if (rows) *rows = b->table ? b->table->rows : 1;
+  if (device_bytes)
+    *device_bytes = b->table ? (size_t)b->table->rows * b->table->npad * 64 : std::max<size_t>(64, b->n * 64);
+  return PM_OK;
+}
+
 int pm_bases_release(pm_bases* b) {
   if (!b) return PM_OK;
   (void)hipSetDevice(b->device);
-  (void)hipFree(b->d);
+  (void)hipFree(b->d);  // the row table's memory when there is one
+  delete b->table;
   delete b;
   return PM_OK;
 }
@@ -572,6 +611,7 @@ static int msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const voi
     if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
     d_s = ctx->in_scalars.p;
   }
+  if (resident_use_table(b, offset, n)) return curve_ops(b->curve)->msm_fixed(ctx, b->table, d_s, n, flags, out);
   return dispatch_msm_device(ctx, b->curve, d_s, (const char*)b->d + offset * 64, n, flags, out, true);
 }
 
@@ -595,8 +635,9 @@ int pm_msm_resident_batch(pm_ctx* ctx, const pm_bases* b, size_t offset, const u
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();
   if (rc) return rc;
-  return curve_ops(b->curve)->msm_resident_batch(ctx, (const char*)b->d + offset * 64, scalars, k, n,
-                                                 flags & ~kBasesR261, out);
+  return curve_ops(b->curve)->msm_resident_batch(ctx, (const char*)b->d + offset * 64,
+                                                 resident_use_table(b, offset, n) ? b->table : nullptr, scalars, k,
+                                                 n, flags & ~kBasesR261, out);
 }
 
 int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads) {
@@ -638,7 +679,7 @@ int pm_fft(pm_ctx* ctx, int curve, uint64_t* data, uint32_t log_n, const uint64_
 }
 
 // ------------------------------------------------- fixed-base MSM (§8f-3)
-static int fixed_create(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, int c,
+static int fixed_create(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, int c, int rows,
                         pm_fixed_bases** out) {
   if (!ctx || !out || (n && !bases)) return set_error(PM_ERR_ARG, "null argument");
   *out = nullptr;
@@ -651,7 +692,8 @@ static int fixed_create(pm_ctx* ctx, int curve, const void* bases, bool host, si
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();
   if (rc) return rc;
-  std::unique_ptr<pm_fixed_bases> ft(new pm_fixed_bases{curve, ctx->device, c, 0, n, 0, nullptr});
+  if (rows < 0) return set_error(PM_ERR_ARG, "negative table rows");
+  std::unique_ptr<pm_fixed_bases> ft(new pm_fixed_bases{curve, ctx->device, c, 0, rows, n, 0, nullptr});
   const void* d = bases;
   if (host) {
     if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
@@ -667,12 +709,17 @@ static int fixed_create(pm_ctx* ctx, int curve, const void* bases, bool host, si
 }
 
 int pm_fixed_bases_create(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, int c, pm_fixed_bases** out) {
-  return fixed_create(ctx, curve, bases, true, n, c, out);
+  return fixed_create(ctx, curve, bases, true, n, c, 0, out);
 }
 
 int pm_fixed_bases_create_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, int c,
                                  pm_fixed_bases** out) {
-  return fixed_create(ctx, curve, d_bases, false, n, c, out);
+  return fixed_create(ctx, curve, d_bases, false, n, c, 0, out);
+}
+
+int pm_fixed_bases_create_rows(pm_ctx* ctx, int curve, const void* bases, int bases_on_device, size_t n, int c,
+                               int rows, pm_fixed_bases** out) {
+  return fixed_create(ctx, curve, bases, bases_on_device == 0, n, c, rows, out);
 }
 
 int pm_fixed_bases_info(const pm_fixed_bases* fb, size_t* n, int* c, int* windows, size_t* table_bytes) {
@@ -680,7 +727,7 @@ int pm_fixed_bases_info(const pm_fixed_bases* fb, size_t* n, int* c, int* window
   if (n) *n = fb->n;
   if (c) *c = fb->c;
   if (windows) *windows = fb->W;
-  if (table_bytes) *table_bytes = (size_t)fb->W * fb->npad * 64;
+  if (table_bytes) *table_bytes = (size_t)fb->rows * fb->npad * 64;
   return PM_OK;
 }
 

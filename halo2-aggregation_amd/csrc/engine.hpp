@@ -165,10 +165,16 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // reduction stream only when window groups overlap; with one group the
   // cross-stream wake-up cost ~12 us between k_accumulate and the fixup
   const hipStream_t st = ctx->stream, st2 = pl.G > 1 ? ctx->red_stream : st;
-  const int Wr = fixed ? 1 : pl.W;                  // bucket sets (reduced windows)
-  const int wpg = fixed ? 1 : pl.wpg;
+  // fixed-base table of `rows` rows: windows w, w + Wr, ... share bucket set
+  // w mod Wr (kmerge = rows; rows = W: one bucket set)
+  const int kmerge = fixed ? ft->rows : 1;
+  const int Wr = pl.W / kmerge;                     // bucket sets (reduced windows)
+  const int wpg = fixed ? Wr : pl.wpg;
   const size_t stride = fixed ? ft->npad : npts;    // digit row length
-  const size_t E = fixed ? (size_t)pl.W * stride : npts;  // entries of one sort row
+  const size_t E = (size_t)kmerge * stride;         // entries of one sort row
+  // merged buckets of many windows span several accumulate slices each: the
+  // bucket-parallel fixup (k_fixup) then beats the chain lists
+  const bool bucket_fixup = fixed && kmerge > 2;
   const size_t TOT = (size_t)Wr * pl.NB + 1;
   const size_t nW = (size_t)stride * pl.W;
   const int NJ = pl.NB2 + kTJobs;                        // bit-sum jobs per window
@@ -177,7 +183,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   g.FB = std::max(0, pl.cmax - 1 - 8);
   // the fixed-base MSM's merged sort rows are W x longer: 4x more coarse bins
   // once they exceed 2^24 entries (2^23, c = 20: FB 11 -> 9, sort 3.4 -> 2.3 ms)
-  if (fixed && (size_t)pl.W * ft->npad > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
+  if (fixed && E > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
   if (ctx->sort_fb > 0) g.FB = std::min(pl.cmax - 1, ctx->sort_fb);  // PM_SORT_FB: tuning experiments
   g.NCB = (pl.K >> g.FB) + 1;
   // points per thread: blocks of 1024 threads x ppt points, ppt the largest
@@ -190,7 +196,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if (ctx->sort_ppt > 0 && !fixed) g.ppt = ctx->sort_ppt;  // PM_SORT_PPT (1, 2, 4, 8): tuning experiments
   g.nblk = (int)((stride + (size_t)g.ppt * kSortThreads - 1) / ((size_t)g.ppt * kSortThreads));
   SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
-  if (fixed) gm.nblk = g.nblk * pl.W;
+  gm.nblk = g.nblk * kmerge;
   const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
   // 4-B coarse entries when the entry index fits beside the fine bits and the sign
   const bool wide = E > (size_t(1) << (31 - g.FB));
@@ -261,7 +267,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
                                                          (uint32_t)stride, st));
   else
     PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, bh, ctx->digits.p,
-                                                     (uint32_t)stride, fixed ? 1u : 0u, st));
+                                                     (uint32_t)stride, (uint32_t)kmerge, st));
   if (rc) return rc;
   PM_LAUNCH(ctx, "scan", {
     k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum);
@@ -331,18 +337,18 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     if (prefetch)
       PM_LAUNCH(ctx, "accumulate",
                 (k_accumulate<F, true><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg,
-                                                                 pl.nthreads, fixed ? nullptr : longs, nlong, shorts, nshort)));
+                                                                 pl.nthreads, bucket_fixup ? nullptr : longs, nlong, shorts, nshort)));
     else
       PM_LAUNCH(ctx, "accumulate",
                 (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg,
-                                                                  pl.nthreads, fixed ? nullptr : longs, nlong, shorts, nshort)));
+                                                                  pl.nthreads, bucket_fixup ? nullptr : longs, nlong, shorts, nshort)));
     if (st2 != st) {
       HIP_TRY(hipEventRecord(gev[2 * gi], st));
       HIP_TRY(hipStreamWaitEvent(st2, gev[2 * gi], 0));
     }
     PM_LAUNCH_ST(ctx, st2, "fixup", {
       const uint32_t lblocks = std::min<uint32_t>(pl.maxlong, 256);
-      if (fixed) {  // merged buckets span ~W*n/2^(c-1)/chunk slices each: one lane per bucket
+      if (bucket_fixup) {  // merged buckets span ~W*n/2^(c-1)/chunk slices each: one lane per bucket
         k_fixup<F><<<(s1 - s0 + 255) / 256, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg,
                                                            longs, nlong);
         k_fixup_long<F><<<lblocks, 256, 0, st2>>>(longs, nlong, buckets, hg);
@@ -419,7 +425,6 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
     return PM_OK;
   }
   const int Wr = t.Wr, NQ = t.NQ, wpg = t.wpg;
-  const bool fixed = t.fixed;
   struct {
     int G, base, extra, log2L1;
   } pl{t.G, t.base, t.extra, t.log2L1};
@@ -431,7 +436,7 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
   terms.reserve((size_t)Wr * NQ);
   std::vector<int> gmax(pl.G, -1);  // highest position of any term of group g
   for (int w = 0; w < Wr; w++) {
-    const int o = fixed ? 0 : w * pl.base + std::min(w, pl.extra);
+    const int o = w * pl.base + std::min(w, pl.extra);  // w < Wr: window w's offset (fixed, one set: 0)
     for (int b = 0; b < NQ; b++) {
       const int q = b < NQ - 1 ? o + kBitsFold * b + pl.log2L1 : o;
       terms.emplace_back(q, w * NQ + b);
@@ -503,8 +508,8 @@ int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint
 // while the GPU works on MSM j: in steady state the GPU never waits for
 // PCIe or for the host.
 template <class Cv>
-int msm_resident_batch_impl(Ctx* ctx, const void* d_bases29, const uint64_t* const* scalars, size_t k, size_t n,
-                            uint32_t flags, uint64_t* out) {
+int msm_resident_batch_impl(Ctx* ctx, const void* d_bases29, const pm_fixed_bases* ft, const uint64_t* const* scalars,
+                            size_t k, size_t n, uint32_t flags, uint64_t* out) {
   using F = typename Cv::Base;
   if (k == 0) return PM_OK;
   if (n == 0) {
@@ -535,7 +540,7 @@ int msm_resident_batch_impl(Ctx* ctx, const void* d_bases29, const uint64_t* con
     const int sl = (int)(j & 1);
     HIP_TRY(hipStreamWaitEvent(st, copied[sl], 0));
     if ((rc = msm_device_impl<Cv>(ctx, (const uint32_t*)dbuf[sl], (const uint32_t*)d_bases29, n,
-                                  flags | kBasesR261, nullptr, nullptr, &tails[sl], sl)))
+                                  ft ? flags : flags | kBasesR261, nullptr, ft, &tails[sl], sl)))
       return rc;
     HIP_TRY(hipEventRecord(consumed[sl], st));
     if (j + 1 < k && (rc = copy(j + 1))) return rc;
@@ -569,11 +574,18 @@ int fixed_table_impl(Ctx* ctx, const void* d_bases, pm_fixed_bases* ft) {
   using F = typename Cv::Base;
   const MsmPlan pl = make_plan_fixed(kSortB, ft->c);
   ft->W = pl.W;
+  if (ft->rows <= 0) ft->rows = pl.W;
+  if (pl.W % ft->rows) return set_error(PM_ERR_ARG, "table rows must divide the window count");
+  // windows w and w + W/rows share a bucket set only if their offsets differ
+  // by the same amount for every w: equal window widths (256 = W x width)
+  if (ft->rows < pl.W && pl.extra)
+    return set_error(PM_ERR_ARG, "fewer table rows than windows needs equal window widths (256 % W == 0)");
   ft->npad = std::max<size_t>(kSortB, (ft->n + kSortB - 1) / kSortB * kSortB);
-  const size_t bytes = (size_t)pl.W * ft->npad * 64;
+  const size_t bytes = (size_t)ft->rows * ft->npad * 64;
   HIP_TRY(hipMalloc(&ft->d, bytes));
   k_fixed_table<F><<<(unsigned)((ft->npad + 255) / 256), 256, 0, ctx->stream>>>(
-      (const uint32_t*)d_bases, (uint32_t)ft->n, (uint32_t)ft->npad, pl.W, pl.base, pl.extra, (uint32_t*)ft->d);
+      (const uint32_t*)d_bases, (uint32_t)ft->n, (uint32_t)ft->npad, pl.W, pl.base, pl.extra, ft->rows,
+      (uint32_t*)ft->d);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return PM_OK;

@@ -299,17 +299,21 @@ struct DigitCode<false> {
 };
 
 // stride: digit row length (n, or the fixed-base table's padded length with
-// zero codes written for i in [n, stride)); merged: histogram rows laid out
-// (coarse bin, window, block) so the windows share one bucket set
-// (fixed-base MSM: entry w * stride + i is table point [2^{o_w}] P_i).
+// zero codes written for i in [n, stride)); kmerge: windows w, w + Wr, ...
+// (Wr = W / kmerge) share bucket set r = w mod Wr: window w's digits go to
+// digit row r * kmerge + j (j = w / Wr) and its histogram rows are laid out
+// (r, coarse bin, j, block), so sort row r is the kmerge digit rows of set r
+// back to back and entry j * stride + i is table point (j, i) = [2^{o_{j Wr}}] P_i
+// (kmerge = 1: plain windows; kmerge = W: the fixed-base MSM's one bucket set).
 template <class Fs, int W, bool D16>
 __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __restrict__ scalars, uint32_t n,
                                                             uint32_t canonical, SortGeom g,
                                                             typename DigitCode<D16>::T* __restrict__ digits,
                                                             uint32_t* __restrict__ bh, uint32_t stride,
-                                                            uint32_t merged) {
+                                                            uint32_t kmerge) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
   const int nbins = W * g.NCB;
+  const uint32_t Wr = (uint32_t)W / kmerge;
   if (blockIdx.x == 0) sort_clear(g);
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
   __syncthreads();
@@ -318,7 +322,8 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
     if (i >= stride) break;
     if (i >= n) {
 #pragma unroll
-      for (int w = 0; w < W; w++) digits[(size_t)w * stride + i] = DigitCode<D16>::enc(0u);
+      for (int w = 0; w < W; w++)
+        digits[(size_t)((w % Wr) * kmerge + w / Wr) * stride + i] = DigitCode<D16>::enc(0u);
       continue;
     }
     const Fe<Fs> s = load_canonical<Fs>(scalars, i, canonical);
@@ -326,14 +331,14 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
 #pragma unroll
     for (int w = 0; w < W; w++) {
       const uint32_t code = signed_digit<W, Fs>(s, w, carry);
-      digits[(size_t)w * stride + i] = DigitCode<D16>::enc(code);
+      digits[(size_t)((w % Wr) * kmerge + w / Wr) * stride + i] = DigitCode<D16>::enc(code);
       if (code) atomicAdd(&hist[w * g.NCB + ((code & ~kNegBit) >> g.FB)], 1u);
     }
   }
   __syncthreads();
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) {
     const uint32_t w = k / g.NCB, cb = k - w * g.NCB;
-    const size_t row = merged ? (size_t)cb * W + w : (size_t)k;
+    const size_t row = ((size_t)(w % Wr) * g.NCB + cb) * kmerge + w / Wr;
     bh[row * g.nblk + blockIdx.x] = hist[k];
   }
 }
@@ -764,14 +769,15 @@ __global__ void __launch_bounds__(256) k_bases_glv(const uint32_t* __restrict__ 
   st29<F>(o2 + 2, y);
 }
 
-// Fixed-base table (pm_fixed_bases_create): entry (w, i) at w * npad + i is
-// [2^{o_w}] P_i as a canonical affine point in the pipeline's R = 2^261 form,
-// o_w the bit offset of window w (WinGeom).  One lane per base: repeated
-// XYZZ doublings, one Fermat inversion per window.  Identity bases and the
-// padding rows [n, npad) stay (0, 0), which k_accumulate skips.
+// Fixed-base table (pm_fixed_bases_create*): entry (j, i) at j * npad + i is
+// [2^{o_{j Wr}}] P_i (Wr = W / rows) as a canonical affine point in the
+// pipeline's R = 2^261 form, o_w the bit offset of window w (WinGeom).  One
+// lane per base: repeated XYZZ doublings, one inversion per row.  Identity
+// bases and the padding rows [n, npad) stay (0, 0), which k_accumulate skips.
 template <class F>
 __global__ void __launch_bounds__(256) k_fixed_table(const uint32_t* __restrict__ in, uint32_t n, uint32_t npad,
-                                                     int W, int base, int extra, uint32_t* __restrict__ out) {
+                                                     int W, int base, int extra, int rows,
+                                                     uint32_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= npad) return;
   F29<F> x = f29_zero<F>(), y = f29_zero<F>();
@@ -794,8 +800,8 @@ __global__ void __launch_bounds__(256) k_fixed_table(const uint32_t* __restrict_
   st29<F>(o, x);
   st29<F>(o + 2, y);
   if (ident) {
-    for (int w = 1; w < W; w++) {
-      uint4* ow = reinterpret_cast<uint4*>(out + 16ull * ((size_t)w * npad + i));
+    for (int j = 1; j < rows; j++) {
+      uint4* ow = reinterpret_cast<uint4*>(out + 16ull * ((size_t)j * npad + i));
       st29<F>(ow, x);
       st29<F>(ow + 2, y);
     }
@@ -803,12 +809,14 @@ __global__ void __launch_bounds__(256) k_fixed_table(const uint32_t* __restrict_
   }
   bool acc_inf = true;
   Xyzz29<F> acc = xyzz29_madd<F>(xyzz29_inf<F>(), x, y, acc_inf);
-  for (int w = 1; w < W; w++) {
-    const int steps = base + (w - 1 < extra ? 1 : 0);
+  const int Wr = W / rows;
+  for (int j = 1; j < rows; j++) {
+    int steps = 0;  // o_{j Wr} - o_{(j-1) Wr}: the widths of windows (j-1) Wr .. j Wr - 1
+    for (int w = (j - 1) * Wr; w < j * Wr; w++) steps += base + (w < extra ? 1 : 0);
     for (int k = 0; k < steps; k++) acc = xyzz29_dbl<F>(acc);  // P has odd prime order: never the identity
     F29<F> ax, ay;
     xyzz29_to_aff<F>(acc, ax, ay);
-    uint4* ow = reinterpret_cast<uint4*>(out + 16ull * ((size_t)w * npad + i));
+    uint4* ow = reinterpret_cast<uint4*>(out + 16ull * ((size_t)j * npad + i));
     st29<F>(ow, ax);
     st29<F>(ow + 2, ay);
   }

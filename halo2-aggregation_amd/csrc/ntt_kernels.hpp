@@ -23,7 +23,10 @@
 
 namespace pm {
 
-constexpr int kNttThreads = 256;
+#ifndef PM_NTT_THREADS
+#define PM_NTT_THREADS 256
+#endif
+constexpr int kNttThreads = PM_NTT_THREADS;
 constexpr int kNttMaxLogL = 12;  // longest sub-transform (2^12 x 32 B = 128 KiB of LDS)
 
 struct FeArg {
@@ -103,6 +106,63 @@ __device__ __forceinline__ void lds_ntt(uint32_t* sm, int logL, int logC, uint32
   }
 }
 
+// The same transform with two stages per LDS round trip (radix-4 units on
+// positions j, j + h, j + 2h, j + 3h, h = 2^t): stage t with the twiddle
+// W_{2h}^lo on both pairs, then stage t + 1 with W_{4h}^lo and W_{4h}^{lo+h}.
+// Same products as two radix-2 stages, half the LDS traffic and barriers.
+// An odd logL starts with one radix-2 stage (twiddle 1).
+#ifndef PM_NTT_RADIX4
+#define PM_NTT_RADIX4 1
+#endif
+template <class Fs>
+__device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint32_t tstride,
+                                         const uint32_t* __restrict__ tw) {
+  const uint32_t plane = 1u << (logL + logC);
+  const uint32_t cmask = (1u << logC) - 1;
+  int t = 0;
+  if (logL & 1) {  // stage 0: twiddle 1
+    for (uint32_t b = threadIdx.x; b < (plane >> 1); b += kNttThreads) {
+      const uint32_t c = b & cmask, j = (b >> logC) << 1;
+      const uint32_t ia = (j << logC) | c, ib = ((j + 1) << logC) | c;
+      const Fe<Fs> u = lds_ld<Fs>(sm, plane, ia), v = lds_ld<Fs>(sm, plane, ib);
+      lds_st<Fs>(sm, plane, ia, fe_add<Fs>(u, v));
+      lds_st<Fs>(sm, plane, ib, fe_sub<Fs>(u, v));
+    }
+    __syncthreads();
+    t = 1;
+  }
+  for (; t + 1 < logL; t += 2) {
+    const uint32_t h = 1u << t;
+    for (uint32_t b = threadIdx.x; b < (plane >> 2); b += kNttThreads) {
+      const uint32_t c = b & cmask, bb = b >> logC;
+      const uint32_t lo = bb & (h - 1);
+      const uint32_t j = ((bb >> t) << (t + 2)) | lo;
+      const uint32_t i0 = (j << logC) | c, i1 = ((j + h) << logC) | c, i2 = ((j + 2 * h) << logC) | c,
+                     i3 = ((j + 3 * h) << logC) | c;
+      Fe<Fs> x0 = lds_ld<Fs>(sm, plane, i0), x1 = lds_ld<Fs>(sm, plane, i1);
+      Fe<Fs> x2 = lds_ld<Fs>(sm, plane, i2), x3 = lds_ld<Fs>(sm, plane, i3);
+      if (t > 0) {
+        const Fe<Fs> w1 =
+            load_fe4<Fs>(reinterpret_cast<const uint4*>(tw + 8ull * ((size_t)(lo << (logL - 1 - t)) * tstride)));
+        x1 = fe_mul<Fs>(x1, w1);
+        x3 = fe_mul<Fs>(x3, w1);
+      }
+      const Fe<Fs> y0 = fe_add<Fs>(x0, x1), y1 = fe_sub<Fs>(x0, x1);
+      const Fe<Fs> y2 = fe_add<Fs>(x2, x3), y3 = fe_sub<Fs>(x2, x3);
+      const Fe<Fs> w2 =
+          load_fe4<Fs>(reinterpret_cast<const uint4*>(tw + 8ull * ((size_t)(lo << (logL - 2 - t)) * tstride)));
+      const Fe<Fs> w3 = load_fe4<Fs>(
+          reinterpret_cast<const uint4*>(tw + 8ull * ((size_t)((lo + h) << (logL - 2 - t)) * tstride)));
+      const Fe<Fs> z2 = fe_mul<Fs>(y2, w2), z3 = fe_mul<Fs>(y3, w3);
+      lds_st<Fs>(sm, plane, i0, fe_add<Fs>(y0, z2));
+      lds_st<Fs>(sm, plane, i2, fe_sub<Fs>(y0, z2));
+      lds_st<Fs>(sm, plane, i1, fe_add<Fs>(y1, z3));
+      lds_st<Fs>(sm, plane, i3, fe_sub<Fs>(y1, z3));
+    }
+    __syncthreads();
+  }
+}
+
 // XCD-aware block order: consecutive logical blocks (adjacent columns / rows,
 // which share 128-B lines) land on the same XCD and its L2.
 __device__ __forceinline__ uint32_t ntt_block(uint32_t nblocks) {
@@ -127,7 +187,8 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, ui
     lds_st<Fs>(sm, plane, (ntt_brev(i1, log1) << logC) | c, v);
   }
   __syncthreads();
-  lds_ntt<Fs>(sm, log1, logC, n2, tw);  // root omega^{n2}
+  if (PM_NTT_RADIX4) lds_ntt4<Fs>(sm, log1, logC, n2, tw);  // root omega^{n2}
+  else lds_ntt<Fs>(sm, log1, logC, n2, tw);
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t k1 = e >> logC, c = e & (C - 1), i2 = col0 + c;
     Fe<Fs> v = lds_ld<Fs>(sm, plane, e);
@@ -153,7 +214,8 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_rows(const uint32_t* in, ui
     lds_st<Fs>(sm, plane, (ntt_brev(i2, log2) << logR) | r, v);
   }
   __syncthreads();
-  lds_ntt<Fs>(sm, log2, logR, n1, tw);  // root omega^{n1}
+  if (PM_NTT_RADIX4) lds_ntt4<Fs>(sm, log2, logR, n1, tw);  // root omega^{n1}
+  else lds_ntt<Fs>(sm, log2, logR, n1, tw);
   const Fe<Fs> sc = fe_of<Fs>(scale);
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t r = e & (R - 1), k2 = e >> logR;  // adjacent rows -> adjacent outputs

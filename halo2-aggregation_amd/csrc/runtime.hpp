@@ -101,12 +101,15 @@ struct TimedSpan {
 
 }  // namespace pm
 
-// Fixed-base table (pm_fixed_bases_create): W x npad affine points in the
-// pipeline's R = 2^261 form, row w = [2^{o_w}] P_i.
+// Fixed-base table (pm_fixed_bases_create*): rows x npad affine points in the
+// pipeline's R = 2^261 form, row j = [2^{o_{j W / rows}}] P_i.  rows = W (the
+// default) merges every window into one bucket set; rows = k < W merges
+// windows w, w + W/k, ... into W/k bucket sets (W/k windows to reduce, a host
+// Horner over 256/k bit positions, k x the bases' memory).
 struct pm_fixed_bases {
   int curve;
   int device;
-  int c, W;
+  int c, W, rows;
   size_t n, npad;
   void* d;
 };
@@ -211,8 +214,9 @@ struct CurveOps {
   // resident bases: Rust-layout affine (R = 2^256) -> the pipeline's R = 2^261 canonical form
   int (*bases_to29)(Ctx* ctx, const void* d_in, size_t n, void* d_out);
   // k MSMs of n host scalars against resident (R = 2^261) bases, pipelined
-  int (*msm_resident_batch)(Ctx* ctx, const void* d_bases29, const uint64_t* const* scalars, size_t k, size_t n,
-                            uint32_t flags, uint64_t* out);
+  // (ft != nullptr: the resident bases' row table, pm_fixed_bases_create_rows)
+  int (*msm_resident_batch)(Ctx* ctx, const void* d_bases29, const pm_fixed_bases* ft, const uint64_t* const* scalars,
+                            size_t k, size_t n, uint32_t flags, uint64_t* out);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

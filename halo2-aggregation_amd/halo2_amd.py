@@ -221,6 +221,8 @@ def _load():
         "pm_bases_upload": ([_vp, ctypes.c_int, _u64p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
         "pm_bases_upload_device": ([_vp, ctypes.c_int, _vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
         "pm_bases_release": ([_vp], ctypes.c_int),
+        "pm_bases_info": ([_vp, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int),
+                           ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "pm_msm_resident_device": ([_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_uint32, _u64p],
                                    ctypes.c_int),
         "pm_ctx_set_h2d_threads": ([_vp, ctypes.c_int], ctypes.c_int),
@@ -246,6 +248,8 @@ def _load():
                                  ctypes.c_int),
         "pm_fixed_bases_create": ([_vp, ctypes.c_int, _u64p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_vp)],
                                   ctypes.c_int),
+        "pm_fixed_bases_create_rows": ([_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
         "pm_fixed_bases_create_device": ([_vp, ctypes.c_int, _vp, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.POINTER(_vp)], ctypes.c_int),
         "pm_fixed_bases_info": ([_vp, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int),
@@ -389,6 +393,9 @@ class Bases:
             self.n = b.shape[0]
             _check(lib().pm_bases_upload(ctx.h, curve, _p(b), self.n, ctypes.byref(h)))
         self.h = h
+        nn, rr, bb = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_size_t()
+        _check(lib().pm_bases_info(h, ctypes.byref(nn), ctypes.byref(rr), ctypes.byref(bb)))
+        self.rows, self.device_bytes = rr.value, bb.value  # rows of [2^{256 j / rows}] P kept at upload
 
     def release(self):
         if self.h:
@@ -404,13 +411,21 @@ class Bases:
 
 class FixedBases:
     """Fixed-base table (pm_fixed_bases_create*): [2^{o_w}] P_i for every
-    window offset, resident on ctx's device.  ``bases`` is a host (n, 8) u64
-    array, or a device pointer with ``n`` given."""
+    window offset (rows = 0), or for every (W / rows)-th one
+    (pm_fixed_bases_create_rows), resident on ctx's device.  ``bases`` is a
+    host (n, 8) u64 array, or a device pointer with ``n`` given."""
 
-    def __init__(self, ctx, curve, bases=None, c=0, d_bases=None, n=None):
-        self.ctx, self.curve = ctx, curve
+    def __init__(self, ctx, curve, bases=None, c=0, d_bases=None, n=None, rows=0):
+        self.ctx, self.curve, self.rows = ctx, curve, rows
         h = _vp()
-        if d_bases is not None:
+        if rows:
+            if d_bases is not None:
+                _check(lib().pm_fixed_bases_create_rows(ctx.h, curve, _vp(d_bases), 1, n, c, rows, ctypes.byref(h)))
+            else:
+                b = _as_u64(bases, 8)
+                _check(lib().pm_fixed_bases_create_rows(ctx.h, curve, _vp(b.ctypes.data), 0, b.shape[0], c, rows,
+                                                        ctypes.byref(h)))
+        elif d_bases is not None:
             _check(lib().pm_fixed_bases_create_device(ctx.h, curve, _vp(d_bases), n, c, ctypes.byref(h)))
         else:
             b = _as_u64(bases, 8)
@@ -540,8 +555,8 @@ class Context:
     def set_h2d_threads(self, threads):
         _check(lib().pm_ctx_set_h2d_threads(self.h, threads))
 
-    def fixed_bases(self, curve, bases=None, c=0, d_bases=None, n=None):
-        return FixedBases(self, curve, bases, c, d_bases, n)
+    def fixed_bases(self, curve, bases=None, c=0, d_bases=None, n=None, rows=0):
+        return FixedBases(self, curve, bases, c, d_bases, n, rows)
 
     def msm_resident(self, bases: Bases, offset, coeffs, canonical=False):
         s = _as_u64(coeffs, 4)

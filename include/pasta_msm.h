@@ -119,7 +119,12 @@ int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size
  * examples/simple-example.rs:638-640) are fixed, so a caller uploads them once
  * and runs many MSMs against a window [offset, offset + n) of them.  The
  * library converts them once, at upload, to the pipeline's internal form
- * (64 B per point on the device, no per-call conversion).
+ * (64 B per point on the device, no per-call conversion).  From 2^18 points
+ * on it also keeps [2^{256 j / rows}] P (rows = 4 up to 2^21 points, else 2;
+ * rows x 64 B per point): an MSM over (at least half of) the set from
+ * offset 0 then runs as a row-table MSM (pm_fixed_bases_create_rows) with a
+ * rows-times shorter bucket reduction and host tail; other windows run the
+ * plain pipeline.  pm_bases_info reports n, the rows and the device bytes.
  * _upload takes host bases (Rust layout, as pm_msm), _upload_device bases
  * already in device memory of ctx's device (copied; the caller keeps its
  * buffer).  pm_msm_resident takes host scalars (staged through pinned
@@ -127,6 +132,7 @@ int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size
  * scalars. */
 int pm_bases_upload(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, pm_bases** out);
 int pm_bases_upload_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, pm_bases** out);
+int pm_bases_info(const pm_bases* b, size_t* n, int* rows, size_t* device_bytes);
 int pm_bases_release(pm_bases* b);
 int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* scalars,
                     size_t n, uint32_t flags, uint64_t out[8]);
@@ -303,6 +309,14 @@ typedef struct pm_fixed_bases pm_fixed_bases;
 int pm_fixed_bases_create(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, int c, pm_fixed_bases** out);
 int pm_fixed_bases_create_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, int c,
                                  pm_fixed_bases** out);
+/* A table of `rows` rows (rows divides W, and rows < W needs equal window
+ * widths, 256 % W == 0, e.g. c = 16; 0 = W): row j = [2^{o_{jW/rows}}] P_i,
+ * so windows w, w + W/rows, ... share one of W/rows bucket sets.  rows = W is
+ * the table above; rows = 2 at c = 16 keeps P and [2^128] P (2 x the bases'
+ * memory), halves the bucket reduction and the host Horner (128 instead of
+ * 256 doublings) of a plain MSM.  bases_on_device: bases is a device pointer. */
+int pm_fixed_bases_create_rows(pm_ctx* ctx, int curve, const void* bases, int bases_on_device, size_t n, int c,
+                               int rows, pm_fixed_bases** out);
 int pm_fixed_bases_info(const pm_fixed_bases* fb, size_t* n, int* c, int* windows, size_t* table_bytes);
 int pm_fixed_bases_release(pm_fixed_bases* fb);
 int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars, size_t n, uint32_t flags,

@@ -153,3 +153,60 @@ def test_fixed_errors(gpu_ctx):
         gpu_ctx.fixed_bases(0, np.zeros((4, 8), np.uint64), c=21)
     with pytest.raises(H.PmError):
         gpu_ctx.fixed_bases(9, np.zeros((4, 8), np.uint64))
+
+
+@pytest.mark.parametrize("c,rows", [(16, 2), (16, 4), (16, 8), (8, 4), (20, 13), (11, 24)])
+def test_fixed_rows_golden(golden, gpu_ctx, c, rows):
+    """Tables of `rows` rows (pm_fixed_bases_create_rows): windows w, w + W/rows,
+    ... share W/rows bucket sets; every golden case bit for bit."""
+    for name in ("pallas_n4096", "pallas_top_bits", "pallas_equal_scalars", "pallas_neg_pairs", "pallas_n1024",
+                 "bn254_n1024"):
+        if name not in golden:
+            continue
+        case = golden[name]
+        fb = gpu_ctx.fixed_bases(case["curve"], case["bases"], c=c, rows=rows)
+        try:
+            assert fb.table_bytes >= rows * case["bases"].shape[0] * 64
+            assert np.array_equal(fb.msm(case["scalars"]), case["expected"]), (name, c, rows)
+            n = 1000
+            want = msm_ref.best_multiexp(case["curve"], case["scalars"][:n], case["bases"][:n])
+            assert np.array_equal(fb.msm(case["scalars"][:n]), want), (name, c, rows, n)
+        finally:
+            fb.release()
+
+
+@pytest.mark.parametrize("curve", [0, 1, 2])
+def test_fixed_rows2_vs_variable(gpu_ctx, curve):
+    """Two-row table ([2^128] P beside P) at 2^20 (Pallas, Vesta, BN254): equal
+    to the variable-base MSM, also with identity bases and all-equal scalars."""
+    import torch
+
+    n = 1 << 20
+    dev = torch.device("cuda", gpu_ctx.device)
+    s = torch.empty((n, 4), dtype=torch.int64, device=dev)
+    b = torch.empty((n, 8), dtype=torch.int64, device=dev)
+    gpu_ctx.synth_scalars(curve, 0xF3 + curve, 0, n, s.data_ptr())
+    gpu_ctx.synth_bases(curve, 0xF4 + curve, 0, n, b.data_ptr())
+    b[17] = 0
+    b[n - 5] = 0
+    torch.cuda.synchronize()
+    want = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+    fb = gpu_ctx.fixed_bases(curve, d_bases=b.data_ptr(), n=n, c=16, rows=2)
+    try:
+        assert fb.windows == 16 and fb.table_bytes >= 2 * n * 64
+        assert np.array_equal(fb.msm_device(s.data_ptr(), n), want)
+        s[:] = s[3]
+        torch.cuda.synchronize()
+        assert np.array_equal(fb.msm_device(s.data_ptr(), n), gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n))
+    finally:
+        fb.release()
+
+
+def test_fixed_rows_errors(gpu_ctx):
+    b = np.zeros((4, 8), np.uint64)
+    with pytest.raises(H.PmError):
+        gpu_ctx.fixed_bases(0, b, c=16, rows=3)   # 3 does not divide W = 16
+    with pytest.raises(H.PmError):
+        gpu_ctx.fixed_bases(0, b, c=16, rows=-1)
+    with pytest.raises(H.PmError):
+        gpu_ctx.fixed_bases(0, b, c=13, rows=4)   # W = 20 windows of 12-13 bits: unequal widths

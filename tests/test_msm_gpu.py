@@ -278,3 +278,32 @@ def test_resident_batch(gpu_ctx, k, groups):
     finally:
         gpu_ctx.set_pipeline(0, 0)
         rb.release()
+
+
+@pytest.mark.parametrize("curve", [0, 1, 2])
+def test_resident_row_table(gpu_ctx, curve):
+    """Resident bases from 2^18 on keep [2^{64 j}] P rows (pm_bases_upload*):
+    full-length MSMs and batches take the row-table path, offset windows the
+    plain pipeline on row 0; all equal the raw-bases MSM."""
+    import torch
+
+    n = (1 << 20) + 3
+    s, b = _torch_inputs(gpu_ctx, curve, n)
+    rb = gpu_ctx.upload_bases(curve, d_bases=b.data_ptr(), n=n)
+    try:
+        want = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+        assert np.array_equal(gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), n), want)
+        m = (1 << 19) + 17   # covers more than half of the table: row-table path
+        assert np.array_equal(gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), m),
+                              gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), m))
+        # offset window: plain pipeline on row 0
+        o = 5
+        assert np.array_equal(gpu_ctx.msm_resident_device(rb, o, s.data_ptr(), m),
+                              gpu_ctx.msm_device(curve, s.data_ptr(), b[o:].data_ptr(), m))
+        S = s.cpu().numpy().view(np.uint64)
+        lists = [S[:m], np.roll(S[:m], 1, axis=0)]
+        got = gpu_ctx.msm_resident_batch(rb, 0, lists)
+        for j, L in enumerate(lists):
+            assert np.array_equal(got[j], gpu_ctx.msm_resident(rb, 0, L)), j
+    finally:
+        rb.release()

@@ -49,11 +49,12 @@ def main():
     ctx.set_timing(False)
     # fixed-base MSM: table build once per (size, c), then timed MSMs
     fcs = [int(x) for x in os.environ.get("FIXED_C", "").split(",") if x]
+    rows = int(os.environ.get("FIXED_ROWS", "0"))  # table rows (0 = one per window)
     for lg in sizes:
         n = 1 << lg
         for c in fcs:
             t = time.time()
-            fb = ctx.fixed_bases(curve, d_bases=b.data_ptr(), n=n, c=c)
+            fb = ctx.fixed_bases(curve, d_bases=b.data_ptr(), n=n, c=c, rows=rows)
             build = time.time() - t
             fb.msm_device(s.data_ptr(), n)
             reps = 5
@@ -67,7 +68,7 @@ def main():
                 fb.msm_device(s.data_ptr(), n)
             ctx.set_timing(False)
             ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}
-            print(json.dumps({"fixed": True, "logn": lg, "c": fb.c, "windows": fb.windows,
+            print(json.dumps({"fixed": True, "logn": lg, "c": fb.c, "windows": fb.windows, "rows": rows,
                               "table_GiB": round(fb.table_bytes / 2**30, 3), "build_s": round(build, 3),
                               "wall_ms": round(wall * 1e3, 3), "Mscalar_s": round(n / wall / 1e6, 2),
                               "kernels_ms": ks}), flush=True)
