@@ -19,7 +19,7 @@ for LG in ${LOGNS:-20 22}; do
   for P in "$sq GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
     D=$OUT/n${LG}_p$i
-    LOGN=$LG timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex k_accumulate -f csv -d $D -o run -- python3 tools/msm_timing.py > $D.log 2>&1 || { echo "pmc pass $i at 2^$LG failed"; tail -20 $D.log; exit 1; }
+    LOGN=$LG RESIDENT=${RESIDENT:-0} timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex k_accumulate -f csv -d $D -o run -- python3 tools/msm_timing.py > $D.log 2>&1 || { echo "pmc pass $i at 2^$LG failed"; tail -20 $D.log; exit 1; }
     find $D -name '*counter_collection.csv' -exec cp {} $OUT/n${LG}_p$i.csv \;
   done
 done

@@ -27,25 +27,36 @@ def main():
     t = time.time()
     ctx.synth_bases(curve, 0xA11CE, 0, nmax, b.data_ptr())
     print(json.dumps({"synth_bases_s": time.time() - t, "n": nmax}), flush=True)
+    resident = os.environ.get("RESIDENT", "0") == "1"  # the bench's path: pm_msm_resident_device
     for lg in sizes:
         n = 1 << lg
+        rb = ctx.upload_bases(curve, d_bases=b.data_ptr(), n=n) if resident else None
+
+        def run(n=n, rb=rb):
+            if rb is not None:
+                return ctx.msm_resident_device(rb, 0, s.data_ptr(), n)
+            return ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+
         for c, G, mc in [(c, G, mc) for c in cs for G in gs for mc in mcs]:
             ctx.set_window(c)
             ctx.set_pipeline(G, mc)
             ctx.set_timing(False)
-            ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+            run()
             reps = 5
             t = time.time()
             for _ in range(reps):
-                ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+                run()
             wall = (time.time() - t) / reps
             ctx.set_timing(True)
             ctx.reset_stats()
             for _ in range(reps):
-                ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
+                run()
             ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}  # per MSM (sum over groups)
-            print(json.dumps({"logn": lg, "c": c, "groups": G, "min_chunk": mc, "wall_ms": round(wall * 1e3, 3), "Mscalar_s": round(n / wall / 1e6, 2),
+            print(json.dumps({"logn": lg, "c": c, "groups": G, "min_chunk": mc, "resident_rows": rb.rows if rb else 0,
+                              "wall_ms": round(wall * 1e3, 3), "Mscalar_s": round(n / wall / 1e6, 2),
                               "kernels_ms": ks}), flush=True)
+        if rb is not None:
+            rb.release()
     ctx.set_timing(False)
     # fixed-base MSM: table build once per (size, c), then timed MSMs
     fcs = [int(x) for x in os.environ.get("FIXED_C", "").split(",") if x]
