@@ -48,9 +48,10 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
 
 // Lanes per item for the latency-bound accumulator kernels: the largest
 // power of two 2^lg <= 2^maxlg that keeps items * 2^lg within about two
-// waves per SIMD of the 1024 on an MI355X.  Split ladder: maxlg = 3 (8 lanes
-// x 16 bits: 112 ladder doublings; 16 x 8 measured no faster, the wider
-// butterfly and the second wave per SIMD cost what the shorter loop saves).
+// waves per SIMD of the 1024 on an MI355X.  Term additions: maxlg = 3 (8
+// lanes share a term's ~85 table additions; 16 measured no faster at B = 256,
+// the wider butterfly and the second wave per SIMD cost what the shorter loop
+// saves).
 constexpr size_t kAccLaneBudget = 1024 * 2 * 64;
 constexpr size_t kAccSumLanes = 16384;
 constexpr size_t kAccScalarsLds = 128 * 1024;
@@ -214,12 +215,13 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
   const size_t nterm = (size_t)B * T;
   uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_lanes(nterm, 3);
-  // 16 / 32 lanes per term only while the term products still fit one wave
-  // per SIMD (B = 16: 0.65 -> 0.58 ms; B = 256 stays at 8 lanes, 16 measured
-  // 0.71 -> 0.75 ms: profiles/r01_s4/accum_split_sweep.jsonl)
+  // 16 / 32 lanes per term only while the term additions still fit one wave
+  // per SIMD (B = 16: k_acc_termadd 0.075 ms at 16 lanes, 0.061 at 32; B = 256
+  // stays at 8 lanes: 0.129 ms, 16 lanes 0.138, 32 lanes 0.197:
+  // profiles/r02/pow/timing_pow1.jsonl)
   if (ctx->acc_split < 0 && lgS == 3)
     while (lgS < 5 && (nterm << (lgS + 1)) <= kAccLaneBudget / 2) lgS++;
-  const uint32_t S = 1u << lgS, Lb = (kGlvBits + S - 1) / S;
+  const uint32_t S = 1u << lgS;
   // Streams: with the split ladder (points only, the critical chain) it goes
   // first on the main stream, and the transcript replay + k_acc_scalars run
   // beside it on the reduction stream (kept off the ladder's CUs by the LDS
@@ -229,15 +231,14 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   hipStream_t side = st;
   hipEvent_t up = nullptr, sc_done = nullptr;
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
-    if ((rc = ctx->acc_lad.ensure(nterm * S * sizeof(Xyzz<F>)))) return rc;
+    if ((rc = ctx->acc_lad.ensure(nterm * kPowPos * kPowPoint * sizeof(uint4)))) return rc;
     up = ctx->next_event();
     sc_done = ctx->next_event();
     if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(up, st));
     PM_LAUNCH(ctx, "acc_ladder",
-              (k_acc_ladder<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, kAccLadderFence, st>>>(
-                  h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, S, Lb,
-                  (Xyzz<F>*)ctx->acc_lad.p)));
+              (k_acc_powers<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, kAccLadderFence, st>>>(
+                  h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, (uint4*)ctx->acc_lad.p)));
     side = ctx->red_stream;
     HIP_TRY(hipStreamWaitEvent(side, up, 0));
   }
@@ -260,8 +261,8 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     HIP_TRY(hipEventRecord(sc_done, side));
     HIP_TRY(hipStreamWaitEvent(st, sc_done, 0));
     PM_LAUNCH(ctx, "acc_termmul",
-              (k_acc_termmul_split<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
-                  h, dcoef, (const Xyzz<F>*)ctx->acc_lad.p, lgS, Lb, dpart)));
+              (k_acc_termadd<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
+                  h, dcoef, (const uint4*)ctx->acc_lad.p, lgS, dpart)));
   } else {
     PM_LAUNCH(ctx, "acc_termmul",
               (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(

@@ -385,56 +385,6 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
   store_xyzz29<F>(&part[g], aff_is_inf<F>(P) ? xyzz29_inf<F>() : glv_mul<Cv>(c, P));
 }
 
-// ---------------------------------------------------------------- split ladder
-// At small batches one lane per term leaves most SIMDs idle and the term
-// multiplication is a 130-step latency chain.  The split form gives each term
-// S lanes: lane j owns bits [j L, (j + 1) L) of both GLV halves and multiplies
-// Q_j = [2^{j L}] P by them (L steps); the S partials are summed by a
-// butterfly of cross-lane shuffles.  The Q_j come from k_acc_ladder, which
-// depends only on the points, so it runs on a second stream while the
-// transcript replay and k_acc_scalars derive the coefficients.
-//
-// k_acc_ladder: one quad per (proof, term) (coop29.hpp: each Jacobian
-// doubling is 3 product levels split over the 4 lanes): Q_0 = P,
-// Q_{j+1} = [2^L] Q_j, stored packed (R261 Jacobian X, Y, Z in the X, Y, ZZ
-// slots of an Xyzz) at lad[g S + j].
-template <class Cv>
-__global__ void __launch_bounds__(256) k_acc_ladder(AccumHdr h, const uint32_t* __restrict__ prog,
-                                                    const uint32_t* __restrict__ points,
-                                                    const uint32_t* __restrict__ vk, uint32_t S, uint32_t L,
-                                                    Xyzz<typename Cv::Base>* __restrict__ lad) {
-  using F = typename Cv::Base;
-  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t g = gl >> 2;
-  if (g >= h.B * h.T) return;  // whole quads (4 B T lanes)
-  const bool st = (gl & 3u) == 0;
-  const uint32_t b = g / h.T, t = g - b * h.T;
-  const uint32_t src = prog[h.p_termsrc + t];
-  const uint32_t idx = src & 0x0FFFFFFFu;
-  const uint32_t* pp = (src >> 28) == 0 ? points + 16ull * ((size_t)h.npts * b + idx) : vk + 16ull * idx;
-  const Aff<F> P = load_aff<F>(pp);
-  Xyzz<F>* out = lad + (size_t)g * S;
-  const uint32_t nq = (kGlvBits + L - 1) / L;  // Q_j actually used (nq <= S)
-  if (aff_is_inf<F>(P)) {
-    if (st)
-      for (uint32_t j = 0; j < nq; j++) store_xyzz29<F>(&out[j], xyzz29_inf<F>());
-    return;
-  }
-  const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
-  Jac29<F> q{px, py, f29_const<F>(F29Consts<F>::ONE)};
-  // stored as Jacobian (X, Y, Z in the X, Y, ZZ slots): the term products
-  // derive ZZ, ZZZ in parallel, off this chain
-  if (st) store_xyzz29<F>(&out[0], Xyzz29<F>{q.X, q.Y, q.Z, q.Z});
-  for (uint32_t j = 1; j < nq; j++) {
-    for (uint32_t d = 0; d < L; d++) q = jac29_dbl_q<F>(q);
-    // Z < 4p can exceed the 2^256 of the packed store (Pasta): canonical
-    if (st) {
-      const F29<F> z = f29_canon<F>(q.Z);
-      store_xyzz29<F>(&out[j], Xyzz29<F>{q.X, q.Y, z, z});
-    }
-  }
-}
-
 template <class F>
 __device__ __forceinline__ Xyzz29<F> xyzz29_shfl_xor(const Xyzz29<F>& p, int m) {
   Xyzz29<F> r;
@@ -448,53 +398,189 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_shfl_xor(const Xyzz29<F>& p, int m) 
   return r;
 }
 
-// k_acc_termmul_split: S lanes per (proof, term) (S a power of two <= 64, so a
-// group never straddles a wave); lane j: sum over i in [j L, (j + 1) L) of
-// [k1_i 2^{i - j L}] (+-Q_j) + [k2_i 2^{i - j L}] (+-phi(Q_j)), joint
-// double-and-add with full XYZZ additions; then log2(S) butterfly steps and
-// lane 0 stores the term's point.  phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ).
-// (A quad-cooperative form (coop29.hpp) measured slower here: it needs
-// ~260 VGPRs, so only one wave per SIMD fits and the 4x larger grid runs in
-// two rounds.)
+// ------------------------------------------------------- powers-of-two table
+// At small batches one lane per term leaves most SIMDs idle and the term
+// multiplication is a 128-step latency chain.  The split form stores every
+// power of two of each term's point first; a term product is then a sum of
+// table points only: [k]P = sum_i d_i [2^i] (+-P) + e_i [2^i] (+-phi P) over
+// the non-adjacent forms d, e of the rounded GLV halves (|k_i| < 2^127, so
+// 128 digits, about a third of them nonzero), spread over S lanes.  The
+// table depends only on the points, so k_acc_powers runs on the main stream
+// while the transcript replay and k_acc_scalars derive the coefficients.
+// (Round 1 stored Q_j = [2^{16 j}] P only and each lane ran 16 dbl + add
+// steps: the additions-only form has a 15-doubling longer table chain but
+// ~40% fewer operations after it)
+//
+// k_acc_powers: one quad per (proof, term) walks P, [2] P, ..., [2^127] P
+// (127 Jacobian doublings, coop29.hpp) and stores every point in XYZZ form
+// plus beta X: coordinates X, Y, ZZ, ZZZ, beta X (and a junk slot) of kPowWords
+// uint4 each (limbs 0-3, 4-7, 8), holding the 9 radix-2^29 limbs as computed (no packing: every
+// instruction on the doubling chain lanes costs, and the termadd lanes load
+// them back as they are).  ZZ, ZZZ and beta X come from quad lanes that idle
+// in the doubling's last two levels (jac29_dbl_q_ext), so the chain is as
+// long as 127 plain doublings plus the stores.
+constexpr uint32_t kPowPos = 128, kPowWords = 3, kPowCoord = 6, kPowPoint = kPowWords * kPowCoord;  // in uint4
+
+template <class F>
+__device__ __forceinline__ void pow_st(uint4* o, const F29<F>& v) {
+  o[0] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
+  o[1] = make_uint4(v.l[4], v.l[5], v.l[6], v.l[7]);
+  reinterpret_cast<uint32_t*>(o + 2)[0] = v.l[8];
+}
+template <class F>
+__device__ __forceinline__ F29<F> pow_ld(const uint4* o) {
+  const uint4 a = o[0], b = o[1];
+  return F29<F>{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, reinterpret_cast<const uint32_t*>(o + 2)[0]}};
+}
+
+// Stores of one step: the owners of jac29_dbl_q_ext's outputs write them,
+// every lane executes the same four stores, and a lane that owns nothing at a
+// site writes its register to the point's junk slot (coordinate 5).  (Stores
+// under lane-dependent ifs were merged by the compiler into one store with a
+// selected address and split into dword stores.)
+//   X    every lane (all hold X3)           -> coordinate 0
+//   Y    lanes 1, 2                         -> 1
+//   zz   lane 3 (ZZ3)                       -> 2
+//   ext  lane 3 (ZZZ3) -> 3, lane 0 (beta X3) -> 4
+struct PowSites {
+  uint32_t y, zz, ext;  // coordinate offsets (uint4) of this lane
+  __device__ explicit PowSites(uint32_t q)
+      : y((q == 1u || q == 2u ? 1u : 5u) * kPowWords),
+        zz((q == 3u ? 2u : 5u) * kPowWords),
+        ext((q == 3u ? 3u : q == 0u ? 4u : 5u) * kPowWords) {}
+};
+template <class F>
+__device__ __forceinline__ void pow_store(uint4* o, const PowSites& ps, const Jac29<F>& p, const F29<F>& zz,
+                                          const F29<F>& ext) {
+  pow_st<F>(o, p.X);
+  pow_st<F>(o + ps.y, p.Y);
+  pow_st<F>(o + ps.zz, zz);
+  pow_st<F>(o + ps.ext, ext);
+}
+
 template <class Cv>
-__global__ void __launch_bounds__(256) k_acc_termmul_split(AccumHdr h, const uint32_t* __restrict__ coef,
-                                                           const Xyzz<typename Cv::Base>* __restrict__ lad,
-                                                           uint32_t lgS, uint32_t L,
-                                                           Xyzz<typename Cv::Base>* __restrict__ part) {
+__global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* __restrict__ prog,
+                                                    const uint32_t* __restrict__ points,
+                                                    const uint32_t* __restrict__ vk, uint4* __restrict__ pw) {
+  using F = typename Cv::Base;
+  using K = F29Consts<F>;
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = gl >> 2, q = gl & 3u;
+  if (g >= h.B * h.T) return;  // whole quads (4 B T lanes)
+  const uint32_t b = g / h.T, t = g - b * h.T;
+  const uint32_t src = prog[h.p_termsrc + t];
+  const uint32_t idx = src & 0x0FFFFFFFu;
+  const uint32_t* pp = (src >> 28) == 0 ? points + 16ull * ((size_t)h.npts * b + idx) : vk + 16ull * idx;
+  const Aff<F> P = load_aff<F>(pp);
+  uint4* out = pw + (size_t)g * kPowPos * kPowPoint;
+  const PowSites ps(q);
+  const F29<F> one = f29_const<F>(K::ONE);
+  if (aff_is_inf<F>(P)) {  // the identity (ZZ = 0) at every power
+    const F29<F> zero = f29_zero<F>();
+    for (uint32_t j = 0; j < kPowPos; j++) pow_store<F>(out + j * kPowPoint, ps, Jac29<F>{one, one, one}, zero, one);
+    return;
+  }
+  const F29<F> beta = f29_const<F>(Glv<Cv>::BETA29);
+  const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
+  Jac29<F> cur{px, py, one};
+  pow_store<F>(out, ps, cur, one, q == 0u ? f29_mul_c<F>(beta, px) : one);
+  for (uint32_t j = 1; j < kPowPos; j++) {
+    F29<F> zz, ext;
+    cur = jac29_dbl_q_ext<F>(cur, beta, zz, ext);
+    pow_store<F>(out + j * kPowPoint, ps, cur, zz, ext);
+  }
+}
+
+// non-adjacent form of k < 2^127 (4 words): with h = 3 k, digit i is
+// h_{i+1} - k_{i+1}; nz = its nonzero positions, ng = the negative ones
+__device__ __forceinline__ void naf128(const uint32_t* k, uint32_t* nz, uint32_t* ng) {
+  uint32_t hw[5];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    c += (uint64_t)k[i] * 3u;
+    hw[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  hw[4] = (uint32_t)c;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t hp = (hw[i] >> 1) | (hw[i + 1] << 31);
+    const uint32_t kp = (k[i] >> 1) | (i < 3 ? k[i + 1] << 31 : 0u);
+    nz[i] = hp ^ kp;
+    ng[i] = kp & ~hp;
+  }
+}
+
+// k_acc_termadd: S lanes per (proof, term) (S a power of two <= 64); the
+// nonzero digits of both halves, in order (k1's, then k2's), are dealt out
+// round-robin, so lane j adds ranks j, j + S, ... (at most ceil(cnt / S)
+// additions, cnt ~ 85) with full XYZZ additions; the next point's loads are
+// issued before each addition.  Then log2(S) butterfly steps; lane 0 stores.
+template <class Cv>
+__global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t* __restrict__ coef,
+                                                     const uint4* __restrict__ pw, uint32_t lgS,
+                                                     Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   using K = F29Consts<F>;
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t S = 1u << lgS, g = gl >> lgS, j = gl & (S - 1);
-  if (g >= h.B * h.T) return;  // whole groups only: B T S lanes, groups aligned
+  if (g >= h.B * h.T) return;  // whole groups only
   uint32_t k1[6], k2[6];
   bool n1, n2;
-  glv_split<Cv>(ldfe<Fs>(coef, g), k1, k2, n1, n2);
-  const uint32_t lo = j * L, hi = min(lo + L, (uint32_t)kGlvBits);
-  Xyzz29<F> acc = xyzz29_inf<F>();
-  if (lo < hi) {
-    const Xyzz29<F> QJ = load_xyzz29<F>(&lad[(size_t)g * S + j]);  // Jacobian X, Y, Z (k_acc_ladder)
-    const Xyzz29<F> Q = jac29_to_xyzz<F>(Jac29<F>{QJ.X, QJ.Y, QJ.ZZ});
-    // Y < 3p -> 6p - Y reduced below 3p (dbl needs Y < 4p)
-    const F29<F> yneg = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), Q.Y, K::K6)));
-    const Xyzz29<F> T1{Q.X, n1 ? yneg : Q.Y, Q.ZZ, Q.ZZZ};
-    const Xyzz29<F> T2{f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), Q.X), n2 ? yneg : Q.Y, Q.ZZ, Q.ZZZ};
-    const Xyzz29<F> T3 = xyzz29_add<F>(T1, T2);
-    for (int i = (int)hi - 1; i >= (int)lo; i--) {
-      acc = xyzz29_dbl<F>(acc);
-      const uint32_t b1 = (k1[i >> 5] >> (i & 31)) & 1u, b2 = (k2[i >> 5] >> (i & 31)) & 1u;
-      const uint32_t sel = b1 | (b2 << 1);
-      if (sel == 0) continue;
-      Xyzz29<F> q;
+  glv_split<Cv, true>(ldfe<Fs>(coef, g), k1, k2, n1, n2);
+  uint32_t nz[8], ng[8];
+  naf128(k1, nz, ng);
+  naf128(k2, nz + 4, ng + 4);
+  const uint32_t f1 = n1 ? ~0u : 0u, f2 = n2 ? ~0u : 0u;
+  uint32_t skip = j;
 #pragma unroll
-      for (int t = 0; t < 9; t++) {
-        q.X.l[t] = sel == 1 ? T1.X.l[t] : sel == 2 ? T2.X.l[t] : T3.X.l[t];
-        q.Y.l[t] = sel == 1 ? T1.Y.l[t] : sel == 2 ? T2.Y.l[t] : T3.Y.l[t];
-        q.ZZ.l[t] = sel == 3 ? T3.ZZ.l[t] : T1.ZZ.l[t];
-        q.ZZZ.l[t] = sel == 3 ? T3.ZZZ.l[t] : T1.ZZZ.l[t];
-      }
-      acc = xyzz29_add<F>(acc, q);
+  for (int w = 0; w < 8; w++) {
+    ng[w] ^= w < 4 ? f1 : f2;  // sign of the half
+    uint32_t m = nz[w], sel = 0;
+    while (m) {
+      const uint32_t lb = m & (0u - m);
+      sel |= skip == 0 ? lb : 0u;
+      skip = skip == 0 ? S - 1 : skip - 1;
+      m ^= lb;
     }
+    nz[w] = sel;
+  }
+  const uint4* base = pw + (size_t)g * kPowPos * kPowPoint;
+  // pops this lane's lowest remaining digit and issues its loads
+  auto next = [&](Xyzz29<F>& Q, uint32_t& negm) -> bool {
+    uint32_t w = 8, m = 0, s = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; i--)
+      if (nz[i]) {
+        w = (uint32_t)i;
+        m = nz[i];
+        s = ng[i];
+      }
+    if (w == 8) return false;
+    const uint32_t bit = __builtin_ctz(m);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      if ((uint32_t)i == w) nz[i] = m & (m - 1);
+    negm = 0u - ((s >> bit) & 1u);
+    const uint4* o = base + (((w & 3u) << 5) | bit) * kPowPoint;
+    Q.X = pow_ld<F>(o + (w < 4 ? 0 : 4 * kPowWords));  // phi: (beta X, Y, ZZ, ZZZ)
+    Q.Y = pow_ld<F>(o + kPowWords);
+    Q.ZZ = pow_ld<F>(o + 2 * kPowWords);
+    Q.ZZZ = pow_ld<F>(o + 3 * kPowWords);
+    return true;
+  };
+  Xyzz29<F> acc = xyzz29_inf<F>(), Q;
+  uint32_t negm = 0;
+  bool have = next(Q, negm);
+  while (have) {
+    const F29<F> yn = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), Q.Y, K::K6)));  // Y < 3p
+    Xyzz29<F> R = Q;
+#pragma unroll
+    for (int i = 0; i < 9; i++) R.Y.l[i] = bsel(negm, yn.l[i], Q.Y.l[i]);
+    have = next(Q, negm);
+    acc = xyzz29_add<F>(acc, R);
   }
   for (uint32_t m = 1; m < S; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
   if (j == 0) store_xyzz29<F>(&part[g], acc);

@@ -90,6 +90,56 @@ __device__ __forceinline__ Jac29<F> jac29_dbl_q(const Jac29<F>& p) {
   return r;
 }
 
+// jac29_dbl_q plus the storage form of the new point, on lanes that idle in
+// the last two levels: L2 lane 3 squares Z3 (-> zz, lane 3), L3 lane 0
+// multiplies beta X3 and lane 3 ZZ Z3 (-> ext).  Only lanes 1 and 2 compute
+// E (D - X3), so only they hold Y3 afterwards; lanes 0 and 3 never read Y
+// (their L1 product is X X) and keep a bounded dummy there.  Outputs on the
+// owning lanes: X3 (all), Y3 (1, 2), ZZ3 < 2p (3), ZZZ3 < 2p (3), beta X3 < 2p
+// (0).  Same chain length as jac29_dbl_q.
+template <class F>
+__device__ __forceinline__ Jac29<F> jac29_dbl_q_ext(const Jac29<F>& p, const F29<F>& beta, F29<F>& zz,
+                                                    F29<F>& ext) {
+  using K = F29Consts<F>;
+  const uint32_t q = quad_id();
+  const uint32_t m12 = (q == 1u || q == 2u) ? ~0u : 0u, m2 = q == 2u ? ~0u : 0u;
+  F29<F> o1a, o1b;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    o1a.l[i] = bsel(m12, p.Y.l[i], p.X.l[i]);
+    o1b.l[i] = bsel(m2, p.Z.l[i], o1a.l[i]);
+  }
+  const F29<F> r1 = f29_mul_c<F>(o1a, o1b);
+  const F29<F> A = qbc<0, F>(r1), B = qbc<1, F>(r1), YZ = qbc<2, F>(r1);
+  Jac29<F> r;
+  r.Z = f29_norm<F>(f29_add<F>(YZ, YZ));                                   // < 4p
+  const F29<F> t = f29_norm<F>(f29_add<F>(p.X, B));
+  const F29<F> E = f29_norm<F>(f29_add<F>(f29_add<F>(A, A), A));
+  const F29<F> r2 = f29_sqr_c<F>(qsel<F>(q, B, t, E, r.Z));
+  const F29<F> C = qbc<0, F>(r2), s = qbc<1, F>(r2), FF = qbc<2, F>(r2);
+  zz = r2;
+  const F29<F> u = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(s, f29_add<F>(A, C), K::K8x3)));
+  const F29<F> D = f29_reduce3<F>(f29_norm<F>(f29_add<F>(u, u)));
+  r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(FF, f29_add<F>(D, D), K::K8x3)));
+  const F29<F> w = f29_sub<F>(D, r.X, K::K6);
+  F29<F> C8 = C;
+#pragma unroll
+  for (int i = 0; i < 9; i++) C8.l[i] = C.l[i] << 3;
+  C8 = f29_reduce3<F>(f29_norm<F>(C8));
+  // operands (beta, X3) / (E, w) / (E, w) / (ZZ3, Z3): two selects per limb
+  const uint32_t m0 = q == 0u ? ~0u : 0u, m3 = q == 3u ? ~0u : 0u;
+  F29<F> o3a, o3b;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    o3a.l[i] = bsel(m0, beta.l[i], bsel(m3, r2.l[i], E.l[i]));
+    o3b.l[i] = bsel(m0, r.X.l[i], bsel(m3, r.Z.l[i], w.l[i]));
+  }
+  const F29<F> r3 = f29_mul_c<F>(o3a, o3b);
+  ext = r3;
+  r.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(r3, C8, K::K8x3)));
+  return r;
+}
+
 // Jacobian -> XYZZ (ZZ = Z^2, ZZZ = Z^3): two levels
 template <class F>
 __device__ __forceinline__ Xyzz29<F> jac29_to_xyzz_q(const Jac29<F>& p) {

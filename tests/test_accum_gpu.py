@@ -36,7 +36,7 @@ def test_golden_accumulator(gpu_ctx):
 @pytest.mark.parametrize("lg", [0, 1, 2, 3, 4, 5])
 def test_split_ladder_widths(gpu_ctx, lg):
     """Every split of the term multiplication (2^lg lanes per term,
-    k_acc_ladder + k_acc_termmul_split; lg = 0 is the one-lane GLV kernel)
+    k_acc_powers + k_acc_termadd; lg = 0 is the one-lane GLV kernel)
     reproduces the golden vectors, including the identity / W_1 = -W_0 edge
     case, and random rich-shape proofs on Pallas."""
     gpu_ctx.set_accum_split(lg)

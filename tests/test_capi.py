@@ -54,8 +54,8 @@ def test_device_code_has_every_launched_kernel():
     assert count("12k_accumulate") == 3 * 2  # 3 curves x {plain, prefetch}
     assert count("15k_sort_hist_glv") == 3 * 5 * 2  # 3 curves x W in 7..11 x {2-B, 4-B digits}
     for stem in ("7k_fixupI", "12k_fixup_long", "12k_bucket_seg", "13k_bucket_bits", "15k_bases_to_r261",
-                 "16k_selftest_field", "13k_acc_termmul", "9k_acc_sum", "13k_acc_scalars", "12k_acc_ladder",
-                 "19k_acc_termmul_split", "11k_bases_glv",
+                 "16k_selftest_field", "13k_acc_termmul", "9k_acc_sum", "13k_acc_scalars", "12k_acc_powers",
+                 "13k_acc_termadd", "11k_bases_glv",
                  "15k_synth_scalars", "13k_synth_bases"):
         assert count(stem) == 3, stem
     assert count("13k_sort_coarse") == 4 * 4  # {2-B, 4-B digits} x {4-B, 8-B entries} x points per thread 1..8

@@ -135,3 +135,45 @@ def test_glv_signed_digits(W):
                 val += d << off
                 off += C
             assert val == (-k if flip else k)
+
+
+def _naf128(k):
+    """k_acc_termadd's naf128 (csrc/accum_kernels.hpp) on 32-bit words: with
+    h = 3 k, digit i is h_{i+1} - k_{i+1}."""
+    kw = [(k >> (32 * i)) & 0xFFFFFFFF for i in range(4)]
+    h = 3 * k
+    hw = [(h >> (32 * i)) & 0xFFFFFFFF for i in range(5)]
+    nz, ng = [], []
+    for i in range(4):
+        hp = ((hw[i] >> 1) | (hw[i + 1] << 31)) & 0xFFFFFFFF
+        kp = ((kw[i] >> 1) | ((kw[i + 1] << 31) if i < 3 else 0)) & 0xFFFFFFFF
+        nz.append(hp ^ kp)
+        ng.append(kp & ~hp & 0xFFFFFFFF)
+    return nz, ng
+
+
+def test_naf_of_rounded_glv_halves():
+    """The term additions' digits: a non-adjacent form of every |k_i| < 2^127
+    within 128 positions (the powers table's length), about a third nonzero,
+    and the round-robin deal over S lanes gives each lane ceil(cnt / S) or
+    fewer additions."""
+    rng = random.Random(0x4AF)
+    total = 0
+    cases = [0, 1, 3, 7, (1 << 127) - 1, 0x5555555555555555555555555555555, 0x2AAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA]
+    cases += [rng.getrandbits(127) for _ in range(400)]
+    for k in cases:
+        nz, ng = _naf128(k)
+        digits = []
+        for i in range(128):
+            w, b = divmod(i, 32)
+            d = ((nz[w] >> b) & 1) * (-1 if (ng[w] >> b) & 1 else 1)
+            assert not ((ng[w] >> b) & 1) or ((nz[w] >> b) & 1)
+            digits.append(d)
+        assert sum(d << i for i, d in enumerate(digits)) == k
+        assert all(not (digits[i] and digits[i + 1]) for i in range(127))
+        cnt = sum(1 for d in digits if d)
+        total += cnt
+        for S in (8, 16, 32):
+            per_lane = [len(range(j, cnt, S)) for j in range(S)]
+            assert max(per_lane) == -(-cnt // S)
+    assert 0.30 < total / (128 * len(cases)) < 0.36
