@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fixed", type=int, default=1, help="also time the fixed-base MSM (1) or skip it (0)")
     ap.add_argument("--ntt-logn", type=int, default=20, help="NTT leg size (0 = skip)")
+    ap.add_argument("--ntt-large-logn", type=int, default=25,
+                    help="second NTT leg, three-pass form (create_proof at k = 23 transforms 2^25) (0 = skip)")
     ap.add_argument("--accum-batch", type=int, default=256, help="proofs per GPU for the accumulator leg (0 = skip)")
     ap.add_argument("--accum-logn", type=int, default=17)
     ap.add_argument("--logn22", type=int, default=1,
@@ -220,6 +222,12 @@ def main():
         del s23, b23
     torch.cuda.empty_cache()
     ntt = run_ntt(args, ctx, dist, dev, world) if args.ntt_logn > 0 else None
+    # the extended-domain size of create_proof at k = 23 (three passes); its
+    # parity is tests/test_ntt_gpu.py (three-pass form vs the oracle, 2^25
+    # properties), no CPU leg
+    ntt_big = run_ntt(args, ctx, dist, dev, world, k=args.ntt_large_logn, keep_state=False) \
+        if args.ntt_large_logn > 0 else None
+    torch.cuda.empty_cache()
     accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
 
     if rank == 0:
@@ -251,6 +259,8 @@ def main():
             else:
                 ntt.pop("_state", None)
             out["ntt"] = ntt
+        if ntt_big is not None:
+            out[f"ntt_2^{args.ntt_large_logn}"] = ntt_big
         if accum is not None:
             if world == 1 and not args.no_cpu:
                 accum["cpu_baseline"] = accum_cpu_baseline(*accum.pop("_state"), budget_s=8.0)
@@ -510,7 +520,7 @@ def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, wan
     return out
 
 
-def run_ntt(args, ctx, dist, dev, world):
+def run_ntt(args, ctx, dist, dev, world, k=None, keep_state=True):
     """NTT over the BN254 scalar field (halo2 best_fft): one step
     = one in-place pm_fft_device of 2^k HBM-resident elements per rank
     (independent transforms, weak scaling; the omega table is built in the
@@ -521,7 +531,7 @@ def run_ntt(args, ctx, dist, dev, world):
     import halo2_amd as H
     import workloads as Wk
 
-    curve, k = H.BN254, args.ntt_logn
+    curve, k = H.BN254, (k or args.ntt_logn)
     n = 1 << k
     r = H.SCALAR_MODULUS[curve]
     wv = Wk.domain_omega(curve, k) * (1 << 256) % r
@@ -529,7 +539,7 @@ def run_ntt(args, ctx, dist, dev, world):
     a = torch.empty((n, 4), dtype=torch.int64, device=dev)
     ctx.synth_scalars(curve, 0x77, 0, n, a.data_ptr())
     torch.cuda.synchronize()
-    src = a.cpu().numpy().view(np.uint64).copy() if args.gpus == 1 or world == 1 else None
+    src = a.cpu().numpy().view(np.uint64).copy() if keep_state and (args.gpus == 1 or world == 1) else None
     ctx.fft_device(curve, a.data_ptr(), k, w)
     first = a.cpu().numpy().view(np.uint64).copy() if src is not None else None
     def step():
@@ -547,24 +557,25 @@ def run_ntt(args, ctx, dist, dev, world):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernels = kernel_breakdown(ctx, step, ("ntt_cols", "ntt_rows"))
+    kernels = kernel_breakdown(ctx, step, ("ntt_cols", "ntt_mid", "ntt_rows"))
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed * 1e3 / args.steps
-    gpu_ms = kernels["ntt_cols"] + kernels["ntt_rows"]
-    # algorithmic bytes: read + write every 32-B element once; the two-pass
-    # four-step form moves each element twice (4 x 32 B) through HBM
+    gpu_ms = kernels["ntt_cols"] + kernels["ntt_mid"] + kernels["ntt_rows"]
+    passes = 3 if kernels["ntt_mid"] else 2
+    # algorithmic bytes: read + write every 32-B element once; the four-step
+    # form moves each element once per pass (2 x 32 B per pass) through HBM
     alg = 2 * 32 * n
     out = {"metric": f"NTT 2^{k} over the BN254 scalar field (halo2 best_fft)", "value": round(world * n / (ms * 1e-3) / 1e6, 1),
            "unit": "Melem/s", "ms_per_ntt": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-           "kernels_ms": kernels,
+           "passes": passes, "kernels_ms": kernels,
            "roofline": {"bound": "hbm", "achieved": round(alg / (gpu_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": load_ntt_traffic(f"ntt_bn254_2^{k}"),
-                        "note": "achieved = 64 B/element (read + write once) over both passes' kernel time; "
-                                "traffic = PMC FETCH+WRITE of both passes (profiles/pmc_ntt.json); the NTT is "
+                        "note": "achieved = 64 B/element (read + write once) over all passes' kernel time; "
+                                "traffic = PMC FETCH+WRITE of all passes (profiles/pmc_ntt.json); the NTT is "
                                 "VALU-bound (n/2 log n Montgomery products)"}}
     if src is not None:
         out["_state"] = (curve, k, src, w, first)

@@ -347,6 +347,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_GROUPS")) c->groups = std::atoi(e);
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
+  if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_GLV")) c->glv = std::atoi(e) != 0;
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("PM_FINE_CACHE")) c->fine_cache = std::max(0, std::atoi(e));
@@ -654,7 +655,7 @@ int pm_fft_device(pm_ctx* ctx, int curve, void* d_data, uint32_t log_n, const ui
   if (!ctx || !d_data || !omega) return set_error(PM_ERR_ARG, "null argument");
   const CurveOps* ops = curve_ops(curve);
   if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
-  if (log_n > 24) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^24");
+  if (log_n > pm::kNttMaxLog) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^28");
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();
   if (rc) return rc;
@@ -665,7 +666,7 @@ int pm_fft(pm_ctx* ctx, int curve, uint64_t* data, uint32_t log_n, const uint64_
   if (!ctx || !data || !omega) return set_error(PM_ERR_ARG, "null argument");
   const CurveOps* ops = curve_ops(curve);
   if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
-  if (log_n > 24) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^24");
+  if (log_n > pm::kNttMaxLog) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^28");
   std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = ctx->begin_call();
   if (rc) return rc;

@@ -59,11 +59,21 @@ inline int ntt_twiddles_lookup(Ctx* ctx, int curve, uint32_t logn, const uint64_
   return PM_OK;
 }
 
+// passes over HBM: one up to 2^7 (one LDS transform), two up to 2^22 (four
+// steps, factors <= 2^11), three above (factors <= 2^10: at 2^23 / 2^24 the
+// two-pass form's 2^12-point transforms need 128 KiB of LDS, one block per
+// CU).  PM_NTT_PASSES (2 or 3) overrides for 2^15 <= n (diagnostics).
+inline int ntt_passes(const Ctx* ctx, uint32_t logn) {
+  if (ctx->ntt_passes == 2 && logn <= 2 * (uint32_t)kNttMaxLogL) return 2;
+  if (ctx->ntt_passes == 3 && logn >= 15) return 3;
+  return logn <= 22 ? 2 : 3;
+}
+
 template <class Cv>
 int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint64_t omega[4],
                     const uint64_t* scale) {
   using Fs = typename Cv::Scalar;
-  if (logn > 2 * kNttMaxLogL) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^24");
+  if (logn > kNttMaxLog) return set_error(PM_ERR_UNSUPPORTED, "NTT longer than 2^28");
   if (logn == 0) {
     if (scale) {  // a_0 *= scale
       // a one-element transform is the identity; apply the scale on the host
@@ -100,7 +110,7 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
                                                    ((size_t)1 << std::min<uint32_t>(logn, 8)) * 32, st>>>(
                                      data, data, (int)logn, 0, (int)std::min<uint32_t>(logn, 8), tw, sc, 1u)));
     }
-  } else {
+  } else if (ntt_passes(ctx, logn) == 2) {
     const int log1 = (int)(logn + 1) / 2, log2 = (int)logn - log1;
     const int logC = std::max(0, std::min(2, 11 - log1)), logR = std::max(0, std::min(2, 11 - log2));
     if ((rc = ctx->ntt_scratch.ensure(n * 32))) return rc;
@@ -110,6 +120,23 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
                                    data, tmp, (int)logn, log1, logC, tw)));
     PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)((size_t)1 << (log1 - logR)), kNttThreads, ldsB, st>>>(
                                    tmp, data, (int)logn, log2, logR, tw, sc, scale ? 1u : 0u)));
+  } else {
+    // three passes (k_ntt_kernels.hpp: k_ntt_mid), factors of at most 2^10,
+    // through two scratch buffers (the middle pass permutes rows)
+    const int log1 = (int)(logn + 2) / 3, loga = ((int)logn - log1 + 1) / 2, logb = (int)logn - log1 - loga;
+    const int logC = std::max(0, std::min(2, 11 - log1)), logM = std::max(0, std::min(2, 11 - loga)),
+              logR = std::max(0, std::min(2, 11 - logb));
+    if ((rc = ctx->ntt_scratch.ensure(n * 32)) || (rc = ctx->ntt_scratch2.ensure(n * 32))) return rc;
+    uint32_t* tmp = (uint32_t*)ctx->ntt_scratch.p;
+    uint32_t* tmp2 = (uint32_t*)ctx->ntt_scratch2.p;
+    const size_t ldsA = ((size_t)1 << (log1 + logC)) * 32, ldsM = ((size_t)1 << (loga + logM)) * 32,
+                 ldsB = ((size_t)1 << (logb + logR)) * 32;
+    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)(n >> (log1 + logC)), kNttThreads, ldsA, st>>>(
+                                   data, tmp, (int)logn, log1, logC, tw)));
+    PM_LAUNCH(ctx, "ntt_mid", (k_ntt_mid<Fs><<<(unsigned)(n >> (loga + logM)), kNttThreads, ldsM, st>>>(
+                                  tmp, tmp2, (int)logn, log1, loga, logM, tw)));
+    PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> (logb + logR)), kNttThreads, ldsB, st>>>(
+                                   tmp2, data, (int)logn, logb, logR, tw, sc, scale ? 1u : 0u)));
   }
   HIP_TRY(hipStreamSynchronize(st));
   ctx->end_call();

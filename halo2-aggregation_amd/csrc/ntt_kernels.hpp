@@ -197,6 +197,42 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, ui
   }
 }
 
+// Three-pass form (n = n1 * na * nb, every factor <= 2^10, for n >= 2^23):
+// pass A is k_ntt_cols with n2 = na * nb; the middle pass (k_ntt_mid) runs
+// the row NTTs of length n2 (root omega^{n1}) as a four-step of their own:
+// for every row k1 and column ib of the row's na x nb matrix, the na-point
+// NTT over ia (root omega^{n1 nb}), times omega^{n1 ib ka}, stored at
+// [(ka n1 + k1) nb + ib] so that pass B (k_ntt_rows over the n1 na rows of
+// length nb, root omega^{n1 na}) writes out[k1 + n1 ka + n1 na kb] =
+// out[k1 + n1 k2] with k2 = ka + na kb: the natural order.
+template <class Fs>
+__global__ void __launch_bounds__(kNttThreads) k_ntt_mid(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                         int logn, int log1, int loga, int logC,
+                                                         const uint32_t* __restrict__ tw) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  const int logb = logn - log1 - loga;
+  const uint32_t n1 = 1u << log1, na = 1u << loga, nb = 1u << logb, C = 1u << logC, half = 1u << (logn - 1);
+  const uint32_t plane = na << logC;
+  const uint32_t groups = nb >> logC;  // column groups per row
+  const uint32_t blk = ntt_block(n1 * groups);
+  const uint32_t k1 = blk / groups, col0 = (blk - k1 * groups) << logC;
+  const uint32_t* row = in + 8ull * ((size_t)k1 << (loga + logb));
+  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
+    const uint32_t ia = e >> logC, c = e & (C - 1);
+    const Fe<Fs> v = load_fe4<Fs>(reinterpret_cast<const uint4*>(row + 8ull * ((size_t)ia * nb + col0 + c)));
+    lds_st<Fs>(sm, plane, (ntt_brev(ia, loga) << logC) | c, v);
+  }
+  __syncthreads();
+  if (PM_NTT_RADIX4) lds_ntt4<Fs>(sm, loga, logC, n1 * nb, tw);  // root omega^{n1 nb}
+  else lds_ntt<Fs>(sm, loga, logC, n1 * nb, tw);
+  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
+    const uint32_t ka = e >> logC, c = e & (C - 1), ib = col0 + c;
+    Fe<Fs> v = lds_ld<Fs>(sm, plane, e);
+    if (ib && ka) v = fe_mul<Fs>(v, tw_full<Fs>(tw, n1 * ib * ka, half));  // n1 ib ka < n
+    store_fe4<Fs>(reinterpret_cast<uint4*>(out + 8ull * (((size_t)ka * n1 + k1) * nb + ib)), v);
+  }
+}
+
 // pass B: R = 2^logR adjacent rows per block; optional output scale
 template <class Fs>
 __global__ void __launch_bounds__(kNttThreads) k_ntt_rows(const uint32_t* in, uint32_t* out,  // may alias (log2 = 0)

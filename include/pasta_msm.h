@@ -330,9 +330,11 @@ int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_sca
  * a_k <- sum_j a_j omega^{jk} over the scalar field of `curve` (Montgomery
  * 4 x u64 per element, like pm_msm's scalars).  omega must be a primitive
  * 2^log_n-th root of unity.  scale (may be NULL) multiplies every output:
- * EvaluationDomain::ifft is pm_fft(omega_inv, scale = 1/n).  log_n <= 24;
- * the omega^i table is cached in the context (4 most recent (curve, log_n,
- * omega)). */
+ * EvaluationDomain::ifft is pm_fft(omega_inv, scale = 1/n).  log_n <= 28
+ * (create_proof at k = 23 transforms the extended domain, 2^25); above 2^22
+ * the transform takes three passes and 2 n x 32 B of context scratch.  The
+ * omega^i table (n/2 x 32 B) is cached in the context (4 most recent
+ * (curve, log_n, omega)). */
 int pm_fft(pm_ctx* ctx, int curve, uint64_t* data, uint32_t log_n, const uint64_t omega[4], const uint64_t* scale);
 int pm_fft_device(pm_ctx* ctx, int curve, void* d_data, uint32_t log_n, const uint64_t omega[4],
                   const uint64_t* scale);

@@ -1,7 +1,9 @@
 """GPU parity tests of the NTT (pm_fft*) against the oracle (oracle/ntt.py):
 golden vectors, every length 2^0 .. 2^14 on every field, scale (ifft),
-device pointers, and at 2^20 / 2^22 / 2^24 the size-independent properties:
-ifft(fft(a)) == a, linearity, and spot outputs A_k = sum_j a_j omega^{jk}."""
+device pointers, the three-pass form (forced at 2^15 .. 2^17) against the
+oracle, and at 2^20 / 2^22 / 2^23 / 2^24 / 2^25 the size-independent
+properties: ifft(fft(a)) == a, A_0, A_{n/2}, linearity, and spot outputs
+A_k = sum_j a_j omega^{jk}."""
 import json
 import os
 import random
@@ -52,7 +54,32 @@ def test_every_length_vs_oracle(gpu_ctx, cid):
         assert np.array_equal(back, arr), k
 
 
-@pytest.mark.parametrize("k", [20, 22, 24])
+@pytest.mark.parametrize("cid", [0, 1, 2])
+def test_three_pass_vs_oracle(gpu_ctx, cid):
+    """The three-pass form (k_ntt_cols, k_ntt_mid, k_ntt_rows; the default
+    above 2^22) forced at small sizes, factor shapes (5,5,5), (6,5,5), (6,6,5),
+    against the oracle, with the ifft round trip."""
+    os.environ["PM_NTT_PASSES"] = "3"
+    try:
+        ctx3 = H.Context(gpu_ctx.device)
+    finally:
+        del os.environ["PM_NTT_PASSES"]
+    r = P.CURVES[cid].r
+    for k in (15, 16, 17):
+        n = 1 << k
+        rng = random.Random(7000 * cid + k)
+        a = [rng.randrange(r) for _ in range(n)]
+        w = A.domain_omega(r, k)
+        want = N.serial_fft(list(a), w, k, r)
+        arr = np.array([mont(r, v) for v in a], dtype=np.uint64).reshape(n, 4)
+        got = ctx3.fft(cid, arr, np.array(mont(r, w), np.uint64))
+        assert np.array_equal(got, np.array([mont(r, v) for v in want], dtype=np.uint64).reshape(n, 4)), k
+        back = ctx3.fft(cid, got, np.array(mont(r, pow(w, -1, r)), np.uint64),
+                        scale=np.array(mont(r, pow(n, -1, r)), np.uint64))
+        assert np.array_equal(back, arr), k
+
+
+@pytest.mark.parametrize("k", [20, 22, 23, 24, 25])
 def test_large_properties(gpu_ctx, k):
     import torch
 

@@ -1,4 +1,5 @@
-"""Per-kernel timing of the NTT (pm_fft_device) at several sizes (diagnostic)."""
+"""Per-kernel timing of the NTT (pm_fft_device) at several sizes (diagnostic;
+PM_NTT_PASSES=2/3 forces the pass count)."""
 import json
 import os
 import sys
@@ -12,7 +13,7 @@ import torch  # noqa: E402
 import halo2_amd as H  # noqa: E402
 import workloads as Wk  # noqa: E402
 
-KERNELS = ["ntt_twiddles", "ntt_cols", "ntt_rows"]
+KERNELS = ["ntt_twiddles", "ntt_cols", "ntt_mid", "ntt_rows"]
 
 
 def mont(r, v):
@@ -43,10 +44,11 @@ def main():
             ctx.fft_device(curve, a.data_ptr(), k, w)
         ctx.set_timing(False)
         ks = {kk: round(ctx.kernel_stats(kk)[1] / reps, 4) for kk in KERNELS}
-        gpu_ms = ks["ntt_cols"] + ks["ntt_rows"]
-        print(json.dumps({"curve": curve, "log_n": k, "wall_ms": round(wall * 1e3, 4),
+        gpu_ms = ks["ntt_cols"] + ks["ntt_mid"] + ks["ntt_rows"]
+        passes = 3 if ks["ntt_mid"] else 2
+        print(json.dumps({"curve": curve, "log_n": k, "passes": passes, "wall_ms": round(wall * 1e3, 4),
                           "Melem_s": round(n / wall / 1e6, 1), "kernels_ms": ks,
-                          "hbm_GBs_2pass": round(4 * 32 * n / (gpu_ms * 1e-3) / 1e9, 1) if gpu_ms else None}),
+                          "hbm_GBs": round(2 * passes * 32 * n / (gpu_ms * 1e-3) / 1e9, 1) if gpu_ms else None}),
               flush=True)
 
 
