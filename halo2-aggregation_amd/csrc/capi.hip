@@ -348,6 +348,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
+  if (const char* e = std::getenv("PM_SEGQ")) c->segq = std::atoi(e);
   if (const char* e = std::getenv("PM_GLV")) c->glv = std::atoi(e) != 0;
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("PM_FINE_CACHE")) c->fine_cache = std::max(0, std::atoi(e));

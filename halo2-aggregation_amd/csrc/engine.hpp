@@ -311,6 +311,10 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
                                     (const uint32_t*)mid, bofs, gm, Wr, pl.NB, cache_n, offsets, sorted)));
   const bool prefetch = ctx->prefetch >= 0 ? ctx->prefetch != 0 : (size_t)n * 64 > kPrefetchBytes;
   const unsigned ablocks = (pl.nthreads + 255) / 256;
+  // chains + segment sums in one quad-cooperative kernel (k_bucket_seg_q);
+  // PM_SEGQ=0: the separate k_fixup* + k_bucket_seg (A/B)
+  static_assert(kL1 == (int)kSegQ, "k_bucket_seg_q takes one quad per segment");
+  const bool segq = ctx->segq != 0;
   // bit sums of few windows (fixed-base: one bucket set) are split over
   // more blocks.  Every extra lane also adds one tree addition, so the split
   // stops at ~16 blocks per job (c = 20, 2^19 buckets: 16 -> 0.33 ms,
@@ -337,28 +341,39 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     if (prefetch)
       PM_LAUNCH(ctx, "accumulate",
                 (k_accumulate<F, true><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg,
-                                                                 pl.nthreads, bucket_fixup ? nullptr : longs, nlong, shorts, nshort)));
+                                                                 pl.nthreads, (bucket_fixup && !segq) ? nullptr : longs, nlong,
+                                                                 segq ? nullptr : shorts, nshort)));
     else
       PM_LAUNCH(ctx, "accumulate",
                 (k_accumulate<F, false><<<ablocks, 256, 0, st>>>(sorted, offsets, s0, s1, bases29, pl.chunk, buckets, hg,
-                                                                  pl.nthreads, bucket_fixup ? nullptr : longs, nlong, shorts, nshort)));
+                                                                  pl.nthreads, (bucket_fixup && !segq) ? nullptr : longs, nlong,
+                                                                 segq ? nullptr : shorts, nshort)));
     if (st2 != st) {
       HIP_TRY(hipEventRecord(gev[2 * gi], st));
       HIP_TRY(hipStreamWaitEvent(st2, gev[2 * gi], 0));
     }
-    PM_LAUNCH_ST(ctx, st2, "fixup", {
-      const uint32_t lblocks = std::min<uint32_t>(pl.maxlong, 256);
-      if (bucket_fixup) {  // merged buckets span ~W*n/2^(c-1)/chunk slices each: one lane per bucket
-        k_fixup<F><<<(s1 - s0 + 255) / 256, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg,
-                                                           longs, nlong);
-        k_fixup_long<F><<<lblocks, 256, 0, st2>>>(longs, nlong, buckets, hg);
-      } else {
-        k_fixup_short<F><<<ablocks + lblocks, 256, 0, st2>>>(shorts, nshort, buckets, hg, ablocks, longs, nlong);
-      }
-    });
-    PM_LAUNCH_ST(ctx, st2, "bucket_seg",
-                 (k_bucket_seg<F><<<(nw * pl.M1 + 255) / 256, 256, 0, st2>>>(offsets, buckets, w0, nw, pl.NB, pl.L1,
-                                                                               S, T)));
+    if (segq) {
+      // long chains (usually none) first, then chains + segment sums in one
+      PM_LAUNCH_ST(ctx, st2, "fixup",
+                   (k_fixup_long<F><<<std::min<uint32_t>(pl.maxlong, 256), 256, 0, st2>>>(longs, nlong, buckets, hg)));
+      PM_LAUNCH_ST(ctx, st2, "bucket_seg",
+                   (k_bucket_seg_q<F><<<(unsigned)((4ull * nw * pl.M1 + 255) / 256), 256, 0, st2>>>(
+                       offsets, s0, pl.chunk, pl.nthreads, buckets, hg, w0, nw, pl.NB, S, T)));
+    } else {
+      PM_LAUNCH_ST(ctx, st2, "fixup", {
+        const uint32_t lblocks = std::min<uint32_t>(pl.maxlong, 256);
+        if (bucket_fixup) {  // merged buckets span ~W*n/2^(c-1)/chunk slices each: one lane per bucket
+          k_fixup<F><<<(s1 - s0 + 255) / 256, 256, 0, st2>>>(offsets, s0, s1, pl.chunk, pl.nthreads, buckets, hg,
+                                                             longs, nlong);
+          k_fixup_long<F><<<lblocks, 256, 0, st2>>>(longs, nlong, buckets, hg);
+        } else {
+          k_fixup_short<F><<<ablocks + lblocks, 256, 0, st2>>>(shorts, nshort, buckets, hg, ablocks, longs, nlong);
+        }
+      });
+      PM_LAUNCH_ST(ctx, st2, "bucket_seg",
+                   (k_bucket_seg<F><<<(nw * pl.M1 + 255) / 256, 256, 0, st2>>>(offsets, buckets, w0, nw, pl.NB, pl.L1,
+                                                                                 S, T)));
+    }
     PM_LAUNCH_ST(ctx, st2, "bucket_bits",
                  (k_bucket_bits<F><<<dim3(NJ, nw, nsplit), kRedThreads, 0, st2>>>(S, T, w0, pl.M1, pl.NB2, G, nsplit,
                                                                                       bitsP, tickets)));

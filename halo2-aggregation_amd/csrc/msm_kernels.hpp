@@ -720,6 +720,7 @@ __global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restric
   uint32_t t_last = t;
   if (owned && bend > end) t_last = min((bend - 1 - base) / chunk, nthreads - 1);
   if (t_last - t > kMaxChain) longs[atomicAdd(nlong, 1u)] = LongChain{gb, t + 1, t_last};
+  if (!shorts) return;  // k_bucket_seg_q folds the short chains itself
   const bool sh = t_last > t && t_last - t <= kMaxChain;
   const uint64_t m = __ballot(sh);
   if (!m) return;
@@ -952,6 +953,51 @@ __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__
   }
   store_xyzz29<F>(&S[gid], s);
   store_xyzz29<F>(&T[gid], t);
+}
+
+// ---------------------------------------- 5 + 6. chains and segment sums
+// One quad per segment of kSegQ = 4 buckets: lane q folds bucket q's
+// slice-boundary chain (buckets[gb] plus head[t] of every later slice the
+// bucket reaches, as k_fixup; chains longer than kMaxChain were queued by
+// k_accumulate and folded into buckets[gb] by k_fixup_long before this
+// launch), then the quad shares the four sums and computes S = B0 + B1 + B2 +
+// B3 and T = B1 + 2 B2 + 3 B3 with quad-cooperative additions (coop29.hpp).
+// Replaces k_fixup_short + k_bucket_seg: one launch and one round trip of
+// the buckets less, and the segment's additions at ~half the latency.
+constexpr uint32_t kSegQ = 4;  // buckets per segment: a quad (= kL1, runtime.hpp)
+template <int K, class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_qbc(const Xyzz29<F>& p) {  // lane K's point, quad-wide
+  return Xyzz29<F>{qbc<K, F>(p.X), qbc<K, F>(p.Y), qbc<K, F>(p.ZZ), qbc<K, F>(p.ZZZ)};
+}
+template <class F>
+__global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restrict__ offsets, uint32_t s0,
+                                                      uint32_t chunk, uint32_t nthreads,
+                                                      const Xyzz<F>* __restrict__ buckets,
+                                                      const Xyzz<F>* __restrict__ head, int w0, int nw, int NB,
+                                                      Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T) {
+  const uint32_t M1 = (uint32_t)NB / kSegQ;
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = gl >> 2, q = gl & 3u;
+  if (g >= (uint32_t)nw * M1) return;  // whole quads
+  const size_t gid = (size_t)w0 * M1 + g;
+  const size_t slot = gid * kSegQ + q;  // w NB + j kSegQ + q
+  const uint32_t base = offsets[s0];
+  const uint32_t bs = offsets[slot], be = offsets[slot + 1];
+  Xyzz29<F> B = xyzz29_inf<F>();
+  if (bs != be) {
+    B = load_xyzz29<F>(&buckets[slot]);
+    const uint32_t tf = (bs - base) / chunk, tl = min((be - 1 - base) / chunk, nthreads - 1);
+    if (tl - tf <= kMaxChain)
+      for (uint32_t t = tf + 1; t <= tl; t++) B = xyzz29_add<F>(B, load_xyzz29<F>(&head[t]));
+  }
+  // broadcast each lane's sum only when it is consumed (fewer live points)
+  const Xyzz29<F> B3 = xyzz29_qbc<3, F>(B);
+  const Xyzz29<F> p23 = xyzz29_add_q<F>(xyzz29_qbc<2, F>(B), B3);
+  const Xyzz29<F> p123 = xyzz29_add_q<F>(xyzz29_qbc<1, F>(B), p23);
+  const Xyzz29<F> tv = xyzz29_add_q<F>(xyzz29_add_q<F>(p123, p23), B3);
+  const Xyzz29<F> sv = xyzz29_add_q<F>(xyzz29_qbc<0, F>(B), p123);
+  if (q == 0) store_xyzz29<F>(&S[gid], sv);
+  if (q == 1) store_xyzz29<F>(&T[gid], tv);
 }
 
 // ------------------------------------------------------ 7. bit sums

@@ -142,6 +142,7 @@ struct pm_ctx {
   int sort_fb = 0;    // fine bits of the two-level sort, 0 = auto (diagnostics: PM_SORT_FB env)
   int fine_cache = 0; // entries of the fine pass's LDS segment cache, 0 = auto (diagnostics: PM_FINE_CACHE env)
   int glv = 0;        // variable-base MSM in GLV mode (pm_ctx_set_glv, PM_GLV env): measured slower, off
+  int segq = 1;        // MSM chains + segment sums fused (k_bucket_seg_q) (diagnostics: PM_SEGQ env)
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;
