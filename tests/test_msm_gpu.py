@@ -307,3 +307,31 @@ def test_resident_row_table(gpu_ctx, curve):
             assert np.array_equal(got[j], gpu_ctx.msm_resident(rb, 0, L)), j
     finally:
         rb.release()
+
+
+@pytest.mark.parametrize("distinct", [0, 40])
+def test_separate_fixup_path(gpu_ctx, distinct):
+    """PM_SEGQ=0 (k_fixup_short + k_bucket_seg instead of k_bucket_seg_q, the
+    A/B alternative) gives the same MSM as the default, on random scalars and
+    on scalars from a small set (long chains)."""
+    import os
+
+    n = (1 << 17) + 99
+    s, b = _torch_inputs(gpu_ctx, 1, n)
+    if distinct:
+        s[:] = s[torch_idx(s, distinct)]
+    os.environ["PM_SEGQ"] = "0"
+    try:
+        ctx0 = H.Context(gpu_ctx.device)
+    finally:
+        del os.environ["PM_SEGQ"]
+    a = ctx0.msm_device(1, s.data_ptr(), b.data_ptr(), n)
+    assert np.array_equal(a, gpu_ctx.msm_device(1, s.data_ptr(), b.data_ptr(), n))
+    assert np.array_equal(a, msm_ref.best_multiexp(1, s.cpu().numpy().view(np.uint64),
+                                                   b.cpu().numpy().view(np.uint64)))
+
+
+def torch_idx(s, distinct):
+    import torch
+
+    return torch.arange(s.shape[0], device=s.device) % distinct
