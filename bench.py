@@ -272,6 +272,20 @@ def main():
         dist.destroy_process_group()
 
 
+def settle(step, seconds=0.3):
+    """Untimed steps for `seconds` before a leg's warmup: right after the
+    setup (input synthesis, base upload) the first ~0.1 s of MSMs ran ~5 %
+    slower than later ones in the same process (the GPU's clocks ramping up;
+    tools/bench_vs_loop.py), which three warmup steps do not cover."""
+    import torch
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        step()
+    torch.cuda.synchronize()
+
+
 def timed_steps(step, steps, warmup, dist, dev):
     """W untimed steps, then K steps between barrier + synchronize on both
     sides; returns (max-over-ranks seconds, last step's result)."""
@@ -335,6 +349,7 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     # timed region: HIP events only around the roofline kernel (every event
     # pair costs ~10 us of stream time on MI355X)
     if roofline:
+        settle(step)
         for _ in range(args.warmup):
             step()
         ctx.set_timing(True, only="accumulate")
