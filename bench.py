@@ -273,7 +273,8 @@ def main():
 
 
 def settle(step, seconds=0.3):
-    """Untimed steps for `seconds` before a leg's warmup: right after the
+    """Untimed local work (never a collective: ranks loop for different
+    counts) for `seconds` before a leg's warmup: right after the
     setup (input synthesis, base upload) the first ~0.1 s of MSMs ran ~5 %
     slower than later ones in the same process (the GPU's clocks ramping up;
     tools/bench_vs_loop.py), which three warmup steps do not cover."""
@@ -349,7 +350,8 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     # timed region: HIP events only around the roofline kernel (every event
     # pair costs ~10 us of stream time on MI355X)
     if roofline:
-        settle(step)
+        # local MSMs only: no collective, so ranks may settle for different counts
+        settle(lambda: ctx.msm_resident_device(rb, 0, d_s.data_ptr(), n) if n else None)
         for _ in range(args.warmup):
             step()
         ctx.set_timing(True, only="accumulate")
