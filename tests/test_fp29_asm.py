@@ -2,7 +2,8 @@
 computes the radix-2^29 Montgomery product a b 2^-261 mod p.
 
 The header is executed here by a small interpreter of exactly the constructs
-the generator emits (v_mad_u64_u32 chains, v_lshrrev_b64, and the C lines that
+the generator emits (v_mad_u64_u32 / v_mad_i64_i32 chains, v_lshrrev_b64 /
+v_ashrrev_i64, and the C lines that
 derive m_k / the output limbs from the accumulator's low word), with 64-bit
 wrap-around checks, so a generator bug is caught without a GPU.  The device
 self-test (tests/test_msm_gpu.py::test_radix29_field_selftest) checks the same
@@ -33,6 +34,7 @@ def _run(body, a, b=None, u=None, v=None):
     env = {"a.l": list(a), "b.l": list(b) if b is not None else None, "m": [0] * 9, "r.l": [0] * 9, "d": [0] * 8,
            "u.l": list(u) if u is not None else None, "v.l": list(v) if v is not None else None}
     acc = 0
+    signed = False
 
     def val(expr):
         expr = expr.strip()
@@ -47,22 +49,34 @@ def _run(body, a, b=None, u=None, v=None):
             ops = [val(x.split("(", 1)[1][:-1]) for x in re.findall(r'"[vs]"\([^)]*\)', ins)]
             for ins_text in text.split("\\n\\t"):
                 f = [x.strip() for x in ins_text.replace(",", " ").split()]
-                if f[0] == "v_mad_u64_u32":
+                if f[0] in ("v_mad_u64_u32", "v_mad_i64_i32"):
                     assert f[1] == "%0" and f[2] == "%1" and f[5] == "%0"
                     x = ops[int(f[3][1:]) - 2] if f[3].startswith("%") else int(f[3])
                     y = ops[int(f[4][1:]) - 2] if f[4].startswith("%") else int(f[4])
-                    assert x < 2 ** 32 and y < 2 ** 32
+                    if f[0] == "v_mad_i64_i32":  # signed 32 x 32 + signed 64
+                        x, y = (v - (1 << 32) if v >= 1 << 31 else v for v in (x % (1 << 32), y % (1 << 32)))
+                    else:
+                        assert 0 <= x < 2 ** 32 and 0 <= y < 2 ** 32
                     acc += x * y
-                    assert acc <= M64, "column overflow"
+                    # unsigned columns (additive form) or signed ones (subtractive)
+                    assert -(1 << 63) <= acc <= M64, "column overflow"
+                    assert not (signed and acc >= 1 << 63), "signed column overflow"
                 elif f[0] == "v_lshrrev_b64":
                     assert f[1:] == ["%0", "29", "%0"]
+                    assert acc >= 0
                     acc >>= 29
+                elif f[0] == "v_ashrrev_i64":
+                    assert f[1:] == ["%0", "29", "%0"]
+                    signed = True
+                    acc >>= 29  # Python's >> floors: arithmetic shift
                 else:
                     raise AssertionError(ins_text)
             continue
         c = cline
         if c.startswith("for (int i = 0; i < 8; i++) d[i] = a.l[i] << 1"):
             env["d"] = [(x << 1) & 0xFFFFFFFF for x in env["a.l"][:8]]
+        elif re.fullmatch(r"m\[\d\] = \(uint32_t\)acc & kM29", c):
+            env["m"][int(c[2])] = acc & M29  # two's complement low bits
         elif re.fullmatch(r"m\[\d\] = \(0u - \(uint32_t\)acc\) & kM29", c):
             env["m"][int(c[2])] = (-(acc & 0xFFFFFFFF)) & M29
         elif re.fullmatch(r"m\[\d\] = \(\(uint32_t\)acc \* \d+u\) & kM29", c):
@@ -73,6 +87,10 @@ def _run(body, a, b=None, u=None, v=None):
         elif c == "r.l[8] = (uint32_t)(acc >> 29)":
             assert acc >> 29 < 2 ** 32
             env["r.l"][8] = acc >> 29
+        elif re.fullmatch(r"r\.l\[8\] = \(uint32_t\)\(\(int64_t\)acc >> 29\) \+ \d+u", c):
+            top = (acc >> 29) + int(re.search(r"\+ (\d+)u", c).group(1))
+            assert 0 <= top < 2 ** 32
+            env["r.l"][8] = top
         elif not re.fullmatch(r"F29<\w+> r|uint32_t (m|d)\[\d\]|uint64_t acc = 0, c|\(void\)c|return r", c):
             raise AssertionError("unhandled line: " + c)
     return env["r.l"]
