@@ -30,6 +30,13 @@ def main():
     ctx.synth_scalars(curve, 0x5EED, 0, n, s.data_ptr())
     ctx.synth_bases(curve, 0xA11CE, 0, n, b.data_ptr())
     torch.cuda.synchronize()
+    # settle the GPU first (bench.py settle(): the first ~0.1 s ran ~5 % slow),
+    # else the N = 1 baseline is the cold one and every ratio is inflated
+    rb = ctx.upload_bases(curve, d_bases=b.data_ptr(), n=n)
+    t = time.perf_counter()
+    while time.perf_counter() - t < 0.5:
+        ctx.msm_resident_device(rb, 0, s.data_ptr(), n)
+    rb.release()
     base = None
     for N in (1, 2, 4, 8, 16):
         per_rank = []
