@@ -214,7 +214,14 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   uint32_t* dcoef = (uint32_t*)ctx->acc_coef.p;
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
   const size_t nterm = (size_t)B * T;
-  uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split : acc_auto_lanes(nterm, 3);
+  // The powers table (a quad per term) pays only while it fits one pass of
+  // the budget: beyond it the table's 127-doubling chains queue behind each
+  // other, while the one-lane GLV products still run in one pass (simple
+  // shape, T = 30: split 1.31 / 1.95 / 2.24 ms vs one-lane 1.54 / 1.57 /
+  // 1.58 ms at B = 1024 / 1536 / 2048, profiles/r02/xover).
+  uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split
+                 : (nterm << 2) > kAccLaneBudget ? 0u
+                                                 : acc_auto_lanes(nterm, 3);
   // 16 / 32 lanes per term only while the term additions still fit one wave
   // per SIMD (B = 16: k_acc_termadd 0.075 ms at 16 lanes, 0.061 at 32; B = 256
   // stays at 8 lanes: 0.129 ms, 16 lanes 0.138, 32 lanes 0.197:

@@ -19,7 +19,8 @@ def main():
     curve = int(os.environ.get("CURVE", "2"))
     ctx = H.Context(0)
     splits = [int(x) for x in os.environ.get("SPLITS", "-1").split(",")]
-    for split, shape, log_n, B in [(sp,) + c for sp in splits for c in [("simple", 14, 16), ("simple", 17, 256), ("simple", 17, 4096), ("rich", 17, 256)]
+    extra = [("simple", 17, int(b)) for b in os.environ.get("BATCHES", "").split(",") if b]
+    for split, shape, log_n, B in [(sp,) + c for sp in splits for c in [("simple", 14, 16), ("simple", 17, 256), ("simple", 17, 4096), ("rich", 17, 256)] + extra
                                           if os.environ.get("CASES", "all") == "all" or "%s:%d" % (c[0], c[2]) in
                                           os.environ["CASES"].split(",")]:
         ctx.set_accum_split(split)
