@@ -167,6 +167,19 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   prog.insert(prog.end(), qprog.begin(), qprog.end());
   h.p_termsrc = (uint32_t)prog.size();
   prog.insert(prog.end(), termsrc.begin(), termsrc.end());
+  // proof-point terms (the powers tables per proof) and each term's rank
+  // among them; VK terms use the per-VK tables (ctx->acc_vkpow)
+  std::vector<uint32_t> psrc, rank(termsrc.size(), 0u);
+  for (size_t t = 0; t < termsrc.size(); t++)
+    if ((termsrc[t] >> 28) == 0) {
+      rank[t] = (uint32_t)psrc.size();
+      psrc.push_back(termsrc[t]);
+    }
+  h.Tp = (uint32_t)psrc.size();
+  h.p_psrc = (uint32_t)prog.size();
+  prog.insert(prog.end(), psrc.begin(), psrc.end());
+  h.p_rank = (uint32_t)prog.size();
+  prog.insert(prog.end(), rank.begin(), rank.end());
 
   // --- constants (Montgomery)
   std::vector<uint32_t> cst;
@@ -213,15 +226,17 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   const uint32_t* dprog = (const uint32_t*)ctx->acc_prog.buf.p;
   uint32_t* dcoef = (uint32_t*)ctx->acc_coef.p;
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
-  const size_t nterm = (size_t)B * T;
-  // The powers table (a quad per term) pays only while it fits one pass of
-  // the budget: beyond it the table's 127-doubling chains queue behind each
-  // other, while the one-lane GLV products still run in one pass (simple
-  // shape, T = 30: split 1.31 / 1.95 / 2.24 ms vs one-lane 1.54 / 1.57 /
-  // 1.58 ms at B = 1024 / 1536 / 2048, profiles/r02/xover).
+  const size_t nterm = (size_t)B * T, nprf = (size_t)B * h.Tp;
+  // The powers tables (a quad per proof-point term) pay only while their
+  // chains stay within ~3/4 of the lane budget: beyond it the 127-doubling
+  // chains share SIMDs and queue, while the one-lane GLV products still run
+  // in one pass at a flat ~1.16 ms.  Simple shape, T = 30 of which 21 proof
+  // points, wall per batch (profiles/r02/vkt/): split 1.13 ms at B = 1024,
+  // 1.67 at 1536 against one-lane 1.54 / 1.57 (the old rule without VK
+  // tables, 4 B T <= budget: profiles/r02/xover/).
   uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split
-                 : (nterm << 2) > kAccLaneBudget ? 0u
-                                                 : acc_auto_lanes(nterm, 3);
+                 : 4 * (nprf << 2) > 3 * kAccLaneBudget ? 0u
+                                                        : acc_auto_lanes(nterm, 3);
   // 16 / 32 lanes per term only while the term additions still fit one wave
   // per SIMD (B = 16: k_acc_termadd 0.075 ms at 16 lanes, 0.061 at 32; B = 256
   // stays at 8 lanes: 0.129 ms, 16 lanes 0.138, 32 lanes 0.197:
@@ -238,14 +253,29 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   hipStream_t side = st;
   hipEvent_t up = nullptr, sc_done = nullptr;
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
-    if ((rc = ctx->acc_lad.ensure(nterm * kPowPos * kPowPoint * sizeof(uint4)))) return rc;
+    const size_t tab = (size_t)kPowPos * kPowPoint * sizeof(uint4), nvk = vk.size() / 8;
+    if ((rc = ctx->acc_lad.ensure(std::max<size_t>(nprf, 1) * tab))) return rc;
+    if ((rc = ctx->acc_vkpow.ensure(std::max<size_t>(nvk, 1) * tab))) return rc;
+    // per-VK tables: rebuilt (in the same launch, beside the proofs' chains)
+    // only when the curve or the VK points differ from the last build, or
+    // the buffer was reallocated
+    std::vector<uint64_t> key(vk);
+    key.push_back((uint64_t)F::MOD[1] << 32 | F::MOD[2]);  // the curve (its base field)
+    const bool vk_current = ctx->acc_vkpow_gen == ctx->acc_vkpow.gen && ctx->acc_vkpow_key == key;
+    const uint32_t nvk_build = vk_current ? 0u : (uint32_t)nvk;
     up = ctx->next_event();
     sc_done = ctx->next_event();
     if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(up, st));
-    PM_LAUNCH(ctx, "acc_ladder",
-              (k_acc_powers<Cv><<<(unsigned)((4 * nterm + 255) / 256), 256, kAccLadderFence, st>>>(
-                  h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, (uint4*)ctx->acc_lad.p)));
+    if (nprf + nvk_build > 0)
+      PM_LAUNCH(ctx, "acc_ladder",
+                (k_acc_powers<Cv><<<(unsigned)((4 * (nprf + nvk_build) + 255) / 256), 256, kAccLadderFence, st>>>(
+                    h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
+                    (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
+    if (!vk_current) {
+      ctx->acc_vkpow_key.swap(key);
+      ctx->acc_vkpow_gen = ctx->acc_vkpow.gen;
+    }
     side = ctx->red_stream;
     HIP_TRY(hipStreamWaitEvent(side, up, 0));
   }
@@ -269,7 +299,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     HIP_TRY(hipStreamWaitEvent(st, sc_done, 0));
     PM_LAUNCH(ctx, "acc_termmul",
               (k_acc_termadd<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
-                  h, dcoef, (const uint4*)ctx->acc_lad.p, lgS, dpart)));
+                  h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p, lgS, dpart)));
   } else {
     PM_LAUNCH(ctx, "acc_termmul",
               (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(

@@ -39,6 +39,10 @@ struct AccumHdr {
   uint32_t h_slot0, nh;
   // constant table (8 u32 per element, Montgomery)
   uint32_t c_user, c_delta, c_omega_eval, c_wpow, c_n;
+  // powers-of-two tables (split path): Tp proof-point terms; p_psrc: their
+  // point indices in slot order (Tp words); p_rank: T words, term t's rank
+  // among the proof-point terms (VK terms read the per-VK tables instead)
+  uint32_t Tp, p_psrc, p_rank;
 };
 
 template <class Fs>
@@ -411,6 +415,10 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_shfl_xor(const Xyzz29<F>& p, int m) 
 // steps: the additions-only form has a 15-doubling longer table chain but
 // ~40% fewer operations after it)
 //
+// The VK terms (fixed and sigma commitments, g1) have the same point in every
+// proof: their tables are built once per verifying key and cached in the
+// context (acc_vkpow), so only the proof commitments get a chain per proof.
+//
 // k_acc_powers: one quad per (proof, term) walks P, [2] P, ..., [2^127] P
 // (127 Jacobian doublings, coop29.hpp) and stores every point in XYZZ form
 // plus beta X: coordinates X, Y, ZZ, ZZZ, beta X (and a junk slot) of kPowWords
@@ -458,21 +466,31 @@ __device__ __forceinline__ void pow_store(uint4* o, const PowSites& ps, const Ja
   pow_st<F>(o + ps.ext, ext);
 }
 
+// Quad g < B Tp: proof b's proof-point term of rank tp (g = b Tp + tp) -> pw;
+// quad B Tp + v (v < nvk): VK point v -> pwv, the per-VK tables shared by
+// every proof of this and later batches (nvk = 0 when they are current).
 template <class Cv>
 __global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* __restrict__ prog,
                                                     const uint32_t* __restrict__ points,
-                                                    const uint32_t* __restrict__ vk, uint4* __restrict__ pw) {
+                                                    const uint32_t* __restrict__ vk, uint32_t nvk,
+                                                    uint4* __restrict__ pw, uint4* __restrict__ pwv) {
   using F = typename Cv::Base;
   using K = F29Consts<F>;
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = gl >> 2, q = gl & 3u;
-  if (g >= h.B * h.T) return;  // whole quads (4 B T lanes)
-  const uint32_t b = g / h.T, t = g - b * h.T;
-  const uint32_t src = prog[h.p_termsrc + t];
-  const uint32_t idx = src & 0x0FFFFFFFu;
-  const uint32_t* pp = (src >> 28) == 0 ? points + 16ull * ((size_t)h.npts * b + idx) : vk + 16ull * idx;
+  const uint32_t nprf = h.B * h.Tp;
+  if (g >= nprf + nvk) return;  // whole quads
+  const uint32_t* pp;
+  uint4* out;
+  if (g < nprf) {
+    const uint32_t b = g / h.Tp, tp = g - b * h.Tp;
+    pp = points + 16ull * ((size_t)h.npts * b + prog[h.p_psrc + tp]);
+    out = pw + (size_t)g * kPowPos * kPowPoint;
+  } else {
+    pp = vk + 16ull * (g - nprf);
+    out = pwv + (size_t)(g - nprf) * kPowPos * kPowPoint;
+  }
   const Aff<F> P = load_aff<F>(pp);
-  uint4* out = pw + (size_t)g * kPowPos * kPowPoint;
   const PowSites ps(q);
   const F29<F> one = f29_const<F>(K::ONE);
   if (aff_is_inf<F>(P)) {  // the identity (ZZ = 0) at every power
@@ -518,9 +536,10 @@ __device__ __forceinline__ void naf128(const uint32_t* k, uint32_t* nz, uint32_t
 // additions, cnt ~ 85) with full XYZZ additions; the next point's loads are
 // issued before each addition.  Then log2(S) butterfly steps; lane 0 stores.
 template <class Cv>
-__global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t* __restrict__ coef,
-                                                     const uint4* __restrict__ pw, uint32_t lgS,
-                                                     Xyzz<typename Cv::Base>* __restrict__ part) {
+__global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t* __restrict__ prog,
+                                                     const uint32_t* __restrict__ coef,
+                                                     const uint4* __restrict__ pw, const uint4* __restrict__ pwv,
+                                                     uint32_t lgS, Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   using K = F29Consts<F>;
@@ -547,7 +566,10 @@ __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t*
     }
     nz[w] = sel;
   }
-  const uint4* base = pw + (size_t)g * kPowPos * kPowPoint;
+  const uint32_t b = g / h.T, t = g - b * h.T;
+  const uint32_t src = prog[h.p_termsrc + t];
+  const uint4* base = (src >> 28) != 0 ? pwv + (size_t)(src & 0x0FFFFFFFu) * kPowPos * kPowPoint
+                                       : pw + ((size_t)b * h.Tp + prog[h.p_rank + t]) * kPowPos * kPowPoint;
   // pops this lane's lowest remaining digit and issues its loads
   auto next = [&](Xyzz29<F>& Q, uint32_t& negm) -> bool {
     uint32_t w = 8, m = 0, s = 0;

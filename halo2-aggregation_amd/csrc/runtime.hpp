@@ -151,8 +151,13 @@ struct pm_ctx {
   std::mutex mu;
   // workspace
   pm::Buf in_scalars, in_scalars2, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
-      win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, tr_canon, ntt_scratch2;
+      win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, tr_canon, ntt_scratch2,
+      acc_vkpow;
   pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
+  // accumulator: powers-of-two tables of the verifying key's points (fixed,
+  // sigma, g1), built once per (curve, VK) and reused by every later batch
+  std::vector<uint64_t> acc_vkpow_key;
+  uint64_t acc_vkpow_gen = ~0ull;  // acc_vkpow.gen when the tables were built
   std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;
@@ -175,7 +180,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow};
   }
   ~pm_ctx();
   int begin_call();

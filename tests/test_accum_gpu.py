@@ -192,3 +192,25 @@ def test_accum_batch_multi(gpu_ctx):
     for b in (0, 10):
         q, hh = A.pack_result(C, A.accumulate_msm(C, sh, proofs[b]))
         assert np.array_equal(q1[b], q) and np.array_equal(h1[b], hh)
+
+
+@pytest.mark.parametrize("lg", [2, 3])
+def test_vk_tables_follow_the_vk(gpu_ctx, lg):
+    """The per-VK powers tables (k_acc_powers' VK quads, cached in the
+    context) are rebuilt whenever the verifying key's points or the curve
+    change: alternate two VKs of the same shape on Pallas, then the same VK
+    bytes' shape on Vesta, and back, each call against the oracle."""
+    gpu_ctx.set_accum_split(lg)
+    try:
+        cases = [(0, 0xA1), (0, 0xB2), (0, 0xA1), (1, 0xA1), (0, 0xA1), (0, 0xA1)]
+        for cid, seed in cases:
+            C, sh, proofs = U.make_case(cid, "simple", 12, 3, seed)
+            ps = U.to_product_shape(cid, sh)
+            pts, scs, chs = A.pack_proofs(C, sh, proofs)
+            quads, h = gpu_ctx.accum_batch(ps, pts, scs, chs)
+            for b, pf in enumerate(proofs):
+                q, hh = A.pack_result(C, A.accumulate_msm(C, sh, pf))
+                assert np.array_equal(h[b], hh), (cid, seed, b)
+                assert np.array_equal(quads[b], q), (cid, seed, b)
+    finally:
+        gpu_ctx.set_accum_split(-1)
