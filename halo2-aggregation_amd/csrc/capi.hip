@@ -216,7 +216,11 @@ MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk, 
   pl.L1 = std::min(kL1, pl.K);
   pl.log2L1 = bit_length((uint32_t)pl.L1) - 1;
   pl.NB = ((pl.K + 1 + pl.L1 - 1) / pl.L1) * pl.L1;
-  pl.M1 = pl.NB / pl.L1;
+  // segments cover slots [0, K); the top bucket K (the only one past them)
+  // is folded by segment 0's unused slot-0 lane and reaches the host Horner
+  // on its own (weight K): K / L1 is a power of two, so the segment grids
+  // fill whole block rounds (2^20: 2048 blocks of k_bucket_seg_q, not 2049)
+  pl.M1 = pl.K / pl.L1;
   pl.NB2 = bit_length((uint32_t)(pl.M1 - 1));
   pl.n = (uint32_t)n;
   // window groups: the bucket reduction (+ host Horner) of group g runs while

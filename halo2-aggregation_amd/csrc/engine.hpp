@@ -124,7 +124,7 @@ constexpr int kGlvMinC = 12;  // below: the plain 256-bit pipeline (small n)
 // window geometry, the pinned slot its bit sums land in and its events.
 template <class F>
 struct MsmTail {
-  int G = 0, Wr = 0, NQ = 0, wpg = 1, base = 0, extra = 0, log2L1 = 0;
+  int G = 0, Wr = 0, NQ = 0, wpg = 1, base = 0, extra = 0, log2L1 = 0, cmax = 0;
   bool fixed = false, empty = true;
   const Xyzz<F>* hG = nullptr;  // pinned host slot
   std::vector<hipEvent_t> ev;    // 2 per window group
@@ -178,7 +178,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const size_t TOT = (size_t)Wr * pl.NB + 1;
   const size_t nW = (size_t)stride * pl.W;
   const int NJ = pl.NB2 + kTJobs;                        // bit-sum jobs per window
-  const int NQ = (pl.NB2 + kBitsFold - 1) / kBitsFold + 1;  // folded terms per window (host Horner)
+  // folded terms per window for the host Horner: bit folds, sum T, bucket K
+  const int NQ = (pl.NB2 + kBitsFold - 1) / kBitsFold + 2;
   SortGeom g{};  // histogram geometry (blocks of scalars)
   g.FB = std::max(0, pl.cmax - 1 - 8);
   // the fixed-base MSM's merged sort rows are W x longer: 4x more coarse bins
@@ -214,7 +215,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->bsum.ensure((size_t)nb * 4))) return rc;
   if ((rc = ctx->buckets.ensure((size_t)Wr * pl.NB * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->head.ensure((size_t)pl.G * pl.nthreads * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->segS.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
+  if ((rc = ctx->segS.ensure((size_t)Wr * (pl.M1 + 1) * sizeof(Xyzz<F>)))) return rc;  // S, then Kb
   if ((rc = ctx->segT.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->bits.ensure((size_t)Wr * NJ * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->bitsQ.ensure((size_t)Wr * NQ * sizeof(Xyzz<F>)))) return rc;
@@ -234,6 +235,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   Xyzz<F>* buckets = (Xyzz<F>*)ctx->buckets.p;
   Xyzz<F>* head = (Xyzz<F>*)ctx->head.p;
   Xyzz<F>* S = (Xyzz<F>*)ctx->segS.p;
+  Xyzz<F>* Kb = S + (size_t)Wr * pl.M1;  // per window: the top bucket K, folded
   Xyzz<F>* T = (Xyzz<F>*)ctx->segT.p;
   Xyzz<F>* G = (Xyzz<F>*)ctx->bits.p;
   Xyzz<F>* Qb = (Xyzz<F>*)ctx->bitsQ.p;
@@ -358,7 +360,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
                    (k_fixup_long<F><<<std::min<uint32_t>(pl.maxlong, 256), 256, 0, st2>>>(longs, nlong, buckets, hg)));
       PM_LAUNCH_ST(ctx, st2, "bucket_seg",
                    (k_bucket_seg_q<F><<<(unsigned)((4ull * nw * pl.M1 + 255) / 256), 256, 0, st2>>>(
-                       offsets, s0, pl.chunk, pl.nthreads, buckets, hg, w0, nw, pl.NB, S, T)));
+                       offsets, s0, pl.chunk, pl.nthreads, buckets, hg, w0, nw, pl.NB, (uint32_t)pl.M1, S, T, Kb)));
     } else {
       PM_LAUNCH_ST(ctx, st2, "fixup", {
         const uint32_t lblocks = std::min<uint32_t>(pl.maxlong, 256);
@@ -371,14 +373,14 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
         }
       });
       PM_LAUNCH_ST(ctx, st2, "bucket_seg",
-                   (k_bucket_seg<F><<<(nw * pl.M1 + 255) / 256, 256, 0, st2>>>(offsets, buckets, w0, nw, pl.NB, pl.L1,
-                                                                                 S, T)));
+                   (k_bucket_seg<F><<<(nw * pl.M1 + 255) / 256, 256, 0, st2>>>(offsets, buckets, w0, nw, pl.NB, pl.M1, pl.L1,
+                                                                                 S, T, Kb)));
     }
     PM_LAUNCH_ST(ctx, st2, "bucket_bits",
                  (k_bucket_bits<F><<<dim3(NJ, nw, nsplit), kRedThreads, 0, st2>>>(S, T, w0, pl.M1, pl.NB2, G, nsplit,
                                                                                       bitsP, tickets)));
     PM_LAUNCH_ST(ctx, st2, "bits_combine",
-                 (k_bits_combine<F><<<(4 * nw * NQ + 63) / 64, 64, 0, st2>>>(G, w0, nw, pl.NB2, Qb)));
+                 (k_bits_combine<F><<<(4 * nw * NQ + 63) / 64, 64, 0, st2>>>(G, Kb, w0, nw, pl.NB2, Qb)));
     HIP_TRY(hipMemcpyAsync(hslot + (size_t)w0 * NQ, Qb + (size_t)w0 * NQ,
                            (size_t)nw * NQ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st2));
     HIP_TRY(hipEventRecord(gev[2 * gi + 1], st2));
@@ -391,6 +393,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   t.base = pl.base;
   t.extra = pl.extra;
   t.log2L1 = pl.log2L1;
+  t.cmax = pl.cmax;
   t.fixed = fixed;
   t.empty = false;
   t.hG = hslot;
@@ -433,7 +436,7 @@ __attribute__((target("bmi2,adx"))) void horner_steps_bmi2(host::Pt<F>& hacc, in
   }
 }
 
-// Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b}) as one
+// Host tail: sum_w 2^{o_w} (sum_j T_{w,j} + sum_b 2^{b+log2 L1} G_{w,b} + K B_{w,K}) as one
 // Horner over absolute bit positions q (host_ec.hpp), consumed group by group.
 template <class F>
 int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
@@ -443,8 +446,8 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
   }
   const int Wr = t.Wr, NQ = t.NQ, wpg = t.wpg;
   struct {
-    int G, base, extra, log2L1;
-  } pl{t.G, t.base, t.extra, t.log2L1};
+    int G, base, extra, log2L1, cmax;
+  } pl{t.G, t.base, t.extra, t.log2L1, t.cmax};
   const hipStream_t st = t.st, st2 = t.st2;
   const Xyzz<F>* hG = t.hG;
   // the terms as (position, index) sorted by descending position: one flat
@@ -455,7 +458,8 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
   for (int w = 0; w < Wr; w++) {
     const int o = w * pl.base + std::min(w, pl.extra);  // w < Wr: window w's offset (fixed, one set: 0)
     for (int b = 0; b < NQ; b++) {
-      const int q = b < NQ - 1 ? o + kBitsFold * b + pl.log2L1 : o;
+      // bit folds at o + 2b + log2 L1, sum T at o, the top bucket (K = 2^(cmax-1)) at o + cmax - 1
+      const int q = b < NQ - 2 ? o + kBitsFold * b + pl.log2L1 : b == NQ - 2 ? o : o + pl.cmax - 1;
       terms.emplace_back(q, w * NQ + b);
       gmax[w / wpg] = std::max(gmax[w / wpg], q);
     }

@@ -918,19 +918,24 @@ __global__ void __launch_bounds__(256) k_fixup_long(const LongChain* __restrict_
 }
 
 // ------------------------------------------------------ 6. segment sums
-// thread (w, j), w in [w0, w0 + nw): slots s = j*L1 + i, i in [0, L1):
-// S = sum B_s, T = sum i * B_s (0-based weight inside the segment).
+// thread (w, j), w in [w0, w0 + nw), j < M1 = K / L1: slots s = j*L1 + i,
+// i in [0, L1): S = sum B_s, T = sum i * B_s (0-based weight inside the
+// segment).  Thread (w, 0) also copies the top bucket K (slot K, after the
+// fixup) to Kb[w] for the host's K-weighted term.
 template <class F>
 __global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__ offsets,
                                                     const Xyzz<F>* __restrict__ buckets, int w0, int nw, int NB,
-                                                    int L1, Xyzz<F>* __restrict__ S,
-                                                    Xyzz<F>* __restrict__ T) {
-  const int M1 = NB / L1;
+                                                    int M1, int L1, Xyzz<F>* __restrict__ S,
+                                                    Xyzz<F>* __restrict__ T, Xyzz<F>* __restrict__ Kb) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nw * M1) return;
   const int gid = w0 * M1 + g;
   const int w = gid / M1, j = gid - w * M1;
   const size_t base = (size_t)w * NB + (size_t)j * L1;
+  if (j == 0) {
+    const size_t sk = (size_t)w * NB + (size_t)M1 * L1;  // slot K
+    store_xyzz29<F>(&Kb[w], offsets[sk] != offsets[sk + 1] ? load_xyzz29<F>(&buckets[sk]) : xyzz29_inf<F>());
+  }
   Xyzz29<F> s = xyzz29_inf<F>(), t = xyzz29_inf<F>();
   if (L1 == 4) {
     // S = B0 + B1 + B2 + B3 and T = B1 + 2 B2 + 3 B3 in 5 additions (the
@@ -969,18 +974,24 @@ template <int K, class F>
 __device__ __forceinline__ Xyzz29<F> xyzz29_qbc(const Xyzz29<F>& p) {  // lane K's point, quad-wide
   return Xyzz29<F>{qbc<K, F>(p.X), qbc<K, F>(p.Y), qbc<K, F>(p.ZZ), qbc<K, F>(p.ZZZ)};
 }
+// Segments cover slots [0, K) (M1 = K / kSegQ); the top bucket K is folded
+// by lane 0 of segment 0 instead of slot 0 (digit 0 has no bucket, and
+// whatever slot 0 holds has weight 0: S_0 enters no bit sum, T_0 weighs lane 0
+// by 0), and stored to Kb[w] for the host's K-weighted term.
 template <class F>
 __global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restrict__ offsets, uint32_t s0,
                                                       uint32_t chunk, uint32_t nthreads,
                                                       const Xyzz<F>* __restrict__ buckets,
                                                       const Xyzz<F>* __restrict__ head, int w0, int nw, int NB,
-                                                      Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T) {
-  const uint32_t M1 = (uint32_t)NB / kSegQ;
+                                                      uint32_t M1, Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T,
+                                                      Xyzz<F>* __restrict__ Kb) {
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = gl >> 2, q = gl & 3u;
   if (g >= (uint32_t)nw * M1) return;  // whole quads
   const size_t gid = (size_t)w0 * M1 + g;
-  const size_t slot = gid * kSegQ + q;  // w NB + j kSegQ + q
+  const uint32_t w = (uint32_t)(gid / M1), j = (uint32_t)(gid - (size_t)w * M1);
+  const bool top = j == 0 && q == 0;
+  const size_t slot = (size_t)w * NB + (top ? M1 * kSegQ : j * kSegQ + q);
   const uint32_t base = offsets[s0];
   const uint32_t bs = offsets[slot], be = offsets[slot + 1];
   Xyzz29<F> B = xyzz29_inf<F>();
@@ -998,6 +1009,7 @@ __global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restr
   const Xyzz29<F> sv = xyzz29_add_q<F>(xyzz29_qbc<0, F>(B), p123);
   if (q == 0) store_xyzz29<F>(&S[gid], sv);
   if (q == 1) store_xyzz29<F>(&T[gid], tv);
+  if (top) store_xyzz29<F>(&Kb[w], B);
 }
 
 // ------------------------------------------------------ 7. bit sums
@@ -1085,17 +1097,20 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
 // it saved on the host; 2 at a time halves the host's additions for ~2 ops.
 constexpr int kBitsFold = 2;
 template <class F>
-__global__ void __launch_bounds__(64) k_bits_combine(const Xyzz<F>* __restrict__ G, int w0, int nw, int NB2,
-                                                     Xyzz<F>* __restrict__ Q) {
+__global__ void __launch_bounds__(64) k_bits_combine(const Xyzz<F>* __restrict__ G, const Xyzz<F>* __restrict__ Kb,
+                                                     int w0, int nw, int NB2, Xyzz<F>* __restrict__ Q) {
   // a quad per output: quad-cooperative doubling / addition (coop29.hpp),
-  // then lane k converts coordinate k
-  const int NJ = NB2 + kTJobs, NQ = (NB2 + kBitsFold - 1) / kBitsFold + 1;
+  // then lane k converts coordinate k.  Per window: the bit folds, sum T
+  // (j = NQ - 2) and the top bucket K (j = NQ - 1)
+  const int NJ = NB2 + kTJobs, NQ = (NB2 + kBitsFold - 1) / kBitsFold + 2;
   const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2, lk = threadIdx.x & 3;
   if (gq >= nw * NQ) return;  // whole quads (blocks of 64 lanes hold 16 quads)
   const int w = w0 + gq / NQ, j = gq % NQ;
   const Xyzz<F>* gw = G + (size_t)w * NJ;
   Xyzz29<F> acc;
   if (j == NQ - 1) {
+    acc = load_xyzz29<F>(&Kb[w]);
+  } else if (j == NQ - 2) {
     acc = load_xyzz29<F>(&gw[NB2]);
     for (int t = 1; t < kTJobs; t++) acc = xyzz29_add_q<F>(acc, load_xyzz29<F>(&gw[NB2 + t]));
   } else {

@@ -73,7 +73,7 @@ struct MsmPlan {
   int L1;         // bucket-segment length of k_bucket_seg
   int log2L1;
   int NB;         // bucket slots per window (K+1 rounded up to L1)
-  int M1;         // segments per window
+  int M1;         // segments per window: K / L1 (slots [0, K); bucket K apart)
   int NB2;        // bits of the segment index
   uint32_t n;
   int G;              // window groups (pipelined, processed from the top window down)

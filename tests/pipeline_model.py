@@ -26,7 +26,7 @@ def make_plan(n, c_override=0, chunk_override=0, groups_override=0):
     K = 1 << (cmax - 1)
     L1 = min(4, K)
     NB = ((K + 1 + L1 - 1) // L1) * L1
-    M1 = NB // L1
+    M1 = K // L1  # segments cover slots [0, K); bucket K is a host term of its own
     NB2 = bit_length(M1 - 1)
     G = groups_override if groups_override > 0 else 1
     G = max(1, min(G, W))
@@ -172,10 +172,13 @@ def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0, groups_override
     for w in range(W):  # k_bucket_bits -> host Horner over absolute bit positions
         G = [sum(S[w * M1 + j] for j in range(M1) if (j >> b) & 1) % r for b in range(NB2)]
         sumT = sum(T[w * M1:(w + 1) * M1]) % r
+        sk = w * NB + M1 * L1  # the top bucket K (folded by segment 0's slot-0 lane)
+        bK = buckets[sk] if offsets[sk] != offsets[sk + 1] else 0
         o = sum(widths[:w])
         for b in range(NB2):
             at.setdefault(o + b + pl["log2L1"], []).append(G[b])
         at.setdefault(o, []).append(sumT)
+        at.setdefault(o + bit_length(pl["K"]) - 1, []).append(bK)
     acc = 0
     for q in range(max(at), -1, -1):
         acc = 2 * acc % r
