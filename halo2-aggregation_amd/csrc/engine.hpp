@@ -196,8 +196,23 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   while (g.ppt < kSortPerThread && stride >= (size_t)256 * g.ppt * kSortThreads) g.ppt *= 2;
   if (ctx->sort_ppt > 0 && !fixed) g.ppt = ctx->sort_ppt;  // PM_SORT_PPT (1, 2, 4, 8): tuning experiments
   g.nblk = (int)((stride + (size_t)g.ppt * kSortThreads - 1) / ((size_t)g.ppt * kSortThreads));
+  // The histogram pass is compute-bound per block (Montgomery -> canonical,
+  // W signed digits and LDS atomics per scalar); with 8192-point blocks 2^20
+  // gives 128 blocks for 256 CUs.  Split each coarse block's points over 2
+  // histogram blocks when the grid is short of the CUs: the coarse pass keeps
+  // its long runs and reads its start offsets at every hsub-th histogram
+  // block.  The scan doubles with it, so one split only (same box, 2^20:
+  // histogram 0.049-0.050 -> 0.035-0.041 ms, scan 0.014 -> 0.019 ms; below
+  // 128 blocks the scan's growth cancels the gain: 2^19 +-0, 2^18 +3-5 us,
+  // profiles/r02/hs/ab.txt and profiles/r02/p/ab.txt).
+  int hsub = 1;
+  if (ctx->sort_ppt == 0 && g.ppt >= 2 && g.nblk >= 128 && g.nblk < 256) hsub = 2;
+  g.hsub = 1;
   SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
+  g.ppt /= hsub;    // histogram geometry
+  g.nblk *= hsub;
   gm.nblk = g.nblk * kmerge;
+  gm.hsub = hsub;
   const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
   // 4-B coarse entries when the entry index fits beside the fine bits and the sign
   const bool wide = E > (size_t(1) << (31 - g.FB));
@@ -276,8 +291,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum, bofs, nullptr);
   });
   {
-    const size_t lds = (size_t)g.ppt * kSortThreads * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
-    const dim3 grid(gm.nblk, Wr);
+    const size_t lds = (size_t)gm.ppt * kSortThreads * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
+    const dim3 grid(gm.nblk / gm.hsub, Wr);
     void* dg = ctx->digits.p;
     const uint32_t ue = (uint32_t)E;
     if (d16 && !wide)

@@ -207,6 +207,7 @@ struct SortGeom {
   int NCB;   // coarse bins per window
   int nblk;  // point blocks of ppt * kSortThreads points
   int ppt;   // points per thread, <= kSortPerThread
+  int hsub;  // coarse geometry: histogram blocks per coarse block (bofs rows hold nblk histogram blocks)
   // words the histogram kernel zeroes for later stages (instead of two
   // hipMemsetAsync fills per call): the scan sentinel, and the chain-list
   // counters (4 words) of each window group
@@ -464,7 +465,7 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename Dig
   const uint32_t nvalid = lstart[g.NCB];
   for (uint32_t e = threadIdx.x; e < nvalid; e += kSortThreads) {
     const uint32_t cb = stage_cb[e];
-    const uint32_t pos = bofs[((size_t)w * g.NCB + cb) * g.nblk + blk] + (e - lstart[cb]);
+    const uint32_t pos = bofs[((size_t)w * g.NCB + cb) * g.nblk + (size_t)blk * g.hsub] + (e - lstart[cb]);
     mid[pos] = stage[e];
   }
 }
