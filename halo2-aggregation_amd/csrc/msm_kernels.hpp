@@ -621,8 +621,11 @@ __device__ __forceinline__ void glds_base(const uint32_t* g, uint4* lds_wave) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 4 * k),
                                      (__attribute__((address_space(3))) void*)(lds_wave + 64 * k), 16, 0, 0);
 }
+#ifndef PM_ACC_WAVES
+#define PM_ACC_WAVES 4  // waves per SIMD the register budget is sized for
+#endif
 template <class F, bool PREFETCH>
-__global__ void __launch_bounds__(256, 4) k_accumulate(const uint32_t* __restrict__ sorted,
+__global__ void __launch_bounds__(256, PM_ACC_WAVES) k_accumulate(const uint32_t* __restrict__ sorted,
                                                     const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
                                                     const uint32_t* __restrict__ bases, uint32_t chunk,
                                                     Xyzz<F>* __restrict__ buckets,
