@@ -72,3 +72,22 @@ def test_host_tail_adx_product(curve):
     if got is None:
         pytest.skip("CPU without BMI2/ADX")
     assert got == 0
+
+
+def test_missing_library_fails_loudly():
+    """The product path has no CPU fallback: without the HIP library every
+    entry point raises instead of computing (here: best_multiexp, the drop-in MSM)."""
+    import subprocess
+    import sys
+
+    code = ("import numpy as np, halo2_amd as H\n"
+            "try:\n"
+            "    H.best_multiexp(H.PALLAS, np.zeros((1, 4), np.uint64), np.zeros((1, 8), np.uint64))\n"
+            "except ImportError as e:\n"
+            "    print('ImportError:', e)\n"
+            "else:\n"
+            "    print('computed without the library')\n")
+    env = dict(os.environ, PM_LIB="/nonexistent/libpasta_msm.so",
+               PYTHONPATH=os.path.join(ROOT, "halo2-aggregation_amd"))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert "ImportError: libpasta_msm.so not built at /nonexistent" in r.stdout, r.stdout + r.stderr
