@@ -19,9 +19,9 @@ synthetic simple-example proofs and runs the batch multiopen accumulator on the
 replayed challenges (pm_accum_batch_transcript_device, SURVEY §8 rows
 a-3..a-9 + §8f-2; BN254, k = 17; weak scaling, proofs are independent),
 followed by an all-gather of the B x 4 accumulator points over RCCL.  Its
-cpu_baseline is the Python oracle (oracle/transcript.py + oracle/accum.py) on a
-bounded sample of the same proofs, with a bit-exact spot check of the GPU's
-challenges and results.
+cpu_baseline is the C restatement of the transcript replay + accumulator
+(oracle/accum_ref.c, all host threads) over the GPU's whole batch, with a
+bit-exact check of every proof's challenges, quad and h_eval.
 """
 import argparse
 import json
@@ -312,8 +312,8 @@ def timed_steps(step, steps, warmup, dist, dev):
     return elapsed, result
 
 
-MSM_KERNELS = ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg",
-               "bucket_bits", "bits_combine", "host_tail"]
+MSM_KERNELS = ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "bucket_seg",
+               "bucket_bits", "host_tail"]
 
 
 def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, n_total=None, check_port=False,
@@ -421,14 +421,12 @@ def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
     """The drop-in path a Rust best_multiexp shim takes:
     scalars in (pageable) host memory, bases resident -> pm_msm_resident.
     Reports the PCIe-inclusive rate and the scalar H2D time on its own
-    (HIP events around the copy), for the default plain pageable
-    hipMemcpyAsync and for the pinned staging through 4 copy threads."""
+    (HIP events around the copy, one pageable hipMemcpyAsync)."""
     import numpy as np
 
     S = d_s.cpu().numpy().view(np.uint64).copy()
     res = {}
-    for label, threads in (("pageable", 0), ("staged_4_threads", 4)):
-        ctx.set_h2d_threads(threads)
+    for label in ("pageable",):
         k = max(3, args.steps // 2)
         el, got = timed_steps(lambda: ctx.msm_resident(rb, 0, S), k, 1, None, dev)
         ctx.set_timing(True, only="h2d")
@@ -441,7 +439,6 @@ def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
         res[label] = {"ms_per_msm": round(el * 1e3 / k, 4), "Mscalar_s": round(n / (el / k) / 1e6, 3),
                       "scalar_h2d_ms": round(h2d, 4), "scalar_h2d_GBps": round(32 * n / (h2d * 1e-3) / 1e9, 2),
                       "matches": bool(np.array_equal(np.asarray(got), np.asarray(want)))}
-    ctx.set_h2d_threads(0)
     # the prover's commit of many polynomials: K MSMs per call
     # (pm_msm_resident_batch), the scalar copy of MSM j+1 and the host tail of
     # MSM j-1 overlapping MSM j's kernels
@@ -520,8 +517,7 @@ def run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, wan
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernels = kernel_breakdown(ctx, step, ["sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup",
-                                           "bucket_seg", "bucket_bits", "bits_combine", "host_tail"])
+    kernels = kernel_breakdown(ctx, step, MSM_KERNELS[1:])
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -252,6 +252,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // cross-stream wake-up on the critical path (profiles/r01_s4/ktrace_*).
   hipStream_t side = st;
   hipEvent_t up = nullptr, sc_done = nullptr;
+  std::vector<uint64_t> built_key;  // VK tables built by this call (committed after its final sync)
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
     const size_t tab = (size_t)kPowPos * kPowPoint * sizeof(uint4), nvk = vk.size() / 8;
     if ((rc = ctx->acc_lad.ensure(std::max<size_t>(nprf, 1) * tab))) return rc;
@@ -273,8 +274,11 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
                     h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
                     (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
     if (!vk_current) {
-      ctx->acc_vkpow_key.swap(key);
-      ctx->acc_vkpow_gen = ctx->acc_vkpow.gen;
+      // the tables count as built only once this call's work has completed
+      // (below): a failed launch or call leaves the cache invalid, so the next
+      // batch rebuilds them instead of reading unwritten tables
+      ctx->acc_vkpow_key.clear();
+      built_key.swap(key);
     }
     side = ctx->red_stream;
     HIP_TRY(hipStreamWaitEvent(side, up, 0));
@@ -315,6 +319,10 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
             (k_acc_sum<Cv><<<(unsigned)((B * 4 * (1u << lgL) + 63) / 64), 64, 0, st>>>(h, dpart, lgL,
                                                                                       (uint32_t*)d_out)));
   HIP_TRY(hipStreamSynchronize(st));
+  if (!built_key.empty()) {
+    ctx->acc_vkpow_key.swap(built_key);
+    ctx->acc_vkpow_gen = ctx->acc_vkpow.gen;
+  }
   ctx->end_call();
   return PM_OK;
 }

@@ -389,18 +389,6 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
   store_xyzz29<F>(&part[g], aff_is_inf<F>(P) ? xyzz29_inf<F>() : glv_mul<Cv>(c, P));
 }
 
-template <class F>
-__device__ __forceinline__ Xyzz29<F> xyzz29_shfl_xor(const Xyzz29<F>& p, int m) {
-  Xyzz29<F> r;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    r.X.l[i] = __shfl_xor(p.X.l[i], m, 64);
-    r.Y.l[i] = __shfl_xor(p.Y.l[i], m, 64);
-    r.ZZ.l[i] = __shfl_xor(p.ZZ.l[i], m, 64);
-    r.ZZZ.l[i] = __shfl_xor(p.ZZZ.l[i], m, 64);
-  }
-  return r;
-}
 
 // ------------------------------------------------------- powers-of-two table
 // At small batches one lane per term leaves most SIMDs idle and the term

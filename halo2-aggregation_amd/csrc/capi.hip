@@ -60,11 +60,6 @@ pm_ctx::~pm_ctx() {
   for (pm::Buf* b : all_bufs()) b->release();
   for (auto& t : ntt_tw) t.buf.release();
   if (h_pinned) (void)hipHostFree(h_pinned);
-  for (int t = 0; t < pm::kMaxStageThreads; t++) {
-    if (stage_pending[t]) (void)hipEventSynchronize(stage_ev[t]);
-    if (h_stage[t]) (void)hipHostFree(h_stage[t]);
-    if (stage_ev[t]) (void)hipEventDestroy(stage_ev[t]);
-  }
   for (auto& e : ev_pool) (void)hipEventDestroy(e);
   for (auto& e : grp_ev) (void)hipEventDestroy(e);
   for (auto& e : batch_ev)
@@ -118,11 +113,6 @@ int pm_ctx::ensure_group_events(int n) {
 int pm_ctx::ensure_pinned(size_t bytes) {
   if (bytes <= h_pinned_cap) return PM_OK;
   if (h_pinned) (void)hipHostFree(h_pinned);
-  for (int t = 0; t < pm::kMaxStageThreads; t++) {
-    if (stage_pending[t]) (void)hipEventSynchronize(stage_ev[t]);
-    if (h_stage[t]) (void)hipHostFree(h_stage[t]);
-    if (stage_ev[t]) (void)hipEventDestroy(stage_ev[t]);
-  }
   h_pinned = nullptr;
   h_pinned_cap = 0;
   HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocDefault));
@@ -137,49 +127,7 @@ int pm_ctx::upload_h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
     tb = next_event();
     HIP_TRY(hipEventRecord(ta, st));
   }
-  const int T = std::max(0, std::min(pm::kMaxStageThreads, h2d_threads));
-  if (T == 0 || bytes < (size_t(1) << 20)) {
-    HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
-  } else {
-    for (int t = 0; t < T; t++) {
-      if (!h_stage[t]) HIP_TRY(hipHostMalloc(&h_stage[t], pm::kStageChunk, hipHostMallocDefault));
-      if (!stage_ev[t]) HIP_TRY(hipEventCreateWithFlags(&stage_ev[t], hipEventDisableTiming));
-    }
-    const size_t nchunks = (bytes + pm::kStageChunk - 1) / pm::kStageChunk;
-    const int nt = (int)std::min<size_t>((size_t)T, nchunks);
-    std::vector<int> rcs(nt, PM_OK);
-    std::vector<std::string> errs(nt);
-    // thread t owns pinned buffer t and copies chunks t, t + nt, ...: refill
-    // after the DMA of its previous chunk (event), host memcpy, async DMA
-    auto worker = [&](int t) {
-      for (size_t k = t; k < nchunks; k += nt) {
-        const size_t off = k * pm::kStageChunk, len = std::min(pm::kStageChunk, bytes - off);
-        hipError_t e = hipSuccess;
-        if (stage_pending[t]) e = hipEventSynchronize(stage_ev[t]);
-        stage_pending[t] = false;
-        if (e == hipSuccess) {
-          std::memcpy(h_stage[t], (const char*)h + off, len);
-          e = hipMemcpyAsync((char*)d + off, h_stage[t], len, hipMemcpyHostToDevice, st);
-        }
-        if (e == hipSuccess) e = hipEventRecord(stage_ev[t], st);
-        if (e != hipSuccess) {
-          rcs[t] = PM_ERR_HIP;
-          errs[t] = std::string("staged H2D: ") + hipGetErrorString(e);
-          return;
-        }
-        stage_pending[t] = true;
-      }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; t++) th.emplace_back([&, t] {
-      (void)hipSetDevice(device);
-      worker(t);
-    });
-    worker(0);
-    for (auto& x : th) x.join();
-    for (int t = 0; t < nt; t++)
-      if (rcs[t]) return pm::set_error(rcs[t], errs[t]);
-  }
+  HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
   if (ta) {
     HIP_TRY(hipEventRecord(tb, st));
     mark("h2d", ta, tb);
@@ -199,7 +147,7 @@ static int bit_length(uint32_t v) {
   return b;
 }
 
-MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk, int nbits) {
+MsmPlan make_plan(size_t n, int c_override, int min_chunk) {
   MsmPlan pl;
   int lg = bit_length((uint32_t)std::max<size_t>(n, 1)) - 1;
   // auto window: lg - 2 from 2^14 up (capped at 16), lg - 4 below; swept on
@@ -208,9 +156,9 @@ MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk, 
   int c = c_override > 0 ? c_override : std::max(4, std::min(kAutoMaxC, lg >= 14 ? lg - 2 : lg - 4));
   c = std::max(kMinC, std::min(kMaxC, c));
   pl.c = c;
-  pl.W = (nbits + c - 1) / c;
-  pl.base = nbits / pl.W;
-  pl.extra = nbits % pl.W;
+  pl.W = (256 + c - 1) / c;
+  pl.base = 256 / pl.W;
+  pl.extra = 256 % pl.W;
   pl.cmax = pl.base + (pl.extra ? 1 : 0);
   pl.K = 1 << (pl.cmax - 1);
   pl.L1 = std::min(kL1, pl.K);
@@ -223,34 +171,26 @@ MsmPlan make_plan(size_t n, int c_override, int groups_override, int min_chunk, 
   pl.M1 = pl.K / pl.L1;
   pl.NB2 = bit_length((uint32_t)(pl.M1 - 1));
   pl.n = (uint32_t)n;
-  // window groups: the bucket reduction (+ host Horner) of group g runs while
-  // group g-1 accumulates.  Measured on MI355X (profiles/r01_s2/pipe2): no
-  // gain -- the reduction kernels compete with accumulate for the same VALU
-  // slots and each smaller accumulate launch loses occupancy -- so the
-  // default is one group (2^20: G=1 2.29 ms, G=2 2.43, G=4 2.95).
-  int G = groups_override > 0 ? groups_override : 1;
-  G = std::max(1, std::min(G, pl.W));
-  pl.wpg = (pl.W + G - 1) / G;
-  pl.G = (pl.W + pl.wpg - 1) / pl.wpg;
-  const size_t work = (size_t)n * pl.wpg;
+  // one window group: round 1 measured pipelined window groups (reduction of
+  // group g beside the accumulation of g-1) slower at every size -- the
+  // reduction kernels compete for the same VALU slots and each smaller
+  // accumulate launch loses occupancy (2^20: G=1 2.29 ms, G=2 2.43, G=4 2.95;
+  // profiles/r01_s2/pipe2) -- and round 3 retired them
+  const size_t work = (size_t)n * pl.W;
   const size_t target = 256 * 1024;  // lanes in flight: 256 CUs x 16 waves x 64
   const size_t mc = min_chunk > 0 ? (size_t)min_chunk : 16;
   pl.chunk = (uint32_t)std::max<size_t>(mc, (work + target - 1) / target);
   pl.nthreads = (uint32_t)((work + pl.chunk - 1) / pl.chunk);
-  pl.maxlong = (uint32_t)(work / ((size_t)kMaxChain * pl.chunk) + 1);
   return pl;
 }
 
 MsmPlan make_plan_fixed(size_t npad, int c, int min_chunk) {
-  MsmPlan pl = make_plan(npad, c, 1, min_chunk);
-  pl.G = 1;
-  pl.wpg = pl.W;
-  const size_t work = npad * pl.W;  // every window's entries in one bucket set
+  MsmPlan pl = make_plan(npad, c, min_chunk);
+  const size_t work = npad * pl.W;  // every window's entries
   const size_t target = 256 * 1024;
   const size_t mc = min_chunk > 0 ? (size_t)min_chunk : 16;
   pl.chunk = (uint32_t)std::max<size_t>(mc, (work + target - 1) / target);
   pl.nthreads = (uint32_t)((work + pl.chunk - 1) / pl.chunk);
-  pl.maxlong = (uint32_t)(work / ((size_t)kMaxChain * pl.chunk) + 1);
   return pl;
 }
 
@@ -317,7 +257,8 @@ bool valid_curve(int c) { return c == PM_CURVE_PALLAS || c == PM_CURVE_VESTA || 
 // ================================================================== C-ABI
 extern "C" {
 
-const char* pm_version(void) { return "pasta_msm 0.1 (gfx950)"; }
+const char* pm_version(void) { return "pasta_msm 0.3 (gfx950)"; }
+int pm_abi_version(void) { return PM_ABI_VERSION; }
 const char* pm_last_error(void) { return pm::g_last_error.c_str(); }
 
 int pm_device_count(int* count) {
@@ -347,16 +288,10 @@ int pm_ctx_create(int device, pm_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault));
   c->stream = c->own_stream;
   HIP_TRY(hipStreamCreateWithFlags(&c->red_stream, hipStreamNonBlocking));
-  if (const char* e = std::getenv("PM_PREFETCH")) c->prefetch = std::atoi(e);
-  if (const char* e = std::getenv("PM_GROUPS")) c->groups = std::atoi(e);
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
-  if (const char* e = std::getenv("PM_SEGQ")) c->segq = std::atoi(e);
-  if (const char* e = std::getenv("PM_GLV")) c->glv = std::atoi(e) != 0;
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
-  if (const char* e = std::getenv("PM_FINE_CACHE")) c->fine_cache = std::max(0, std::atoi(e));
-  if (const char* e = std::getenv("PM_H2D_THREADS")) c->h2d_threads = std::max(0, std::min(kMaxStageThreads, std::atoi(e)));
   if (const char* e = std::getenv("PM_SORT_PPT")) {
     const int v = std::atoi(e);
     c->sort_ppt = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
@@ -373,7 +308,12 @@ int pm_ctx_destroy(pm_ctx* ctx) {
 int pm_ctx_set_stream(pm_ctx* ctx, void* s) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  ctx->stream = (hipStream_t)s;  // NULL = the legacy null stream itself
+  // NULL = the context's own stream (the round-1 meaning, which callers
+  // compiled against that header rely on); PM_STREAM_LEGACY = the legacy
+  // null stream itself
+  if (s == nullptr) ctx->stream = ctx->own_stream;
+  else if (s == PM_STREAM_LEGACY) ctx->stream = nullptr;
+  else ctx->stream = (hipStream_t)s;
   return PM_OK;
 }
 
@@ -386,8 +326,7 @@ int pm_ctx_use_own_stream(pm_ctx* ctx) {
 
 int pm_ctx_set_glv(pm_ctx* ctx, int enable) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  ctx->glv = enable != 0;
+  if (enable) return set_error(PM_ERR_UNSUPPORTED, "GLV mode retired (measured slower on MI355X, DESIGN.md §7)");
   return PM_OK;
 }
 
@@ -409,10 +348,10 @@ int pm_ctx_set_window(pm_ctx* ctx, int c) {
 
 int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
-  if (groups < 0 || groups > 64 || min_chunk < 0 || min_chunk > (1 << 20))
-    return set_error(PM_ERR_ARG, "pipeline setting out of range");
+  if (groups < 0 || min_chunk < 0 || min_chunk > (1 << 20)) return set_error(PM_ERR_ARG, "pipeline setting out of range");
+  if (groups > 1)
+    return set_error(PM_ERR_UNSUPPORTED, "window groups retired (measured slower on MI355X, DESIGN.md §7)");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  ctx->groups = groups;
   ctx->min_chunk = min_chunk;
   return PM_OK;
 }
@@ -648,9 +587,9 @@ int pm_msm_resident_batch(pm_ctx* ctx, const pm_bases* b, size_t offset, const u
 
 int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
-  if (threads < 0 || threads > kMaxStageThreads) return set_error(PM_ERR_ARG, "h2d threads out of range (0..8)");
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  ctx->h2d_threads = threads;
+  if (threads < 0) return set_error(PM_ERR_ARG, "h2d threads out of range");
+  if (threads > 0)
+    return set_error(PM_ERR_UNSUPPORTED, "pinned staging threads retired (measured slower on MI355X, DESIGN.md §5)");
   return PM_OK;
 }
 

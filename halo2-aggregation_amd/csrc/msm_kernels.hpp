@@ -30,7 +30,6 @@
 #pragma once
 #include "coop29.hpp"
 #include "curve29.hpp"
-#include "glv.hpp"
 
 namespace pm {
 
@@ -240,32 +239,6 @@ __device__ __forceinline__ uint32_t signed_digit(const Fe<Fs>& s, int w, uint32_
   return d ? (d | (neg << 31)) : 0u;
 }
 
-// GLV mode: signed digit of window w of a 128-bit magnitude k (4 words,
-// |k| < 2^127 - 2^112 so the top window never carries), negated when `flip`.
-// A flipped scalar is recoded into [-2^(C-1), 2^(C-1) - 1] (negate when
-// d >= 2^(C-1)) so that after the flip every digit is in the usual
-// [-2^(C-1) + 1, 2^(C-1)]: the 2-byte digit code has no room for -2^15.
-template <int W>
-__device__ __forceinline__ uint32_t signed_digit128(const uint32_t k[4], int w, uint32_t& carry, uint32_t flip) {
-  using G = WinGeom<W, 128>;
-  const int C = G::width(w);
-  const int bit = G::offset(w);
-  const int limb = bit >> 5, sh = bit & 31;
-  const uint32_t lo = k[limb] >> sh;
-  const uint32_t hi = (sh != 0 && limb + 1 < 4) ? (k[limb + 1] << (32 - sh)) : 0u;
-  const uint32_t raw = (lo | hi) & ((1u << C) - 1u);
-  uint32_t d = raw + carry;
-  uint32_t neg = 0;
-  if (w != W - 1 && d + flip > (1u << (C - 1))) {
-    d = (1u << C) - d;
-    neg = 1;
-    carry = 1;
-  } else {
-    carry = 0;
-  }
-  return d ? (d | ((neg ^ flip) << 31)) : 0u;
-}
-
 template <class Fs>
 __device__ __forceinline__ Fe<Fs> load_canonical(const uint32_t* scalars, uint32_t i, uint32_t canonical) {
   Fe<Fs> s = load_fe4<Fs>(reinterpret_cast<const uint4*>(scalars + 8ull * i));
@@ -342,45 +315,6 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
     const size_t row = ((size_t)(w % Wr) * g.NCB + cb) * kmerge + w / Wr;
     bh[row * g.nblk + blockIdx.x] = hist[k];
   }
-}
-
-// GLV mode: sort entry v < n is (k1 of scalar v, base P_v), entry n + v is
-// (k2 of scalar v, base phi(P_v)); both scalars < 2^127 in W windows over
-// 128 bits (Babai-rounded split, glv.hpp), the split's signs folded into the
-// digit signs.  stride = 2n.
-template <class Cv, int W, bool D16>
-__global__ void __launch_bounds__(kSortThreads) k_sort_hist_glv(const uint32_t* __restrict__ scalars, uint32_t n,
-                                                                uint32_t canonical, SortGeom g,
-                                                                typename DigitCode<D16>::T* __restrict__ digits,
-                                                                uint32_t* __restrict__ bh, uint32_t stride) {
-  using Fs = typename Cv::Scalar;
-  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
-  const int nbins = W * g.NCB;
-  if (blockIdx.x == 0) sort_clear(g);
-  for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
-  __syncthreads();
-  for (int r = 0; r < g.ppt; r++) {
-    const uint32_t v = (blockIdx.x * g.ppt + r) * kSortThreads + threadIdx.x;
-    if (v >= stride) break;
-    const bool hi = v >= n;
-    const Fe<Fs> s = load_canonical<Fs>(scalars, hi ? v - n : v, canonical);
-    uint32_t k1[6], k2[6];
-    bool n1, n2;
-    glv_split<Cv, true>(s, k1, k2, n1, n2);
-    uint32_t k[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) k[i] = hi ? k2[i] : k1[i];
-    const uint32_t flip = (hi ? n2 : n1) ? 1u : 0u;
-    uint32_t carry = 0;
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      const uint32_t code = signed_digit128<W>(k, w, carry, flip);
-      digits[(size_t)w * stride + v] = DigitCode<D16>::enc(code);
-      if (code) atomicAdd(&hist[w * g.NCB + ((code & ~kNegBit) >> g.FB)], 1u);
-    }
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < nbins; k += kSortThreads) bh[(size_t)k * g.nblk + blockIdx.x] = hist[k];
 }
 
 // coarse-segment entry: WIDE = slot << 32 | index | sign << 31;
@@ -584,12 +518,13 @@ __global__ void __launch_bounds__(kFineThreads) k_sort_fine(const typename SortE
 }
 
 // ----------------------------------------------------------- 4. accumulate
-// One launch covers the windows [w0, w1) of a window group, i.e. the sorted
-// positions [offsets[s0], offsets[s1]) with s0 = w0*NB, s1 = w1*NB.  Slice t
-// covers positions [start + t*chunk, ...).  A bucket is *owned* by the slice
-// holding its first element; the owner writes its (possibly partial) sum to
-// buckets[]; a slice whose first bucket started in an earlier slice writes
-// that partial to head[t] for k_fixup.
+// One launch covers every bucket set: the sorted positions [offsets[0],
+// offsets[s1]) with s1 = Wr * NB.  Slice t covers positions [t*chunk, ...).
+// A bucket is *owned* by the slice holding its first element; the owner
+// writes its (possibly partial) sum to buckets[]; a slice whose first bucket
+// started in an earlier slice writes that partial to head[t], and
+// k_bucket_seg_q folds the chain buckets[gb] + head[t_first + 1 ..] of every
+// bucket (found from the offsets alone, so this kernel queues nothing).
 __device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ offsets, uint32_t lo, uint32_t hi,
                                                 uint32_t pos) {
   // largest gb in [lo, hi) with offsets[gb] <= pos
@@ -600,21 +535,17 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ off
   return lo;
 }
 
-// A bucket whose sorted run crosses slice boundaries is started by slice
-// t_first (which stores its partial in buckets[gb]); every later slice it
-// reaches stores its first partial in head[].  Chains up to kMaxChain slices
-// are folded serially (k_bucket_seg, or k_fixup for the fixed-base MSM);
-// longer ones (giant buckets: adversarial or highly repetitive scalars) are
-// queued for k_fixup_long, one workgroup per bucket with an LDS tree.
-constexpr uint32_t kMaxChain = 32;
-struct LongChain {
-  uint32_t gb, t_first, t_last;
-};
+// Chains up to kSerialChain later slices are folded by the bucket's own lane
+// in k_bucket_seg_q; longer ones (giant buckets: adversarial or highly
+// repetitive scalars, e.g. many scalars equal to 1) by the whole wave, one
+// chain at a time: a strided sum over 64 lanes and a butterfly.
+constexpr uint32_t kSerialChain = 8;
 
-// Base gather by LDS-DMA one entry ahead (PREFETCH): global_load_lds writes
-// the next entry's 64-B base straight into LDS (no VGPRs held across the
-// addition), so its L2 / Infinity Cache latency hides behind this entry's
-// mixed addition.  Per wave 4 KiB: [16-B chunk][lane].
+// Base gather by LDS-DMA one entry ahead: global_load_lds writes the next
+// entry's 64-B base straight into LDS (no VGPRs held across the addition), so
+// its L2 / Infinity Cache latency hides behind this entry's mixed addition.
+// Per wave 4 KiB: [16-B chunk][lane].  (The plain register-load form measured
+// slower at every size, round 2: profiles/r02/xp/.)
 __device__ __forceinline__ void glds_base(const uint32_t* g, uint4* lds_wave) {
 #pragma unroll
   for (int k = 0; k < 4; k++)
@@ -624,38 +555,34 @@ __device__ __forceinline__ void glds_base(const uint32_t* g, uint4* lds_wave) {
 #ifndef PM_ACC_WAVES
 #define PM_ACC_WAVES 4  // waves per SIMD the register budget is sized for
 #endif
-template <class F, bool PREFETCH>
+template <class F>
 __global__ void __launch_bounds__(256, PM_ACC_WAVES) k_accumulate(const uint32_t* __restrict__ sorted,
-                                                    const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
+                                                    const uint32_t* __restrict__ offsets, uint32_t s1,
                                                     const uint32_t* __restrict__ bases, uint32_t chunk,
                                                     Xyzz<F>* __restrict__ buckets,
-                                                    Xyzz<F>* __restrict__ head, uint32_t nthreads,
-                                                    LongChain* __restrict__ longs, uint32_t* __restrict__ nlong,
-                                                    LongChain* __restrict__ shorts, uint32_t* __restrict__ nshort) {
-  __shared__ uint4 sb[PREFETCH ? 4 * 4 * 64 : 1];
+                                                    Xyzz<F>* __restrict__ head) {
+  __shared__ uint4 sb[4 * 4 * 64];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t base = offsets[s0], total = offsets[s1];
+  const uint32_t base = offsets[0], total = offsets[s1];
   const uint32_t start = base + t * chunk;
   if (start >= total) return;
   const uint32_t end = min(start + chunk, total);
-  uint32_t gb = find_bucket(offsets, s0, s1, start);
+  uint32_t gb = find_bucket(offsets, 0, s1, start);
   uint32_t bend = offsets[gb + 1];
   bool owned = offsets[gb] == start;
   // acc is empty ("fresh") at a bucket start and after a cancellation; an
   // empty acc has ZZ = 0, so it stores as the identity
   Xyzz29<F> acc = xyzz29_inf<F>();
   bool fresh = true;
-  uint32_t code = sorted[start], nxt = 0;  // PREFETCH: code = entry p (base in LDS), nxt = entry p + 1
-  uint4* sw = sb + (PREFETCH ? 256 * (threadIdx.x >> 6) : 0);
+  uint32_t code = sorted[start], nxt = 0;  // code = entry p (base in LDS), nxt = entry p + 1
+  uint4* sw = sb + 256 * (threadIdx.x >> 6);
   const uint32_t ln = threadIdx.x & 63;
-  if (PREFETCH) {
-    glds_base(bases + 16ull * (code & ~kNegBit), sw);
-    if (start + 1 < end) nxt = sorted[start + 1];
-  }
+  glds_base(bases + 16ull * (code & ~kNegBit), sw);
+  if (start + 1 < end) nxt = sorted[start + 1];
   for (uint32_t p = start; p < end; p++) {
     F29<F> x, y;
     const uint32_t ccode = code;
-    if (PREFETCH) {
+    {
       // this entry's base landed in LDS (vmcnt covers LDS-DMA; everything
       // outstanding was issued before the previous addition); read it, and
       // only then (lgkmcnt) let the next entry's DMA overwrite the slots
@@ -686,15 +613,10 @@ __global__ void __launch_bounds__(256, PM_ACC_WAVES) k_accumulate(const uint32_t
       }
       owned = true;
     }
-    if (PREFETCH) {
-      if (p + 1 < end) {
-        glds_base(bases + 16ull * (nxt & ~kNegBit), sw);
-        code = nxt;
-        if (p + 2 < end) nxt = sorted[p + 2];
-      }
-    } else {
-      load_aff29<F>(bases + 16ull * (ccode & ~kNegBit), x, y);
-      if (p + 1 < end) code = sorted[p + 1];
+    if (p + 1 < end) {
+      glds_base(bases + 16ull * (nxt & ~kNegBit), sw);
+      code = nxt;
+      if (p + 2 < end) nxt = sorted[p + 2];
     }
     // identity base (0, 0): y = 0 holds for no point of odd order
     if (f29_is_zero_exact<F>(y)) continue;
@@ -716,23 +638,6 @@ __global__ void __launch_bounds__(256, PM_ACC_WAVES) k_accumulate(const uint32_t
     acc = r;
   }
   store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc);
-  // owner of a bucket that runs on past this slice: queue the chain for
-  // k_fixup_short / k_fixup_long (longs == nullptr: k_fixup walks buckets).
-  // The short list is compacted (one atomic per wave), so the fixup's lanes
-  // are dense: a per-slice fixup lane idled or diverged (~55 us at 2^20).
-  if (!longs) return;
-  uint32_t t_last = t;
-  if (owned && bend > end) t_last = min((bend - 1 - base) / chunk, nthreads - 1);
-  if (t_last - t > kMaxChain) longs[atomicAdd(nlong, 1u)] = LongChain{gb, t + 1, t_last};
-  if (!shorts) return;  // k_bucket_seg_q folds the short chains itself
-  const bool sh = t_last > t && t_last - t <= kMaxChain;
-  const uint64_t m = __ballot(sh);
-  if (!m) return;
-  const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-  uint32_t k0 = 0;
-  if (lane == leader) k0 = atomicAdd(nshort, (uint32_t)__popcll(m));
-  k0 = __shfl(k0, (int)leader, 64);
-  if (sh) shorts[k0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = LongChain{gb, t + 1, t_last};
 }
 
 // Base conversion (once per MSM): Rust-layout R = 2^256 Montgomery -> the
@@ -750,28 +655,6 @@ __global__ void __launch_bounds__(256) k_bases_to_r261(const uint32_t* __restric
     const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     st29<F>(o + 2 * c, f29_canon<F>(f29_from_r256<F>(w)));
   }
-}
-
-// GLV mode: out[i] = P_i and out[n + i] = phi(P_i) = (beta x, y), R261 canonical
-// ((0, 0) stays (0, 0), which k_accumulate skips).
-template <class Cv>
-__global__ void __launch_bounds__(256) k_bases_glv(const uint32_t* __restrict__ in, uint32_t n,
-                                                   uint32_t* __restrict__ out) {
-  using F = typename Cv::Base;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint4* q = reinterpret_cast<const uint4*>(in + 16ull * i);
-  uint4* o = reinterpret_cast<uint4*>(out + 16ull * i);
-  uint4* o2 = reinterpret_cast<uint4*>(out + 16ull * ((size_t)n + i));
-  const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
-  const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
-  const F29<F> x = f29_canon<F>(f29_from_r256<F>(wx));
-  const F29<F> y = f29_canon<F>(f29_from_r256<F>(wy));
-  st29<F>(o, x);
-  st29<F>(o + 2, y);
-  st29<F>(o2, f29_canon<F>(f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), x)));
-  st29<F>(o2 + 2, y);
 }
 
 // Fixed-base table (pm_fixed_bases_create*): entry (j, i) at j * npad + i is
@@ -827,183 +710,85 @@ __global__ void __launch_bounds__(256) k_fixed_table(const uint32_t* __restrict_
   }
 }
 
-// --------------------------------------------------------------- 5. fixup
-// Slice-boundary partials (see kMaxChain).  Variable-base MSM: k_accumulate
-// queued every chain (short list: k_fixup_short; long list: k_fixup_long).
-// Fixed-base MSM (merged buckets span ~8 slices each): k_fixup, one lane per
-// bucket, queues the long ones.  Then k_fixup_long.
-
-// Long chains (> kMaxChain slices): one workgroup per bucket, grid-stride
-// over the list (usually empty), strided partial sums then an LDS tree.
-template <class F>
-__device__ __forceinline__ void fixup_long_blocks(const LongChain* __restrict__ longs, uint32_t nl,
-                                                  Xyzz<F>* __restrict__ buckets, const Xyzz<F>* __restrict__ head,
-                                                  uint32_t blk, uint32_t nblk) {
-  __shared__ Xyzz29<F> lds[256];
-  const int tid = threadIdx.x;
-  for (uint32_t k = blk; k < nl; k += nblk) {
-    const LongChain lc = longs[k];
-    Xyzz29<F> acc = xyzz29_inf<F>();
-    for (uint32_t t2 = lc.t_first + tid; t2 <= lc.t_last; t2 += 256)
-      acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
-    lds[tid] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (tid < s) {
-        acc = xyzz29_add<F>(acc, lds[tid + s]);
-        lds[tid] = acc;
-      }
-      __syncthreads();
-    }
-    if (tid == 0) store_xyzz29<F>(&buckets[lc.gb], xyzz29_add<F>(load_xyzz29<F>(&buckets[lc.gb]), acc));
-    __syncthreads();
-  }
-}
-
-// Blocks [0, nsb): one lane per queued short chain (k_accumulate's compacted
-// list).  Blocks [nsb, grid): the long chains (fixup_long_blocks), in the
-// same launch (a separate, almost always empty launch cost ~5 us per MSM).
-// Short and long chains belong to different buckets.
-template <class F>
-__global__ void __launch_bounds__(256) k_fixup_short(const LongChain* __restrict__ shorts,
-                                                     const uint32_t* __restrict__ nshort,
-                                                     Xyzz<F>* __restrict__ buckets,
-                                                     const Xyzz<F>* __restrict__ head, uint32_t nsb,
-                                                     const LongChain* __restrict__ longs,
-                                                     const uint32_t* __restrict__ nlong) {
-  if (blockIdx.x >= nsb) {
-    fixup_long_blocks<F>(longs, *nlong, buckets, head, blockIdx.x - nsb, gridDim.x - nsb);
-    return;
-  }
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= *nshort) return;
-  const LongChain lc = shorts[k];
-  Xyzz29<F> acc = load_xyzz29<F>(&buckets[lc.gb]);
-  for (uint32_t t2 = lc.t_first; t2 <= lc.t_last; t2++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
-  store_xyzz29<F>(&buckets[lc.gb], acc);
-}
-
-// One lane per bucket gb in [s0, s1): a bucket whose sorted run crosses
-// slice boundaries was started by slice t_first (which stored its partial in
-// buckets[gb]); every later slice it reaches stored its first partial in
-// head[].  Bucket-parallel, so the lanes that walk a chain are dense even
-// when every bucket spans several slices (fixed-base MSM: ~8 per bucket).
-template <class F>
-__global__ void __launch_bounds__(256) k_fixup(const uint32_t* __restrict__ offsets, uint32_t s0, uint32_t s1,
-                                               uint32_t chunk, uint32_t nthreads,
-                                               Xyzz<F>* __restrict__ buckets,
-                                               const Xyzz<F>* __restrict__ head,
-                                               LongChain* __restrict__ longs,
-                                               uint32_t* __restrict__ nlong) {
-  const uint32_t gb = s0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (gb >= s1) return;
-  const uint32_t base = offsets[s0];
-  const uint32_t bstart = offsets[gb], bend = offsets[gb + 1];
-  if (bstart == bend) return;
-  const uint32_t t_first = (bstart - base) / chunk;
-  const uint32_t t_last = min((bend - 1 - base) / chunk, nthreads - 1);
-  if (t_last == t_first) return;
-  if (t_last - t_first > kMaxChain) {
-    const uint32_t k = atomicAdd(nlong, 1u);
-    longs[k] = LongChain{gb, t_first + 1, t_last};
-    return;
-  }
-  Xyzz29<F> acc = load_xyzz29<F>(&buckets[gb]);
-  for (uint32_t t2 = t_first + 1; t2 <= t_last; t2++) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&head[t2]));
-  store_xyzz29<F>(&buckets[gb], acc);
-}
-
-template <class F>
-__global__ void __launch_bounds__(256) k_fixup_long(const LongChain* __restrict__ longs,
-                                                    const uint32_t* __restrict__ nlong,
-                                                    Xyzz<F>* __restrict__ buckets,
-                                                    const Xyzz<F>* __restrict__ head) {
-  fixup_long_blocks<F>(longs, *nlong, buckets, head, blockIdx.x, gridDim.x);
-}
-
-// ------------------------------------------------------ 6. segment sums
-// thread (w, j), w in [w0, w0 + nw), j < M1 = K / L1: slots s = j*L1 + i,
-// i in [0, L1): S = sum B_s, T = sum i * B_s (0-based weight inside the
-// segment).  Thread (w, 0) also copies the top bucket K (slot K, after the
-// fixup) to Kb[w] for the host's K-weighted term.
-template <class F>
-__global__ void __launch_bounds__(256) k_bucket_seg(const uint32_t* __restrict__ offsets,
-                                                    const Xyzz<F>* __restrict__ buckets, int w0, int nw, int NB,
-                                                    int M1, int L1, Xyzz<F>* __restrict__ S,
-                                                    Xyzz<F>* __restrict__ T, Xyzz<F>* __restrict__ Kb) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nw * M1) return;
-  const int gid = w0 * M1 + g;
-  const int w = gid / M1, j = gid - w * M1;
-  const size_t base = (size_t)w * NB + (size_t)j * L1;
-  if (j == 0) {
-    const size_t sk = (size_t)w * NB + (size_t)M1 * L1;  // slot K
-    store_xyzz29<F>(&Kb[w], offsets[sk] != offsets[sk + 1] ? load_xyzz29<F>(&buckets[sk]) : xyzz29_inf<F>());
-  }
-  Xyzz29<F> s = xyzz29_inf<F>(), t = xyzz29_inf<F>();
-  if (L1 == 4) {
-    // S = B0 + B1 + B2 + B3 and T = B1 + 2 B2 + 3 B3 in 5 additions (the
-    // running-sum walk below needs 7): P23 = B2 + B3, P123 = B1 + P23,
-    // S = B0 + P123, T = (P123 + P23) + B3
-    Xyzz29<F> B[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-      B[i] = offsets[base + i] != offsets[base + i + 1] ? load_xyzz29<F>(&buckets[base + i]) : xyzz29_inf<F>();
-    const Xyzz29<F> p23 = xyzz29_add<F>(B[2], B[3]);
-    const Xyzz29<F> p123 = xyzz29_add<F>(B[1], p23);
-    s = xyzz29_add<F>(B[0], p123);
-    t = xyzz29_add<F>(xyzz29_add<F>(p123, p23), B[3]);
-  } else {
-    for (int i = L1 - 1; i >= 1; i--) {
-      if (offsets[base + i] != offsets[base + i + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base + i]));
-      t = xyzz29_add<F>(t, s);
-    }
-    if (offsets[base] != offsets[base + 1]) s = xyzz29_add<F>(s, load_xyzz29<F>(&buckets[base]));
-  }
-  store_xyzz29<F>(&S[gid], s);
-  store_xyzz29<F>(&T[gid], t);
-}
-
-// ---------------------------------------- 5 + 6. chains and segment sums
+// ------------------------------------------- 5. chains and segment sums
 // One quad per segment of kSegQ = 4 buckets: lane q folds bucket q's
 // slice-boundary chain (buckets[gb] plus head[t] of every later slice the
-// bucket reaches, as k_fixup; chains longer than kMaxChain were queued by
-// k_accumulate and folded into buckets[gb] by k_fixup_long before this
-// launch), then the quad shares the four sums and computes S = B0 + B1 + B2 +
-// B3 and T = B1 + 2 B2 + 3 B3 with quad-cooperative additions (coop29.hpp).
-// Replaces k_fixup_short + k_bucket_seg: one launch and one round trip of
-// the buckets less, and the segment's additions at ~half the latency.
+// bucket reaches), then the quad shares the four sums and computes S = B0 +
+// B1 + B2 + B3 and T = B1 + 2 B2 + 3 B3 with quad-cooperative additions
+// (coop29.hpp).  A chain of more than kSerialChain slices (a giant bucket)
+// is folded by the whole wave instead: the lanes stride over its partials,
+// a butterfly sums the 64 results, and the owning lane adds them -- so no
+// separate long-chain launch (round 2: k_fixup_long, ~5 us per MSM, almost
+// always empty) and no chain list from k_accumulate.
 constexpr uint32_t kSegQ = 4;  // buckets per segment: a quad (= kL1, runtime.hpp)
 template <int K, class F>
 __device__ __forceinline__ Xyzz29<F> xyzz29_qbc(const Xyzz29<F>& p) {  // lane K's point, quad-wide
   return Xyzz29<F>{qbc<K, F>(p.X), qbc<K, F>(p.Y), qbc<K, F>(p.ZZ), qbc<K, F>(p.ZZZ)};
 }
+template <class F>
+__device__ __forceinline__ F29<F> f29_shfl_xor(const F29<F>& v, int m) {
+  F29<F> r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = (uint32_t)__shfl_xor((int)v.l[i], m, 64);
+  return r;
+}
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_shfl_xor(const Xyzz29<F>& p, int m) {
+  return Xyzz29<F>{f29_shfl_xor<F>(p.X, m), f29_shfl_xor<F>(p.Y, m), f29_shfl_xor<F>(p.ZZ, m),
+                   f29_shfl_xor<F>(p.ZZZ, m)};
+}
+// lane k of a quad stores coordinate k of p (Norm, < 4p) converted to the
+// Rust R = 2^256 layout into *dst (the host Horner's term format)
+template <class F>
+__device__ __forceinline__ void store_r256_q(Xyzz<F>* dst, const Xyzz29<F>& p, uint32_t lk) {
+  const F29<F> c = qsel<F>(lk, p.X, p.Y, p.ZZ, p.ZZZ);
+  uint32_t o[8];
+  f29_to_r256<F>(c, o);
+  uint4* q = reinterpret_cast<uint4*>(dst);
+  q[2 * lk] = make_uint4(o[0], o[1], o[2], o[3]);
+  q[2 * lk + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
 // Segments cover slots [0, K) (M1 = K / kSegQ); the top bucket K is folded
 // by lane 0 of segment 0 instead of slot 0 (digit 0 has no bucket, and
 // whatever slot 0 holds has weight 0: S_0 enters no bit sum, T_0 weighs lane 0
-// by 0), and stored to Kb[w] for the host's K-weighted term.
+// by 0); that quad converts it and stores it as the set's last host term,
+// Q[w * NQ + NQ - 1].
 template <class F>
-__global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restrict__ offsets, uint32_t s0,
-                                                      uint32_t chunk, uint32_t nthreads,
-                                                      const Xyzz<F>* __restrict__ buckets,
-                                                      const Xyzz<F>* __restrict__ head, int w0, int nw, int NB,
+__global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restrict__ offsets, uint32_t chunk,
+                                                      uint32_t nthreads, const Xyzz<F>* __restrict__ buckets,
+                                                      const Xyzz<F>* __restrict__ head, int Wr, int NB,
                                                       uint32_t M1, Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T,
-                                                      Xyzz<F>* __restrict__ Kb) {
+                                                      Xyzz<F>* __restrict__ Q, int NQ) {
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = gl >> 2, q = gl & 3u;
-  if (g >= (uint32_t)nw * M1) return;  // whole quads
-  const size_t gid = (size_t)w0 * M1 + g;
-  const uint32_t w = (uint32_t)(gid / M1), j = (uint32_t)(gid - (size_t)w * M1);
-  const bool top = j == 0 && q == 0;
+  // lanes past the last segment stay (inactive values) for the wave-wide fold
+  const bool valid = g < (uint32_t)Wr * M1;
+  const uint32_t w = valid ? g / M1 : 0u, j = valid ? g - w * M1 : 1u;
+  const bool top = valid && j == 0 && q == 0;
   const size_t slot = (size_t)w * NB + (top ? M1 * kSegQ : j * kSegQ + q);
-  const uint32_t base = offsets[s0];
-  const uint32_t bs = offsets[slot], be = offsets[slot + 1];
+  const uint32_t base = offsets[0];
+  const uint32_t bs = valid ? offsets[slot] : 0u, be = valid ? offsets[slot + 1] : 0u;
   Xyzz29<F> B = xyzz29_inf<F>();
+  uint32_t tf = 0, tl = 0;
   if (bs != be) {
     B = load_xyzz29<F>(&buckets[slot]);
-    const uint32_t tf = (bs - base) / chunk, tl = min((be - 1 - base) / chunk, nthreads - 1);
-    if (tl - tf <= kMaxChain)
+    tf = (bs - base) / chunk;
+    tl = min((be - 1 - base) / chunk, nthreads - 1);
+    if (tl - tf <= kSerialChain)
       for (uint32_t t = tf + 1; t <= tl; t++) B = xyzz29_add<F>(B, load_xyzz29<F>(&head[t]));
+  }
+  // giant buckets: the wave folds each long chain in turn (wave-uniform loop)
+  uint64_t lm = __ballot(tl - tf > kSerialChain);
+  const uint32_t ln = __lane_id();
+  while (lm) {
+    const int L = __ffsll((unsigned long long)lm) - 1;
+    lm &= lm - 1;
+    const uint32_t a = (uint32_t)__shfl((int)tf, L, 64) + 1u, z = (uint32_t)__shfl((int)tl, L, 64);
+    Xyzz29<F> c = xyzz29_inf<F>();
+    for (uint32_t t = a + ln; t <= z; t += 64) c = xyzz29_add<F>(c, load_xyzz29<F>(&head[t]));
+#pragma unroll 1
+    for (int m = 32; m > 0; m >>= 1) c = xyzz29_add<F>(c, xyzz29_shfl_xor<F>(c, m));
+    if (ln == (uint32_t)L) B = xyzz29_add<F>(B, c);
   }
   // broadcast each lane's sum only when it is consumed (fewer live points)
   const Xyzz29<F> B3 = xyzz29_qbc<3, F>(B);
@@ -1011,31 +796,55 @@ __global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restr
   const Xyzz29<F> p123 = xyzz29_add_q<F>(xyzz29_qbc<1, F>(B), p23);
   const Xyzz29<F> tv = xyzz29_add_q<F>(xyzz29_add_q<F>(p123, p23), B3);
   const Xyzz29<F> sv = xyzz29_add_q<F>(xyzz29_qbc<0, F>(B), p123);
-  if (q == 0) store_xyzz29<F>(&S[gid], sv);
-  if (q == 1) store_xyzz29<F>(&T[gid], tv);
-  if (top) store_xyzz29<F>(&Kb[w], B);
+  if (!valid) return;
+  if (q == 0) store_xyzz29<F>(&S[g], sv);
+  if (q == 1) store_xyzz29<F>(&T[g], tv);
+  if (j == 0) store_r256_q<F>(&Q[(size_t)w * NQ + NQ - 1], xyzz29_qbc<0, F>(B), q);
 }
 
-// ------------------------------------------------------ 7. bit sums
-// block (job, w - w0, z): job < NB2 -> G_job = sum_{j : (j >> job) & 1} S_j
+// ------------------------------------------------------ 6. bit sums
+// block (job, w, z): job < NB2 -> G_job = sum_{j : (j >> job) & 1} S_j
 // (only the j with that bit set are enumerated, so no lane idles); job >= NB2
 // -> partial sum of T_j over part (job - NB2) of kTJobs equal ranges.
 // kRedThreads lanes: strided partial sums, then an LDS tree.  With nsplit > 1
-// (few windows, e.g. the fixed-base MSM's single bucket set) nsplit blocks
-// share a job: each reduces every nsplit-th stride, parks its partial in P,
-// and the last block to finish (atomic ticket) folds the nsplit partials.
-// Serial depth ~ M1/2/(kRedThreads nsplit) + log2(kRedThreads) + log2(nsplit).
+// (few bucket sets, e.g. the row tables' 4 or the fixed-base MSM's one)
+// nsplit blocks share a job: each reduces every nsplit-th stride, parks its
+// partial in P, and the last block to finish (atomic ticket) folds the
+// nsplit partials with log2(nsplit) quad-cooperative levels (round 2 ran a
+// fixed 6-level plain tree here, i.e. four wasted addition latencies at
+// nsplit = 4).  The result goes out converted to the Rust R = 2^256 layout
+// as host term Q[w * NQ + job] (round 2 folded pairs of bit sums and
+// converted them in a separate k_bits_combine launch, ~19 us per MSM).
 constexpr int kRedThreads = 512;
 constexpr int kTJobs = 2;
 constexpr int kMaxSplit = 64;
+// reduce lds[0 .. count) (count a power of two <= kRedThreads; acc = this
+// lane's lds[tid]) into lds[0]; quad-cooperative once 4 s lanes are free
+template <class F>
+__device__ __forceinline__ void lds_tree(Xyzz29<F>* lds, int count, Xyzz29<F> acc) {
+  const int tid = threadIdx.x;
+  for (int s = count / 2; s > 0; s >>= 1) {
+    if (4 * s <= (int)blockDim.x) {
+      const int v = tid >> 2;
+      if (v < s) {
+        const Xyzz29<F> r = xyzz29_add_q<F>(lds[v], lds[v + s]);
+        if ((tid & 3) == 0) lds[v] = r;  // the quad read lds[v] in this same wave
+      }
+    } else if (tid < s) {
+      acc = xyzz29_add<F>(acc, lds[tid + s]);
+      lds[tid] = acc;
+    }
+    __syncthreads();
+  }
+}
 template <class F>
 __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __restrict__ S,
-                                                             const Xyzz<F>* __restrict__ T, int w0, int M1,
-                                                             int NB2, Xyzz<F>* __restrict__ G, int nsplit,
+                                                             const Xyzz<F>* __restrict__ T, int M1, int NB2,
+                                                             Xyzz<F>* __restrict__ Q, int NQ, int nsplit,
                                                              Xyzz<F>* __restrict__ P, uint32_t* __restrict__ tickets) {
   __shared__ Xyzz29<F> lds[kRedThreads];
   __shared__ uint32_t last;
-  const int w = w0 + blockIdx.y, job = blockIdx.x, tid = threadIdx.x, z = blockIdx.z;
+  const int w = blockIdx.y, job = blockIdx.x, tid = threadIdx.x, z = blockIdx.z;
   const int lane = z * kRedThreads + tid, stride = kRedThreads * nsplit;
   Xyzz29<F> acc = xyzz29_inf<F>();
   if (job < NB2) {
@@ -1052,82 +861,27 @@ __global__ void __launch_bounds__(kRedThreads) k_bucket_bits(const Xyzz<F>* __re
   }
   lds[tid] = acc;
   __syncthreads();
-  // tree: once 4 s lanes are free, each addition is quad-cooperative
-  // (coop29.hpp: ~2x lower latency; the tree levels run one wave per SIMD)
-  for (int s = kRedThreads / 2; s > 0; s >>= 1) {
-    if (4 * s <= kRedThreads) {
-      const int v = tid >> 2;
-      if (v < s) {
-        const Xyzz29<F> r = xyzz29_add_q<F>(lds[v], lds[v + s]);
-        if ((tid & 3) == 0) lds[v] = r;  // the quad read lds[v] in this same wave
-      }
-    } else if (tid < s) {
-      acc = xyzz29_add<F>(acc, lds[tid + s]);
-      lds[tid] = acc;
-    }
-    __syncthreads();
-  }
-  acc = lds[0];
-  const size_t out = (size_t)w * (NB2 + kTJobs) + job;
+  lds_tree<F>(lds, kRedThreads, acc);
   if (nsplit > 1) {
+    const size_t out = (size_t)w * (NB2 + kTJobs) + job;
     if (tid == 0) {
-      store_xyzz29<F>(&P[out * nsplit + z], acc);
+      store_xyzz29<F>(&P[out * nsplit + z], lds[0]);
       __threadfence();
       last = atomicAdd(&tickets[out], 1u) == (uint32_t)nsplit - 1;
     }
     __syncthreads();
     if (!last) return;
     __threadfence();
+    int cnt = 1;
+    while (cnt < nsplit) cnt <<= 1;
     acc = tid < nsplit ? load_xyzz29<F>(&P[out * nsplit + tid]) : xyzz29_inf<F>();
-    if (tid < kMaxSplit) lds[tid] = acc;
+    __syncthreads();  // every lane has read lds[0] above
+    if (tid < cnt) lds[tid] = acc;
     __syncthreads();
-    for (int s = kMaxSplit / 2; s > 0; s >>= 1) {
-      if (tid < s) {
-        acc = xyzz29_add<F>(acc, lds[tid + s]);
-        lds[tid] = acc;
-      }
-      __syncthreads();
-    }
+    lds_tree<F>(lds, cnt, acc);
     if (tid == 0) tickets[out] = 0;  // ready for the next MSM
   }
-  if (tid == 0) store_xyzz29<F>(&G[out], acc);  // packed R261; k_bits_combine converts
-}
-
-// Per window: the NB2 bit sums folded kBitsFold at a time by Horner,
-// Q_j = G_{2j} + 2 G_{2j+1} (one doubling, one addition), plus T = the kTJobs
-// T-partials; converted to the Rust-layout R = 2^256 form for the host Horner.
-// A dependent EC operation costs one wave ~8 us, so folding pays only while
-// the chain stays short: 4 at a time (3 dbl + 3 add) cost as much GPU time as
-// it saved on the host; 2 at a time halves the host's additions for ~2 ops.
-constexpr int kBitsFold = 2;
-template <class F>
-__global__ void __launch_bounds__(64) k_bits_combine(const Xyzz<F>* __restrict__ G, const Xyzz<F>* __restrict__ Kb,
-                                                     int w0, int nw, int NB2, Xyzz<F>* __restrict__ Q) {
-  // a quad per output: quad-cooperative doubling / addition (coop29.hpp),
-  // then lane k converts coordinate k.  Per window: the bit folds, sum T
-  // (j = NQ - 2) and the top bucket K (j = NQ - 1)
-  const int NJ = NB2 + kTJobs, NQ = (NB2 + kBitsFold - 1) / kBitsFold + 2;
-  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2, lk = threadIdx.x & 3;
-  if (gq >= nw * NQ) return;  // whole quads (blocks of 64 lanes hold 16 quads)
-  const int w = w0 + gq / NQ, j = gq % NQ;
-  const Xyzz<F>* gw = G + (size_t)w * NJ;
-  Xyzz29<F> acc;
-  if (j == NQ - 1) {
-    acc = load_xyzz29<F>(&Kb[w]);
-  } else if (j == NQ - 2) {
-    acc = load_xyzz29<F>(&gw[NB2]);
-    for (int t = 1; t < kTJobs; t++) acc = xyzz29_add_q<F>(acc, load_xyzz29<F>(&gw[NB2 + t]));
-  } else {
-    const int b0 = j * kBitsFold, b1 = min(NB2, b0 + kBitsFold);
-    acc = load_xyzz29<F>(&gw[b1 - 1]);
-    for (int b = b1 - 2; b >= b0; b--) acc = xyzz29_add_q<F>(xyzz29_dbl_q<F>(acc), load_xyzz29<F>(&gw[b]));
-  }
-  const F29<F> c = qsel<F>((uint32_t)lk, acc.X, acc.Y, acc.ZZ, acc.ZZZ);
-  uint32_t o[8];
-  f29_to_r256<F>(c, o);
-  uint4* q = reinterpret_cast<uint4*>(&Q[(size_t)w * NQ + j]);
-  q[2 * lk] = make_uint4(o[0], o[1], o[2], o[3]);
-  q[2 * lk + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+  if (tid < 4) store_r256_q<F>(&Q[(size_t)w * NQ + job], lds[0], (uint32_t)tid);
 }
 
 // ------------------------------------------------------ synthetic inputs

@@ -28,22 +28,11 @@ constexpr int kMaxC = 20;
 // in accumulate vs 6.1 ms at c = 16; at 2^20, c = 20 took 23.8 ms vs 1.4 ms.
 constexpr int kAutoMaxC = 16;
 constexpr size_t kMaxPoints = size_t(1) << 26;
-constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg (serial chain: 2*L1-1 adds)
-// bases larger than this (bytes) use the prefetching accumulate kernel: the
-// next entry's base arrives by LDS-DMA (global_load_lds) during this entry's
-// addition.  Round 2, same box A/B (profiles/r02/xp/): 2^20 1.04-1.05 ->
-// 1.027 ms, 2^22 4.29-4.30 -> 4.12 ms, so it is on at every size (the
-// round-1 register-prefetch form measured slower and is gone); PM_PREFETCH=0
-// selects the plain kernel.
-constexpr size_t kPrefetchBytes = 0;
+constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg_q (one quad per segment)
 // internal msm flag (never in the public header; the C-ABI strips it from
 // caller flags): d_bases already hold the pipeline's R = 2^261 canonical
 // form (resident pm_bases converted at upload), so no per-call conversion
 constexpr uint32_t kBasesR261 = 1u << 30;
-// host -> device staging of large host inputs (pm_msm, pm_msm_resident):
-// chunks of this size through pinned buffers, one per copy thread
-constexpr size_t kStageChunk = size_t(4) << 20;
-constexpr int kMaxStageThreads = 8;
 
 struct Buf {
   void* p = nullptr;
@@ -70,24 +59,20 @@ struct MsmPlan {
   int base, extra;
   int cmax;       // widest window
   int K;          // max |digit| = 2^(cmax-1)
-  int L1;         // bucket-segment length of k_bucket_seg
+  int L1;         // bucket-segment length of k_bucket_seg_q
   int log2L1;
   int NB;         // bucket slots per window (K+1 rounded up to L1)
   int M1;         // segments per window: K / L1 (slots [0, K); bucket K apart)
   int NB2;        // bits of the segment index
   uint32_t n;
-  int G;              // window groups (pipelined, processed from the top window down)
-  int wpg;            // windows per group
   uint32_t chunk;     // sorted entries per accumulate lane
-  uint32_t nthreads;  // accumulate lanes per group
-  uint32_t maxlong;   // bound on buckets needing k_fixup_long, per group
+  uint32_t nthreads;  // accumulate lanes
   int width(int w) const { return base + (w < extra ? 1 : 0); }
 };
 
-// nbits: scalar bits covered by the windows (256; 128 in GLV mode, n = 2 x points)
-MsmPlan make_plan(size_t n, int c_override, int groups_override = 0, int min_chunk = 0, int nbits = 256);
-// fixed-base MSM over a table of npad rows per window (one window group,
-// accumulate work = W * npad entries)
+MsmPlan make_plan(size_t n, int c_override, int min_chunk = 0);
+// fixed-base MSM over a table of npad rows per window (accumulate work =
+// W * npad entries)
 MsmPlan make_plan_fixed(size_t npad, int c, int min_chunk = 0);
 // fixed-base windows: one bucket set of 2^(c-1) buckets
 constexpr int kFixedMaxC = 20;
@@ -130,19 +115,14 @@ struct pm_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  hipStream_t red_stream = nullptr;  // bucket reduction of window group g overlaps accumulation of g-1
+  hipStream_t red_stream = nullptr;  // accumulator side stream (accum_engine.hpp)
   hipStream_t copy_stream = nullptr; // H2D of the next MSM's scalars (pm_msm_resident_batch)
   hipEvent_t batch_ev[4] = {};       // batch pipelining: copied[2], consumed[2]
-  std::vector<hipEvent_t> grp_ev;    // 2 per window group (accumulated, reduced+copied)
+  std::vector<hipEvent_t> grp_ev;    // MSM: one per pinned term slot (terms copied)
   int window_c = 0;
-  int prefetch = -1;  // -1 auto, 0 off, 1 on (diagnostics: PM_PREFETCH env)
-  int groups = 0;     // window groups, 0 = auto (diagnostics: PM_GROUPS env)
   int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
   int sort_ppt = 0;   // sort points per thread, 0 = auto (diagnostics: PM_SORT_PPT env, 1/2/4/8)
   int sort_fb = 0;    // fine bits of the two-level sort, 0 = auto (diagnostics: PM_SORT_FB env)
-  int fine_cache = 0; // entries of the fine pass's LDS segment cache, 0 = auto (diagnostics: PM_FINE_CACHE env)
-  int glv = 0;        // variable-base MSM in GLV mode (pm_ctx_set_glv, PM_GLV env): measured slower, off
-  int segq = 1;        // MSM chains + segment sums fused (k_bucket_seg_q) (diagnostics: PM_SEGQ env)
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;
@@ -160,17 +140,8 @@ struct pm_ctx {
   uint64_t acc_vkpow_gen = ~0ull;  // acc_vkpow.gen when the tables were built
   std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
   uint64_t ntt_clock = 0;
-  void* h_pinned = nullptr;
+  void* h_pinned = nullptr;  // MSM host terms: two slots (batch pipelining)
   size_t h_pinned_cap = 0;
-  // pinned staging for host inputs (upload_h2d): one chunk buffer + one
-  // event per copy thread; h2d_threads = 0 -> plain pageable hipMemcpyAsync.
-  // Default 0: on MI355X the runtime's pageable copy of 32 MB already runs at
-  // ~52 GB/s (82 % of PCIe 5 x16) vs ~38 GB/s through 4 staging threads
-  // (profiles/r02/b/bench.json host_scalars)
-  int h2d_threads = 0;
-  void* h_stage[pm::kMaxStageThreads] = {};
-  hipEvent_t stage_ev[pm::kMaxStageThreads] = {};
-  bool stage_pending[pm::kMaxStageThreads] = {};
   // timing
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -186,9 +157,9 @@ struct pm_ctx {
   int begin_call();
   int end_call();
   int ensure_pinned(size_t bytes);
-  // host -> device copy of a large caller buffer on `st`: chunks are copied
-  // by h2d_threads host threads into pinned buffers and DMA'd from there
-  // (pageable hipMemcpyAsync stages through the runtime's own small buffer)
+  // host -> device copy of a caller buffer on `st` (one pageable
+  // hipMemcpyAsync: ~52 GB/s for 32 MB on MI355X, faster than the pinned
+  // staging threads round 2 measured, ~38 GB/s, and retired)
   int upload_h2d(void* d, const void* h, size_t bytes, hipStream_t st);
   int ensure_group_events(int n);
   hipEvent_t next_event();

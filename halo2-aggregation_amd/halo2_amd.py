@@ -26,6 +26,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "pasta_msm.h")
 
 PALLAS, VESTA, BN254 = 0, 1, 2
 SCALARS_CANONICAL = 1
+LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
 ACCUM_CURVES = (PALLAS, VESTA, BN254)
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -190,15 +191,17 @@ def _load():
     # the dynamic loader resolve our DT_NEEDED libamdhip64.so.7 to that same
     # copy, so the process runs ONE HIP runtime whether or not torch is used
     # (two runtimes in one process fail with "No HIP GPUs are available").
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    if not os.environ.get("PM_NO_TORCH"):  # PM_NO_TORCH: host-only checks (tests/test_asan.py)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libpasta_msm.so not built at {LIB_PATH} (run __graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH)
     sig = {
         "pm_version": ([], ctypes.c_char_p),
+        "pm_abi_version": ([], ctypes.c_int),
         "pm_last_error": ([], ctypes.c_char_p),
         "pm_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "pm_ctx_create": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
@@ -284,6 +287,11 @@ def lib():
     if _lib is None:
         _lib = _load()
     return _lib
+
+
+def abi_version():
+    """pm_abi_version(): bumped on every C-ABI signature / meaning change."""
+    return int(lib().pm_abi_version())
 
 
 def header_symbols(path=HEADER_PATH):
@@ -481,9 +489,9 @@ class Context:
             pass
 
     def set_stream(self, stream_handle):
-        """Run on the caller's HIP stream (0 = the legacy null stream);
-        use_own_stream() restores the context's own (blocking) stream."""
-        _check(lib().pm_ctx_set_stream(self.h, _vp(stream_handle or 0)))
+        """Run on the caller's HIP stream; 0 / None = the context's own
+        (blocking) stream again, LEGACY_STREAM = the legacy null stream."""
+        _check(lib().pm_ctx_set_stream(self.h, _vp(stream_handle or None)))
 
     def use_own_stream(self):
         _check(lib().pm_ctx_use_own_stream(self.h))
@@ -492,10 +500,12 @@ class Context:
         _check(lib().pm_ctx_set_window(self.h, c))
 
     def set_pipeline(self, groups=0, min_chunk=0):
+        """Minimum accumulate slice per lane (0 = automatic); groups must be
+        0 or 1 (window groups are retired)."""
         _check(lib().pm_ctx_set_pipeline(self.h, groups, min_chunk))
 
     def set_glv(self, enable=True):
-        """Variable-base MSM in GLV mode (2n points, 128-bit scalars); results do not depend on it."""
+        """Retired GLV mode: only enable=False is accepted."""
         _check(lib().pm_ctx_set_glv(self.h, 1 if enable else 0))
 
     def set_accum_split(self, lg_lanes=-1):
@@ -553,6 +563,7 @@ class Context:
         return out
 
     def set_h2d_threads(self, threads):
+        """Retired pinned staging: only threads=0 is accepted."""
         _check(lib().pm_ctx_set_h2d_threads(self.h, threads))
 
     def fixed_bases(self, curve, bases=None, c=0, d_bases=None, n=None, rows=0):

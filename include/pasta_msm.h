@@ -41,11 +41,18 @@ enum pm_status {
   PM_ERR_UNSUPPORTED = -4  /* shape or option not supported by this build */
 };
 
+/* ABI version: bumped on every change of a signature or of an argument's
+ * meaning.  3 = round 3 (pm_ctx_set_stream(ctx, NULL) selects the context's
+ * own stream again; the accumulator entries take the trailing out_status
+ * argument).  A binding asserts pm_abi_version() == PM_ABI_VERSION at load. */
+#define PM_ABI_VERSION 3
+
 typedef struct pm_ctx pm_ctx;     /* one device + one HIP stream + workspace */
 typedef struct pm_bases pm_bases; /* device-resident base points (SRS cache) */
 
 /* ---------------------------------------------------------------- misc */
 const char* pm_version(void);
+int pm_abi_version(void);
 const char* pm_last_error(void);
 int pm_device_count(int* count);
 
@@ -60,23 +67,24 @@ int pm_ctx_destroy(pm_ctx* ctx);
  *     ordered after everything queued on the legacy null stream (torch's
  *     default stream, the hipMemcpy / hipMemset default);
  *   - pm_ctx_set_stream(ctx, s) runs on the caller's stream s instead
- *     (e.g. torch.cuda.current_stream().cuda_stream); s == NULL is the legacy
- *     null stream itself, not "the context's own stream";
- *   - pm_ctx_use_own_stream(ctx) goes back to the context's own stream.
+ *     (e.g. torch.cuda.current_stream().cuda_stream); s == NULL goes back to
+ *     the context's own stream, s == PM_STREAM_LEGACY selects the legacy
+ *     null stream itself;
+ *   - pm_ctx_use_own_stream(ctx) also goes back to the context's own stream.
  * Work the caller queues on any other non-blocking stream must be
  * synchronised by the caller before the call. */
+#define PM_STREAM_LEGACY ((void*)1) /* the HIP legacy null stream (hipStreamLegacy) */
 int pm_ctx_set_stream(pm_ctx* ctx, void* hip_stream);
 int pm_ctx_use_own_stream(pm_ctx* ctx);
 /* Force the window width c (0 = automatic). */
 int pm_ctx_set_window(pm_ctx* ctx, int c);
-/* Pipeline tuning: number of window groups whose bucket reduction overlaps
- * the next group's accumulation (0 = automatic, 1 = no pipelining) and the
- * minimum accumulate slice per lane (0 = automatic). */
+/* Pipeline tuning: the minimum accumulate slice per lane (0 = automatic).
+ * `groups` must be 0 or 1: pipelined window groups measured slower on MI355X
+ * and were retired (PM_ERR_UNSUPPORTED for groups > 1). */
 int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk);
-/* Variable-base MSM in GLV mode (default off): s P = k1 P + k2 phi(P) with
- * |k1|, |k2| < 2^127, an MSM of 2n points with 128-bit scalars and half the
- * windows; used when the chosen window is >= 12 bits.  Measured slower on
- * MI355X.  Results do not depend on it. */
+/* Retired: the GLV-mode variable-base MSM measured slower on MI355X
+ * (DESIGN.md §7).  enable == 0 succeeds, anything else returns
+ * PM_ERR_UNSUPPORTED.  Kept so older bindings still link. */
 int pm_ctx_set_glv(pm_ctx* ctx, int enable);
 /* Batch accumulator: each MSM term's scalar is split into 2^lg_lanes bit
  * segments, one lane each (0..5; 0 = one lane per term; -1 = automatic: more
@@ -127,9 +135,8 @@ int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size
  * plain pipeline.  pm_bases_info reports n, the rows and the device bytes.
  * _upload takes host bases (Rust layout, as pm_msm), _upload_device bases
  * already in device memory of ctx's device (copied; the caller keeps its
- * buffer).  pm_msm_resident takes host scalars (staged through pinned
- * memory, see pm_ctx_set_h2d_threads), pm_msm_resident_device device
- * scalars. */
+ * buffer).  pm_msm_resident takes host scalars (one pageable copy),
+ * pm_msm_resident_device device scalars. */
 int pm_bases_upload(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, pm_bases** out);
 int pm_bases_upload_device(pm_ctx* ctx, int curve, const void* d_bases, size_t n, pm_bases** out);
 int pm_bases_info(const pm_bases* b, size_t* n, int* rows, size_t* device_bytes);
@@ -146,12 +153,9 @@ int pm_msm_resident_device(pm_ctx* ctx, const pm_bases* b, size_t offset, const 
  * tail overlaps them too.  Same results as k pm_msm_resident calls. */
 int pm_msm_resident_batch(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* const* scalars,
                           size_t k, size_t n, uint32_t flags, uint64_t* out);
-/* Host inputs of pm_msm / pm_msm_ctx / pm_msm_resident / pm_msm_fixed /
- * pm_bases_upload: threads = 0 (default) copies them with one pageable
- * hipMemcpyAsync; 1..8 stages them in 4 MiB chunks through pinned buffers,
- * `threads` host threads each (env PM_H2D_THREADS).  Measured on MI355X the
- * pageable copy is the faster one (~52 vs ~38 GB/s for 32 MB).  Results never
- * depend on it. */
+/* Retired: host inputs are copied with one pageable hipMemcpyAsync, which
+ * measured faster on MI355X than pinned staging threads (~52 vs ~38 GB/s for
+ * 32 MB).  threads == 0 succeeds, threads > 0 returns PM_ERR_UNSUPPORTED. */
 int pm_ctx_set_h2d_threads(pm_ctx* ctx, int threads);
 
 /* Device self-test of the MSM pipeline's radix-2^29 lazy field arithmetic

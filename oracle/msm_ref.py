@@ -10,7 +10,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libmsm_ref.so")
+# PM_REF_LIB: an alternative build of the same sources (the ASan / UBSan one,
+# oracle/_asan/libmsm_ref.so, in tests/test_asan.py)
+_LIB_PATH = os.environ.get("PM_REF_LIB") or os.path.join(_HERE, "libmsm_ref.so")
 _lib = None
 
 

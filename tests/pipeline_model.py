@@ -4,7 +4,7 @@ Mirrors halo2-aggregation_amd/csrc/{capi.hip:make_plan, msm_kernels.hpp} step
 by step, but over the additive group Z_r (a point is replaced by its discrete
 log, point addition by integer addition mod r).  It lets the CPU test-suite
 check the design's algebra -- signed digits, counting sort, slice ownership +
-fixup, segment / bit-decomposed bucket reduction and the window Horner --
+chain folds, segment / bit-decomposed bucket reduction and the window Horner --
 independently of any curve arithmetic.
 """
 from __future__ import annotations
@@ -16,7 +16,7 @@ def bit_length(v):
     return int(v).bit_length()
 
 
-def make_plan(n, c_override=0, chunk_override=0, groups_override=0):
+def make_plan(n, c_override=0, chunk_override=0):
     lg = bit_length(max(n, 1)) - 1
     c = c_override if c_override > 0 else max(4, min(16, lg - 2 if lg >= 14 else lg - 4))
     c = max(4, min(20, c))
@@ -28,11 +28,7 @@ def make_plan(n, c_override=0, chunk_override=0, groups_override=0):
     NB = ((K + 1 + L1 - 1) // L1) * L1
     M1 = K // L1  # segments cover slots [0, K); bucket K is a host term of its own
     NB2 = bit_length(M1 - 1)
-    G = groups_override if groups_override > 0 else 1
-    G = max(1, min(G, W))
-    wpg = (W + G - 1) // G
-    G = (W + wpg - 1) // wpg
-    work = n * wpg
+    work = n * W  # one window group (capi.hip make_plan)
     target = 256 * 1024
     chunk = max(16, (work + target - 1) // target)
     if chunk_override:
@@ -40,7 +36,7 @@ def make_plan(n, c_override=0, chunk_override=0, groups_override=0):
     nthreads = (work + chunk - 1) // chunk
     widths = [base + (1 if w < extra else 0) for w in range(W)]
     return dict(c=c, W=W, widths=widths, K=K, L1=L1, log2L1=L1.bit_length() - 1, NB=NB, M1=M1, NB2=NB2, chunk=chunk,
-                nthreads=nthreads, G=G, wpg=wpg)
+                nthreads=nthreads, cmax=cmax)
 
 
 def window_widths(W):
@@ -68,11 +64,14 @@ def digits(s, W):
     return out
 
 
-def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0, groups_override=0):
+K_TJOBS = 2  # msm_kernels.hpp kTJobs
+
+
+def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0):
     n = len(scalars)
     if n == 0:
         return 0
-    pl = make_plan(n, c_override, chunk_override, groups_override)
+    pl = make_plan(n, c_override, chunk_override)
     c, W, NB, L1, M1, NB2 = pl["c"], pl["W"], pl["NB"], pl["L1"], pl["M1"], pl["NB2"]
     TOT = W * NB + 1
     counts = [0] * TOT
@@ -108,77 +107,62 @@ def msm_model(scalars, dlogs, r, c_override=0, chunk_override=0, groups_override
 
     buckets = [0] * nslots
     chunk = pl["chunk"]
-    for g in range(pl["G"] - 1, -1, -1):  # window groups, top down (engine.hpp)
-        w0, w1 = g * pl["wpg"], min(W, (g + 1) * pl["wpg"])
-        s0, s1 = w0 * NB, w1 * NB
-        base, total = offsets[s0], offsets[s1]
-        head = [0] * pl["nthreads"]
-        for t in range(pl["nthreads"]):  # k_accumulate
-            start = base + t * chunk
-            if start >= total:
-                continue
-            end = min(start + chunk, total)
-            gb = find_bucket(s0, s1, start)
-            bend = offsets[gb + 1]
-            owned = offsets[gb] == start
-            acc = 0
-            for p in range(start, end):
-                if p == bend:
-                    if owned:
-                        buckets[gb] = acc
-                    else:
-                        head[t] = acc
-                    acc = 0
+    s1 = W * NB
+    head = [0] * pl["nthreads"]
+    for t in range(pl["nthreads"]):  # k_accumulate (one launch over every window)
+        start = t * chunk
+        if start >= total:
+            continue
+        end = min(start + chunk, total)
+        gb = find_bucket(0, s1, start)
+        bend = offsets[gb + 1]
+        owned = offsets[gb] == start
+        acc = 0
+        for p in range(start, end):
+            if p == bend:
+                if owned:
+                    buckets[gb] = acc
+                else:
+                    head[t] = acc
+                acc = 0
+                gb += 1
+                while offsets[gb + 1] <= p:
                     gb += 1
-                    while offsets[gb + 1] <= p:
-                        gb += 1
-                    bend = offsets[gb + 1]
-                    owned = True
-                i, neg = sorted_[p]
-                acc = (acc + (-dlogs[i] if neg else dlogs[i])) % r
-            if owned:
-                buckets[gb] = acc
-            else:
-                head[t] = acc
-        for t in range(pl["nthreads"]):  # k_fixup
-            start = base + t * chunk
-            if start >= total:
-                continue
-            end = min(start + chunk, total)
-            gb = find_bucket(s0, s1, end - 1)
-            bstart, bend = offsets[gb], offsets[gb + 1]
-            if bstart < start or bend <= end:
-                continue
-            acc = buckets[gb]
-            t_last = min((bend - 1 - base) // chunk, pl["nthreads"] - 1)
-            for t2 in range(t + 1, t_last + 1):
-                acc = (acc + head[t2]) % r
+                bend = offsets[gb + 1]
+                owned = True
+            i, neg = sorted_[p]
+            acc = (acc + (-dlogs[i] if neg else dlogs[i])) % r
+        if owned:
             buckets[gb] = acc
+        else:
+            head[t] = acc
+
+    def folded(slot):  # k_bucket_seg_q: the bucket plus its slice-boundary chain
+        bs, be = offsets[slot], offsets[slot + 1]
+        if bs == be:
+            return 0
+        tf, tl = bs // chunk, min((be - 1) // chunk, pl["nthreads"] - 1)
+        return (buckets[slot] + sum(head[tf + 1:tl + 1])) % r  # serial or wave-wide: same sum
+
     S = [0] * (W * M1)
     T = [0] * (W * M1)
-    for w in range(W):  # k_bucket_seg
+    for w in range(W):  # k_bucket_seg_q: S = B0 + .. + B3, T = B1 + 2 B2 + 3 B3
         for j in range(M1):
-            base = w * NB + j * L1
-            s = t_ = 0
-            for i in range(L1 - 1, 0, -1):
-                if offsets[base + i] != offsets[base + i + 1]:
-                    s = (s + buckets[base + i]) % r
-                t_ = (t_ + s) % r
-            if offsets[base] != offsets[base + 1]:
-                s = (s + buckets[base]) % r
-            S[w * M1 + j], T[w * M1 + j] = s, t_
+            Bq = [folded(w * NB + j * L1 + q) for q in range(L1)]
+            S[w * M1 + j] = sum(Bq) % r
+            T[w * M1 + j] = sum(q * Bq[q] for q in range(L1)) % r
     widths = pl["widths"]
     at = {}
     for w in range(W):  # k_bucket_bits -> host Horner over absolute bit positions
         G = [sum(S[w * M1 + j] for j in range(M1) if (j >> b) & 1) % r for b in range(NB2)]
-        sumT = sum(T[w * M1:(w + 1) * M1]) % r
-        sk = w * NB + M1 * L1  # the top bucket K (folded by segment 0's slot-0 lane)
-        bK = buckets[sk] if offsets[sk] != offsets[sk + 1] else 0
+        per = (M1 + K_TJOBS - 1) // K_TJOBS
+        Tp = [sum(T[w * M1 + j0:w * M1 + min(M1, j0 + per)]) % r for j0 in range(0, K_TJOBS * per, per)]
+        bK = folded(w * NB + M1 * L1)  # the top bucket K (segment 0's slot-0 lane)
         o = sum(widths[:w])
         for b in range(NB2):
             at.setdefault(o + b + pl["log2L1"], []).append(G[b])
-        at.setdefault(o, []).append(sumT)
-        at.setdefault(o + bit_length(pl["K"]) - 1, []).append(bK)
+        at.setdefault(o, []).extend(Tp)
+        at.setdefault(o + pl["cmax"] - 1, []).append(bK)
     acc = 0
     for q in range(max(at), -1, -1):
         acc = 2 * acc % r

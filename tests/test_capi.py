@@ -30,6 +30,12 @@ def test_header_is_plain_c():
     assert not re.search(r"\b(torch|at::|std::|hip[A-Z])", code)
 
 
+def test_abi_version_matches_header():
+    """pm_abi_version() == PM_ABI_VERSION: what a binding asserts at load."""
+    m = re.search(r"#define PM_ABI_VERSION (\d+)", open(H.HEADER_PATH).read())
+    assert m and H.abi_version() == int(m.group(1))
+
+
 def test_last_error_is_thread_local_string():
     assert isinstance(H.lib().pm_last_error(), bytes)
 
@@ -51,13 +57,14 @@ def test_device_code_has_every_launched_kernel():
         return sum(1 for n in names if stem in n)
 
     assert count("11k_sort_hist") == 3 * 16 * 2  # 3 scalar fields x 16 window counts x {2-B, 4-B digits}
-    assert count("12k_accumulate") == 3 * 2  # 3 curves x {plain, prefetch}
-    assert count("15k_sort_hist_glv") == 3 * 5 * 2  # 3 curves x W in 7..11 x {2-B, 4-B digits}
-    for stem in ("7k_fixupI", "12k_fixup_long", "12k_bucket_seg", "13k_bucket_bits", "15k_bases_to_r261",
+    for stem in ("12k_accumulate", "14k_bucket_seg_q", "13k_bucket_bits", "15k_bases_to_r261",
                  "16k_selftest_field", "13k_acc_termmul", "9k_acc_sum", "13k_acc_scalars", "12k_acc_powers",
-                 "13k_acc_termadd", "11k_bases_glv",
-                 "15k_synth_scalars", "13k_synth_bases"):
+                 "13k_acc_termadd", "15k_synth_scalars", "13k_synth_bases"):
         assert count(stem) == 3, stem
+    # the retired A/B kernels are gone (GLV mode, separate fixups, bit-sum fold pass)
+    for stem in ("15k_sort_hist_glv", "11k_bases_glv", "7k_fixupI", "12k_fixup_long", "13k_fixup_short",
+                 "12k_bucket_segI", "14k_bits_combine"):
+        assert count(stem) == 0, stem
     assert count("13k_sort_coarse") == 4 * 4  # {2-B, 4-B digits} x {4-B, 8-B entries} x points per thread 1..8
     assert count("11k_sort_fine") == 2
     for stem in ("13k_scan_reduce", "11k_scan_down"):

@@ -35,28 +35,27 @@ def test_every_window_width(golden, gpu_ctx, c):
         gpu_ctx.set_window(0)
 
 
-@pytest.mark.parametrize("c", [0, 12, 13, 16, 18, 20])
-def test_glv_off_matches(golden, gpu_ctx, c):
-    """GLV mode (2n points, 128-bit Babai-rounded halves) gives the same
-    points as the default plain 256-bit pipeline."""
-    try:
-        for name, case in golden.items():
-            gpu_ctx.set_window(c)
-            gpu_ctx.set_glv(True)
-            a = gpu_ctx.msm(case["curve"], case["scalars"], case["bases"])
-            gpu_ctx.set_glv(False)
-            b = gpu_ctx.msm(case["curve"], case["scalars"], case["bases"])
-            assert np.array_equal(a, case["expected"]) and np.array_equal(b, case["expected"]), name
-    finally:
-        gpu_ctx.set_glv(False)
-        gpu_ctx.set_window(0)
+def test_retired_options(gpu_ctx):
+    """The A/B paths measured slower (GLV mode, window groups, pinned staging
+    threads) are retired: their setters accept only the default and refuse
+    the rest with PM_ERR_UNSUPPORTED (-4) instead of silently ignoring it."""
+    gpu_ctx.set_glv(False)
+    gpu_ctx.set_pipeline(0, 0)
+    gpu_ctx.set_pipeline(1, 0)
+    gpu_ctx.set_h2d_threads(0)
+    for call in (lambda: gpu_ctx.set_glv(True), lambda: gpu_ctx.set_pipeline(2, 0),
+                 lambda: gpu_ctx.set_h2d_threads(4)):
+        with pytest.raises(H.PmError, match="error -4"):
+            call()
+    with pytest.raises(H.PmError, match="error -1"):
+        gpu_ctx.set_h2d_threads(-1)
 
 
-@pytest.mark.parametrize("groups,min_chunk", [(1, 0), (2, 1), (3, 7), (5, 0), (16, 64), (64, 2)])
-def test_pipeline_groups(golden, gpu_ctx, groups, min_chunk):
-    """Window-group pipelining (reduction of group g overlapping accumulation
-    of g-1, host Horner per group) and slice lengths do not change results."""
-    gpu_ctx.set_pipeline(groups, min_chunk)
+@pytest.mark.parametrize("min_chunk", [1, 2, 7, 64])
+def test_slice_lengths(golden, gpu_ctx, min_chunk):
+    """The accumulate slice length (every chain shape, from one-entry slices
+    to whole buckets per lane) does not change results."""
+    gpu_ctx.set_pipeline(0, min_chunk)
     try:
         for name in ("pallas_n4096", "pallas_equal_scalars", "pallas_neg_pairs", "vesta_n1024", "bn254_n1024"):
             if name not in golden:
@@ -65,7 +64,7 @@ def test_pipeline_groups(golden, gpu_ctx, groups, min_chunk):
             for c in (0, 5, 11):
                 gpu_ctx.set_window(c)
                 got = gpu_ctx.msm(case["curve"], case["scalars"], case["bases"])
-                assert np.array_equal(got, case["expected"]), (name, groups, min_chunk, c)
+                assert np.array_equal(got, case["expected"]), (name, min_chunk, c)
     finally:
         gpu_ctx.set_window(0)
         gpu_ctx.set_pipeline(0, 0)
@@ -152,8 +151,8 @@ def test_all_equal_scalars_large(gpu_ctx):
 @pytest.mark.parametrize("distinct", [3, 40, 700])
 def test_few_distinct_scalars(gpu_ctx, distinct):
     """Scalars from a small set: buckets of ~n/distinct points whose runs
-    cross several accumulate slices (the short chains folded inside
-    k_bucket_seg) or more than kMaxChain of them (k_fixup_long)."""
+    cross a few accumulate slices (chains folded by the bucket's own lane in
+    k_bucket_seg_q) or more than kSerialChain of them (folded wave-wide)."""
     import torch
 
     n = 1 << 16
@@ -200,12 +199,10 @@ def test_errors():
 
 
 @pytest.mark.parametrize("curve,n", [(0, (1 << 20) + 3), (1, 70001), (2, 5000)])
-def test_resident_device_and_staged_host_paths(gpu_ctx, curve, n):
+def test_resident_device_and_host_paths(gpu_ctx, curve, n):
     """Resident bases (converted to the pipeline form at upload, from device
-    or host memory) give the raw-bases result, with device scalars, host
-    scalars staged through pinned buffers by 0 (pageable), 1, 3 and 8 copy
-    threads (4 MiB chunks, ragged tail), windows at an offset, and GLV on
-    (ignored for pre-converted bases)."""
+    or host memory) give the raw-bases result, with device and host scalars,
+    and for windows at an offset."""
     s, b = _torch_inputs(gpu_ctx, curve, n)
     want = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
     S = s.cpu().numpy().view(np.uint64)
@@ -215,44 +212,29 @@ def test_resident_device_and_staged_host_paths(gpu_ctx, curve, n):
     try:
         assert np.array_equal(gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), n), want)
         assert np.array_equal(gpu_ctx.msm_resident_device(rh, 0, s.data_ptr(), n), want)
-        for t in (0, 1, 3, 8):
-            gpu_ctx.set_h2d_threads(t)
-            assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S), want), t
-            assert np.array_equal(gpu_ctx.msm(curve, S, B), want), t
-        gpu_ctx.set_h2d_threads(0)
+        assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S), want)
+        assert np.array_equal(gpu_ctx.msm(curve, S, B), want)
         k = n // 3
         part = gpu_ctx.msm_device(curve, s[k:].data_ptr(), b[k:].data_ptr(), n - k)
         assert np.array_equal(gpu_ctx.msm_resident(rb, k, S[k:]), part)
-        gpu_ctx.set_glv(True)
-        assert np.array_equal(gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), n), want)
     finally:
-        gpu_ctx.set_glv(False)
-        gpu_ctx.set_h2d_threads(0)
         rb.release()
         rh.release()
     if n < (1 << 20):
         assert np.array_equal(want, msm_ref.best_multiexp(curve, S, B))
 
 
-def test_h2d_threads_argument_checked(gpu_ctx):
-    with pytest.raises(H.PmError):
-        gpu_ctx.set_h2d_threads(9)
-    with pytest.raises(H.PmError):
-        gpu_ctx.set_h2d_threads(-1)
-
-
-@pytest.mark.parametrize("k,groups", [(1, 0), (2, 0), (5, 0), (3, 2)])
-def test_resident_batch(gpu_ctx, k, groups):
+@pytest.mark.parametrize("k", [1, 2, 5])
+def test_resident_batch(gpu_ctx, k):
     """pm_msm_resident_batch (copies of MSM j+1 and the host tail of MSM j-1
     overlapping MSM j's kernels) == k single pm_msm_resident calls, also with
-    window groups (no overlap then), canonical scalars and an offset window."""
+    canonical scalars and an offset window."""
     import torch
 
     n = (1 << 16) + 7
     s, b = _torch_inputs(gpu_ctx, 0, n + 100)
     B = b.cpu().numpy().view(np.uint64)
     rb = gpu_ctx.upload_bases(0, B)
-    gpu_ctx.set_pipeline(groups, 0)
     try:
         lists = []
         for j in range(k):
@@ -276,7 +258,6 @@ def test_resident_batch(gpu_ctx, k, groups):
         with pytest.raises(H.PmError):
             gpu_ctx.msm_resident_batch(rb, 200, lists[:1])   # window past the resident bases
     finally:
-        gpu_ctx.set_pipeline(0, 0)
         rb.release()
 
 
@@ -309,29 +290,28 @@ def test_resident_row_table(gpu_ctx, curve):
         rb.release()
 
 
-@pytest.mark.parametrize("distinct", [0, 40])
-def test_separate_fixup_path(gpu_ctx, distinct):
-    """PM_SEGQ=0 (k_fixup_short + k_bucket_seg instead of k_bucket_seg_q, the
-    A/B alternative) gives the same MSM as the default, on random scalars and
-    on scalars from a small set (long chains)."""
-    import os
-
-    n = (1 << 17) + 99
-    s, b = _torch_inputs(gpu_ctx, 1, n)
-    if distinct:
-        s[:] = s[torch_idx(s, distinct)]
-    os.environ["PM_SEGQ"] = "0"
-    try:
-        ctx0 = H.Context(gpu_ctx.device)
-    finally:
-        del os.environ["PM_SEGQ"]
-    a = ctx0.msm_device(1, s.data_ptr(), b.data_ptr(), n)
-    assert np.array_equal(a, gpu_ctx.msm_device(1, s.data_ptr(), b.data_ptr(), n))
-    assert np.array_equal(a, msm_ref.best_multiexp(1, s.cpu().numpy().view(np.uint64),
-                                                   b.cpu().numpy().view(np.uint64)))
-
-
-def torch_idx(s, distinct):
+@pytest.mark.parametrize("curve,min_chunk", [(1, 0), (0, 16), (2, 3)])
+def test_adjacent_giant_buckets(gpu_ctx, curve, min_chunk):
+    """Scalars 1 .. 64 (canonical): window 0's buckets 1 .. 64 hold n/64
+    points each and lie in ONE wave of k_bucket_seg_q, so almost every lane
+    of that wave owns a chain longer than kSerialChain slices and the wave
+    folds them one after another (wave-wide strided sums + butterfly)."""
     import torch
 
-    return torch.arange(s.shape[0], device=s.device) % distinct
+    n = (1 << 17) + 99
+    s, b = _torch_inputs(gpu_ctx, curve, n)
+    small = (torch.arange(n, device=s.device) % 64) + 1
+    s.zero_()
+    s[:, 0] = small
+    torch.cuda.synchronize()
+    gpu_ctx.set_pipeline(0, min_chunk)
+    try:
+        got = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n, canonical=True)
+    finally:
+        gpu_ctx.set_pipeline(0, 0)
+    C = P.CURVES[curve]
+    B = b.cpu().numpy().view(np.uint64)
+    # sum_i (i % 64 + 1) P_i == the C port on the Montgomery form of the scalars
+    mont = np.array([P.to_limbs((i % 64 + 1) * P.R_MONT % C.r) for i in range(64)], dtype=np.uint64)
+    S = mont[np.arange(n) % 64]
+    assert np.array_equal(got, msm_ref.best_multiexp(curve, S, B))

@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 import halo2_amd as H  # noqa: E402
 
-KERNELS = ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg", "bucket_bits", "bits_combine", "host_tail"]
+KERNELS = ["bases_r261", "sort_hist", "scan", "sort_coarse", "sort_fine", "accumulate", "fixup", "bucket_seg", "bucket_bits", "bits_combine", "host_tail"]  # round-2 names kept for A/B against older builds
 
 
 def main():
