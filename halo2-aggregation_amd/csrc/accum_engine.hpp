@@ -428,7 +428,7 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
-  template int msm_device_to_aff<Cv>(Ctx*, const void*, const void*, size_t, uint32_t, uint64_t*); \
+  template int msm_device_to_aff<Cv>(Ctx*, const void*, const void*, size_t, uint32_t, uint64_t*, const void*); \
   template int synth_scalars_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, uint32_t, void*);     \
   template int synth_bases_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, void*);                 \
   template int accum_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, void*, void*, \
@@ -436,7 +436,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
   template int selftest_field_impl<Cv>(Ctx*, uint64_t, uint32_t, uint64_t*);                      \
   template int fixed_table_impl<Cv>(Ctx*, const void*, pm_fixed_bases*);                          \
   template int ntt_device_impl<Cv>(Ctx*, int, void*, uint32_t, const uint64_t*, const uint64_t*);  \
-  template int msm_fixed_to_aff<Cv>(Ctx*, const pm_fixed_bases*, const void*, size_t, uint32_t, uint64_t*); \
+  template int msm_fixed_to_aff<Cv>(Ctx*, const pm_fixed_bases*, const void*, size_t, uint32_t, uint64_t*, \
+                                    const void*);                                                  \
   template int bases_to29_impl<Cv>(Ctx*, const void*, size_t, void*);                            \
   template int msm_resident_batch_impl<Cv>(Ctx*, const void*, const pm_fixed_bases*, const uint64_t* const*, size_t, \
                                            size_t, uint32_t, uint64_t*);                             \

@@ -11,6 +11,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <sched.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -55,8 +56,14 @@ void pm::Buf::release() {
   cap = 0;
 }
 
+static void dropin_release_all(pm_ctx* ctx);
+
 pm_ctx::~pm_ctx() {
   (void)hipSetDevice(device);
+  dropin_release_all(this);
+  delete pool;
+  for (auto& e : copy_ev) (void)hipEventDestroy(e);
+  if (copy_fence) (void)hipEventDestroy(copy_fence);
   for (pm::Buf* b : all_bufs()) b->release();
   for (auto& t : ntt_tw) t.buf.release();
   if (h_pinned) (void)hipHostFree(h_pinned);
@@ -108,6 +115,86 @@ int pm_ctx::ensure_group_events(int n) {
     grp_ev.push_back(e);
   }
   return PM_OK;
+}
+
+int pm_ctx::ensure_copy_events(int n) {
+  while ((int)copy_ev.size() < n) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    copy_ev.push_back(e);
+  }
+  return PM_OK;
+}
+
+int pm_ctx::copy_wait_for(hipStream_t st) {
+  if (!copy_fence) HIP_TRY(hipEventCreateWithFlags(&copy_fence, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(copy_fence, st));
+  HIP_TRY(hipStreamWaitEvent(copy_stream, copy_fence, 0));
+  return PM_OK;
+}
+
+// threads for host-side data-parallel work: this process's CPUs, capped by
+// OMP_NUM_THREADS (the GPU pool's 16-CPU share per GPU) and 16
+static int host_threads() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = CPU_COUNT(&cs);
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int k = std::atoi(e);
+    if (k > 0) n = std::min(n, k);
+  }
+  return std::max(1, std::min(16, n));
+}
+
+pm::HostPool& pm_ctx::host_pool() {
+  if (!pool) pool = new pm::HostPool(host_threads());
+  return *pool;
+}
+
+pm::HostPool::HostPool(int threads) {
+  for (int t = 1; t < threads; t++) th_.emplace_back([this, t] { loop(t); });
+}
+pm::HostPool::~HostPool() {
+  {
+    std::lock_guard<std::mutex> lk(m_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : th_) t.join();
+}
+void pm::HostPool::loop(int t) {
+  uint64_t seen = 0;
+  for (;;) {
+    std::function<void(int, int)> job;
+    int nt;
+    {
+      std::unique_lock<std::mutex> lk(m_);
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      if (t >= nt_) continue;
+      job = job_;
+      nt = nt_;
+    }
+    job(t, nt);
+    std::lock_guard<std::mutex> lk(m_);
+    if (--pending_ == 0) done_.notify_all();
+  }
+}
+void pm::HostPool::start(int nt, std::function<void(int, int)> job) {
+  nt = std::max(1, std::min(nt, size()));
+  {
+    std::lock_guard<std::mutex> lk(m_);
+    job_ = std::move(job);
+    nt_ = nt;
+    pending_ = nt - 1;
+    gen_++;
+  }
+  cv_.notify_all();
+}
+void pm::HostPool::wait() {
+  std::unique_lock<std::mutex> lk(m_);
+  done_.wait(lk, [&] { return pending_ == 0; });
 }
 
 int pm_ctx::ensure_pinned(size_t bytes) {
@@ -207,28 +294,14 @@ const CurveOps* curve_ops(int curve) {
   }
 }
 
-// pre29: d_b holds resident bases already in the R = 2^261 form (pm_bases)
+// pre29: d_b holds resident bases already in the R = 2^261 form (pm_bases);
+// h_s != nullptr: the scalars are still on the host (d_s is their buffer)
 int dispatch_msm_device(Ctx* ctx, int curve, const void* d_s, const void* d_b, size_t n, uint32_t flags,
-                        uint64_t out[8], bool pre29 = false) {
+                        uint64_t out[8], bool pre29 = false, const void* h_s = nullptr) {
   const CurveOps* ops = curve_ops(curve);
   if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
   flags &= ~kBasesR261;  // internal bit: never taken from the caller
-  return ops->msm(ctx, d_s, d_b, n, flags | (pre29 ? kBasesR261 : 0u), out);
-}
-
-int msm_host_inputs(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
-                    uint32_t flags, uint64_t out[8]) {
-  int rc;
-  if (n == 0) {
-    std::memset(out, 0, 64);
-    return PM_OK;
-  }
-  if ((rc = ctx->begin_call())) return rc;
-  if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
-  if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
-  if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
-  if ((rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) return rc;
-  return dispatch_msm_device(ctx, curve, ctx->in_scalars.p, ctx->in_bases.p, n, flags, out);
+  return ops->msm(ctx, d_s, d_b, n, flags | (pre29 ? kBasesR261 : 0u), out, h_s);
 }
 
 // default context per device (lazily created, process lifetime)
@@ -386,12 +459,15 @@ int pm_ctx_reset_stats(pm_ctx* ctx) {
   return PM_OK;
 }
 
+static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
+                      uint64_t out[8]);
+
 int pm_msm_ctx(pm_ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
                uint64_t out[8]) {
   if (!ctx || !out || (n && (!scalars || !bases))) return set_error(PM_ERR_ARG, "null argument");
   if (!valid_curve(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  return msm_host_inputs(ctx, curve, scalars, bases, n, flags, out);
+  return dropin_msm(ctx, curve, scalars, bases, n, flags, out);
 }
 
 int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags, uint64_t out[8]) {
@@ -476,15 +552,10 @@ bool resident_use_table(const pm_bases* b, size_t offset, size_t n) {
 }
 }  // namespace
 
-static int bases_upload(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, pm_bases** out) {
-  if (!ctx || !out || (n && !bases)) return set_error(PM_ERR_ARG, "null argument");
-  *out = nullptr;
+// the caller holds ctx->mu and has run begin_call
+static int bases_upload_locked(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, pm_bases** out) {
   const CurveOps* ops = curve_ops(curve);
-  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
-  if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "more than 2^26 resident bases");
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  int rc = ctx->begin_call();
-  if (rc) return rc;
+  int rc;
   std::unique_ptr<pm_bases> b(new pm_bases{curve, ctx->device, n, nullptr, nullptr});
   const void* src = bases;
   if (host && n) {
@@ -510,6 +581,17 @@ static int bases_upload(pm_ctx* ctx, int curve, const void* bases, bool host, si
   }
   *out = b.release();
   return PM_OK;
+}
+
+static int bases_upload(pm_ctx* ctx, int curve, const void* bases, bool host, size_t n, pm_bases** out) {
+  if (!ctx || !out || (n && !bases)) return set_error(PM_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (!curve_ops(curve)) return set_error(PM_ERR_ARG, "unknown curve id");
+  if (n > kMaxPoints) return set_error(PM_ERR_UNSUPPORTED, "more than 2^26 resident bases");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return bases_upload_locked(ctx, curve, bases, host, n, out);
 }
 
 int pm_bases_upload(pm_ctx* ctx, int curve, const uint64_t* bases, size_t n, pm_bases** out) {
@@ -551,13 +633,148 @@ static int msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const voi
   int rc = ctx->begin_call();
   if (rc) return rc;
   const void* d_s = scalars;
-  if (host) {
+  if (host) {  // the copy is chunked behind the histogram pass (msm_device_impl)
     if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
-    if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
     d_s = ctx->in_scalars.p;
   }
-  if (resident_use_table(b, offset, n)) return curve_ops(b->curve)->msm_fixed(ctx, b->table, d_s, n, flags, out);
-  return dispatch_msm_device(ctx, b->curve, d_s, (const char*)b->d + offset * 64, n, flags, out, true);
+  const void* h_s = host ? scalars : nullptr;
+  if (resident_use_table(b, offset, n))
+    return curve_ops(b->curve)->msm_fixed(ctx, b->table, d_s, n, flags & ~kBasesR261, out, h_s);
+  return dispatch_msm_device(ctx, b->curve, d_s, (const char*)b->d + offset * 64, n, flags, out, true, h_s);
+}
+
+// ------------------------------------------------ drop-in base cache (pm_msm)
+// halo2 calls best_multiexp with the same SRS bases over and over
+// (commit_lagrange over params.g_lagrange, the commits inside create_proof:
+// examples/simple-example.rs:606,638-640,702).  pm_msm / pm_msm_ctx keep base
+// sets of >= kDropinMinN points resident, keyed by (curve, n, a 64-bit XXH64-
+// style digest of every chunk of the base bytes, folded twice), so a repeated
+// set skips its 64 B/point upload and runs as a resident (row-table) MSM.
+// The digest is computed on the host pool while the scalars cross PCIe; any
+// change of the bytes (same pointer or not) changes the key and re-uploads.
+// The digest is not cryptographic: it guards against stale data, not against
+// a caller forging colliding base sets.
+namespace {
+constexpr uint64_t kX1 = 0x9E3779B185EBCA87ull, kX2 = 0xC2B2AE3D27D4EB4Full, kX3 = 0x165667B19E3779F9ull,
+                   kX4 = 0x85EBCA77C2B2AE63ull;
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t xround(uint64_t acc, uint64_t w) { return rotl64(acc + w * kX2, 31) * kX1; }
+inline uint64_t xmerge(uint64_t h, uint64_t v) { return (h ^ xround(0, v)) * kX1 + kX4; }
+inline uint64_t xaval(uint64_t h) {
+  h ^= h >> 33;
+  h *= kX2;
+  h ^= h >> 29;
+  h *= kX3;
+  return h ^ (h >> 32);
+}
+// XXH64-style hash of nwords (a multiple of 4) 64-bit words
+uint64_t stripe_hash(const uint64_t* p, size_t nwords, uint64_t seed) {
+  uint64_t v1 = seed + kX1 + kX2, v2 = seed + kX2, v3 = seed, v4 = seed - kX1;
+  for (size_t i = 0; i + 4 <= nwords; i += 4) {
+    v1 = xround(v1, p[i]);
+    v2 = xround(v2, p[i + 1]);
+    v3 = xround(v3, p[i + 2]);
+    v4 = xround(v4, p[i + 3]);
+  }
+  uint64_t h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+  h = xmerge(xmerge(xmerge(xmerge(h, v1), v2), v3), v4);
+  return xaval(h + nwords * 8);
+}
+constexpr size_t kDigestChunk = size_t(1) << 15;  // points per chunk (2 MiB)
+}  // namespace
+
+static void dropin_release_all(pm_ctx* ctx) {
+  for (auto& e : ctx->dropin) pm_bases_release(e.b);
+  ctx->dropin.clear();
+}
+
+static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
+                      uint64_t out[8]) {
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  int rc;
+  if ((rc = ctx->begin_call())) return rc;
+  if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
+  if (n < kDropinMinN || n > kMaxPoints) {  // small MSMs: both inputs uploaded, plain pipeline
+    if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
+    if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
+    if ((rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) return rc;
+    return dispatch_msm_device(ctx, curve, ctx->in_scalars.p, ctx->in_bases.p, n, flags, out);
+  }
+  // digest of the bases on the pool's workers while this thread copies the scalars
+  const size_t nch = (n + kDigestChunk - 1) / kDigestChunk;
+  std::vector<uint64_t> part((nch + 3) & ~size_t(3), 0);
+  pm::HostPool& pool = ctx->host_pool();
+  const int nw = std::max(1, pool.size() - 1);
+  auto job = [&](int t, int) {
+    for (size_t k = (size_t)(t - 1); k < nch; k += (size_t)nw) {
+      const size_t p0 = k * kDigestChunk, p1 = std::min(n, p0 + kDigestChunk);
+      part[k] = stripe_hash(bases + 8 * p0, 8 * (p1 - p0), k);
+    }
+  };
+  const bool threaded = pool.size() > 1;
+  if (threaded) pool.start(pool.size(), job);
+  const int copy_rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream);
+  if (threaded) pool.wait();
+  else job(1, 1);
+  if (copy_rc) return copy_rc;
+  const uint64_t d0 = stripe_hash(part.data(), part.size(), 0x5EEDull + (uint64_t)curve);
+  const uint64_t d1 = stripe_hash(part.data(), part.size(), 0xA11CEull ^ ((uint64_t)n << 8));
+  pm_bases* b = nullptr;
+  for (auto& e : ctx->dropin)
+    if (e.curve == curve && e.n == n && e.d0 == d0 && e.d1 == d1) {
+      e.last_use = ++ctx->dropin_clock;
+      b = e.b;
+      ctx->dropin_hits++;
+      break;
+    }
+  if (!b) {
+    ctx->dropin_misses++;
+    if ((rc = bases_upload_locked(ctx, curve, bases, true, n, &b))) return rc;
+    size_t bytes = 0;
+    pm_bases_info(b, nullptr, nullptr, &bytes);
+    // evict least recently used sets beyond the entry / memory budget
+    auto total = [&] {
+      size_t s = 0;
+      for (auto& e : ctx->dropin) s += e.bytes;
+      return s;
+    };
+    while (!ctx->dropin.empty() &&
+           ((int)ctx->dropin.size() >= kDropinEntries || total() + bytes > kDropinBytes)) {
+      auto lru = std::min_element(ctx->dropin.begin(), ctx->dropin.end(),
+                                  [](const pm::DropinEntry& x, const pm::DropinEntry& y) { return x.last_use < y.last_use; });
+      pm_bases_release(lru->b);
+      ctx->dropin.erase(lru);
+    }
+    ctx->dropin.push_back(pm::DropinEntry{curve, n, d0, d1, b, bytes, ++ctx->dropin_clock});
+  }
+  if (resident_use_table(b, 0, n))
+    return curve_ops(curve)->msm_fixed(ctx, b->table, ctx->in_scalars.p, n, flags & ~kBasesR261, out, nullptr);
+  return dispatch_msm_device(ctx, curve, ctx->in_scalars.p, b->d, n, flags, out, true);
+}
+
+int pm_ctx_dropin_stats(pm_ctx* ctx, uint64_t* hits, uint64_t* misses, int* entries, size_t* device_bytes) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (hits) *hits = ctx->dropin_hits;
+  if (misses) *misses = ctx->dropin_misses;
+  if (entries) *entries = (int)ctx->dropin.size();
+  if (device_bytes) {
+    size_t s = 0;
+    for (auto& e : ctx->dropin) s += e.bytes;
+    *device_bytes = s;
+  }
+  return PM_OK;
+}
+
+int pm_ctx_dropin_clear(pm_ctx* ctx) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  dropin_release_all(ctx);
+  return PM_OK;
 }
 
 int pm_msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* scalars, size_t n,
@@ -696,7 +913,7 @@ int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_sca
   }
   int rc = ctx->begin_call();
   if (rc) return rc;
-  return curve_ops(fb->curve)->msm_fixed(ctx, fb, d_scalars, n, flags & ~kBasesR261, out);
+  return curve_ops(fb->curve)->msm_fixed(ctx, fb, d_scalars, n, flags & ~kBasesR261, out, nullptr);
 }
 
 int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars, size_t n, uint32_t flags,
@@ -712,8 +929,7 @@ int pm_msm_fixed(pm_ctx* ctx, const pm_fixed_bases* fb, const uint64_t* scalars,
   int rc = ctx->begin_call();
   if (rc) return rc;
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
-  if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
-  return curve_ops(fb->curve)->msm_fixed(ctx, fb, ctx->in_scalars.p, n, flags & ~kBasesR261, out);
+  return curve_ops(fb->curve)->msm_fixed(ctx, fb, ctx->in_scalars.p, n, flags & ~kBasesR261, out, scalars);
 }
 
 int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {

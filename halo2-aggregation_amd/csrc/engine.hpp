@@ -54,25 +54,26 @@ void launch_coarse(const void* dg, uint32_t ue, SortGeom gm, const uint32_t* bof
   }
 }
 
+// k_sort_hist over blocks [g.blk0, g.blk0 + nb)
 template <class Fs, int W>
-void launch_sort_w(bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* bh,
+void launch_sort_w(bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, int nb, uint32_t* bh,
                    void* digits, uint32_t stride, uint32_t merged, hipStream_t st) {
   const size_t lds = (size_t)W * g.NCB * 4;
   if (d16)
-    k_sort_hist<Fs, W, true><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint16_t*)digits, bh, stride,
-                                                                merged);
+    k_sort_hist<Fs, W, true><<<nb, kSortThreads, lds, st>>>(s, n, canonical, g, (uint16_t*)digits, bh, stride,
+                                                            merged);
   else
-    k_sort_hist<Fs, W, false><<<g.nblk, kSortThreads, lds, st>>>(s, n, canonical, g, (uint32_t*)digits, bh, stride,
-                                                                 merged);
+    k_sort_hist<Fs, W, false><<<nb, kSortThreads, lds, st>>>(s, n, canonical, g, (uint32_t*)digits, bh, stride,
+                                                             merged);
 }
 
 // one instance per window count reachable from c in [kMinC, kMaxC]
 template <class Fs>
-int launch_sort(int W, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, uint32_t* bh,
+int launch_sort(int W, bool d16, const uint32_t* s, uint32_t n, uint32_t canonical, SortGeom g, int nb, uint32_t* bh,
                 void* digits, uint32_t stride, uint32_t merged, hipStream_t st) {
   switch (W) {
 #define PM_W(k) \
-  case k: launch_sort_w<Fs, k>(d16, s, n, canonical, g, bh, digits, stride, merged, st); return PM_OK;
+  case k: launch_sort_w<Fs, k>(d16, s, n, canonical, g, nb, bh, digits, stride, merged, st); return PM_OK;
     PM_W(13) PM_W(14) PM_W(15) PM_W(16) PM_W(18) PM_W(19) PM_W(20) PM_W(22) PM_W(24) PM_W(26) PM_W(29)
     PM_W(32) PM_W(37) PM_W(43) PM_W(52) PM_W(64)
 #undef PM_W
@@ -114,10 +115,15 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result);
 // *tail; msm_tail then waits for it and runs the Horner.  Two MSMs can be in
 // flight (slots 0 and 1): the tail of one overlaps the kernels of the next
 // (pm_msm_resident_batch).  tail == nullptr: run the tail here.
+//
+// h_scalars != nullptr: the scalars are still in (pageable) host memory and
+// d_scalars is their device buffer; the copy goes over the copy stream in
+// chunks, and the histogram pass runs chunk by chunk behind it, so all but
+// the last chunk's histogram overlaps the PCIe transfer.
 template <class Cv>
 int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases, size_t n, uint32_t flags,
                     Xyzz<typename Cv::Base>* result, const pm_fixed_bases* ft = nullptr,
-                    MsmTail<typename Cv::Base>* tail = nullptr, int slot = 0) {
+                    MsmTail<typename Cv::Base>* tail = nullptr, int slot = 0, const void* h_scalars = nullptr) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   if (n == 0) {
@@ -225,9 +231,44 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
               (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
   }
   const uint32_t canon = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
-  PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, bh, ctx->digits.p,
-                                                   (uint32_t)stride, (uint32_t)kmerge, st));
-  if (rc) return rc;
+  if (h_scalars) {
+    // chunks of whole histogram blocks, ~8 MB each (2^20: 4 chunks of 64 blocks)
+    const size_t pts_blk = (size_t)g.ppt * kSortThreads;
+    const int nch = (int)std::max<size_t>(1, std::min<size_t>(kH2DChunks, n * 32 / kH2DChunkMin));
+    const int bpc = (int)((((n + pts_blk - 1) / pts_blk) + nch - 1) / nch);
+    if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    if ((rc = ctx->ensure_copy_events(nch))) return rc;
+    hipEvent_t ta = nullptr, tb = nullptr;  // "h2d" timing: first chunk's start to last chunk's end
+    if (ctx->timed("h2d")) {
+      ta = ctx->next_event();
+      tb = ctx->next_event();
+    }
+    for (int c = 0; c * bpc < g.nblk; c++) {
+      const size_t p0 = std::min(n, (size_t)c * bpc * pts_blk), p1 = std::min(n, (size_t)(c + 1) * bpc * pts_blk);
+      if (p1 > p0) {
+        if (c == 0 && (rc = ctx->copy_wait_for(st))) return rc;  // the buffer's previous reader
+        if (c == 0 && ta) HIP_TRY(hipEventRecord(ta, ctx->copy_stream));
+        HIP_TRY(hipMemcpyAsync((char*)d_scalars + p0 * 32, (const char*)h_scalars + p0 * 32, (p1 - p0) * 32,
+                               hipMemcpyHostToDevice, ctx->copy_stream));
+        HIP_TRY(hipEventRecord(ctx->copy_ev[c], ctx->copy_stream));
+        if (p1 == n && tb) {
+          HIP_TRY(hipEventRecord(tb, ctx->copy_stream));
+          ctx->mark("h2d", ta, tb);
+        }
+        HIP_TRY(hipStreamWaitEvent(st, ctx->copy_ev[c], 0));
+      }
+      SortGeom gc = g;
+      gc.blk0 = c * bpc;
+      const int nb = std::min(bpc, g.nblk - gc.blk0);
+      PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, gc, nb, bh, ctx->digits.p,
+                                                       (uint32_t)stride, (uint32_t)kmerge, st));
+      if (rc) return rc;
+    }
+  } else {
+    PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, g.nblk, bh, ctx->digits.p,
+                                                     (uint32_t)stride, (uint32_t)kmerge, st));
+    if (rc) return rc;
+  }
   PM_LAUNCH(ctx, "scan", {
     k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum);
     k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum, bofs, nullptr);
@@ -403,10 +444,11 @@ Aff<F> aff_from_u64(const uint64_t in[8]) {
 }
 
 template <class Cv>
-int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint32_t flags, uint64_t out[8]) {
+int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint32_t flags, uint64_t out[8],
+                      const void* h_s) {
   using F = typename Cv::Base;
   Xyzz<F> r;
-  int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, (const uint32_t*)d_b, n, flags, &r);
+  int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, (const uint32_t*)d_b, n, flags, &r, nullptr, nullptr, 0, h_s);
   if (rc) return rc;
   aff_to_u64<F>(xyzz_to_aff<F>(r), out);
   return PM_OK;
@@ -498,10 +540,11 @@ int fixed_table_impl(Ctx* ctx, const void* d_bases, pm_fixed_bases* ft) {
 }
 
 template <class Cv>
-int msm_fixed_to_aff(Ctx* ctx, const pm_fixed_bases* ft, const void* d_s, size_t n, uint32_t flags, uint64_t out[8]) {
+int msm_fixed_to_aff(Ctx* ctx, const pm_fixed_bases* ft, const void* d_s, size_t n, uint32_t flags, uint64_t out[8],
+                     const void* h_s) {
   using F = typename Cv::Base;
   Xyzz<F> r;
-  int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, nullptr, n, flags, &r, ft);
+  int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, nullptr, n, flags, &r, ft, nullptr, 0, h_s);
   if (rc) return rc;
   aff_to_u64<F>(xyzz_to_aff<F>(r), out);
   return PM_OK;

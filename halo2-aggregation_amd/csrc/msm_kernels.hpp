@@ -205,6 +205,7 @@ struct SortGeom {
   int FB;    // fine bits
   int NCB;   // coarse bins per window
   int nblk;  // point blocks of ppt * kSortThreads points
+  int blk0;  // k_sort_hist: first block of this launch (chunked launches behind a chunked scalar copy)
   int ppt;   // points per thread, <= kSortPerThread
   int hsub;  // coarse geometry: histogram blocks per coarse block (bofs rows hold nblk histogram blocks)
   // words the histogram kernel zeroes for later stages (instead of two
@@ -288,11 +289,12 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // W * NCB
   const int nbins = W * g.NCB;
   const uint32_t Wr = (uint32_t)W / kmerge;
-  if (blockIdx.x == 0) sort_clear(g);
+  const uint32_t blk = blockIdx.x + (uint32_t)g.blk0;
+  if (blk == 0) sort_clear(g);
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
   __syncthreads();
   for (int r = 0; r < g.ppt; r++) {
-    const uint32_t i = (blockIdx.x * g.ppt + r) * kSortThreads + threadIdx.x;
+    const uint32_t i = (blk * g.ppt + r) * kSortThreads + threadIdx.x;
     if (i >= stride) break;
     if (i >= n) {
 #pragma unroll
@@ -313,7 +315,7 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) {
     const uint32_t w = k / g.NCB, cb = k - w * g.NCB;
     const size_t row = ((size_t)(w % Wr) * g.NCB + cb) * kmerge + w / Wr;
-    bh[row * g.nblk + blockIdx.x] = hist[k];
+    bh[row * g.nblk + blk] = hist[k];
   }
 }
 

@@ -9,10 +9,13 @@
 
 #include "../../include/pasta_msm.h"
 
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -33,6 +36,17 @@ constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg_q (one quad per
 // caller flags): d_bases already hold the pipeline's R = 2^261 canonical
 // form (resident pm_bases converted at upload), so no per-call conversion
 constexpr uint32_t kBasesR261 = 1u << 30;
+// host scalars (pm_msm_resident, pm_msm_fixed, pm_msm): the copy is split into
+// at most kH2DChunks chunks of >= kH2DChunkMin bytes on the copy stream, and
+// k_sort_hist runs chunk by chunk behind it
+constexpr int kH2DChunks = 4;
+constexpr size_t kH2DChunkMin = size_t(4) << 20;
+// drop-in base cache of pm_msm / pm_msm_ctx (capi.hip): base sets of at least
+// kDropinMinN points are kept resident, keyed by a content digest; at most
+// kDropinEntries sets and kDropinBytes of device memory per context
+constexpr size_t kDropinMinN = size_t(1) << 12;
+constexpr int kDropinEntries = 4;
+constexpr size_t kDropinBytes = size_t(16) << 30;
 
 struct Buf {
   void* p = nullptr;
@@ -84,6 +98,39 @@ struct TimedSpan {
   hipEvent_t a, b;
 };
 
+// A few persistent host threads for data-parallel host work inside a call
+// (the drop-in cache's content digest of the caller's bases runs on them
+// while the scalars cross PCIe).  run() starts job(t, nt) for t = 1 .. nt-1
+// on the workers; the caller runs t = 0 itself and then wait()s.
+class HostPool {
+ public:
+  explicit HostPool(int threads);
+  ~HostPool();
+  int size() const { return (int)th_.size() + 1; }
+  void start(int nt, std::function<void(int, int)> job);
+  void wait();
+
+ private:
+  void loop(int t);
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  std::function<void(int, int)> job_;
+  int nt_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// resident base set of the drop-in cache (pm_msm): key = (curve, n, digest)
+struct DropinEntry {
+  int curve;
+  size_t n;
+  uint64_t d0, d1;
+  pm_bases* b;
+  size_t bytes;
+  uint64_t last_use;
+};
+
 }  // namespace pm
 
 // Fixed-base table (pm_fixed_bases_create*): rows x npad affine points in the
@@ -116,7 +163,13 @@ struct pm_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t red_stream = nullptr;  // accumulator side stream (accum_engine.hpp)
-  hipStream_t copy_stream = nullptr; // H2D of the next MSM's scalars (pm_msm_resident_batch)
+  hipStream_t copy_stream = nullptr; // H2D of host scalars (chunked; pm_msm_resident_batch: the next MSM's)
+  std::vector<hipEvent_t> copy_ev;   // chunk c of the current host-scalar copy has landed
+  hipEvent_t copy_fence = nullptr;   // copy_wait_for: the copy stream waits for the context stream
+  pm::HostPool* pool = nullptr;      // lazily created (drop-in digest)
+  std::vector<pm::DropinEntry> dropin;  // drop-in base cache (pm_msm / pm_msm_ctx)
+  uint64_t dropin_clock = 0;
+  uint64_t dropin_hits = 0, dropin_misses = 0;
   hipEvent_t batch_ev[4] = {};       // batch pipelining: copied[2], consumed[2]
   std::vector<hipEvent_t> grp_ev;    // MSM: one per pinned term slot (terms copied)
   int window_c = 0;
@@ -162,6 +215,9 @@ struct pm_ctx {
   // staging threads round 2 measured, ~38 GB/s, and retired)
   int upload_h2d(void* d, const void* h, size_t bytes, hipStream_t st);
   int ensure_group_events(int n);
+  int ensure_copy_events(int n);
+  int copy_wait_for(hipStream_t st);
+  pm::HostPool& host_pool();
   hipEvent_t next_event();
   void mark(const char* name, hipEvent_t a, hipEvent_t b);
 };
@@ -175,7 +231,9 @@ namespace pm {
 // Per-curve engine entry points, one translation unit per curve
 // (inst_pallas.hip, inst_vesta.hip, inst_bn254.hip) so they build in parallel.
 struct CurveOps {
-  int (*msm)(Ctx* ctx, const void* d_scalars, const void* d_bases, size_t n, uint32_t flags, uint64_t out[8]);
+  // h_scalars != nullptr: scalars still in host memory, d_scalars their device buffer (chunked copy)
+  int (*msm)(Ctx* ctx, const void* d_scalars, const void* d_bases, size_t n, uint32_t flags, uint64_t out[8],
+             const void* h_scalars);
   int (*point_add)(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
   int (*synth_scalars)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, uint32_t mont, void* d_out);
   int (*synth_bases)(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, void* d_out);
@@ -189,7 +247,7 @@ struct CurveOps {
   int (*fixed_table)(Ctx* ctx, const void* d_bases, pm_fixed_bases* ft);
   int (*ntt)(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint64_t omega[4], const uint64_t* scale);
   int (*msm_fixed)(Ctx* ctx, const pm_fixed_bases* ft, const void* d_scalars, size_t n, uint32_t flags,
-                   uint64_t out[8]);
+                   uint64_t out[8], const void* h_scalars);
   // resident bases: Rust-layout affine (R = 2^256) -> the pipeline's R = 2^261 canonical form
   int (*bases_to29)(Ctx* ctx, const void* d_in, size_t n, void* d_out);
   // k MSMs of n host scalars against resident (R = 2^261) bases, pipelined

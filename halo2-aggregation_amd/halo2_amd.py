@@ -216,6 +216,9 @@ def _load():
         "pm_ctx_set_timing_filter": ([_vp, ctypes.c_char_p], ctypes.c_int),
         "pm_ctx_kernel_stats": ([_vp, ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "pm_ctx_reset_stats": ([_vp], ctypes.c_int),
+        "pm_ctx_dropin_stats": ([_vp, _u64p, _u64p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)],
+                                ctypes.c_int),
+        "pm_ctx_dropin_clear": ([_vp], ctypes.c_int),
         "pm_msm": ([ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_msm_ctx": ([_vp, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_msm_device": ([_vp, ctypes.c_int, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
@@ -527,7 +530,20 @@ class Context:
         _check(lib().pm_ctx_kernel_stats(self.h, name.encode(), ctypes.byref(n), ctypes.byref(ms)))
         return n.value, ms.value
 
+    def dropin_stats(self):
+        """pm_ctx_dropin_stats -> dict(hits, misses, entries, device_bytes) of
+        pm_msm_ctx's resident base cache."""
+        hi, mi, en, by = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_size_t()
+        _check(lib().pm_ctx_dropin_stats(self.h, ctypes.byref(hi), ctypes.byref(mi), ctypes.byref(en),
+                                         ctypes.byref(by)))
+        return {"hits": hi.value, "misses": mi.value, "entries": en.value, "device_bytes": by.value}
+
+    def dropin_clear(self):
+        _check(lib().pm_ctx_dropin_clear(self.h))
+
     def msm(self, curve, coeffs, bases, canonical=False):
+        """pm_msm_ctx: host scalars and host bases (the transparent
+        best_multiexp drop-in, with the resident base cache)."""
         s, b = _as_u64(coeffs, 4), _as_u64(bases, 8)
         out = np.zeros(8, dtype=np.uint64)
         _check(lib().pm_msm_ctx(self.h, curve, _p(s), _p(b), s.shape[0], SCALARS_CANONICAL if canonical else 0,

@@ -110,9 +110,22 @@ int pm_ctx_reset_stats(pm_ctx* ctx);
  * it into C::Curve with `to_curve()`.  n == 0 yields the identity. */
 int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
            uint64_t out[8]);
-/* Same, on an explicit context (host pointers). */
+/* Same, on an explicit context (host pointers).
+ * Drop-in base cache: from 4096 points on, pm_msm / pm_msm_ctx keep each base
+ * set they see resident on the device (converted, with the row table from
+ * 2^18 points, like pm_bases_upload), keyed by (curve, n, a 64-bit content
+ * digest of the base bytes computed on host threads while the scalars are
+ * copied).  A repeated set -- halo2's commits against params.g /
+ * params.g_lagrange -- then costs only its scalars' transfer; changed bytes
+ * (at the same address or not) miss and re-upload.  At most 4 sets / 16 GiB
+ * per context, least recently used evicted.  The digest is not
+ * cryptographic (it does not defend against forged collisions). */
 int pm_msm_ctx(pm_ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
                uint32_t flags, uint64_t out[8]);
+/* Drop-in cache counters of ctx (any pointer may be NULL), and a way to
+ * release its sets early. */
+int pm_ctx_dropin_stats(pm_ctx* ctx, uint64_t* hits, uint64_t* misses, int* entries, size_t* device_bytes);
+int pm_ctx_dropin_clear(pm_ctx* ctx);
 /* Same, with scalars and bases already in device memory of ctx's device. */
 int pm_msm_device(pm_ctx* ctx, int curve, const void* d_scalars, const void* d_bases, size_t n,
                   uint32_t flags, uint64_t out[8]);

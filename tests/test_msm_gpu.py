@@ -315,3 +315,67 @@ def test_adjacent_giant_buckets(gpu_ctx, curve, min_chunk):
     mont = np.array([P.to_limbs((i % 64 + 1) * P.R_MONT % C.r) for i in range(64)], dtype=np.uint64)
     S = mont[np.arange(n) % 64]
     assert np.array_equal(got, msm_ref.best_multiexp(curve, S, B))
+
+
+@pytest.mark.parametrize("curve", [0, 2])
+def test_dropin_base_cache(curve):
+    """pm_msm_ctx (host scalars + host bases, the transparent best_multiexp
+    drop-in) keeps base sets resident keyed by a content digest: a repeated
+    set hits (also for other scalars), bytes changed in place at the same
+    address miss and re-upload with a bit-exact result, small MSMs bypass the
+    cache, at most 4 sets stay, and clear() releases them."""
+    ctx = H.Context(0)
+    try:
+        n = (1 << 14) + 3
+        s, b = _torch_inputs(ctx, curve, 2 * n)
+        S = s.cpu().numpy().view(np.uint64).copy()
+        B = b.cpu().numpy().view(np.uint64).copy()
+        Bn = np.ascontiguousarray(B[:n])
+        want = msm_ref.best_multiexp(curve, S[:n], Bn)
+        assert np.array_equal(ctx.msm(curve, S[:n], Bn), want)
+        assert ctx.dropin_stats()["misses"] == 1 and ctx.dropin_stats()["hits"] == 0
+        assert np.array_equal(ctx.msm(curve, S[n:], Bn), msm_ref.best_multiexp(curve, S[n:], Bn))
+        st = ctx.dropin_stats()
+        assert st["hits"] == 1 and st["entries"] == 1
+        # mutate one base in place (same pointer): must miss and stay exact
+        Bn[5] = B[n + 5]
+        assert np.array_equal(ctx.msm(curve, S[:n], Bn), msm_ref.best_multiexp(curve, S[:n], Bn))
+        st = ctx.dropin_stats()
+        assert st["misses"] == 2 and st["entries"] == 2
+        # small MSMs bypass the cache
+        ctx.msm(curve, S[:100], B[:100])
+        assert ctx.dropin_stats()["entries"] == 2
+        # LRU bound
+        for k in range(4):
+            Bk = np.ascontiguousarray(B[k + 1:k + 1 + n])
+            assert np.array_equal(ctx.msm(curve, S[:n], Bk), msm_ref.best_multiexp(curve, S[:n], Bk))
+        assert ctx.dropin_stats()["entries"] == 4
+        ctx.dropin_clear()
+        assert ctx.dropin_stats()["entries"] == 0
+    finally:
+        ctx.close()
+
+
+def test_dropin_row_table_and_host_chunks(gpu_ctx):
+    """A full-length repeated set from 2^18 points runs as a resident
+    row-table MSM; pm_msm_resident / pm_msm_fixed with host scalars copy them
+    in chunks behind the histogram pass; all equal the device-input MSM."""
+    n = (1 << 18) + 11
+    s, b = _torch_inputs(gpu_ctx, 0, n)
+    want = gpu_ctx.msm_device(0, s.data_ptr(), b.data_ptr(), n)
+    S = s.cpu().numpy().view(np.uint64).copy()
+    B = b.cpu().numpy().view(np.uint64).copy()
+    ctx = H.Context(0)
+    try:
+        for _ in range(3):
+            assert np.array_equal(ctx.msm(0, S, B), want)
+        assert ctx.dropin_stats()["hits"] == 2
+        rb = ctx.upload_bases(0, d_bases=b.data_ptr(), n=n)
+        assert rb.rows > 1
+        assert np.array_equal(ctx.msm_resident(rb, 0, S), want)
+        rb.release()
+        fb = ctx.fixed_bases(0, d_bases=b.data_ptr(), n=n)
+        assert np.array_equal(fb.msm(S), want)
+        fb.release()
+    finally:
+        ctx.close()
