@@ -9,7 +9,12 @@ all-gather of the per-rank partial points over RCCL and their fold on the host
 (EC addition is not limb-wise, so no all-reduce).  `value` = N*2^20 / step time.
 
 `roofline` is for the dominant kernel (k_accumulate), its duration measured
-live with HIP events on the context stream over the timed region.
+live with HIP events on the context stream over the timed region.  The
+headline runs against the resident SRS bases (their row table, like
+params.g in halo2); `variable_base` is the same MSM from raw bases (non-SRS
+bases, e.g. the verifier's proof commitments) with its own roofline,
+`dropin_pm_msm` the literal pm_msm_ctx drop-in call with host inputs (cold and
+warm), `small_n` its latency against the C port for n = 2^0 .. 2^16.
 `cpu_baseline` times the C restatement of halo2 best_multiexp (oracle/msm_ref.c)
 on the host cores of the same box, on the same inputs, at N=1 on rank 0.
 
@@ -60,6 +65,9 @@ def parse():
                     help="also time the fixed-base MSM at 2^23 per GPU (the outer prover's k = 23 commit) (1) or skip (0)")
     ap.add_argument("--strong-logn", type=int, default=22,
                     help="strong-scaling leg: a fixed 2^k Vesta MSM split over the ranks (SURVEY config 4); 0 = skip")
+    ap.add_argument("--small-n", type=int, default=1, help="drop-in latency curve n = 2^0..2^16 vs the C port (1/0)")
+    ap.add_argument("--accum-b16", type=int, default=1,
+                    help="also time BASELINE config 3: 16 simple-example proofs at k = 14 per GPU (1) or skip (0)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check only: no GPU work (gloo), prints the JSON skeleton")
     return ap.parse_args()
@@ -229,6 +237,8 @@ def main():
         if args.ntt_large_logn > 0 else None
     torch.cuda.empty_cache()
     accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
+    # BASELINE config 3: 16 simple-example proofs at k = 14 per GPU
+    accum16 = run_accumulator(args, ctx, dist, dev, rank, world, B=16, logn=14) if args.accum_b16 else None
 
     if rank == 0:
         out = {
@@ -240,7 +250,7 @@ def main():
             "kernels_ms": leg["kernels_ms"],
             "roofline": leg["roofline"],
         }
-        for k in ("raw_device_bases_ms_per_step", "raw_device_bases_matches", "host_scalars"):
+        for k in ("variable_base", "host_scalars", "dropin_pm_msm", "small_n"):
             if k in leg:
                 out[k] = leg[k]
         if cpu is not None:
@@ -267,6 +277,12 @@ def main():
             else:
                 accum.pop("_state", None)
             out["accumulator"] = accum
+        if accum16 is not None:
+            if world == 1 and not args.no_cpu:
+                accum16["cpu_baseline"] = accum_cpu_baseline(*accum16.pop("_state"), budget_s=4.0)
+            else:
+                accum16.pop("_state", None)
+            out["accumulator_b16_k14"] = accum16
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -369,7 +385,8 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
                       "curve": name, "n_per_gpu": n, "n_total": total, "scalars": "montgomery, HBM-resident",
                       "bases": "affine, HBM-resident SRS (pm_bases_upload_device: converted once at upload"
                                + (f" and kept as {rb.rows} rows [2^(256 j/{rb.rows})] P, "
-                                  f"{rb.device_bytes / 2**20:.0f} MiB" if rb is not None and rb.rows > 1 else "")
+                                  f"{rb.device_bytes / 2**20:.0f} MiB -- the row-table path; see "
+                                  f"variable_base for non-SRS bases" if rb is not None and rb.rows > 1 else "")
                                + f"; {upload_ms:.1f} ms, untimed)",
                       "parallelism": f"point-slice x{world} + RCCL all-gather of partial points"}}
     if breakdown:
@@ -377,33 +394,18 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
         # events around every launch
         out["kernels_ms"] = kernel_breakdown(ctx, step, MSM_KERNELS)
     if roofline and launches:
-        acc_launches_per_msm = launches / args.steps
-        acc_avg_ms = acc_ms / launches
-        # algorithmic bytes of one accumulate launch: the MSM consumes all n
-        # (scalar, base) pairs -> 96 B x n; one launch covers one
-        # window group, i.e. 1 / (launches per MSM) of it
-        alg_bytes = BYTES_PER_PAIR * n / acc_launches_per_msm
-        achieved = alg_bytes / (acc_avg_ms * 1e-3) / 1e9
-        workload = f"{name}_msm_2^{lg}_per_gpu"
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc_traffic(workload, acc_launches_per_msm),
-                "kernel": "k_accumulate", "avg_launch_ms": round(acc_avg_ms, 4),
-                "launches_per_msm": acc_launches_per_msm, "alg_bytes_per_launch": int(alg_bytes)}
-        valu = load_valu_counters(workload, acc_avg_ms)
-        if valu:
-            roof["valu_int"] = valu
-        out["roofline"] = roof
+        # one k_accumulate launch consumes all n (scalar, base) pairs of the MSM
+        out["roofline"] = roofline_of(n, acc_ms / launches, launches / args.steps, f"{name}_msm_2^{lg}_per_gpu")
     if roofline:
-        # the same MSM from raw device bases (R = 2^256 layout converted on
-        # every call, pm_msm_device), for comparison
-        def raw():
-            return ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n)
-        raw_s, raw_res = timed_steps(raw, max(3, args.steps // 4), 1, dist, dev)
-        out["raw_device_bases_ms_per_step"] = round(raw_s * 1e3 / max(3, args.steps // 4), 4)
-        if world == 1:
-            out["raw_device_bases_matches"] = bool(np.array_equal(np.asarray(raw_res), np.asarray(result)))
+        out["variable_base"] = run_variable_base(args, ctx, dist, dev, world, curve, d_s, d_b, n, result, name, lg)
     if host_leg and n:
         out["host_scalars"] = run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, result)
+        S = d_s.cpu().numpy().view(np.uint64).copy()
+        B = d_b.cpu().numpy().view(np.uint64).copy()
+        out["dropin_pm_msm"] = run_dropin(args, curve, S, B, n, result)
+        del S, B
+        if args.small_n:
+            out["small_n"] = run_small_n(curve)
     if check_port and n:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import msm_ref
@@ -415,6 +417,130 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
         rb.release()
     out.update(_d_s=d_s, _d_b=d_b, _result=result)
     return out
+
+
+def roofline_of(n, avg_ms, launches_per_msm, workload):
+    """HBM roofline of k_accumulate: algorithmic bytes 96 B x n
+    per MSM over the live HIP-event launch time."""
+    alg_bytes = BYTES_PER_PAIR * n / launches_per_msm
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc_traffic(workload, launches_per_msm),
+            "kernel": "k_accumulate", "avg_launch_ms": round(avg_ms, 4),
+            "launches_per_msm": launches_per_msm, "alg_bytes_per_launch": int(alg_bytes)}
+    valu = load_valu_counters(workload, avg_ms)
+    if valu:
+        roof["valu_int"] = valu
+    return roof
+
+
+def run_variable_base(args, ctx, dist, dev, world, curve, d_s, d_b, n, want, name, lg):
+    """The plain variable-base MSM on the same inputs, from raw device bases
+    (Rust R = 2^256 layout, converted on every call; no row table):
+    pm_msm_device.  This is the number for best_multiexp over bases that are
+    not a resident SRS -- e.g. verify_proof's MSMs over proof commitments
+    (examples/simple-example.rs:620,722) -- with its own roofline and kernel
+    breakdown."""
+    import numpy as np
+    import torch
+
+    import halo2_amd as H
+    from sharded import combine_partials
+
+    gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
+
+    def raw():
+        part = ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n)
+        return combine_partials(part, dist, dev, lambda a, b: H.point_add(curve, a, b), world, gathered)
+
+    steps = max(5, args.steps // 2)
+    for _ in range(args.warmup):
+        raw()
+    ctx.set_timing(True, only="accumulate")
+    ctx.reset_stats()
+    el, got = timed_steps(raw, steps, 0, dist, dev)
+    launches, acc_ms = ctx.kernel_stats("accumulate")
+    ctx.set_timing(False)
+    out = {"metric": f"{name} variable-base MSM Mscalar/s at 2^{lg} (raw bases, no table)",
+           "value": round(world * n / (el / steps) / 1e6, 3), "unit": "Mscalar/s",
+           "ms_per_step": round(el * 1e3 / steps, 4),
+           "bases": "raw device bases, R = 2^256 Rust layout, converted per call (pm_msm_device)",
+           "kernels_ms": kernel_breakdown(ctx, raw, MSM_KERNELS)}
+    if launches:
+        out["roofline"] = roofline_of(n, acc_ms / launches, launches / steps, f"{name}_msm_2^{lg}_raw")
+    if world == 1:
+        out["matches_row_table_path"] = bool(np.array_equal(np.asarray(got), np.asarray(want)))
+    return out
+
+
+def run_dropin(args, curve, S, B, n, want):
+    """The literal drop-in call of INTEGRATION.md §2: pm_msm_ctx with host
+    scalars AND host bases on a fresh context.  The first call uploads the
+    bases and builds the resident set (cold); repeated calls with the same
+    base bytes hit the drop-in cache (warm: the scalars' PCIe copy, the
+    content digest of the bases on host threads beside it, and the MSM)."""
+    import numpy as np
+
+    import halo2_amd as H
+
+    ctx = H.Context(0)
+    try:
+        t0 = time.perf_counter()
+        first = ctx.msm(curve, S, B)
+        cold = (time.perf_counter() - t0) * 1e3
+        k = max(5, args.steps // 2)
+        for _ in range(2):
+            ctx.msm(curve, S, B)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            got = ctx.msm(curve, S, B)
+        warm = (time.perf_counter() - t0) * 1e3 / k
+        st = ctx.dropin_stats()
+        return {"call": "pm_msm_ctx(curve, host scalars, host bases, n)", "cold_ms": round(cold, 3),
+                "warm_ms_per_msm": round(warm, 4), "warm_Mscalar_s": round(n / (warm * 1e-3) / 1e6, 3),
+                "cache": st, "matches": bool(np.array_equal(first, want) and np.array_equal(got, want))}
+    finally:
+        ctx.close()
+
+
+def run_small_n(curve, budget_s=4.0):
+    """Latency of the drop-in call at n = 2^0 .. 2^16 (pm_msm_ctx, host
+    inputs, fresh data each size) against the C port of best_multiexp on the
+    host's threads: where the GPU call starts to win (the shim's threshold,
+    halo2_amd.MSM_GPU_MIN_N)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import halo2_amd as H
+    import msm_ref
+
+    ctx = H.Context(0)
+    threads = cpu_threads()
+    rows = []
+    try:
+        S = msm_ref.synth_scalars(curve, SEED_SCALARS, 0, 1 << 16, threads=threads)
+        B = msm_ref.synth_bases(curve, SEED_BASES, 0, 1 << 16, threads=threads)
+        for lg in range(0, 17):
+            n = 1 << lg
+            s, b = np.ascontiguousarray(S[:n]), np.ascontiguousarray(B[:n])
+            g = ctx.msm(curve, s, b)
+            reps = 20 if lg <= 12 else 8
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.msm(curve, s, b)
+            gpu_us = (time.perf_counter() - t0) * 1e6 / reps
+            c = msm_ref.best_multiexp(curve, s, b, threads=threads)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                msm_ref.best_multiexp(curve, s, b, threads=threads)
+            cpu_us = (time.perf_counter() - t0) * 1e6 / reps
+            rows.append({"n": n, "gpu_us": round(gpu_us, 1), "cpu_us": round(cpu_us, 1),
+                         "match": bool(np.array_equal(g, c))})
+    finally:
+        ctx.close()
+    cross = next((r["n"] for r in rows if r["gpu_us"] < r["cpu_us"]), None)
+    return {"call": "pm_msm_ctx vs oracle/msm_ref.c best_multiexp", "cpu_threads": threads, "curve": rows,
+            "gpu_faster_from_n": cross, "shim_threshold": H.MSM_GPU_MIN_N}
 
 
 def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
@@ -621,7 +747,7 @@ def ntt_cpu_baseline(curve, k, src, w, first, budget_s):
             "matches_gpu": match}
 
 
-def run_accumulator(args, ctx, dist, dev, rank, world):
+def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
     """Batch multiopen accumulator: B proofs per rank, timed like the MSM leg."""
     import numpy as np
     import torch
@@ -629,8 +755,8 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
     import halo2_amd as H
     import workloads as Wk
 
-    curve, B = H.BN254, args.accum_batch
-    shape = Wk.simple_example_shape(ctx, curve, args.accum_logn)
+    curve, B, logn = H.BN254, B or args.accum_batch, logn or args.accum_logn
+    shape = Wk.simple_example_shape(ctx, curve, logn)
     batch = Wk.SyntheticBatch(ctx, shape, B, i0=rank * B)
     from sharded import gather_batches
 
@@ -660,7 +786,7 @@ def run_accumulator(args, ctx, dist, dev, rank, world):
     ms = elapsed * 1e3 / args.steps
     out = {"metric": "aggregated proofs verified/s", "value": round(world * B / (ms * 1e-3), 1), "unit": "proofs/s",
            "ms_per_batch": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-           "config": {"workload": f"multiopen_accumulator_simple_example_k{args.accum_logn}", "curve": "bn254",
+           "config": {"workload": f"multiopen_accumulator_simple_example_k{logn}", "curve": "bn254",
                       "proofs_per_gpu": B, "proofs_total": world * B,
                       "challenges": "Blake2b transcript replayed on the device (pm_accum_batch_transcript_device)",
                       "per_proof_work": "transcript replay + scalar block + multiopen accumulator quad (w, zw, f, e) "

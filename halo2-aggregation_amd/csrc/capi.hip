@@ -147,7 +147,7 @@ static int host_threads() {
 }
 
 pm::HostPool& pm_ctx::host_pool() {
-  if (!pool) pool = new pm::HostPool(host_threads());
+  if (!pool) pool = new pm::HostPool(pool_threads > 0 ? pool_threads : host_threads());
   return *pool;
 }
 
@@ -362,6 +362,8 @@ int pm_ctx_create(int device, pm_ctx** out) {
   c->stream = c->own_stream;
   HIP_TRY(hipStreamCreateWithFlags(&c->red_stream, hipStreamNonBlocking));
   if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
+  if (const char* e = std::getenv("PM_H2D_CHUNKS")) c->h2d_chunks = std::max(1, std::min(64, std::atoi(e)));
+  if (const char* e = std::getenv("PM_POOL_THREADS")) c->pool_threads = std::max(1, std::min(64, std::atoi(e)));
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));

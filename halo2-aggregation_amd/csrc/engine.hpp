@@ -234,7 +234,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if (h_scalars) {
     // chunks of whole histogram blocks, ~8 MB each (2^20: 4 chunks of 64 blocks)
     const size_t pts_blk = (size_t)g.ppt * kSortThreads;
-    const int nch = (int)std::max<size_t>(1, std::min<size_t>(kH2DChunks, n * 32 / kH2DChunkMin));
+    const int nch = (int)std::max<size_t>(1, std::min<size_t>(ctx->h2d_chunks, n * 32 / kH2DChunkMin));
     const int bpc = (int)((((n + pts_blk - 1) / pts_blk) + nch - 1) / nch);
     if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     if ((rc = ctx->ensure_copy_events(nch))) return rc;

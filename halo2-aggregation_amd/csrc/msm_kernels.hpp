@@ -540,8 +540,11 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* __restrict__ off
 // Chains up to kSerialChain later slices are folded by the bucket's own lane
 // in k_bucket_seg_q; longer ones (giant buckets: adversarial or highly
 // repetitive scalars, e.g. many scalars equal to 1) by the whole wave, one
-// chain at a time: a strided sum over 64 lanes and a butterfly.
-constexpr uint32_t kSerialChain = 8;
+// chain at a time (a strided sum over 64 lanes and a butterfly), when that
+// beats the lane's own walk.  (A cut at 8 slices sent the fixed-base MSM's
+// merged buckets, ~8-9 slices each, wave-wide: 2^20 k_bucket_seg_q 0.05 ->
+// 1.29 ms, gpurun_out/b of round 3.)
+constexpr uint32_t kSerialChain = 32;
 
 // Base gather by LDS-DMA one entry ahead: global_load_lds writes the next
 // entry's 64-B base straight into LDS (no VGPRs held across the addition), so
@@ -782,6 +785,22 @@ __global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restr
   // giant buckets: the wave folds each long chain in turn (wave-uniform loop)
   uint64_t lm = __ballot(tl - tf > kSerialChain);
   const uint32_t ln = __lane_id();
+  if (lm) {
+    // wave-wide only while it beats the lanes' own walks: ~ceil(len / 64) + 6
+    // additions per chain, one chain after another, against the longest
+    // chain's len serial additions (64 adjacent 100-slice buckets: serial;
+    // one 10^4-slice bucket: wave-wide)
+    uint32_t mx = tl - tf;
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m, 64));
+    uint32_t coop = 0;
+    for (uint64_t r = lm; r; r &= r - 1) coop += (mx + 63) / 64 + 6;
+    if (mx <= kSerialChain + coop) {
+      if (tl - tf > kSerialChain)
+        for (uint32_t t = tf + 1; t <= tl; t++) B = xyzz29_add<F>(B, load_xyzz29<F>(&head[t]));
+      lm = 0;
+    }
+  }
   while (lm) {
     const int L = __ffsll((unsigned long long)lm) - 1;
     lm &= lm - 1;

@@ -173,7 +173,9 @@ struct pm_ctx {
   hipEvent_t batch_ev[4] = {};       // batch pipelining: copied[2], consumed[2]
   std::vector<hipEvent_t> grp_ev;    // MSM: one per pinned term slot (terms copied)
   int window_c = 0;
-  int min_chunk = 0;  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
+  int min_chunk = 0;
+  int h2d_chunks = pm::kH2DChunks;  // host-scalar copy chunks (diagnostics: PM_H2D_CHUNKS env)
+  int pool_threads = 0;             // host pool size, 0 = auto (diagnostics: PM_POOL_THREADS env)  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
   int sort_ppt = 0;   // sort points per thread, 0 = auto (diagnostics: PM_SORT_PPT env, 1/2/4/8)
   int sort_fb = 0;    // fine bits of the two-level sort, 0 = auto (diagnostics: PM_SORT_FB env)
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)

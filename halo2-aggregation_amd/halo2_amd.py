@@ -27,6 +27,10 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "pasta_msm.h")
 PALLAS, VESTA, BN254 = 0, 1, 2
 SCALARS_CANONICAL = 1
 LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
+# PM_MSM_GPU_MIN_N: below this many terms the Rust shim keeps halo2's CPU
+# multiexp (a pm_msm call's fixed latency loses there).
+# best_multiexp below still runs every n on the GPU: there is no CPU path here.
+MSM_GPU_MIN_N = 1024
 ACCUM_CURVES = (PALLAS, VESTA, BN254)
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -276,6 +280,8 @@ def _load():
                                               _u64p, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
+        if not hasattr(L, name) and os.environ.get("PM_LIB"):
+            continue  # an older A/B build (PM_LIB) without this entry point
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res

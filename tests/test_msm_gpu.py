@@ -294,8 +294,9 @@ def test_resident_row_table(gpu_ctx, curve):
 def test_adjacent_giant_buckets(gpu_ctx, curve, min_chunk):
     """Scalars 1 .. 64 (canonical): window 0's buckets 1 .. 64 hold n/64
     points each and lie in ONE wave of k_bucket_seg_q, so almost every lane
-    of that wave owns a chain longer than kSerialChain slices and the wave
-    folds them one after another (wave-wide strided sums + butterfly)."""
+    of that wave owns a chain longer than kSerialChain slices: the wave's
+    rule picks the lanes' own walks over 64 wave-wide folds.  (A single giant
+    bucket, test_all_equal_scalars_large, takes the wave-wide fold.)"""
     import torch
 
     n = (1 << 17) + 99

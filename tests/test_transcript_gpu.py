@@ -131,3 +131,30 @@ def test_single_proof_k9_fused(gpu_ctx, cid):
     assert np.array_equal(ch, chs) and not st.any()
     q, hh = A.pack_result(C, A.accumulate_msm(C, sh, proofs[0]))
     assert np.array_equal(quads[0], q) and np.array_equal(h[0], hh)
+
+
+@pytest.mark.parametrize("cid", [0, 2])
+def test_config3_sixteen_proofs_k14(gpu_ctx, cid):
+    """BASELINE config 3 at its exact size: 16 simple-example proofs at k = 14
+    (examples/simple-example.rs:99-159, 561) through the fused transcript
+    replay + accumulator, every proof's challenges, quad and h_eval bit for
+    bit against the C port (oracle/accum_ref.c), two of them also against the
+    literal Python restatement."""
+    import accum_ref as R
+
+    C, sh, proofs = U.make_case(cid, "simple", 14, 16, 0xC3 + cid)
+    ps = U.to_product_shape(cid, sh)
+    vkr = T.vk_repr(C.r, b"simple-example")
+    vk = np.array(A.to_limbs_mont(C.r, vkr), dtype=np.uint64)
+    pts, scs, _ = A.pack_proofs(C, sh, proofs)
+    quads, h, ch, st = gpu_ctx.accum_batch_transcript(ps, pts, scs, vk)
+    assert not st.any()
+    rch, rq, rh, rst = R.accum_batch(cid, ps.c, pts, scs, vk_repr=vk, threads=4)
+    assert not rst.any()
+    assert np.array_equal(ch, rch.reshape(ch.shape))
+    assert np.array_equal(quads, rq.reshape(quads.shape))
+    assert np.array_equal(h, rh.reshape(h.shape))
+    T.with_replayed_challenges(C, sh, proofs, vkr)
+    for b in (0, 15):
+        q, hh = A.pack_result(C, A.accumulate_msm(C, sh, proofs[b]))
+        assert np.array_equal(quads[b], q) and np.array_equal(h[b], hh), b
