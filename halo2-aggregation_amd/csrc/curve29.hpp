@@ -75,8 +75,7 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_dbl_impl(const F29<F>& X, const F29<
   Xyzz29<F> r;
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(M), f29_add<F>(S, S), K::K8x3)));  // < 3p
   const F29<F> D = f29_norm<F>(f29_sub<F>(S, r.X, K::K6));     // < 8p
-  const F29<F> nW = f29_norm<F>(f29_sub<F>(f29_zero<F>(), W, K::K2));  // -W, < 2p
-  r.Y = f29_mul2_c<F>(M, D, nW, Y);                              // M D - W Y: 48p^2 + 8p^2, < 2p
+  r.Y = f29_mul2n_c<F>(M, D, W, Y);                              // M D - W Y (48p^2, W Y < 8p^2), < 3p
   r.ZZ = AFF ? V : f29_mul_c<F>(V, ZZ);
   r.ZZZ = AFF ? W : f29_mul_c<F>(W, ZZZ);
   return r;
@@ -151,8 +150,7 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_madd(const Xyzz29<F>& acc, const F29
   Xyzz29<F> r;
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
   const F29<F> D = f29_norm<F>(f29_sub<F>(Q, r.X, K::K6));     // < 8p
-  const F29<F> nY = f29_norm<F>(f29_sub<F>(f29_zero<F>(), acc.Y, K::K6));  // -Y1, < 6p
-  r.Y = f29_mul2_c<F>(R, D, nY, PPP);                            // R D - Y1 PPP: 64p^2 + 12p^2, < 2p
+  r.Y = f29_mul2n_c<F>(R, D, acc.Y, PPP);                        // R D - Y1 PPP (64p^2, 6p^2), < 3p
   r.ZZ = f29_mul_c<F>(acc.ZZ, PP);
   r.ZZZ = f29_mul_c<F>(acc.ZZZ, PPP);
   return r;
@@ -165,13 +163,17 @@ __device__ __forceinline__ F29<F> f29_neg_canon(const F29<F>& y);
 // k_accumulate's step: acc + (x2, (-1)^s y2) for a canonical base, with the
 // digit's sign folded into R instead of negating y2:
 //   R = 8p + (-1)^s S2 - Y1   (limbs: K8x3 >= 3 * 2^29 - 3 covers the
-//   -S2 - Y1 case, value in (3p, 10p)), the rest as madd-2008-s.
+//   -S2 - Y1 case, value in (3p, 10p) for Y1 < 3p), the rest as madd-2008-s,
+//   and Y3 = R D - Y1 PPP as one difference of products (f29_mul2n: no
+//   negated -Y1, ~34 VALU instructions less per addition than round 2's
+//   R D + (6p - Y1) PPP).
 // No branches: the caller overwrites the result of a lane whose acc is empty,
 // and detects the exceptional P = 0 (acc = +-point) from the output: then
 // ZZ3 = ZZ1 P^2 = 0 and X3 = R^2, so X3 = 0 iff acc = point (double it),
 // else the sum is O (xyzz29_madd_fix).
-// Bounds: R^2 < 100 p^2 < 2^261 p; Y3 = R D + (-Y1) PPP < 80 p^2 + 12 p^2,
-// both fine for p < 2^254.3 (Pasta, BN254): outputs X < 3p, Y, ZZ, ZZZ < 2p.
+// Bounds: R^2 < 100 p^2 < 2^261 p; Y3 = R D - Y1 PPP with R D < 80 p^2 and
+// Y1 PPP < 6 p^2, fine for p < 2^254.3 (Pasta, BN254): outputs X, Y < 3p,
+// ZZ, ZZZ < 2p.
 template <class F>
 __device__ __forceinline__ Xyzz29<F> xyzz29_madd_signed(const Xyzz29<F>& acc, const F29<F>& x2, const F29<F>& y2,
                                                         uint32_t negm) {
@@ -189,8 +191,7 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_madd_signed(const Xyzz29<F>& acc, co
   Xyzz29<F> r;
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
   const F29<F> D = f29_norm<F>(f29_sub<F>(Q, r.X, K::K6));     // < 8p
-  const F29<F> nY = f29_norm<F>(f29_sub<F>(f29_zero<F>(), acc.Y, K::K6));  // -Y1, < 6p
-  r.Y = f29_mul2_c<F>(R, D, nY, PPP);
+  r.Y = f29_mul2n_c<F>(R, D, acc.Y, PPP);                        // R D - Y1 PPP, < 3p
   r.ZZ = f29_mul_c<F>(acc.ZZ, PP);
   r.ZZZ = f29_mul_c<F>(acc.ZZZ, PPP);
   return r;
@@ -231,8 +232,7 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_add(const Xyzz29<F>& p, const Xyzz29
   Xyzz29<F> r;
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3)));
   const F29<F> D = f29_norm<F>(f29_sub<F>(Q, r.X, K::K6));     // < 8p
-  const F29<F> nS1 = f29_norm<F>(f29_sub<F>(f29_zero<F>(), S1, K::K2));  // -S1, < 2p
-  r.Y = f29_mul2_c<F>(R, D, nS1, PPP);                           // 64p^2 + 4p^2, < 2p
+  r.Y = f29_mul2n_c<F>(R, D, S1, PPP);                           // R D - S1 PPP (64p^2, 4p^2), < 3p
   r.ZZ = f29_mul_c<F>(f29_mul_c<F>(p.ZZ, q.ZZ), PP);
   r.ZZZ = f29_mul_c<F>(f29_mul_c<F>(p.ZZZ, q.ZZZ), PPP);
   return r;

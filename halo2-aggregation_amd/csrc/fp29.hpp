@@ -316,6 +316,18 @@ template <class P>
 __device__ __forceinline__ F29<P> f29_mul2_c(const F29<P>& a, const F29<P>& b, const F29<P>& u, const F29<P>& v) {
   return f29_mul2_a<P>(a, b, u, v);
 }
+// Difference of two products with one Montgomery reduction: (a b - u v)
+// 2^-261 (+ a multiple of p).  The u v terms enter the signed columns as
+// multiply-adds by the negated limbs of v, so no negation of u or v as a field
+// element (K - x + normalise) is needed.  All four operands Norm, a b < 80 p^2,
+// u < 3p, v < 2p -> Norm, < 3p (tests/test_fp29_asm.py runs it in the
+// interpreter with signed-overflow checks).
+template <class P>
+__device__ F29<P> f29_mul2n_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, const F29<P>& v);
+template <class P>
+__device__ __forceinline__ F29<P> f29_mul2n_c(const F29<P>& a, const F29<P>& b, const F29<P>& u, const F29<P>& v) {
+  return f29_mul2n_a<P>(a, b, u, v);
+}
 template <class P>
 __device__ __forceinline__ F29<P> f29_sqr_c(const F29<P>& a) {
   return f29_sqr_a<P>(a);

@@ -39,7 +39,7 @@ constexpr uint32_t kBasesR261 = 1u << 30;
 // host scalars (pm_msm_resident, pm_msm_fixed, pm_msm): the copy is split into
 // at most kH2DChunks chunks of >= kH2DChunkMin bytes on the copy stream, and
 // k_sort_hist runs chunk by chunk behind it
-constexpr int kH2DChunks = 4;
+constexpr int kH2DChunks = 1;  // 4 chunks measured ~0.1 ms slower per 2^20 MSM than one copy (round 3, tools/h2d_timing.py)
 constexpr size_t kH2DChunkMin = size_t(4) << 20;
 // drop-in base cache of pm_msm / pm_msm_ctx (capi.hip): base sets of at least
 // kDropinMinN points are kept resident, keyed by a content digest; at most

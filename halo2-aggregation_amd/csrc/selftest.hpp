@@ -72,6 +72,9 @@ __global__ void k_selftest_field(uint64_t seed, uint32_t n, uint32_t* __restrict
   const F29<F> T = f29_reduce3<F>(f29_norm<F>(f29_add<F>(L, L)));
   nb += !f29_eq_r256<F>(T, fe_add<F>(a, a));
   nb += !f29_eq_r256<F>(f29_canon<F>(T), fe_add<F>(a, a));
+  // difference of products: a b - (2a) b = -a b, u = 2A reduced below 3p
+  nb += !f29_eq_r256<F>(f29_mul2n_c<F>(A, B, T, B), fe_neg<F>(ab));
+  nb += !f29_eq_r256<F>(f29_mul2n_c<F>(Ln, B, A, B), fe_sub<F>(fe_mul<F>(a, b), ab));
   // zero mod p: A - A + 6p = 6p
   nb += !f29_is_zero_mod<F>(f29_norm<F>(f29_sub<F>(A, A, K::K6)));
   nb += f29_is_zero_mod<F>(A) != fe_is_zero<F>(a);

@@ -25,14 +25,14 @@ FIELDS = {"PallasFp": P.PALLAS_P, "VestaFp": P.VESTA_P, "Bn254Fq": P.BN254_P, "B
 def _functions():
     src = open(HDR).read()
     out = {}
-    for m in re.finditer(r"F29<(\w+)> (f29_(?:mul|sqr|mul2)_a)<\w+>\((.*?)\) \{\n(.*?)\n\}\n", src, re.S):
+    for m in re.finditer(r"F29<(\w+)> (f29_(?:mul|sqr|mul2|mul2n)_a)<\w+>\((.*?)\) \{\n(.*?)\n\}\n", src, re.S):
         out[(m.group(2), m.group(1))] = m.group(4)
     return out
 
 
 def _run(body, a, b=None, u=None, v=None):
     env = {"a.l": list(a), "b.l": list(b) if b is not None else None, "m": [0] * 9, "r.l": [0] * 9, "d": [0] * 8,
-           "u.l": list(u) if u is not None else None, "v.l": list(v) if v is not None else None}
+           "u.l": list(u) if u is not None else None, "v.l": list(v) if v is not None else None, "nv": [0] * 9}
     acc = 0
     signed = False
 
@@ -75,6 +75,8 @@ def _run(body, a, b=None, u=None, v=None):
         c = cline
         if c.startswith("for (int i = 0; i < 8; i++) d[i] = a.l[i] << 1"):
             env["d"] = [(x << 1) & 0xFFFFFFFF for x in env["a.l"][:8]]
+        elif c.startswith("for (int i = 0; i < 9; i++) nv[i] = 0u - v.l[i]"):
+            env["nv"] = [(-x) & 0xFFFFFFFF for x in env["v.l"]]
         elif re.fullmatch(r"m\[\d\] = \(uint32_t\)acc & kM29", c):
             env["m"][int(c[2])] = acc & M29  # two's complement low bits
         elif re.fullmatch(r"m\[\d\] = \(0u - \(uint32_t\)acc\) & kM29", c):
@@ -91,7 +93,7 @@ def _run(body, a, b=None, u=None, v=None):
             top = (acc >> 29) + int(re.search(r"\+ (\d+)u", c).group(1))
             assert 0 <= top < 2 ** 32
             env["r.l"][8] = top
-        elif not re.fullmatch(r"F29<\w+> r|uint32_t (m|d)\[\d\]|uint64_t acc = 0, c|\(void\)c|return r", c):
+        elif not re.fullmatch(r"F29<\w+> r|uint32_t (m|d|nv)\[\d\]|uint64_t acc = 0, c|\(void\)c|return r", c):
             raise AssertionError("unhandled line: " + c)
     return env["r.l"]
 
@@ -155,3 +157,25 @@ def test_column_asm_sum_of_products(field):
         assert all(l <= M29 for l in r[:8])
         assert _value(r) % p == (a * b + u * v) * rinv % p
         assert _value(r) < 2 * p + p // 4  # < 2p for p < 2^254.7 (Pasta, BN254)
+
+
+@pytest.mark.parametrize("field", sorted(FIELDS))
+def test_column_asm_difference_of_products(field):
+    """f29_mul2n_a: (a b - u v) 2^-261 with one reduction and signed columns,
+    for the operand bounds of its callers (R, D < 10p / 8p; u, v < 4p:
+    Y3 = R D - Y1 PPP of the bucket addition, M D - W Y of the doubling,
+    R D - S1 PPP of the full addition), including a b = 0 with u v maximal
+    (the most negative column sums) -> Norm, < 3p."""
+    p = FIELDS[field]
+    mul2n = _functions()[("f29_mul2n_a", field)]
+    rinv = pow(1 << 261, -1, p)
+    rng = random.Random(0x2A2A + len(field))
+    for t in range(80):
+        a = [0, 1, 10 * p - 1][t % 3] if t < 9 else rng.randrange(10 * p)
+        b = [0, 8 * p - 1, 8 * p - 1][(t // 3) % 3] if t < 9 else rng.randrange(8 * p)
+        u = rng.randrange(4 * p) if t % 4 else 4 * p - 1
+        v = rng.randrange(4 * p) if t % 5 else 4 * p - 1
+        r = _run(mul2n, _limbs(a), _limbs(b), _limbs(u), _limbs(v))
+        assert all(0 <= l <= M29 for l in r[:8])
+        assert _value(r) % p == (a * b - u * v) * rinv % p
+        assert 0 <= _value(r) < 3 * p

@@ -106,12 +106,21 @@ def statement(k, sq, P):
     return body, ins
 
 
-def statement2(k, P):
+def statement2(k, P, neg=False):
     """f29_mul2_a, column k: statement A = carry-in + the a b terms, statement B
     = the u v terms + the reduction terms (one statement would exceed the
-    inline-asm operand limit)."""
+    inline-asm operand limit).
+
+    neg (f29_mul2n_a): the u v terms are subtracted -- multiply-adds of u_i
+    by the negated limbs nv_j (signed: v_mad_i64_i32), so the columns are
+    signed (arithmetic carries) in both reduction forms, and the result gets
+    p R more than the plain form (2 p R subtractive, p R additive) to stay
+    positive: a b - u v > -R p / 16 for the operand bounds the curve
+    routines use (u v < 6 p^2 < R p / 16)."""
     insA, bodyA, insB, bodyB = [], [], [], []
     sub = P[0] == 1
+    signed = sub or neg
+    kp = (2 if sub else 1) if neg else (1 if sub else 0)  # multiple of p R added
 
     def mad(body, x, y):
         body.append("v_mad_u64_u32 %%0, %%1, %s, %s, %%0" % (x, y))
@@ -119,20 +128,21 @@ def statement2(k, P):
     if k >= 10:
         opnd(insA, "v", "r.l[%d]" % (k - 10))
     if k > 0:
-        if sub:
-            bodyA.append("v_ashrrev_i64 %0, 29, %0")
-            if k >= 9 and P[k - 9]:
-                mad(bodyA, "1", const(insA, P[k - 9]))
-        else:
-            if k - 1 < 9:
-                mad(bodyA, opnd(insA, "v", "m[%d]" % (k - 1)), const(insA, P[0]))
-            bodyA.append("v_lshrrev_b64 %0, 29, %0")
+        if not sub and k - 1 < 9:
+            mad(bodyA, opnd(insA, "v", "m[%d]" % (k - 1)), const(insA, P[0]))
+        bodyA.append("v_ashrrev_i64 %0, 29, %0" if signed else "v_lshrrev_b64 %0, 29, %0")
+        if kp and k >= 9 and P[k - 9]:
+            mad(bodyA, "1", const(insA, kp * P[k - 9]))
     if k < 17:
         for i in range(9):
             j = k - i
             if 0 <= j < 9:
                 mad(bodyA, opnd(insA, "v", "a.l[%d]" % i), opnd(insA, "v", "b.l[%d]" % j))
-                mad(bodyB, opnd(insB, "v", "u.l[%d]" % i), opnd(insB, "v", "v.l[%d]" % j))
+                if neg:
+                    bodyB.append("v_mad_i64_i32 %%0, %%1, %s, %s, %%0" % (opnd(insB, "v", "u.l[%d]" % i),
+                                                                          opnd(insB, "v", "nv[%d]" % j)))
+                else:
+                    mad(bodyB, opnd(insB, "v", "u.l[%d]" % i), opnd(insB, "v", "v.l[%d]" % j))
         for i in range(9):
             j = k - i
             if i < k and 1 <= j < 9 and P[j] != 0:
@@ -144,17 +154,23 @@ def statement2(k, P):
     return [(bodyA, insA), (bodyB, insB)]
 
 
-def gen_fn2(field):
-    """(a b + u v) 2^-261 mod p with ONE Montgomery reduction (sum of products)."""
+def gen_fn2(field, neg=False):
+    """(a b + u v) 2^-261 mod p with ONE Montgomery reduction (sum of products);
+    neg: (a b - u v) 2^-261 (f29_mul2n_a)."""
     p = FIELDS[field]
     P = limbs(p)
     inv = (-pow(p, -1, 1 << 29)) % (1 << 29)
+    sub = P[0] == 1
+    kp = (2 if sub else 1) if neg else (1 if sub else 0)
+    name = "f29_mul2n_a" if neg else "f29_mul2_a"
     L = []
-    L.append("template <>\n__device__ __forceinline__ F29<%s> f29_mul2_a<%s>(const F29<%s>& a, const F29<%s>& b, "
-             "const F29<%s>& u, const F29<%s>& v) {" % ((field,) * 6))
+    L.append("template <>\n__device__ __forceinline__ F29<%s> %s<%s>(const F29<%s>& a, const F29<%s>& b, "
+             "const F29<%s>& u, const F29<%s>& v) {" % (field, name, field, field, field, field, field))
     L.append("  F29<%s> r;\n  uint32_t m[9];\n  uint64_t acc = 0, c;" % field)
+    if neg:
+        L.append("  uint32_t nv[9];\n#pragma unroll\n  for (int i = 0; i < 9; i++) nv[i] = 0u - v.l[i];")
     for k in range(17):
-        for body, ins in statement2(k, P):
+        for body, ins in statement2(k, P, neg):
             if not body:
                 continue
             text = "\\n\\t".join(body)
@@ -169,8 +185,8 @@ def gen_fn2(field):
                 L.append("  m[%d] = ((uint32_t)acc * %du) & kM29;" % (k, inv))
         else:
             L.append("  r.l[%d] = (uint32_t)acc & kM29;" % (k - 9))
-    if P[0] == 1:
-        L.append("  r.l[8] = (uint32_t)((int64_t)acc >> 29) + %du;\n  (void)c;\n  return r;\n}\n" % P[8])
+    if kp:
+        L.append("  r.l[8] = (uint32_t)((int64_t)acc >> 29) + %du;\n  (void)c;\n  return r;\n}\n" % (kp * P[8]))
     else:
         L.append("  r.l[8] = (uint32_t)(acc >> 29);\n  (void)c;\n  return r;\n}\n")
     return "\n".join(L)
@@ -214,11 +230,14 @@ def main():
            "template <class P>\n__device__ F29<P> f29_mul_a(const F29<P>& a, const F29<P>& b);",
            "template <class P>\n__device__ F29<P> f29_sqr_a(const F29<P>& a);",
            "template <class P>\n__device__ F29<P> f29_mul2_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, "
+           "const F29<P>& v);",
+           "template <class P>\n__device__ F29<P> f29_mul2n_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, "
            "const F29<P>& v);", ""]
     for f in FIELDS:
         out.append(gen_fn("f29_mul_a", f, False))
         out.append(gen_fn("f29_sqr_a", f, True))
         out.append(gen_fn2(f))
+        out.append(gen_fn2(f, neg=True))
     out.append("}  // namespace pm")
     print("\n".join(out))
 
