@@ -145,11 +145,14 @@ def load_pmc_traffic(workload, launches_per_msm):
 
 
 def load_ntt_traffic(workload):
+    """HBM bytes per NTT (all passes) from the committed PMC passes
+    (profiles/pmc_ntt.json: one entry per workload)."""
     p = os.path.join(ROOT, "profiles", "pmc_ntt.json")
     if os.path.exists(p):
         d = json.load(open(p))
-        if d.get("workload") == workload:
+        if d.get("workload") == workload:  # single-workload layout
             return d.get("hbm_bytes_per_ntt")
+        return d.get("workloads", {}).get(workload, {}).get("hbm_bytes_per_ntt")
     return None
 
 

@@ -6,7 +6,8 @@ TAG=${1:-ntt}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="python3 bench.py --no-cpu --fixed 0 --accum-batch 0 --steps 5 --warmup 1"
+# NTT_ARGS: which legs run (default the 2^20 leg); e.g. "--ntt-logn 0 --ntt-large-logn 25" for 2^25
+BENCH="python3 bench.py --no-cpu --fixed 0 --accum-batch 0 --accum-b16 0 --logn22 0 --strong-logn 0 --small-n 0 --steps 5 --warmup 1 ${NTT_ARGS:---ntt-large-logn 0}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run -- $BENCH > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
 for C in FETCH_SIZE WRITE_SIZE; do
@@ -23,7 +24,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for r in rows:
         if r["Counter_Name"] != c:
             continue
-        k = "k_ntt_cols" if "k_ntt_cols" in r["Kernel_Name"] else "k_ntt_rows" if "k_ntt_rows" in r["Kernel_Name"] else None
+        k = next((x for x in ("k_ntt_cols", "k_ntt_mid", "k_ntt_rows") if x in r["Kernel_Name"]), None)
         if k:
             by.setdefault(k, []).append(float(r["Counter_Value"]))
     res[c] = {k: statistics.median(v) for k, v in by.items()}

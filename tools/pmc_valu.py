@@ -13,7 +13,9 @@ chains), v_and_b32 61.164 T/s.  The INT64 class (multiply-adds, 64-bit shifts
 and adds) issues at the former, every other VALU instruction at the latter, so
 issue_frac = (INT64 * 64 / 33.944T + (VALU - INT64) * 64 / 61.164T) / duration.
 
-Usage: python tools/pmc_valu.py profiles/r02/pmc
+Usage: python tools/pmc_valu.py profiles/r03/pmc [per_gpu|raw]
+  (per_gpu: the headline's resident row-table MSM, RESIDENT=1; raw: the
+  plain pipeline from raw device bases, bench.py's variable_base leg)
 """
 import collections
 import csv
@@ -51,13 +53,18 @@ def median(xs):
 
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r02", "pmc")
+    suffix = sys.argv[2] if len(sys.argv) > 2 else "per_gpu"  # workload key: pallas_msm_2^lg_<suffix>
     rel = os.path.relpath(src, ROOT)
-    valu, traffic = {}, {}
-    for lg in (20, 22):
+    pv = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    pa = os.path.join(ROOT, "profiles", "pmc_accumulate.json")
+    # merge into the existing files: other workloads' entries stay
+    valu = json.load(open(pv)) if os.path.exists(pv) else {}
+    traffic = json.load(open(pa)).get("workloads", {}) if os.path.exists(pa) else {}
+    for lg in (19, 20, 22):
         f1 = os.path.join(src, f"n{lg}_p1.csv")
         if not os.path.exists(f1):
             continue
-        wl = f"pallas_msm_2^{lg}_per_gpu"
+        wl = f"pallas_msm_2^{lg}_{suffix}"
         agg, dur = per_dispatch(f1)
         # the first dispatch of the driver is a warm-up with cold caches; take medians
         c = {k: median([agg[d][k] for d in agg]) for k in next(iter(agg.values()))}
@@ -76,6 +83,8 @@ def main():
                     "issue_frac": round(need / s, 4),
                     "int64_peak_Tops": INT64_PEAK_T, "simple_peak_Tops": SIMPLE_PEAK_T,
                     "source": f"{rel}/n{lg}_p1.csv (rocprofv3 --pmc, SQ pass; tools/gpu_pmc_r02.sh)"}
+        if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
+            valu[wl]["wait_inst_frac"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
         fe, _ = per_dispatch(os.path.join(src, f"n{lg}_p2.csv"))
         wr, _ = per_dispatch(os.path.join(src, f"n{lg}_p3.csv"))
         fkb = median([fe[d]["FETCH_SIZE"] for d in fe])
@@ -87,8 +96,8 @@ def main():
                        "note": "L2 memory-side requests (Infinity-Cache hits included); no x2 streaming "
                                "correction: the dominant reads are random 64-B base gathers, one 128-B line "
                                "each. Algorithmic bytes are 96 B x n (SURVEY 8d)."}
-    json.dump(valu, open(os.path.join(ROOT, "profiles", "pmc_valu.json"), "w"), indent=1)
-    json.dump({"workloads": traffic}, open(os.path.join(ROOT, "profiles", "pmc_accumulate.json"), "w"), indent=1)
+    json.dump(valu, open(pv, "w"), indent=1)
+    json.dump({"workloads": traffic}, open(pa, "w"), indent=1)
     print(json.dumps(valu, indent=1))
     print(json.dumps(traffic, indent=1))
 
