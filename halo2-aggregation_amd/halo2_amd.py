@@ -30,7 +30,7 @@ LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
 # PM_MSM_GPU_MIN_N: below this many terms the Rust shim keeps halo2's CPU
 # multiexp (a pm_msm call's fixed latency loses there).
 # best_multiexp below still runs every n on the GPU: there is no CPU path here.
-MSM_GPU_MIN_N = 1024
+MSM_GPU_MIN_N = 4
 ACCUM_CURVES = (PALLAS, VESTA, BN254)
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)

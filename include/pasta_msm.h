@@ -110,11 +110,13 @@ int pm_ctx_reset_stats(pm_ctx* ctx);
  * it into C::Curve with `to_curve()`.  n == 0 yields the identity. */
 int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
            uint64_t out[8]);
-/* Below this many terms a pm_msm call (fixed launch + PCIe latency) is slower
- * than halo2's CPU multiexp on the host's cores; the Rust shim keeps the CPU
- * path there (measured: bench.py small_n).
- * pm_msm itself computes any n. */
-#define PM_MSM_GPU_MIN_N 1024
+/* Below this many terms a pm_msm call (~230-300 us of launches, copies and the
+ * host Horner whatever n is below ~2^10) is slower than halo2's CPU multiexp
+ * (serial for so few terms); the Rust shim keeps the CPU path there
+ * (measured on MI355X + EPYC, 16 threads: bench.py small_n,
+ * 1-2 terms CPU, from 4 terms the GPU call).  pm_msm itself
+ * computes any n. */
+#define PM_MSM_GPU_MIN_N 4
 /* Same, on an explicit context (host pointers).
  * Drop-in base cache: from 4096 points on, pm_msm / pm_msm_ctx keep each base
  * set they see resident on the device (converted, with the row table from

@@ -36,6 +36,16 @@ def test_abi_version_matches_header():
     assert m and H.abi_version() == int(m.group(1))
 
 
+def test_crossover_threshold_is_one_number():
+    """The GPU/CPU crossover of the drop-in: the header's PM_MSM_GPU_MIN_N,
+    the Rust shim's constant in INTEGRATION.md and halo2_amd.MSM_GPU_MIN_N are
+    the same measured number (bench.py small_n)."""
+    h = re.search(r"#define PM_MSM_GPU_MIN_N (\d+)", open(H.HEADER_PATH).read())
+    doc = re.search(r"pub const PM_MSM_GPU_MIN_N: usize = (\d+);", open(os.path.join(ROOT, "INTEGRATION.md")).read())
+    assert h and doc
+    assert int(h.group(1)) == int(doc.group(1)) == H.MSM_GPU_MIN_N
+
+
 def test_last_error_is_thread_local_string():
     assert isinstance(H.lib().pm_last_error(), bytes)
 
