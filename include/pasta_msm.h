@@ -111,7 +111,7 @@ int pm_ctx_reset_stats(pm_ctx* ctx);
 int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
            uint64_t out[8]);
 /* Below this many terms a pm_msm call (~230-300 us of launches, copies and the
- * host Horner whatever n is below ~2^10) is slower than halo2's CPU multiexp
+ * host Horner whatever n is up to 2^8) is slower than halo2's CPU multiexp
  * (serial for so few terms); the Rust shim keeps the CPU path there
  * (measured on MI355X + EPYC, 16 threads: bench.py small_n,
  * 1-2 terms CPU, from 4 terms the GPU call).  pm_msm itself
