@@ -367,6 +367,8 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("PM_FINE_CACHE_KB")) c->fine_cache_kb = std::max(0, std::min(144, std::atoi(e)));
+  if (const char* e = std::getenv("PM_FINE_CHUNK_KB")) c->fine_chunk_kb = std::max(0, std::min(144, std::atoi(e)));
   if (const char* e = std::getenv("PM_SORT_PPT")) {
     const int v = std::atoi(e);
     c->sort_ppt = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;

@@ -287,27 +287,38 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     else
       PM_LAUNCH(ctx, "sort_coarse", launch_coarse<false, true>(dg, ue, gm, bofs, mid, grid, lds, st));
   }
-  // LDS cache: room for 1.5x the mean segment (random digits fill segments
-  // evenly; a skewed segment falls back to re-reading mid), capped at 64 KiB
+  // fine sort LDS: segment cache + chunk buffer (k_sort_fine).  A mean
+  // segment that fits 24 KiB is cached whole with room for 1.5x its size and
+  // sorted as one chunk; larger ones are re-read from mid in 32 KiB chunks
+  // (2 blocks per CU).  Sweep with 16-B loads (profiles/r03/sort_fine/): 16
+  // KiB chunks 2^20 0.065 / 2^22 0.233 ms, 24-32 KiB 0.056 / 0.210, 40-64 KiB
+  // (one block per CU) 0.064-0.074 / 0.256-0.288; the whole segment cached in
+  // LDS (64-136 KiB) 0.069-0.107 / 0.34-0.44.  PM_FINE_CACHE_KB /
+  // PM_FINE_CHUNK_KB override both (A/B).
   const size_t esz = wide ? 8 : 4;
   const size_t mean_seg = E / std::max(1, g.NCB - 1) + 1;
-  // A mean segment that fits 24 KiB is cached whole (1.5x its size); larger
-  // ones go through the chunked path in 16 KiB chunks, which keeps 3 blocks
-  // per CU instead of one (2^22: sort_fine 0.48 -> 0.27 ms, fixed-base 2^23:
-  // 2.5 -> 1.06 ms; profiles/r02/sort/fb_sweep.jsonl)
-  size_t cache_cap = (mean_seg * 3 / 2 + 63) & ~size_t(63);
-  if (cache_cap > kFineCacheSmall / esz) cache_cap = kFineChunkBytes / esz;
-  uint32_t cache_n = (uint32_t)std::min<size_t>(cache_cap, kFineCacheBytes / esz);
   const size_t fine_fixed = ((size_t)3 * (1 << g.FB) + kFineThreads / 64 + 1) * 4;  // hist, lcur, lst, scan
-  if (fine_fixed + 64 * (esz + 4) > kMaxLds) return set_error(PM_ERR_UNSUPPORTED, "sort: fine bits too wide");
-  while (cache_n > 64 && (size_t)cache_n * (esz + 4) + fine_fixed > kMaxLds) cache_n /= 2;
-  const size_t lds_fine = (size_t)cache_n * (esz + 4) + fine_fixed;
+  size_t cache_n = (mean_seg * 3 / 2 + 63) & ~size_t(63), ch;
+  if (cache_n * esz > 24576) cache_n = kFineChunkBytes / esz;
+  ch = cache_n;
+  if (ctx->fine_cache_kb > 0) cache_n = ((size_t)ctx->fine_cache_kb * 1024 / esz) & ~size_t(63);
+  if (ctx->fine_chunk_kb > 0) ch = ((size_t)ctx->fine_chunk_kb * 1024 / esz) & ~size_t(63);
+  ch = std::max<size_t>(64, std::min(ch, cache_n));
+  cache_n = std::max(cache_n, ch);
+  if (fine_fixed + 128 * esz > kMaxLds) return set_error(PM_ERR_UNSUPPORTED, "sort: fine bits too wide");
+  while (cache_n > 64 && (cache_n + ch) * esz + fine_fixed > kMaxLds) {
+    cache_n /= 2;
+    ch = std::min(ch, cache_n);
+  }
+  const size_t lds_fine = (cache_n + ch) * esz + fine_fixed;
   if (wide)
     PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<true><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
-                                    (const uint64_t*)mid, bofs, gm, Wr, pl.NB, cache_n, offsets, sorted)));
+                                    (const uint64_t*)mid, bofs, gm, Wr, pl.NB, (uint32_t)cache_n, (uint32_t)ch,
+                                    offsets, sorted)));
   else
     PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<false><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
-                                    (const uint32_t*)mid, bofs, gm, Wr, pl.NB, cache_n, offsets, sorted)));
+                                    (const uint32_t*)mid, bofs, gm, Wr, pl.NB, (uint32_t)cache_n, (uint32_t)ch,
+                                    offsets, sorted)));
   const uint32_t s1 = (uint32_t)((size_t)Wr * pl.NB);
   PM_LAUNCH(ctx, "accumulate",
             (k_accumulate<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, s1, bases29, pl.chunk,

@@ -195,9 +195,7 @@ static __global__ void __launch_bounds__(kScanThreads) k_scan_down(const uint32_
 constexpr int kSortThreads = 1024;
 constexpr int kSortPerThread = 8;                      // max points per thread (SortGeom::ppt)
 constexpr int kSortB = kSortThreads * kSortPerThread;  // max points per block (fixed-base padding)
-constexpr uint32_t kFineCacheBytes = 65536;            // max LDS cache of one fine segment (64 KiB)
-constexpr uint32_t kFineCacheSmall = 24576;            // auto: whole-segment cache up to this size
-constexpr uint32_t kFineChunkBytes = 16384;            // auto: chunk size of larger segments
+constexpr uint32_t kFineChunkBytes = 32768;            // auto: chunk buffer of segments larger than one chunk
 constexpr size_t kMaxLds = 160 * 1024;                 // LDS per CU (one workgroup may take all of it)
 constexpr int kFineThreads = 512;
 
@@ -349,6 +347,35 @@ struct SortEntry<false> {
 // block (blk = blockIdx.x, w = blockIdx.y) of PPT x kSortThreads points.
 // PPT is a template parameter: with g.ppt read at run time the kernel ran
 // ~45% slower at the same geometry (0.069 vs 0.047 ms at 2^20).
+// Each lane takes PPT consecutive codes with one vector load (when the row is
+// aligned for it); the block's global bin starts are read once into LDS
+// (round 2 loaded bofs[] per entry in the write-out loop).
+template <int PPT, class DT>
+__device__ __forceinline__ void load_codes(const DT* __restrict__ row, uint32_t i0, uint32_t n, bool vec,
+                                           uint32_t (&code)[PPT]) {
+  constexpr int bytes = PPT * (int)sizeof(DT);
+  if (vec && i0 + PPT <= n && (bytes == 16 || bytes == 8 || bytes == 4)) {
+    DT v[PPT];
+    if constexpr (bytes == 16) {
+      *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(row + i0);
+    } else if constexpr (bytes == 8) {
+      *reinterpret_cast<uint2*>(v) = *reinterpret_cast<const uint2*>(row + i0);
+    } else if constexpr (bytes == 4) {
+      *reinterpret_cast<uint32_t*>(v) = *reinterpret_cast<const uint32_t*>(row + i0);
+    }
+#pragma unroll
+    for (int r = 0; r < PPT; r++) code[r] = DigitCode<sizeof(DT) == 2>::dec(v[r]);
+  } else if (vec && i0 + PPT <= n && bytes == 32) {
+    DT v[PPT];
+    reinterpret_cast<uint4*>(v)[0] = reinterpret_cast<const uint4*>(row + i0)[0];
+    reinterpret_cast<uint4*>(v)[1] = reinterpret_cast<const uint4*>(row + i0)[1];
+#pragma unroll
+    for (int r = 0; r < PPT; r++) code[r] = DigitCode<sizeof(DT) == 2>::dec(v[r]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < PPT; r++) code[r] = i0 + r < n ? DigitCode<sizeof(DT) == 2>::dec(row[i0 + r]) : 0u;
+  }
+}
 template <bool D16, bool WIDE, int PPT>
 __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename DigitCode<D16>::T* __restrict__ digits,
                                                               uint32_t n, SortGeom g,
@@ -356,6 +383,7 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename Dig
                                                               typename SortEntry<WIDE>::T* __restrict__ mid) {
   using E = SortEntry<WIDE>;
   using T = typename E::T;
+  using DT = typename DigitCode<D16>::T;
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   constexpr uint32_t sortb = (uint32_t)PPT * kSortThreads;
   T* stage = reinterpret_cast<T*>(sm);                                        // sortb entries
@@ -366,13 +394,15 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename Dig
   const uint32_t w = blockIdx.y, blk = blockIdx.x;
   for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) cnt[k] = 0;
   __syncthreads();
+  const DT* row = digits + (size_t)w * n;
+  // vector loads need the row start aligned to PPT codes (n % PPT == 0 or w == 0)
+  const bool vec = (((size_t)w * n) % PPT) == 0;
+  const uint32_t i0 = blk * sortb + threadIdx.x * PPT;
   uint32_t code[PPT];
+  load_codes<PPT, DT>(row, i0, n, vec, code);
 #pragma unroll
-  for (int r = 0; r < PPT; r++) {
-    const uint32_t i = blk * sortb + r * kSortThreads + threadIdx.x;
-    code[r] = i < n ? DigitCode<D16>::dec(digits[(size_t)w * n + i]) : 0u;
+  for (int r = 0; r < PPT; r++)
     if (code[r]) atomicAdd(&cnt[(code[r] & ~kNegBit) >> g.FB], 1u);
-  }
   __syncthreads();
   uint32_t run = 0;
   for (int base = 0; base < g.NCB; base += kSortThreads) {
@@ -385,50 +415,85 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename Dig
   }
   if (threadIdx.x == 0) lstart[g.NCB] = run;
   __syncthreads();
-  for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) cnt[k] = lstart[k];  // cursors
+  const uint32_t nvalid = lstart[g.NCB];
+  // cursors; lstart becomes (global start of the bin's run) - (its LDS start)
+  for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) {
+    const uint32_t ls = lstart[k];
+    cnt[k] = ls;
+    lstart[k] = bofs[((size_t)w * g.NCB + k) * g.nblk + (size_t)blk * g.hsub] - ls;
+  }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < PPT; r++) {
     if (!code[r]) continue;
-    const uint32_t i = blk * sortb + r * kSortThreads + threadIdx.x;
     const uint32_t slot = code[r] & ~kNegBit;
     const uint32_t cb = slot >> g.FB;
     const uint32_t pos = atomicAdd(&cnt[cb], 1u);
-    stage[pos] = E::make(slot, i, code[r] >> 31, g.FB);
+    stage[pos] = E::make(slot, i0 + r, code[r] >> 31, g.FB);
     stage_cb[pos] = (uint16_t)cb;
   }
   __syncthreads();
-  const uint32_t nvalid = lstart[g.NCB];
-  for (uint32_t e = threadIdx.x; e < nvalid; e += kSortThreads) {
-    const uint32_t cb = stage_cb[e];
-    const uint32_t pos = bofs[((size_t)w * g.NCB + cb) * g.nblk + (size_t)blk * g.hsub] + (e - lstart[cb]);
-    mid[pos] = stage[e];
-  }
+  for (uint32_t e = threadIdx.x; e < nvalid; e += kSortThreads) mid[lstart[stage_cb[e]] + e] = stage[e];
 }
 
-// block per (w, cb) segment; offsets[w*NB + slot] for its slots, sorted[]
-// (cache_n: entries of the LDS segment cache, sized from the mean segment).
-// A segment that fits the cache is read once, counting-sorted into LDS and
-// written out coalesced.  A larger one (n >= 2^22, or the fixed-base MSM's
-// merged segments) is sorted in chunks of the cache size: each chunk is
-// staged in LDS, counting-sorted there by its fine bits, and every fine bin's
-// run of the chunk is written to that bin's global cursor, so the stores go
-// out as runs instead of scattered 4-B writes (fixed-base 2^23: 3.0 ms of
-// scattered stores before).
+// block per (w, cb) segment; offsets[w*NB + slot] for its slots, sorted[].
+// LDS: a segment cache of cache_n entries and a chunk buffer of ch entries.
+//   pass 1  the segment is read once with 16-B loads (4 in flight per lane)
+//           into the cache while its fine histogram is counted;
+//   pass 2  chunk by chunk (ch entries; one chunk when the segment fits the
+//           chunk buffer): LDS counting sort of the chunk by fine bits into
+//           the chunk buffer, then every fine bin's run goes out to that bin's
+//           global cursor, so the stores leave as runs, not scattered 4-B
+//           writes (fixed-base 2^23: 3.0 ms of scattered stores before).
+// A segment larger than the cache (skewed digits, the fixed-base MSM's merged
+// rows at small caches) re-reads each chunk from mid into the cache instead.
+template <class T>
+__device__ __forceinline__ void fine_entry(T v, T* cache, uint32_t at, uint32_t* hist, uint32_t fmask, int FB) {
+  if (cache) cache[at] = v;
+  atomicAdd(&hist[SortEntry<sizeof(T) == 8>::fine(v, fmask, FB)], 1u);
+}
+template <class T>
+__device__ __forceinline__ void fine_pass1(const T* __restrict__ mid, uint32_t s0, uint32_t s1, T* cache,
+                                           uint32_t* hist, uint32_t fmask, int FB) {
+  constexpr uint32_t per = 16 / sizeof(T);  // entries per 16-B load
+  constexpr int kUnroll = 4;
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  const uint32_t a0 = min(s1, (s0 + per - 1) & ~(per - 1));
+  const uint32_t a1 = max(a0, s1 & ~(per - 1));
+  for (uint32_t e = s0 + tid; e < a0; e += nt) fine_entry<T>(mid[e], cache, e - s0, hist, fmask, FB);
+  for (uint32_t e = a1 + tid; e < s1; e += nt) fine_entry<T>(mid[e], cache, e - s0, hist, fmask, FB);
+  const uint4* v4 = reinterpret_cast<const uint4*>(mid + a0);
+  const uint32_t nv = (a1 - a0) / per;
+  for (uint32_t k = tid; k < nv; k += kUnroll * nt) {
+    uint4 x[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++)
+      if (k + u * nt < nv) x[u] = v4[k + u * nt];
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++) {
+      if (k + u * nt >= nv) break;
+      const T* ev = reinterpret_cast<const T*>(&x[u]);
+      const uint32_t at = a0 - s0 + (k + u * nt) * per;
+#pragma unroll
+      for (uint32_t q = 0; q < per; q++) fine_entry<T>(ev[q], cache, at + q, hist, fmask, FB);
+    }
+  }
+}
 template <bool WIDE>
 __global__ void __launch_bounds__(kFineThreads) k_sort_fine(const typename SortEntry<WIDE>::T* __restrict__ mid,
                                                             const uint32_t* __restrict__ bofs, SortGeom g, int W,
-                                                            int NB, uint32_t cache_n, uint32_t* __restrict__ offsets,
+                                                            int NB, uint32_t cache_n, uint32_t ch,
+                                                            uint32_t* __restrict__ offsets,
                                                             uint32_t* __restrict__ sorted) {
   using E = SortEntry<WIDE>;
   using T = typename E::T;
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int nf = 1 << g.FB;
-  T* cache = reinterpret_cast<T*>(sm);                                 // cache_n entries
-  uint32_t* obuf = reinterpret_cast<uint32_t*>(cache + cache_n);       // cache_n output codes
-  uint32_t* hist = obuf + cache_n;                                     // nf
-  uint32_t* lcur = hist + nf;                                          // nf (chunked path)
-  uint32_t* lst = lcur + nf;                                           // nf (chunked path)
+  T* cache = reinterpret_cast<T*>(sm);                                 // cache_n entries (>= ch)
+  T* otmp = cache + cache_n;                                           // ch entries
+  uint32_t* hist = reinterpret_cast<uint32_t*>(otmp + ch);             // nf global cursors
+  uint32_t* lcur = hist + nf;                                          // nf chunk cursors
+  uint32_t* lst = lcur + nf;                                           // nf chunk starts
   uint32_t* scan_tmp = lst + nf;                                       // kFineThreads/64 + 1
   const uint32_t seg = blockIdx.x;     // = w * NCB + cb
   const uint32_t w = seg / g.NCB, cb = seg - w * g.NCB;
@@ -438,13 +503,9 @@ __global__ void __launch_bounds__(kFineThreads) k_sort_fine(const typename SortE
   const uint32_t fmask = (uint32_t)nf - 1u;
   for (int k = threadIdx.x; k < nf; k += kFineThreads) hist[k] = 0;
   __syncthreads();
-  for (uint32_t e = s0 + threadIdx.x; e < s1; e += kFineThreads) {
-    const T v = mid[e];
-    if (cached) cache[e - s0] = v;
-    atomicAdd(&hist[E::fine(v, fmask, g.FB)], 1u);
-  }
+  fine_pass1<T>(mid, s0, s1, cached ? cache : nullptr, hist, fmask, g.FB);
   __syncthreads();
-  // exclusive scan of the fine histogram; emit bucket offsets
+  // exclusive scan of the fine histogram: bucket offsets and global cursors
   uint32_t run = 0;
   for (int base = 0; base < nf; base += kFineThreads) {
     const int k = base + threadIdx.x;
@@ -453,7 +514,7 @@ __global__ void __launch_bounds__(kFineThreads) k_sort_fine(const typename SortE
     const uint32_t ex = block_excl_scan(v, scan_tmp, total);
     if (k < nf) {
       const uint32_t slot = (cb << g.FB) + k;
-      hist[k] = (cached ? 0u : s0) + ex + run;  // cursor (segment-relative when staged in LDS)
+      hist[k] = s0 + ex + run;
       if (slot < (uint32_t)NB) offsets[(size_t)w * NB + slot] = s0 + ex + run;
     }
     run += total;
@@ -465,28 +526,15 @@ __global__ void __launch_bounds__(kFineThreads) k_sort_fine(const typename SortE
     if (threadIdx.x == 0 && w == (uint32_t)W - 1) offsets[(size_t)W * NB] = s1;
   }
   __syncthreads();
-  if (cached) {
-    // counting-sort scatter into LDS, then one coalesced copy of the segment
-    // (scattered 4-B global stores made this pass write-bound)
-    for (uint32_t e = threadIdx.x; e < s1 - s0; e += kFineThreads) {
-      const T v = cache[e];
-      obuf[atomicAdd(&hist[E::fine(v, fmask, g.FB)], 1u)] = E::code(v, g.FB);
-    }
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < s1 - s0; e += kFineThreads) sorted[s0 + e] = obuf[e];
-    return;
-  }
-  // chunked: obuf holds a chunk's entries (type T) in fine-bin order
-  T* otmp = reinterpret_cast<T*>(obuf);
-  const uint32_t ch = WIDE ? cache_n / 2 : cache_n;
   for (uint32_t c0 = s0; c0 < s1; c0 += ch) {
     const uint32_t m = min(ch, s1 - c0);
+    const T* src = cached ? cache + (c0 - s0) : cache;
     for (int k = threadIdx.x; k < nf; k += kFineThreads) lcur[k] = 0;
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < m; e += kFineThreads) {
-      const T v = mid[c0 + e];
-      cache[e] = v;
-      atomicAdd(&lcur[E::fine(v, fmask, g.FB)], 1u);
+    if (cached) {
+      for (uint32_t e = threadIdx.x; e < m; e += kFineThreads) atomicAdd(&lcur[E::fine(src[e], fmask, g.FB)], 1u);
+    } else {
+      fine_pass1<T>(mid, c0, c0 + m, cache, lcur, fmask, g.FB);  // stage the chunk (16-B loads)
     }
     __syncthreads();
     uint32_t lrun = 0;
@@ -503,7 +551,7 @@ __global__ void __launch_bounds__(kFineThreads) k_sort_fine(const typename SortE
     }
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < m; e += kFineThreads) {
-      const T v = cache[e];
+      const T v = src[e];
       otmp[atomicAdd(&lcur[E::fine(v, fmask, g.FB)], 1u)] = v;
     }
     __syncthreads();
