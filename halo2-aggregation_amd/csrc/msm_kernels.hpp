@@ -291,8 +291,12 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
   if (blk == 0) sort_clear(g);
   for (int k = threadIdx.x; k < nbins; k += kSortThreads) hist[k] = 0;
   __syncthreads();
+  // the next point's scalar is loaded while this one is digitised
+  const uint32_t ib = blk * g.ppt * kSortThreads + threadIdx.x;
+  Fe<Fs> nx;
+  if (ib < n) nx = load_fe4<Fs>(reinterpret_cast<const uint4*>(scalars + 8ull * ib));
   for (int r = 0; r < g.ppt; r++) {
-    const uint32_t i = (blk * g.ppt + r) * kSortThreads + threadIdx.x;
+    const uint32_t i = ib + (uint32_t)r * kSortThreads;
     if (i >= stride) break;
     if (i >= n) {
 #pragma unroll
@@ -300,7 +304,10 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_hist(const uint32_t* __re
         digits[(size_t)((w % Wr) * kmerge + w / Wr) * stride + i] = DigitCode<D16>::enc(0u);
       continue;
     }
-    const Fe<Fs> s = load_canonical<Fs>(scalars, i, canonical);
+    const Fe<Fs> raw = nx;
+    if (r + 1 < g.ppt && i + kSortThreads < n)
+      nx = load_fe4<Fs>(reinterpret_cast<const uint4*>(scalars + 8ull * (i + kSortThreads)));
+    const Fe<Fs> s = canonical ? raw : fe_from_mont<Fs>(raw);
     uint32_t carry = 0;
 #pragma unroll
     for (int w = 0; w < W; w++) {
