@@ -138,6 +138,27 @@ def test_known_dlog(gpu_ctx, curve, logn):
                                                          b.cpu().numpy().view(np.uint64)))
 
 
+@pytest.mark.parametrize("cache_kb,chunk_kb", [(4, 4), (8, 8), (68, 8), (136, 16)])
+def test_fine_sort_lds_modes(monkeypatch, cache_kb, chunk_kb):
+    """k_sort_fine with its segment cache and chunk buffer forced (PM_FINE_*,
+    read when a context is created): 4-8 KiB re-read every segment from HBM
+    in many chunks, 68 / 136 KiB hold whole segments in LDS and sort them in
+    8 / 16 KiB chunks.  2^18 resident (8-row table: 16 K-entry segments) and
+    2^20 raw bases, against the C restatement."""
+    monkeypatch.setenv("PM_FINE_CACHE_KB", str(cache_kb))
+    monkeypatch.setenv("PM_FINE_CHUNK_KB", str(chunk_kb))
+    ctx = H.Context(0)
+    for curve, n in [(0, (1 << 18) + 5), (1, 1 << 20)]:
+        s, b = _torch_inputs(ctx, curve, n)
+        want = msm_ref.best_multiexp(curve, s.cpu().numpy().view(np.uint64), b.cpu().numpy().view(np.uint64))
+        assert np.array_equal(ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n), want)
+        rb = H.Bases(ctx, curve, d_bases=b.data_ptr(), n=n)
+        try:
+            assert np.array_equal(ctx.msm_resident_device(rb, 0, s.data_ptr(), n), want)
+        finally:
+            rb.release()
+
+
 def test_all_equal_scalars_large(gpu_ctx):
     """One bucket per window holds every point: long fixup chains."""
     n = 1 << 16
