@@ -41,7 +41,7 @@ def _run(body, a, b=None, u=None, v=None):
         mm = re.fullmatch(r"([a-z.]+)\[(\d+)\]", expr)
         if mm:
             return env[mm.group(1)][int(mm.group(2))]
-        return int(expr.rstrip("u"))
+        return int(expr.rstrip("ul"))
 
     stmts = re.findall(r'asm\("(.*?)"\s*:\s*"\+v"\(acc\), "=&s"\(c\)\s*:\s*(.*?)\);|^  (?!asm)([^\n]*?);$', body, re.S | re.M)
     for text, ins, cline in stmts:
@@ -59,6 +59,11 @@ def _run(body, a, b=None, u=None, v=None):
                         assert 0 <= x < 2 ** 32 and 0 <= y < 2 ** 32
                     acc += x * y
                     # unsigned columns (additive form) or signed ones (subtractive)
+                    assert -(1 << 63) <= acc <= M64, "column overflow"
+                    assert not (signed and acc >= 1 << 63), "signed column overflow"
+                elif f[0] == "v_lshl_add_u64":  # + a 64-bit SGPR-pair constant (p R limbs)
+                    assert f[1] == "%0" and f[3] == "0" and f[4] == "%0"
+                    acc += ops[int(f[2][1:]) - 2]
                     assert -(1 << 63) <= acc <= M64, "column overflow"
                     assert not (signed and acc >= 1 << 63), "signed column overflow"
                 elif f[0] == "v_lshrrev_b64":

@@ -19,7 +19,8 @@ columns are signed 64-bit: the reduction terms m_i p_j enter as
 v_mad_i64_i32 with -p_j).  Adding p R (p_j into column 9 + j) keeps the
 result (T - M p) / R + p in (T / R, T / R + p], the range of the additive
 form.  Per column: one AND instead of SUB + AND + a multiply-add, i.e. 18
-instructions less per product for 6 constant adds.
+instructions less per product; p R costs 3 adds (limbs paired into 64-bit
+constants, pr_add).
 
 Usage: python tools/gen_fp29_asm.py > halo2-aggregation_amd/csrc/fp29_asm.hpp
 """
@@ -52,6 +53,23 @@ def nconst(ins, v):
     return opnd(ins, "s", "%du" % ((-v) & 0xFFFFFFFF))
 
 
+def pr_add(body, ins, k, P, kp):
+    """+ kp p R at output column k (9 <= k <= 17): p_j goes into column 9 + j.
+    Two limbs per 64-bit add (v_lshl_add_u64 of an SGPR-pair constant): column
+    9 + 2i takes kp (p_2i + p_2i+1 2^29), the carry moves p_2i+1 into column
+    10 + 2i (round 2 spent one multiply-add by 1 per limb)."""
+    j = k - 9
+    if j % 2:
+        return
+    v = kp * P[j] + (kp * P[j + 1] << 29 if j + 1 < 9 else 0)
+    if not v:
+        return
+    if v < 1 << 32:
+        body.append("v_mad_u64_u32 %%0, %%1, 1, %s, %%0" % const(ins, v))
+    else:
+        body.append("v_lshl_add_u64 %%0, %s, 0, %%0" % opnd(ins, "s", "%dull" % v))
+
+
 def opnd(ins, c, e):
     for n, (c2, e2) in enumerate(ins):
         if (c2, e2) == (c, e):
@@ -75,8 +93,8 @@ def statement(k, sq, P):
     if k > 0:
         if sub:
             body.append("v_ashrrev_i64 %0, 29, %0")
-            if k >= 9 and P[k - 9]:
-                mad("1", const(ins, P[k - 9]))  # + p R: p_j into column 9 + j
+            if k >= 9:
+                pr_add(body, ins, k, P, 1)  # + p R
         else:
             if k - 1 < 9:
                 mad(opnd(ins, "v", "m[%d]" % (k - 1)), const(ins, P[0]))
@@ -131,8 +149,8 @@ def statement2(k, P, neg=False):
         if not sub and k - 1 < 9:
             mad(bodyA, opnd(insA, "v", "m[%d]" % (k - 1)), const(insA, P[0]))
         bodyA.append("v_ashrrev_i64 %0, 29, %0" if signed else "v_lshrrev_b64 %0, 29, %0")
-        if kp and k >= 9 and P[k - 9]:
-            mad(bodyA, "1", const(insA, kp * P[k - 9]))
+        if kp and k >= 9:
+            pr_add(bodyA, insA, k, P, kp)
     if k < 17:
         for i in range(9):
             j = k - i
