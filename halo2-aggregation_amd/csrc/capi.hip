@@ -202,7 +202,7 @@ int pm_ctx::ensure_pinned(size_t bytes) {
   if (h_pinned) (void)hipHostFree(h_pinned);
   h_pinned = nullptr;
   h_pinned_cap = 0;
-  HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocMapped));
   h_pinned_cap = bytes;
   return PM_OK;
 }
@@ -367,6 +367,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("PM_TERMS_COPY")) c->terms_copy = std::atoi(e) != 0;
   if (const char* e = std::getenv("PM_FINE_CACHE_KB")) c->fine_cache_kb = std::max(0, std::min(144, std::atoi(e)));
   if (const char* e = std::getenv("PM_FINE_CHUNK_KB")) c->fine_chunk_kb = std::max(0, std::min(144, std::atoi(e)));
   if (const char* e = std::getenv("PM_SORT_PPT")) {

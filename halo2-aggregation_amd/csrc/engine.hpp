@@ -212,7 +212,16 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   Xyzz<F>* head = (Xyzz<F>*)ctx->head.p;
   Xyzz<F>* S = (Xyzz<F>*)ctx->segS.p;
   Xyzz<F>* T = (Xyzz<F>*)ctx->segT.p;
+  // host terms: the reduction kernels store them straight into the pinned
+  // slot (mapped; visible to the host once the event below completes), which
+  // saves the blit of a D2H copy (~11 us per MSM, profiles/r03/kernel_stats.csv
+  // __amd_rocclr_copyBuffer).  PM_TERMS_COPY=1: the device buffer + copy (A/B).
   Xyzz<F>* Qd = (Xyzz<F>*)ctx->bitsQ.p;
+  if (!ctx->terms_copy) {
+    void* dq = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dq, hslot, 0));
+    Qd = (Xyzz<F>*)dq;
+  }
   const uint32_t un = (uint32_t)n;
 
   g.clr_bh = bh + (TOTB - 1);  // zeroed by the histogram kernel's block 0
@@ -345,7 +354,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   PM_LAUNCH(ctx, "bucket_bits",
             (k_bucket_bits<F><<<dim3(NJ, Wr, nsplit), kRedThreads, 0, st>>>(S, T, pl.M1, pl.NB2, Qd, NQ, nsplit,
                                                                              bitsP, tickets)));
-  HIP_TRY(hipMemcpyAsync(hslot, Qd, nQ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
+  if (ctx->terms_copy) HIP_TRY(hipMemcpyAsync(hslot, Qd, nQ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
   hipEvent_t ev = ctx->grp_ev[slot];
   HIP_TRY(hipEventRecord(ev, st));
   MsmTail<F> t;
