@@ -189,7 +189,7 @@ def main():
     leg = run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline=True, breakdown=True,
                       host_leg=(world == 1))
     d_s, d_b, result = leg.pop("_d_s"), leg.pop("_d_b"), leg.pop("_result")
-    gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
+    gathered = torch.zeros(world * 8, dtype=torch.int64, device=dev)  # one all-gather target
 
     def padd(a, b):
         return H.point_add(curve, a, b)
@@ -306,13 +306,18 @@ def settle(step, seconds=0.3):
     torch.cuda.synchronize()
 
 
-def timed_steps(step, steps, warmup, dist, dev):
+def timed_steps(step, steps, warmup, dist, dev, drain=None):
     """W untimed steps, then K steps between barrier + synchronize on both
-    sides; returns (max-over-ranks seconds, last step's result)."""
+    sides; returns (max-over-ranks seconds, last step's result).  drain: a
+    pipelined step (sharded.PartialPipe) returns step k - 1's result; drain()
+    completes the last one, after the warmup (untimed) and inside the timed
+    region."""
     import torch
 
     for _ in range(warmup):
         step()
+    if drain:
+        drain()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -320,6 +325,9 @@ def timed_steps(step, steps, warmup, dist, dev):
     result = None
     for _ in range(steps):
         result = step()
+    if drain:
+        last = drain()
+        result = last if last is not None else result
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -347,7 +355,7 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     import torch
 
     import halo2_amd as H
-    from sharded import combine_partials
+    from sharded import PartialPipe
 
     d_s = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
     d_b = torch.empty((max(n, 1), 8), dtype=torch.int64, device=dev)
@@ -357,14 +365,19 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     t0 = time.perf_counter()
     rb = ctx.upload_bases(curve, d_bases=d_b.data_ptr(), n=n) if n else None
     upload_ms = (time.perf_counter() - t0) * 1e3
-    gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
+    gathered = torch.zeros(world * 8, dtype=torch.int64, device=dev)  # one all-gather target
 
     def padd(a, b):
         return H.point_add(curve, a, b)
 
+    # the exchange of MSM k (all-gather of the partials + fold) runs behind
+    # MSM k + 1's kernels; every partial is still gathered and folded inside
+    # the timed region (sharded.PartialPipe, drained at the end)
+    pipe = PartialPipe(dist, dev, padd, world)
+
     def step():
         part = ctx.msm_resident_device(rb, 0, d_s.data_ptr(), n) if n else np.zeros(8, np.uint64)
-        return combine_partials(part, dist, dev, padd, world, gathered)
+        return pipe.step(part)
 
     # timed region: HIP events only around the roofline kernel (every event
     # pair costs ~10 us of stream time on MI355X)
@@ -375,7 +388,7 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
             step()
         ctx.set_timing(True, only="accumulate")
         ctx.reset_stats()
-    elapsed, result = timed_steps(step, args.steps, 0 if roofline else args.warmup, dist, dev)
+    elapsed, result = timed_steps(step, args.steps, 0 if roofline else args.warmup, dist, dev, drain=pipe.drain)
     launches, acc_ms = ctx.kernel_stats("accumulate") if roofline else (0, 0.0)
     ctx.set_timing(False)
     lg = (n_total or n).bit_length() - 1
@@ -396,6 +409,7 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
         # per-MSM kernel breakdown from a separate, untimed diagnostic run with
         # events around every launch
         out["kernels_ms"] = kernel_breakdown(ctx, step, MSM_KERNELS)
+        pipe.drain()
     if roofline and launches:
         # one k_accumulate launch consumes all n (scalar, base) pairs of the MSM
         out["roofline"] = roofline_of(n, acc_ms / launches, launches / args.steps, f"{name}_msm_2^{lg}_per_gpu")
@@ -450,7 +464,7 @@ def run_variable_base(args, ctx, dist, dev, world, curve, d_s, d_b, n, want, nam
     import halo2_amd as H
     from sharded import combine_partials
 
-    gathered = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(world)]
+    gathered = torch.zeros(world * 8, dtype=torch.int64, device=dev)  # one all-gather target
 
     def raw():
         part = ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n)

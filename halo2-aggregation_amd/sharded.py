@@ -25,23 +25,72 @@ def split_range(rank: int, world: int, n_total: int):
     return lo, hi - lo
 
 
+def _fold(rows, point_add):
+    acc = np.zeros(8, dtype=np.uint64)
+    for r in rows:
+        acc = point_add(acc, r)
+    return acc
+
+
+def start_gather(part, dist, device, world: int, out=None):
+    """Enqueue the all-gather of this rank's affine partial (8 x u64) into one
+    (world * 8) int64 tensor and return (work handle, tensor); finish_gather
+    folds it.  One collective and one device-to-host copy per MSM (round 2:
+    a copy per rank)."""
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(part, dtype=np.uint64).reshape(8).view(np.int64).copy()).to(device)
+    if out is None:
+        out = torch.empty(world * 8, dtype=torch.int64, device=device)
+    work = dist.all_gather_into_tensor(out, t, async_op=True)
+    return work, out
+
+
+def finish_gather(pending, point_add):
+    """Wait for start_gather's collective and fold the partials in rank order."""
+    work, out = pending
+    work.wait()
+    rows = out.cpu().numpy().view(np.uint64).reshape(-1, 8)
+    return _fold(rows, point_add)
+
+
 def combine_partials(part, dist, device, point_add, world: int, gathered=None):
     """All-gather each rank's affine partial (8 x u64) and fold them in rank
     order with `point_add(a, b) -> 8 x u64`.  Returns the full MSM result on
-    every rank."""
-    import torch
-
+    every rank.  (`gathered`: an optional reusable (world * 8) int64 tensor.)"""
     part = np.ascontiguousarray(part, dtype=np.uint64).reshape(8)
     if world == 1:
         return part
-    t = torch.from_numpy(part.view(np.int64).copy()).to(device)
-    if gathered is None:
-        gathered = [torch.zeros(8, dtype=torch.int64, device=device) for _ in range(world)]
-    dist.all_gather(gathered, t)
-    acc = np.zeros(8, dtype=np.uint64)
-    for g in gathered:
-        acc = point_add(acc, g.cpu().numpy().view(np.uint64))
-    return acc
+    return finish_gather(start_gather(part, dist, device, world, gathered), point_add)
+
+
+class PartialPipe:
+    """The exchange of MSM k overlapped with MSM k + 1: step(part) starts
+    partial k's all-gather and folds partial k - 1's (returned), drain()
+    folds the last one.  Every partial is gathered and folded; only the
+    collective's latency moves behind the next MSM's kernels."""
+
+    def __init__(self, dist, device, point_add, world: int):
+        import torch
+
+        self.dist, self.device, self.point_add, self.world = dist, device, point_add, world
+        self.bufs = [torch.empty(world * 8, dtype=torch.int64, device=device) for _ in range(2)]
+        self.k = 0
+        self.pending = None
+
+    def step(self, part):
+        if self.world == 1:
+            return np.ascontiguousarray(part, dtype=np.uint64).reshape(8)
+        nxt = start_gather(part, self.dist, self.device, self.world, self.bufs[self.k & 1])
+        self.k += 1
+        prev, self.pending = self.pending, nxt
+        return finish_gather(prev, self.point_add) if prev is not None else None
+
+    def drain(self):
+        if self.pending is None:
+            return None
+        prev, self.pending = self.pending, None
+        return finish_gather(prev, self.point_add)
 
 
 def gather_batches(local, dist, world: int, gathered=None):

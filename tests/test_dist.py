@@ -32,7 +32,7 @@ def _worker(rank, world, port, n_per_rank, q):
     import halo2_amd as H
     import msm_ref
     import pasta as P
-    from sharded import combine_partials, shard_range
+    from sharded import PartialPipe, combine_partials, shard_range
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -45,7 +45,12 @@ def _worker(rank, world, port, n_per_rank, q):
         return H.point_add(0, a, b)
 
     full = combine_partials(part, dist, torch.device("cpu"), padd, world)
-    q.put((rank, [int(x) for x in full]))
+    # bench.py's pipelined form (sharded.PartialPipe): step k returns step
+    # k - 1's fold, drain() the last one -- every step must equal the full MSM
+    pipe = PartialPipe(dist, torch.device("cpu"), padd, world)
+    piped = [pipe.step(part) for _ in range(3)] + [pipe.drain()]
+    assert piped[0] is None and pipe.drain() is None
+    q.put((rank, [int(x) for x in full], [[int(x) for x in r] for r in piped[1:]]))
     dist.destroy_process_group()
 
 
@@ -61,7 +66,9 @@ def test_sharded_msm_gloo(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_per_rank, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(world))
+    got = [q.get(timeout=240) for _ in range(world)]
+    res = {r: full for r, full, _ in got}
+    piped = {r: p for r, _, p in got}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -71,6 +78,7 @@ def test_sharded_msm_gloo(world):
     want = [int(x) for x in msm_ref.best_multiexp(0, S, B, threads=4)]
     for r in range(world):
         assert res[r] == want, r
+        assert piped[r] == [want] * 3, r
 
 
 def test_split_range_covers():
