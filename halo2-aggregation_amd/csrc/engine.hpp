@@ -190,7 +190,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->counts.ensure(TOTB * 4))) return rc;
   if ((rc = ctx->cursor.ensure(TOTB * 4))) return rc;
   if ((rc = ctx->offsets.ensure(TOT * 4))) return rc;
-  const uint32_t nb = (uint32_t)((TOTB + kScanChunk - 1) / kScanChunk);
+  const ScanTiles tiles = scan_tiles((uint32_t)(pl.W * g.NCB), (uint32_t)g.nblk);  // k_sort_hist's layout
+  const uint32_t nb = (uint32_t)((TOTB + tiles.chunk - 1) / tiles.chunk);
   if ((rc = ctx->bsum.ensure((size_t)nb * 4))) return rc;
   if ((rc = ctx->buckets.ensure((size_t)Wr * pl.NB * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->head.ensure((size_t)pl.nthreads * sizeof(Xyzz<F>)))) return rc;
@@ -279,8 +280,8 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     if (rc) return rc;
   }
   PM_LAUNCH(ctx, "scan", {
-    k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum);
-    k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, bsum, bofs, nullptr);
+    k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, tiles, bsum);
+    k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, tiles, bsum, bofs, nullptr);
   });
   {
     const size_t lds = (size_t)gm.ppt * kSortThreads * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
