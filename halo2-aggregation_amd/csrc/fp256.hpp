@@ -306,6 +306,42 @@ __device__ __forceinline__ Fe<P> fe_mul_fips_g(const Fe<P>& a, const Fe<P>& b) {
   return fe_reduce_once<P>(r, (uint32_t)(acc >> 32));
 }
 
+// Montgomery reduction alone, in the FIPS column form of fe_mul_fips_g:
+// column k < 8 takes a_k (a multiply-add by 1) and sum m_i p_{k-i} over p's
+// nonzero limbs, then m_k; columns 8..14 the remaining m_i p_{k-i}.  Pasta:
+// 8 + 40 multiply-adds instead of fe_mul(a, 1)'s 104.
+template <class P>
+__device__ __forceinline__ Fe<P> fe_redc_fips_g(const Fe<P>& a) {
+  uint32_t m[8], r[8];
+  uint64_t acc = 0;
+  uint32_t acc2 = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    uint32_t ms[8], ps[8];
+    int nr = 0;
+    const int lo = k < 8 ? 0 : k - 7, hi = k < 8 ? k : 7;
+#pragma unroll
+    for (int i = lo; i <= hi && i < 8; i++)
+      if (i < k && P::MOD[k - i] != 0u) {
+        ms[nr] = m[i];
+        ps[nr] = P::MOD[k - i];
+        nr++;
+      }
+    if (k < 8) mac_vs(acc, acc2, a.l[k], 1u);
+    mac_n<true>(acc, acc2, ms, ps, nr);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * P::INV;
+      mac_vs(acc, acc2, m[k], P::MOD[0]);
+    } else {
+      r[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)acc2 << 32);
+    acc2 = 0;
+  }
+  r[7] = (uint32_t)acc;
+  return fe_reduce_once<P>(r, (uint32_t)(acc >> 32));
+}
+
 // Montgomery product by finely integrated product scanning (FIPS): column k
 // accumulates sum a_i b_{k-i} + sum m_i p_{k-i}; the low columns also produce
 // m_k = acc * (-p^-1) so that column k becomes divisible by 2^32.  Modulus
@@ -355,16 +391,56 @@ PM_HD Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
 }
 
 template <class P>
+PM_HD Fe<P> fe_redc_portable(const Fe<P>& a);
+template <class P>
+PM_HD Fe<P> fe_redc(const Fe<P>& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fe_redc_fips_g<P>(a);
+#else
+  return fe_redc_portable<P>(a);
+#endif
+}
+
+template <class P>
 PM_HD Fe<P> fe_sqr(const Fe<P>& a) {
   return fe_mul<P>(a, a);
 }
 
+// a R^-1 mod p for a < p (Montgomery -> canonical): the Montgomery reduction
+// of the single-width a alone -- 8 rounds of m = t_0 (-p^-1) and t += m p,
+// with p's zero limbs skipped at compile time (Pasta: 5 of 8), instead of a
+// full product by 1 (the histogram pass spent 7 us of 29 at 2^20 and 34 of
+// 97 us at 2^22 on it, profiles/r03/ab/hist_probe.jsonl).
+template <class P>
+PM_HD Fe<P> fe_redc_portable(const Fe<P>& a) {
+  uint32_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = a.l[i];
+  uint32_t top = 0;  // carry out of the window: t < 2^256 + p after each round
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t m = t[0] * P::INV;
+    uint64_t acc = (uint64_t)m * P::MOD[0] + t[0];  // low word 0 by construction
+    uint64_t c = acc >> 32;
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      acc = (P::MOD[j] != 0u ? (uint64_t)m * P::MOD[j] : 0ull) + t[j] + c;
+      t[j - 1] = (uint32_t)acc;
+      c = acc >> 32;
+    }
+    acc = (uint64_t)top + c;
+    t[7] = (uint32_t)acc;
+    top = (uint32_t)(acc >> 32);
+  }
+  return fe_reduce_once<P>(t, top);
+}
+
+template <class P>
+PM_HD Fe<P> fe_redc(const Fe<P>& a);  // device: FIPS columns (below); host: fe_redc_portable
+
 template <class P>
 PM_HD Fe<P> fe_from_mont(const Fe<P>& a) {
-  Fe<P> one;
-#pragma unroll
-  for (int i = 0; i < 8; i++) one.l[i] = i == 0 ? 1u : 0u;
-  return fe_mul<P>(a, one);
+  return fe_redc<P>(a);
 }
 template <class P>
 PM_HD Fe<P> fe_to_mont(const Fe<P>& a) {

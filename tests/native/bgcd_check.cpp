@@ -1,7 +1,7 @@
 // Host build of csrc/inv_bgcd.hpp for tests/test_inv_bgcd.py: reads lines
 // "<field> <y as 64 hex digits, big endian>" and prints bg_inverse(y) and
 // fe_inv_bgcd(y) (y read as a Montgomery element) as 64 hex digits each,
-// plus fe_inv(y) (Fermat) for the Montgomery form.
+// plus fe_inv(y) (Fermat) for the Montgomery form, and fe_redc(y) = y R^-1.
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -33,6 +33,8 @@ static void run(const uint32_t y[8]) {
   emit(fe_inv_bgcd<P>(a).l);
   printf(" ");
   emit(fe_inv<P>(a).l);
+  printf(" ");
+  emit(fe_redc<P>(a).l);  // y R^-1 mod p (fe_from_mont)
   printf("\n");
 }
 

@@ -40,6 +40,9 @@ def test_inverse_matches_python(exe):
     rows = out.split("\n")[:-1]
     assert len(rows) == len(want)
     for line, row, (inv, inv_m) in zip(lines, rows, want):
-        got, got_m, fermat = (int(x, 16) for x in row.split())
+        got, got_m, fermat, redc = (int(x, 16) for x in row.split())
         assert got == inv, line
         assert got_m == inv_m == fermat, line
+        f, y = line.split()
+        p = FIELDS[f]
+        assert redc == int(y, 16) * pow(P.R_MONT, -1, p) % p, line  # fe_redc = fe_from_mont
