@@ -239,7 +239,10 @@ constexpr int kSortPerThread = 8;                      // max points per thread 
 constexpr int kSortB = kSortThreads * kSortPerThread;  // max points per block (fixed-base padding)
 constexpr uint32_t kFineChunkBytes = 32768;            // auto: chunk buffer of segments larger than one chunk
 constexpr size_t kMaxLds = 160 * 1024;                 // LDS per CU (one workgroup may take all of it)
-constexpr int kFineThreads = 512;
+#ifndef PM_FINE_THREADS  // A/B builds only: 256 / 1024 measured slower (profiles/r03/sort_fine/fine_threads.jsonl)
+#define PM_FINE_THREADS 512
+#endif
+constexpr int kFineThreads = PM_FINE_THREADS;
 
 struct SortGeom {
   int FB;    // fine bits
