@@ -340,8 +340,9 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // bit sums of few sets (the row tables, the fixed-base MSM's one set) are
   // split over more blocks.  Every extra lane also adds one tree addition, so
   // the split stops at ~16 blocks per job (c = 20, 2^19 buckets: 16 -> 0.33
-  // ms, 64 -> 0.47 ms).
-  const int nsplit = std::max(1, std::min(kMaxSplit, 16 / Wr));
+  // ms, 64 -> 0.47 ms; round 3, 16 / Wr against 4, 8, 32, 64 / Wr at 2^19 -
+  // 2^22, resident and raw: profiles/r03/ab/bits_split_sweep.jsonl).
+  const int nsplit = std::max(1, std::min(kMaxSplit, ctx->bits_split_k / Wr));
   Xyzz<F>* bitsP = nullptr;
   uint32_t* tickets = nullptr;
   if (nsplit > 1) {

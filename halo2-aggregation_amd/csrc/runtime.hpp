@@ -179,6 +179,7 @@ struct pm_ctx {
   int sort_ppt = 0;   // sort points per thread, 0 = auto (diagnostics: PM_SORT_PPT env, 1/2/4/8)
   int sort_fb = 0;    // fine bits of the two-level sort, 0 = auto (diagnostics: PM_SORT_FB env)
   int fine_cache_kb = 0, fine_chunk_kb = 0;  // fine-sort LDS cache / chunk, 0 = auto (PM_FINE_CACHE_KB / _CHUNK_KB)
+  int bits_split_k = 16;    // k_bucket_bits blocks per job = bits_split_k / Wr (PM_BITS_SPLIT_K, A/B)
   bool terms_copy = false;  // MSM host terms through a device buffer + D2H copy (PM_TERMS_COPY=1, A/B)
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
