@@ -159,6 +159,26 @@ def test_fine_sort_lds_modes(monkeypatch, cache_kb, chunk_kb):
             rb.release()
 
 
+@pytest.mark.parametrize("env", [{"PM_TERMS_COPY": "1"}, {"PM_BITS_SPLIT_K": "64"}, {"PM_BITS_SPLIT_K": "4"}])
+def test_reduction_knobs(monkeypatch, env):
+    """The host terms through a device buffer + D2H copy instead of the mapped
+    pinned slot, and other bit-sum splits (PM_*, read when a context is
+    created): raw bases (16 bucket sets) and a resident 4-row table, against
+    the C restatement."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ctx = H.Context(0)
+    for curve, n in [(2, 70001), (0, 1 << 20)]:
+        s, b = _torch_inputs(ctx, curve, n)
+        want = msm_ref.best_multiexp(curve, s.cpu().numpy().view(np.uint64), b.cpu().numpy().view(np.uint64))
+        assert np.array_equal(ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n), want)
+        rb = H.Bases(ctx, curve, d_bases=b.data_ptr(), n=n)
+        try:
+            assert np.array_equal(ctx.msm_resident_device(rb, 0, s.data_ptr(), n), want)
+        finally:
+            rb.release()
+
+
 def test_all_equal_scalars_large(gpu_ctx):
     """One bucket per window holds every point: long fixup chains."""
     n = 1 << 16
