@@ -318,7 +318,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   PM_LAUNCH(ctx, "acc_sum",
             (k_acc_sum<Cv><<<(unsigned)((B * 4 * (1u << lgL) + 63) / 64), 64, 0, st>>>(h, dpart, lgL,
                                                                                       (uint32_t*)d_out)));
-  HIP_TRY(hipStreamSynchronize(st));
+  {
+    hipEvent_t done = ctx->next_event();
+    if (!done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+    HIP_TRY(hipEventRecord(done, st));
+    if (int rc = wait_event(ctx, done)) return rc;
+  }
   if (!built_key.empty()) {
     ctx->acc_vkpow_key.swap(built_key);
     ctx->acc_vkpow_gen = ctx->acc_vkpow.gen;

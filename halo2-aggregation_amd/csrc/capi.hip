@@ -368,6 +368,7 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("PM_BITS_SPLIT_K")) c->bits_split_k = std::max(1, std::min(1024, std::atoi(e)));
+  if (const char* e = std::getenv("PM_SPIN_WAIT")) c->spin_wait = std::atoi(e) != 0;
   if (const char* e = std::getenv("PM_TERMS_COPY")) c->terms_copy = std::atoi(e) != 0;
   if (const char* e = std::getenv("PM_FINE_CACHE_KB")) c->fine_cache_kb = std::max(0, std::min(144, std::atoi(e)));
   if (const char* e = std::getenv("PM_FINE_CHUNK_KB")) c->fine_chunk_kb = std::max(0, std::min(144, std::atoi(e)));

@@ -429,7 +429,7 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
   std::sort(terms.begin(), terms.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
     return a.first > b.first || (a.first == b.first && a.second < b.second);
   });
-  HIP_TRY(hipEventSynchronize(t.ev));
+  if (int rc = wait_event(ctx, t.ev)) return rc;
   const auto t0 = std::chrono::steady_clock::now();
   host::Pt<F> hacc = host::inf<F>();
   const int q = terms.front().first;

@@ -180,6 +180,7 @@ struct pm_ctx {
   int sort_fb = 0;    // fine bits of the two-level sort, 0 = auto (diagnostics: PM_SORT_FB env)
   int fine_cache_kb = 0, fine_chunk_kb = 0;  // fine-sort LDS cache / chunk, 0 = auto (PM_FINE_CACHE_KB / _CHUNK_KB)
   int bits_split_k = 16;    // k_bucket_bits blocks per job = bits_split_k / Wr (PM_BITS_SPLIT_K, A/B)
+  bool spin_wait = false;   // host waits poll their event (PM_SPIN_WAIT=1, A/B; within noise, not default)
   bool terms_copy = false;  // MSM host terms through a device buffer + D2H copy (PM_TERMS_COPY=1, A/B)
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
@@ -282,6 +283,22 @@ int CachedUpload::put(const std::vector<T>& v, hipStream_t st, size_t pad) {
   if (bytes) HIP_TRY(hipMemcpyAsync(buf.p, v.data(), bytes, hipMemcpyHostToDevice, st));
   host.assign((const uint8_t*)v.data(), (const uint8_t*)v.data() + bytes);
   gen_at_upload = buf.gen;
+  return PM_OK;
+}
+
+// Wait for `ev` on the host: the runtime's blocking wait, or (PM_SPIN_WAIT=1)
+// a hipEventQuery poll.  Polling measured within run-to-run noise (2^19-2^22
+// MSM, accumulator, bench; profiles/r03/ab/spin_wait/), so it stays off and
+// leaves the host core to the caller.
+inline int wait_event(const pm_ctx* ctx, hipEvent_t ev) {
+  if (!ctx->spin_wait) {
+    HIP_TRY(hipEventSynchronize(ev));
+    return PM_OK;
+  }
+  hipError_t q;
+  while ((q = hipEventQuery(ev)) == hipErrorNotReady) {
+  }
+  HIP_TRY(q);
   return PM_OK;
 }
 }  // namespace pm
