@@ -550,11 +550,13 @@ constexpr size_t kResidentRowsMinN = size_t(1) << 18;
 int resident_rows(size_t n) {
   if (const char* e = std::getenv("PM_RESIDENT_ROWS")) return std::max(1, std::atoi(e));  // A/B experiments
   if (n < kResidentRowsMinN) return 1;
-  // round 3 sweep (gpurun_out/b, same box): 8 rows (two bucket sets) win at
-  // 2^19 (0.738 vs 0.759 ms) and tie at 2^20; 4 rows up to 2^21; the 2^22 table
-  // must stay near the Infinity Cache: 2 rows (4.92 ms, 8 rows 5.15)
-  if (n <= (size_t(1) << 19)) return 8;
-  return n <= (size_t(1) << 21) ? 4 : 2;
+  // round 3, after the sort changes (profiles/r03/rows_ab/, same box, 3
+  // interleaved runs): 8 rows (two bucket sets) win up to 2^20 (2^20
+  // 1.193-1.221 vs 1.224-1.273 ms; 2^19 0.738 vs 0.759), 4 rows at 2^21
+  // (2.33-2.35 vs 2.35-2.39) and 2^22 (4.73-4.75 vs 2 rows 4.80-4.98);
+  // larger sets keep 2 rows (unmeasured: the table grows past 1 GiB)
+  if (n <= (size_t(1) << 20)) return 8;
+  return n <= (size_t(1) << 22) ? 4 : 2;
 }
 // a resident MSM takes the row-table path when it starts at the first base
 // and covers at least half of the table (rows past n are zero digits)

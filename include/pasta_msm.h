@@ -148,7 +148,7 @@ int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size
  * and runs many MSMs against a window [offset, offset + n) of them.  The
  * library converts them once, at upload, to the pipeline's internal form
  * (64 B per point on the device, no per-call conversion).  From 2^18 points
- * on it also keeps [2^{256 j / rows}] P (rows = 8 up to 2^19 points, 4 up to 2^21, else 2;
+ * on it also keeps [2^{256 j / rows}] P (rows = 8 up to 2^20 points, 4 up to 2^22, else 2;
  * rows x 64 B per point): an MSM over (at least half of) the set from
  * offset 0 then runs as a row-table MSM (pm_fixed_bases_create_rows) with a
  * rows-times shorter bucket reduction and host tail; other windows run the

@@ -42,7 +42,7 @@ def main():
             ctx.set_pipeline(G, mc)
             ctx.set_timing(False)
             run()
-            reps = 5
+            reps = int(os.environ.get("REPS", "5"))
             t = time.time()
             for _ in range(reps):
                 run()
