@@ -59,6 +59,15 @@ inline int ntt_twiddles_lookup(Ctx* ctx, int curve, uint32_t logn, const uint64_
   return PM_OK;
 }
 
+// elements per block (2^kNttPlaneLog): C = 2^logC adjacent columns / rows of a
+// short sub-transform share one block so that global accesses move C x 32
+// contiguous bytes (A/B: PM_NTT_PLANE_LOG=10 measured within noise,
+// profiles/r03/ntt_f29/ab.jsonl)
+#ifndef PM_NTT_PLANE_LOG
+#define PM_NTT_PLANE_LOG 11
+#endif
+constexpr int kNttPlaneLog = PM_NTT_PLANE_LOG;
+
 // passes over HBM: one up to 2^7 (one LDS transform), two up to 2^22 (four
 // steps, factors <= 2^11), three above (factors <= 2^10: at 2^23 / 2^24 the
 // two-pass form's 2^12-point transforms need 128 KiB of LDS, one block per
@@ -101,38 +110,38 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
   uint32_t* data = (uint32_t*)d_data;
   if (logn <= (uint32_t)kNttOnePassLog) {
     // one sub-transform in LDS (pass A with a single column, in place)
-    const size_t lds = n * 32;
-    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<1, kNttThreads, lds, st>>>(data, data, (int)logn, (int)logn, 0, tw)));
+    const size_t lds = n * kNttLdsBytes;
+    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<1, kNttThreads, lds, st>>>(data, data, (int)logn, (int)logn, 0, tw, scale ? 0u : 1u)));
     if (scale) {
       // scaling rides on a rows pass of length 1 would be wasteful: fold it in
       // with a trivial rows pass of log2 = 0 (one element per row)
       PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> std::min<uint32_t>(logn, 8)), kNttThreads,
-                                                   ((size_t)1 << std::min<uint32_t>(logn, 8)) * 32, st>>>(
+                                                   ((size_t)1 << std::min<uint32_t>(logn, 8)) * kNttLdsBytes, st>>>(
                                      data, data, (int)logn, 0, (int)std::min<uint32_t>(logn, 8), tw, sc, 1u)));
     }
   } else if (ntt_passes(ctx, logn) == 2) {
     const int log1 = (int)(logn + 1) / 2, log2 = (int)logn - log1;
-    const int logC = std::max(0, std::min(2, 11 - log1)), logR = std::max(0, std::min(2, 11 - log2));
+    const int logC = std::max(0, std::min(2, kNttPlaneLog - log1)), logR = std::max(0, std::min(2, kNttPlaneLog - log2));
     if ((rc = ctx->ntt_scratch.ensure(n * 32))) return rc;
     uint32_t* tmp = (uint32_t*)ctx->ntt_scratch.p;
-    const size_t ldsA = ((size_t)1 << (log1 + logC)) * 32, ldsB = ((size_t)1 << (log2 + logR)) * 32;
+    const size_t ldsA = ((size_t)1 << (log1 + logC)) * kNttLdsBytes, ldsB = ((size_t)1 << (log2 + logR)) * kNttLdsBytes;
     PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)((size_t)1 << (log2 - logC)), kNttThreads, ldsA, st>>>(
-                                   data, tmp, (int)logn, log1, logC, tw)));
+                                   data, tmp, (int)logn, log1, logC, tw, 0u)));
     PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)((size_t)1 << (log1 - logR)), kNttThreads, ldsB, st>>>(
                                    tmp, data, (int)logn, log2, logR, tw, sc, scale ? 1u : 0u)));
   } else {
     // three passes (k_ntt_kernels.hpp: k_ntt_mid), factors of at most 2^10,
     // through two scratch buffers (the middle pass permutes rows)
     const int log1 = (int)(logn + 2) / 3, loga = ((int)logn - log1 + 1) / 2, logb = (int)logn - log1 - loga;
-    const int logC = std::max(0, std::min(2, 11 - log1)), logM = std::max(0, std::min(2, 11 - loga)),
-              logR = std::max(0, std::min(2, 11 - logb));
+    const int logC = std::max(0, std::min(2, kNttPlaneLog - log1)), logM = std::max(0, std::min(2, kNttPlaneLog - loga)),
+              logR = std::max(0, std::min(2, kNttPlaneLog - logb));
     if ((rc = ctx->ntt_scratch.ensure(n * 32)) || (rc = ctx->ntt_scratch2.ensure(n * 32))) return rc;
     uint32_t* tmp = (uint32_t*)ctx->ntt_scratch.p;
     uint32_t* tmp2 = (uint32_t*)ctx->ntt_scratch2.p;
-    const size_t ldsA = ((size_t)1 << (log1 + logC)) * 32, ldsM = ((size_t)1 << (loga + logM)) * 32,
-                 ldsB = ((size_t)1 << (logb + logR)) * 32;
+    const size_t ldsA = ((size_t)1 << (log1 + logC)) * kNttLdsBytes, ldsM = ((size_t)1 << (loga + logM)) * kNttLdsBytes,
+                 ldsB = ((size_t)1 << (logb + logR)) * kNttLdsBytes;
     PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)(n >> (log1 + logC)), kNttThreads, ldsA, st>>>(
-                                   data, tmp, (int)logn, log1, logC, tw)));
+                                   data, tmp, (int)logn, log1, logC, tw, 0u)));
     PM_LAUNCH(ctx, "ntt_mid", (k_ntt_mid<Fs><<<(unsigned)(n >> (loga + logM)), kNttThreads, ldsM, st>>>(
                                   tmp, tmp2, (int)logn, log1, loga, logM, tw)));
     PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> (logb + logR)), kNttThreads, ldsB, st>>>(

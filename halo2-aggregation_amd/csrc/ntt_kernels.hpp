@@ -11,11 +11,11 @@
 //   pass B (k_ntt_rows): for every row k1, the n2-point NTT over the contiguous
 //     row (root omega^{n1}), stored at out[k1 + n1 * k2]  (natural order),
 //     optionally times a scale (ifft: the 1/n divisor).
-// Each sub-transform runs in LDS (structure of arrays: 8 limb planes, so
-// lane-consecutive elements hit consecutive banks) as a radix-2 DIT on
-// bit-reversed positions.  A workgroup takes C adjacent columns (pass A) or
+// Each sub-transform runs in LDS (structure of arrays: 9 limb planes of the
+// radix-2^29 form, so lane-consecutive elements hit consecutive banks) as a
+// radix-4 DIT on bit-reversed positions.  A workgroup takes C adjacent columns (pass A) or
 // rows (pass B) so its global loads / stores move C x 32 contiguous bytes.
-// All roots come from one table tw[i] = omega^i, i < n/2, built once per
+// All roots come from one table tw[i] = omega^i (R = 2^261 form), i < n/2, built once per
 // (field, omega, log_n) and cached in the context (omega^{n/2} = -1 covers
 // the upper half).
 #pragma once
@@ -27,7 +27,8 @@ namespace pm {
 #define PM_NTT_THREADS 256
 #endif
 constexpr int kNttThreads = PM_NTT_THREADS;
-constexpr int kNttMaxLogL = 12;  // longest sub-transform (2^12 x 32 B = 128 KiB of LDS)
+constexpr int kNttMaxLogL = 12;  // longest sub-transform (2^12 x 36 B = 144 KiB of LDS)
+constexpr size_t kNttLdsBytes = 36;  // LDS bytes per element (9 limb planes)
 
 struct FeArg {
   uint32_t l[8];
@@ -41,7 +42,27 @@ __device__ __forceinline__ Fe<Fs> fe_of(const FeArg& a) {
   return r;
 }
 
-// tw[i] = omega^i for i < half (one square-and-multiply per entry, built once)
+// Arithmetic (round 3): the radix-2^29 lazy Montgomery form of the MSM
+// (fp29.hpp) instead of 8 x 32-bit limbs.  A 32-bit-limb product needs a
+// v_mad_u64_u32 plus a carry add per limb pair (~300 VALU instructions for
+// BN254 Fr); the 29-bit columns chain their multiply-adds in one 64-bit
+// accumulator (~210), and additions are limb-wise with one carry pass per
+// radix-4 output instead of a borrow chain and a select per add / sub.
+// The DATA keeps the caller's R = 2^256 Montgomery meaning, only unpacked
+// into 29-bit limbs; the TWIDDLES are stored in the R = 2^261 form, so the
+// product x 2^256 * w 2^261 * 2^-261 = x w 2^256 stays in the data's form and
+// no per-element conversion is needed.  Bounds (p < 2^254 for Pasta, ~2^253.6
+// for BN254 Fr, so R / p >= 128): LDS holds Norm values < 3p; a twiddle is
+// canonical (< p) or its negation 2p - w (< 2p), both Norm; f29_mul_c of a
+// value < 5p with limbs < 2^30 by a Norm twiddle < 2p is Norm, < 2p
+// (tests/test_fp29_asm.py::test_ntt_operand_bounds runs these operand shapes
+// through the interpreter with its overflow checks); each radix-4 output
+// (< 7p, limbs < 2^32 - 8) is normalised and reduced to < 3p.  Between
+// passes elements are stored packed but not canonical (< 3p < 2^256); the
+// last pass canonicalises.
+
+// tw[i] = omega^i 2^261 mod p (canonical, packed) for i < half: one
+// square-and-multiply per entry in the R256 form, then the R261 conversion
 template <class Fs>
 __global__ void __launch_bounds__(256) k_ntt_twiddles(FeArg omega, uint32_t half, uint32_t* __restrict__ tw) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -51,72 +72,71 @@ __global__ void __launch_bounds__(256) k_ntt_twiddles(FeArg omega, uint32_t half
     if (e & 1) r = fe_mul<Fs>(r, b);
     b = fe_sqr<Fs>(b);
   }
-  store_fe4<Fs>(reinterpret_cast<uint4*>(tw + 8ull * i), r);
+  Fe<Fs> o;
+  f29_pack<Fs>(f29_canon<Fs>(f29_from_r256<Fs>(r.l)), o.l);
+  store_fe4<Fs>(reinterpret_cast<uint4*>(tw + 8ull * i), o);
 }
 
 __device__ __forceinline__ uint32_t ntt_brev(uint32_t x, int bits) { return bits ? __brev(x) >> (32 - bits) : 0u; }
 
+// packed element (8 x u32, value < 2^256) <-> Norm 29-bit limbs
 template <class Fs>
-__device__ __forceinline__ Fe<Fs> lds_ld(const uint32_t* sm, uint32_t plane, uint32_t idx) {
-  Fe<Fs> r;
+__device__ __forceinline__ F29<Fs> g_ld29(const uint32_t* __restrict__ g, size_t idx) {
+  const Fe<Fs> v = load_fe4<Fs>(reinterpret_cast<const uint4*>(g + 8ull * idx));
+  return f29_unpack<Fs>(v.l);
+}
+template <class Fs>
+__device__ __forceinline__ void g_st29(uint32_t* g, size_t idx, const F29<Fs>& v) {  // v Norm, < 2^256
+  Fe<Fs> w;
+  f29_pack<Fs>(v, w.l);
+  store_fe4<Fs>(reinterpret_cast<uint4*>(g + 8ull * idx), w);
+}
+
+// LDS image: 9 limb planes of `plane` words (lane-consecutive elements hit
+// consecutive banks)
+template <class Fs>
+__device__ __forceinline__ F29<Fs> lds_ld(const uint32_t* sm, uint32_t plane, uint32_t idx) {
+  F29<Fs> r;
 #pragma unroll
-  for (int k = 0; k < 8; k++) r.l[k] = sm[k * plane + idx];
+  for (int k = 0; k < 9; k++) r.l[k] = sm[k * plane + idx];
   return r;
 }
 template <class Fs>
-__device__ __forceinline__ void lds_st(uint32_t* sm, uint32_t plane, uint32_t idx, const Fe<Fs>& v) {
+__device__ __forceinline__ void lds_st(uint32_t* sm, uint32_t plane, uint32_t idx, const F29<Fs>& v) {
 #pragma unroll
-  for (int k = 0; k < 8; k++) sm[k * plane + idx] = v.l[k];
+  for (int k = 0; k < 9; k++) sm[k * plane + idx] = v.l[k];
 }
 
-// omega^e for e < n from the half table (omega^{n/2} = -1)
+// twiddle omega^e (R261, Norm): e < half from the table, else its negation
+// (omega^{n/2} = -1) as 2p - w
 template <class Fs>
-__device__ __forceinline__ Fe<Fs> tw_full(const uint32_t* __restrict__ tw, uint32_t e, uint32_t half) {
-  if (e < half) return load_fe4<Fs>(reinterpret_cast<const uint4*>(tw + 8ull * e));
-  return fe_neg<Fs>(load_fe4<Fs>(reinterpret_cast<const uint4*>(tw + 8ull * (e - half))));
+__device__ __forceinline__ F29<Fs> tw_half(const uint32_t* __restrict__ tw, size_t e) {
+  return g_ld29<Fs>(tw, e);
 }
-
-// In-LDS radix-2 DIT over C interleaved transforms of length L = 2^logL
-// (layout [position][c], positions already bit-reversed).  Root of unity of
-// the sub-transform: omega^{tstride}, looked up as tw[m * tstride].
 template <class Fs>
-__device__ __forceinline__ void lds_ntt(uint32_t* sm, int logL, int logC, uint32_t tstride,
-                                        const uint32_t* __restrict__ tw) {
-  const uint32_t plane = 1u << (logL + logC);
-  const uint32_t nbf = plane >> 1;  // butterflies per stage
-  const uint32_t cmask = (1u << logC) - 1;
-  for (int t = 0; t < logL; t++) {
-    const uint32_t h = 1u << t;
-    for (uint32_t b = threadIdx.x; b < nbf; b += kNttThreads) {
-      const uint32_t c = b & cmask, bb = b >> logC;
-      const uint32_t lo = bb & (h - 1);
-      const uint32_t j = ((bb >> t) << (t + 1)) | lo;
-      const uint32_t ia = (j << logC) | c, ib = ((j + h) << logC) | c;
-      const Fe<Fs> u = lds_ld<Fs>(sm, plane, ia);
-      Fe<Fs> v = lds_ld<Fs>(sm, plane, ib);
-      if (t > 0) {  // stage 0 twiddle is 1
-        const Fe<Fs> w =
-            load_fe4<Fs>(reinterpret_cast<const uint4*>(tw + 8ull * ((size_t)(lo << (logL - 1 - t)) * tstride)));
-        v = fe_mul<Fs>(v, w);
-      }
-      lds_st<Fs>(sm, plane, ia, fe_add<Fs>(u, v));
-      lds_st<Fs>(sm, plane, ib, fe_sub<Fs>(u, v));
-    }
-    __syncthreads();
-  }
+__device__ __forceinline__ F29<Fs> tw_full(const uint32_t* __restrict__ tw, uint32_t e, uint32_t half) {
+  if (e < half) return tw_half<Fs>(tw, e);
+  return f29_norm<Fs>(f29_sub<Fs>(f29_zero<Fs>(), tw_half<Fs>(tw, e - half), F29Consts<Fs>::K2));
 }
 
-// The same transform with two stages per LDS round trip (radix-4 units on
-// positions j, j + h, j + 2h, j + 3h, h = 2^t): stage t with the twiddle
-// W_{2h}^lo on both pairs, then stage t + 1 with W_{4h}^lo and W_{4h}^{lo+h}.
-// Same products as two radix-2 stages, half the LDS traffic and barriers.
-// An odd logL starts with one radix-2 stage (twiddle 1).
-#ifndef PM_NTT_RADIX4
-#define PM_NTT_RADIX4 1
-#endif
+// lazy sum / difference -> Norm, < 3p
+template <class Fs>
+__device__ __forceinline__ F29<Fs> f29_nr(const F29<Fs>& a) {
+  return f29_reduce3<Fs>(f29_norm<Fs>(a));
+}
+
+// In-LDS DIT over C interleaved transforms of length L = 2^logL (layout
+// [position][c], positions already bit-reversed), two stages per LDS round
+// trip: radix-4 units on positions j, j + h, j + 2h, j + 3h (h = 2^t), stage
+// t with the twiddle W_{2h}^lo on both pairs, then stage t + 1 with W_{4h}^lo
+// and W_{4h}^{lo+h}.  An odd logL starts with one radix-2 stage (twiddle 1).
+// Root of the sub-transform: omega^{tstride}, looked up as tw[m * tstride].
+// (Round 2 measured the radix-4 rounds against radix-2 stages: half the LDS
+// traffic and barriers, 2^20 0.221 -> 0.205 ms; the radix-2 form is retired.)
 template <class Fs>
 __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint32_t tstride,
                                          const uint32_t* __restrict__ tw) {
+  using K = F29Consts<Fs>;
   const uint32_t plane = 1u << (logL + logC);
   const uint32_t cmask = (1u << logC) - 1;
   int t = 0;
@@ -124,9 +144,9 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
     for (uint32_t b = threadIdx.x; b < (plane >> 1); b += kNttThreads) {
       const uint32_t c = b & cmask, j = (b >> logC) << 1;
       const uint32_t ia = (j << logC) | c, ib = ((j + 1) << logC) | c;
-      const Fe<Fs> u = lds_ld<Fs>(sm, plane, ia), v = lds_ld<Fs>(sm, plane, ib);
-      lds_st<Fs>(sm, plane, ia, fe_add<Fs>(u, v));
-      lds_st<Fs>(sm, plane, ib, fe_sub<Fs>(u, v));
+      const F29<Fs> u = lds_ld<Fs>(sm, plane, ia), v = lds_ld<Fs>(sm, plane, ib);
+      lds_st<Fs>(sm, plane, ia, f29_nr<Fs>(f29_add<Fs>(u, v)));
+      lds_st<Fs>(sm, plane, ib, f29_nr<Fs>(f29_sub<Fs>(u, v, K::K2)));
     }
     __syncthreads();
     t = 1;
@@ -139,25 +159,24 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
       const uint32_t j = ((bb >> t) << (t + 2)) | lo;
       const uint32_t i0 = (j << logC) | c, i1 = ((j + h) << logC) | c, i2 = ((j + 2 * h) << logC) | c,
                      i3 = ((j + 3 * h) << logC) | c;
-      Fe<Fs> x0 = lds_ld<Fs>(sm, plane, i0), x1 = lds_ld<Fs>(sm, plane, i1);
-      Fe<Fs> x2 = lds_ld<Fs>(sm, plane, i2), x3 = lds_ld<Fs>(sm, plane, i3);
+      F29<Fs> x0 = lds_ld<Fs>(sm, plane, i0), x1 = lds_ld<Fs>(sm, plane, i1);
+      F29<Fs> x2 = lds_ld<Fs>(sm, plane, i2), x3 = lds_ld<Fs>(sm, plane, i3);
       if (t > 0) {
-        const Fe<Fs> w1 =
-            load_fe4<Fs>(reinterpret_cast<const uint4*>(tw + 8ull * ((size_t)(lo << (logL - 1 - t)) * tstride)));
-        x1 = fe_mul<Fs>(x1, w1);
-        x3 = fe_mul<Fs>(x3, w1);
+        const F29<Fs> w1 = tw_half<Fs>(tw, (size_t)(lo << (logL - 1 - t)) * tstride);
+        x1 = f29_mul_c<Fs>(x1, w1);  // < 2p
+        x3 = f29_mul_c<Fs>(x3, w1);
       }
-      const Fe<Fs> y0 = fe_add<Fs>(x0, x1), y1 = fe_sub<Fs>(x0, x1);
-      const Fe<Fs> y2 = fe_add<Fs>(x2, x3), y3 = fe_sub<Fs>(x2, x3);
-      const Fe<Fs> w2 =
-          load_fe4<Fs>(reinterpret_cast<const uint4*>(tw + 8ull * ((size_t)(lo << (logL - 2 - t)) * tstride)));
-      const Fe<Fs> w3 = load_fe4<Fs>(
-          reinterpret_cast<const uint4*>(tw + 8ull * ((size_t)((lo + h) << (logL - 2 - t)) * tstride)));
-      const Fe<Fs> z2 = fe_mul<Fs>(y2, w2), z3 = fe_mul<Fs>(y3, w3);
-      lds_st<Fs>(sm, plane, i0, fe_add<Fs>(y0, z2));
-      lds_st<Fs>(sm, plane, i2, fe_sub<Fs>(y0, z2));
-      lds_st<Fs>(sm, plane, i1, fe_add<Fs>(y1, z3));
-      lds_st<Fs>(sm, plane, i3, fe_sub<Fs>(y1, z3));
+      // y0, y2 < 5p (limbs < 2^30); y1 < 5p, normalised for the product
+      const F29<Fs> y0 = f29_add<Fs>(x0, x1), y1 = f29_sub<Fs>(x0, x1, K::K2);
+      const F29<Fs> y2 = f29_add<Fs>(x2, x3), y3 = f29_norm<Fs>(f29_sub<Fs>(x2, x3, K::K2));
+      const F29<Fs> w2 = tw_half<Fs>(tw, (size_t)(lo << (logL - 2 - t)) * tstride);
+      const F29<Fs> w3 = tw_half<Fs>(tw, (size_t)((lo + h) << (logL - 2 - t)) * tstride);
+      const F29<Fs> z2 = f29_mul_c<Fs>(y2, w2), z3 = f29_mul_c<Fs>(y3, w3);  // < 2p
+      // outputs < 7p, limbs < 2^31 + 2^30
+      lds_st<Fs>(sm, plane, i0, f29_nr<Fs>(f29_add<Fs>(y0, z2)));
+      lds_st<Fs>(sm, plane, i2, f29_nr<Fs>(f29_sub<Fs>(y0, z2, K::K2)));
+      lds_st<Fs>(sm, plane, i1, f29_nr<Fs>(f29_add<Fs>(y1, z3)));
+      lds_st<Fs>(sm, plane, i3, f29_nr<Fs>(f29_sub<Fs>(y1, z3, K::K2)));
     }
     __syncthreads();
   }
@@ -171,11 +190,12 @@ __device__ __forceinline__ uint32_t ntt_block(uint32_t nblocks) {
   return (b % 8) * (nblocks / 8) + b / 8;
 }
 
-// pass A: C = 2^logC adjacent columns per block
+// pass A: C = 2^logC adjacent columns per block.  last != 0: this is the
+// whole transform (one pass), so the output is canonicalised.
 template <class Fs>
 __global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, uint32_t* out,  // may alias
                                                           int logn, int log1, int logC,
-                                                          const uint32_t* __restrict__ tw) {
+                                                          const uint32_t* __restrict__ tw, uint32_t last) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int log2 = logn - log1;
   const uint32_t n2 = 1u << log2, L = 1u << log1, C = 1u << logC, half = 1u << (logn - 1);
@@ -183,17 +203,16 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, ui
   const uint32_t col0 = ntt_block(n2 >> logC) << logC;
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t i1 = e >> logC, c = e & (C - 1);
-    const Fe<Fs> v = load_fe4<Fs>(reinterpret_cast<const uint4*>(in + 8ull * ((size_t)i1 * n2 + col0 + c)));
-    lds_st<Fs>(sm, plane, (ntt_brev(i1, log1) << logC) | c, v);
+    lds_st<Fs>(sm, plane, (ntt_brev(i1, log1) << logC) | c, g_ld29<Fs>(in, (size_t)i1 * n2 + col0 + c));
   }
   __syncthreads();
-  if (PM_NTT_RADIX4) lds_ntt4<Fs>(sm, log1, logC, n2, tw);  // root omega^{n2}
-  else lds_ntt<Fs>(sm, log1, logC, n2, tw);
+  lds_ntt4<Fs>(sm, log1, logC, n2, tw);  // root omega^{n2}
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t k1 = e >> logC, c = e & (C - 1), i2 = col0 + c;
-    Fe<Fs> v = lds_ld<Fs>(sm, plane, e);
-    if (log2 > 0 && i2 && k1) v = fe_mul<Fs>(v, tw_full<Fs>(tw, i2 * k1, half));  // i2 k1 < n
-    store_fe4<Fs>(reinterpret_cast<uint4*>(out + 8ull * ((size_t)k1 * n2 + i2)), v);
+    F29<Fs> v = lds_ld<Fs>(sm, plane, e);
+    if (log2 > 0 && i2 && k1) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, i2 * k1, half));  // i2 k1 < n
+    if (last) v = f29_canon<Fs>(v);
+    g_st29<Fs>(out, (size_t)k1 * n2 + i2, v);
   }
 }
 
@@ -219,21 +238,20 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_mid(const uint32_t* __restr
   const uint32_t* row = in + 8ull * ((size_t)k1 << (loga + logb));
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t ia = e >> logC, c = e & (C - 1);
-    const Fe<Fs> v = load_fe4<Fs>(reinterpret_cast<const uint4*>(row + 8ull * ((size_t)ia * nb + col0 + c)));
-    lds_st<Fs>(sm, plane, (ntt_brev(ia, loga) << logC) | c, v);
+    lds_st<Fs>(sm, plane, (ntt_brev(ia, loga) << logC) | c, g_ld29<Fs>(row, (size_t)ia * nb + col0 + c));
   }
   __syncthreads();
-  if (PM_NTT_RADIX4) lds_ntt4<Fs>(sm, loga, logC, n1 * nb, tw);  // root omega^{n1 nb}
-  else lds_ntt<Fs>(sm, loga, logC, n1 * nb, tw);
+  lds_ntt4<Fs>(sm, loga, logC, n1 * nb, tw);  // root omega^{n1 nb}
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t ka = e >> logC, c = e & (C - 1), ib = col0 + c;
-    Fe<Fs> v = lds_ld<Fs>(sm, plane, e);
-    if (ib && ka) v = fe_mul<Fs>(v, tw_full<Fs>(tw, n1 * ib * ka, half));  // n1 ib ka < n
-    store_fe4<Fs>(reinterpret_cast<uint4*>(out + 8ull * (((size_t)ka * n1 + k1) * nb + ib)), v);
+    F29<Fs> v = lds_ld<Fs>(sm, plane, e);
+    if (ib && ka) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, n1 * ib * ka, half));  // n1 ib ka < n
+    g_st29<Fs>(out, ((size_t)ka * n1 + k1) * nb + ib, v);
   }
 }
 
-// pass B: R = 2^logR adjacent rows per block; optional output scale
+// pass B: R = 2^logR adjacent rows per block; optional output scale (R256
+// form, converted once per thread); the output is canonical
 template <class Fs>
 __global__ void __launch_bounds__(kNttThreads) k_ntt_rows(const uint32_t* in, uint32_t* out,  // may alias (log2 = 0)
                                                           int logn, int log2, int logR,
@@ -246,18 +264,16 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_rows(const uint32_t* in, ui
   const uint32_t row0 = ntt_block(n1 >> logR) << logR;
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t r = e >> log2, i2 = e & (L - 1);  // row-contiguous loads
-    const Fe<Fs> v = load_fe4<Fs>(reinterpret_cast<const uint4*>(in + 8ull * ((size_t)(row0 + r) * L + i2)));
-    lds_st<Fs>(sm, plane, (ntt_brev(i2, log2) << logR) | r, v);
+    lds_st<Fs>(sm, plane, (ntt_brev(i2, log2) << logR) | r, g_ld29<Fs>(in, (size_t)(row0 + r) * L + i2));
   }
   __syncthreads();
-  if (PM_NTT_RADIX4) lds_ntt4<Fs>(sm, log2, logR, n1, tw);  // root omega^{n1}
-  else lds_ntt<Fs>(sm, log2, logR, n1, tw);
-  const Fe<Fs> sc = fe_of<Fs>(scale);
+  lds_ntt4<Fs>(sm, log2, logR, n1, tw);  // root omega^{n1}
+  const F29<Fs> sc = use_scale ? f29_from_r256<Fs>(scale.l) : f29_zero<Fs>();  // Norm, < 2p
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t r = e & (R - 1), k2 = e >> logR;  // adjacent rows -> adjacent outputs
-    Fe<Fs> v = lds_ld<Fs>(sm, plane, e);
-    if (use_scale) v = fe_mul<Fs>(v, sc);
-    store_fe4<Fs>(reinterpret_cast<uint4*>(out + 8ull * ((size_t)(row0 + r) + (size_t)n1 * k2)), v);
+    F29<Fs> v = lds_ld<Fs>(sm, plane, e);
+    if (use_scale) v = f29_mul_c<Fs>(v, sc);
+    g_st29<Fs>(out, (size_t)(row0 + r) + (size_t)n1 * k2, f29_canon<Fs>(v));
   }
 }
 

@@ -184,3 +184,89 @@ def test_column_asm_difference_of_products(field):
         assert all(0 <= l <= M29 for l in r[:8])
         assert _value(r) % p == (a * b - u * v) * rinv % p
         assert 0 <= _value(r) < 3 * p
+
+
+def _f29_consts(field):
+    src = open(os.path.join(ROOT, "halo2-aggregation_amd", "csrc", "fp29.hpp")).read()
+    body = src[src.index("struct F29Consts<%s>" % field):]
+    body = body[:body.index("\n};")]
+    k2 = [int(x, 16) for x in re.search(r"K2\[9\] = \{(.*?)\}", body).group(1).replace("u", "").split(",")]
+    qm = int(re.search(r"QMAGIC = (0x[0-9a-f]+)u", body).group(1), 16)
+    return k2, qm
+
+
+@pytest.mark.parametrize("field", ["PallasFp", "VestaFp", "Bn254Fr"])
+def test_ntt_operand_bounds(field):
+    """The NTT's radix-4 unit (csrc/ntt_kernels.hpp lds_ntt4) in the
+    radix-2^29 form: inputs Norm < 3p, twiddles canonical or negated (2p - w),
+    the lazy sums / differences (limbs < 2^30 into the products, y3
+    normalised), each output normalised and reduced to < 3p.  Every limb is
+    checked against its 32-bit register, the products run through the
+    interpreter with its column-overflow checks, and the outputs are the
+    radix-4 butterfly of the inputs mod p."""
+    p = FIELDS[field]
+    mul = _functions()[("f29_mul_a", field)]
+    K2, qmagic = _f29_consts(field)
+    P9 = _limbs(p)
+    rinv = pow(1 << 261, -1, p)
+
+    def add(a, b):
+        r = [x + y for x, y in zip(a, b)]
+        assert all(0 <= x < 2 ** 32 for x in r)
+        return r
+
+    def sub(a, b):  # a + 2p - b, limb-wise
+        r = [x + k - y for x, k, y in zip(a, K2, b)]
+        assert all(0 <= x < 2 ** 32 for x in r)
+        return r
+
+    def norm(a):
+        r, c = [0] * 9, 0
+        for i in range(8):
+            v = a[i] + c
+            assert v < 2 ** 32 - 8
+            r[i], c = v & M29, v >> 29
+        r[8] = a[8] + c
+        assert r[8] < 2 ** 32
+        return r
+
+    def reduce3(a):
+        assert _value(a) < 16 * p
+        q = (a[8] * qmagic) >> 40
+        r, c = [0] * 9, 0
+        for i in range(9):
+            v = a[i] - q * P9[i] + c
+            r[i] = v & M29 if i < 8 else v % (1 << 32)
+            c = v >> 29
+        assert 0 <= _value(r) < 3 * p and all(x <= M29 for x in r[:8])
+        return r
+
+    def mmul(a, w):
+        r = _run(mul, a, w)
+        assert all(x <= M29 for x in r[:8]) and _value(r) < 2 * p
+        assert _value(r) % p == _value(a) * _value(w) * rinv % p
+        return r
+
+    def twiddle(v, neg):
+        w = _limbs(v)
+        return norm(sub([0] * 9, w)) if neg else w
+
+    rng = random.Random(0x7E7E + len(field))
+    edge = [0, 1, p - 1, 2 * p, 3 * p - 1]
+    for t in range(40):
+        xs = [_limbs(edge[(t + k) % len(edge)] if t < 10 else rng.randrange(3 * p)) for k in range(4)]
+        ws = [twiddle(p - 1 if t < 10 else rng.randrange(1, p), (t >> k) & 1) for k in range(3)]
+        x0, x1, x2, x3 = xs
+        x1, x3 = mmul(x1, ws[0]), mmul(x3, ws[0])
+        y0, y1 = add(x0, x1), sub(x0, x1)
+        y2, y3 = add(x2, x3), norm(sub(x2, x3))
+        assert all(x < 2 ** 30 for x in y2)
+        z2, z3 = mmul(y2, ws[1]), mmul(y3, ws[2])
+        outs = [reduce3(norm(add(y0, z2))), reduce3(norm(add(y1, z3))), reduce3(norm(sub(y0, z2))),
+                reduce3(norm(sub(y1, z3)))]
+        X = [_value(v) for v in xs]
+        W = [_value(w) * rinv % p for w in ws]
+        a1, a3 = X[1] * W[0] % p, X[3] * W[0] % p
+        b0, b1, b2, b3 = X[0] + a1, X[0] - a1, X[2] + a3, X[2] - a3
+        want = [b0 + b2 * W[1], b1 + b3 * W[2], b0 - b2 * W[1], b1 - b3 * W[2]]
+        assert [_value(o) % p for o in outs] == [v % p for v in want]
