@@ -121,7 +121,8 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
     }
   } else if (ntt_passes(ctx, logn) == 2) {
     const int log1 = (int)(logn + 1) / 2, log2 = (int)logn - log1;
-    const int logC = std::max(0, std::min(2, kNttPlaneLog - log1)), logR = std::max(0, std::min(2, kNttPlaneLog - log2));
+    const int mc = ctx->ntt_maxlogc;
+    const int logC = std::max(0, std::min(mc, kNttPlaneLog - log1)), logR = std::max(0, std::min(mc, kNttPlaneLog - log2));
     if ((rc = ctx->ntt_scratch.ensure(n * 32))) return rc;
     uint32_t* tmp = (uint32_t*)ctx->ntt_scratch.p;
     const size_t ldsA = ((size_t)1 << (log1 + logC)) * kNttLdsBytes, ldsB = ((size_t)1 << (log2 + logR)) * kNttLdsBytes;
@@ -132,9 +133,12 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
   } else {
     // three passes (k_ntt_kernels.hpp: k_ntt_mid), factors of at most 2^10,
     // through two scratch buffers (the middle pass permutes rows)
-    const int log1 = (int)(logn + 2) / 3, loga = ((int)logn - log1 + 1) / 2, logb = (int)logn - log1 - loga;
-    const int logC = std::max(0, std::min(2, kNttPlaneLog - log1)), logM = std::max(0, std::min(2, kNttPlaneLog - loga)),
-              logR = std::max(0, std::min(2, kNttPlaneLog - logb));
+    int log1 = (int)(logn + 2) / 3;
+    if (ctx->ntt_log1 > 0) log1 = std::max((int)logn - 2 * kNttMaxLogL, std::min(std::min(kNttMaxLogL, ctx->ntt_log1), (int)logn - 2));
+    const int loga = ((int)logn - log1 + 1) / 2, logb = (int)logn - log1 - loga;
+    const int mc = ctx->ntt_maxlogc;
+    const int logC = std::max(0, std::min(mc, kNttPlaneLog - log1)), logM = std::max(0, std::min(mc, kNttPlaneLog - loga)),
+              logR = std::max(0, std::min(mc, kNttPlaneLog - logb));
     if ((rc = ctx->ntt_scratch.ensure(n * 32)) || (rc = ctx->ntt_scratch2.ensure(n * 32))) return rc;
     uint32_t* tmp = (uint32_t*)ctx->ntt_scratch.p;
     uint32_t* tmp2 = (uint32_t*)ctx->ntt_scratch2.p;

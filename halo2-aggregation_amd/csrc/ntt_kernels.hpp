@@ -92,19 +92,29 @@ __device__ __forceinline__ void g_st29(uint32_t* g, size_t idx, const F29<Fs>& v
   store_fe4<Fs>(reinterpret_cast<uint4*>(g + 8ull * idx), w);
 }
 
-// LDS image: 9 limb planes of `plane` words (lane-consecutive elements hit
-// consecutive banks)
+// LDS image: 9 limb planes of `plane` words.  Logical position idx sits at
+// word lds_swz(idx) of each plane: bits 0-5 XORed with bits 2-7 and 8-13.
+// Unswizzled, the bit-reversed scatter of the load phase put a wave's 64
+// stores into 1-2 banks (32-way conflicts) and the short-stride radix-4
+// rounds 2-4-way (rocprofv3: SQ_LDS_BANK_CONFLICT 78 % of SQ_LDS_IDX_ACTIVE
+// in k_ntt_rows at 2^20, profiles/r03/ntt_f29/stall_*); a bank model of every
+// access pattern of lds_ntt4 and the load / store phases picked this swizzle
+// (conflict cycles / 9.7).  The map is upper triangular on the bits, so it
+// permutes [0, 2^m) for every plane size 2^m.
+__device__ __forceinline__ uint32_t lds_swz(uint32_t i) { return i ^ (((i >> 2) ^ (i >> 8)) & 63u); }
 template <class Fs>
 __device__ __forceinline__ F29<Fs> lds_ld(const uint32_t* sm, uint32_t plane, uint32_t idx) {
+  const uint32_t s = lds_swz(idx);
   F29<Fs> r;
 #pragma unroll
-  for (int k = 0; k < 9; k++) r.l[k] = sm[k * plane + idx];
+  for (int k = 0; k < 9; k++) r.l[k] = sm[k * plane + s];
   return r;
 }
 template <class Fs>
 __device__ __forceinline__ void lds_st(uint32_t* sm, uint32_t plane, uint32_t idx, const F29<Fs>& v) {
+  const uint32_t s = lds_swz(idx);
 #pragma unroll
-  for (int k = 0; k < 9; k++) sm[k * plane + idx] = v.l[k];
+  for (int k = 0; k < 9; k++) sm[k * plane + s] = v.l[k];
 }
 
 // twiddle omega^e (R261, Norm): e < half from the table, else its negation

@@ -183,6 +183,8 @@ struct pm_ctx {
   bool spin_wait = false;   // host waits poll their event (PM_SPIN_WAIT=1, A/B; within noise, not default)
   bool terms_copy = false;  // MSM host terms through a device buffer + D2H copy (PM_TERMS_COPY=1, A/B)
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
+  int ntt_log1 = 0;    // three-pass first factor, 0 = auto (A/B: PM_NTT_LOG1 env)
+  int ntt_maxlogc = 2; // most columns / rows per block, log2 (A/B: PM_NTT_MAXLOGC env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)
