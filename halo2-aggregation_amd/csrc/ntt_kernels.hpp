@@ -57,7 +57,9 @@ __device__ __forceinline__ Fe<Fs> fe_of(const FeArg& a) {
 // value < 5p with limbs < 2^30 by a Norm twiddle < 2p is Norm, < 2p
 // (tests/test_fp29_asm.py::test_ntt_operand_bounds runs these operand shapes
 // through the interpreter with its overflow checks); each radix-4 output
-// (< 7p, limbs < 2^32 - 8) is normalised and reduced to < 3p.  Between
+// (< 11p, limbs < 2^32 - 8) is normalised and reduced to < 3p.  A difference
+// adds 2p when its subtrahend is a product (< 2p) and 6p when it is an
+// unmultiplied input (< 3p, the twiddle-1 stage 0), so it never goes negative.  Between
 // passes elements are stored packed but not canonical (< 3p < 2^256); the
 // last pass canonicalises.
 
@@ -150,13 +152,13 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
   const uint32_t plane = 1u << (logL + logC);
   const uint32_t cmask = (1u << logC) - 1;
   int t = 0;
-  if (logL & 1) {  // stage 0: twiddle 1
+  if (logL & 1) {  // stage 0: twiddle 1; v < 3p unmultiplied, so u - v + 6p (< 9p)
     for (uint32_t b = threadIdx.x; b < (plane >> 1); b += kNttThreads) {
       const uint32_t c = b & cmask, j = (b >> logC) << 1;
       const uint32_t ia = (j << logC) | c, ib = ((j + 1) << logC) | c;
       const F29<Fs> u = lds_ld<Fs>(sm, plane, ia), v = lds_ld<Fs>(sm, plane, ib);
       lds_st<Fs>(sm, plane, ia, f29_nr<Fs>(f29_add<Fs>(u, v)));
-      lds_st<Fs>(sm, plane, ib, f29_nr<Fs>(f29_sub<Fs>(u, v, K::K2)));
+      lds_st<Fs>(sm, plane, ib, f29_nr<Fs>(f29_sub<Fs>(u, v, K::K6)));
     }
     __syncthreads();
     t = 1;
@@ -171,18 +173,26 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
                      i3 = ((j + 3 * h) << logC) | c;
       F29<Fs> x0 = lds_ld<Fs>(sm, plane, i0), x1 = lds_ld<Fs>(sm, plane, i1);
       F29<Fs> x2 = lds_ld<Fs>(sm, plane, i2), x3 = lds_ld<Fs>(sm, plane, i3);
+      F29<Fs> y0, y1, y2, y3;
       if (t > 0) {
         const F29<Fs> w1 = tw_half<Fs>(tw, (size_t)(lo << (logL - 1 - t)) * tstride);
         x1 = f29_mul_c<Fs>(x1, w1);  // < 2p
         x3 = f29_mul_c<Fs>(x3, w1);
+        // y0, y2 < 5p (limbs < 2^30); y1, y3 < 5p, y3 normalised for the product
+        y1 = f29_sub<Fs>(x0, x1, K::K2);
+        y3 = f29_norm<Fs>(f29_sub<Fs>(x2, x3, K::K2));
+      } else {
+        // stage 0 twiddle 1: x1, x3 < 3p unmultiplied, so + 6p (< 9p; a + 2p - b
+        // would go negative for b > a + 2p)
+        y1 = f29_sub<Fs>(x0, x1, K::K6);
+        y3 = f29_norm<Fs>(f29_sub<Fs>(x2, x3, K::K6));
       }
-      // y0, y2 < 5p (limbs < 2^30); y1 < 5p, normalised for the product
-      const F29<Fs> y0 = f29_add<Fs>(x0, x1), y1 = f29_sub<Fs>(x0, x1, K::K2);
-      const F29<Fs> y2 = f29_add<Fs>(x2, x3), y3 = f29_norm<Fs>(f29_sub<Fs>(x2, x3, K::K2));
+      y0 = f29_add<Fs>(x0, x1);
+      y2 = f29_add<Fs>(x2, x3);
       const F29<Fs> w2 = tw_half<Fs>(tw, (size_t)(lo << (logL - 2 - t)) * tstride);
       const F29<Fs> w3 = tw_half<Fs>(tw, (size_t)((lo + h) << (logL - 2 - t)) * tstride);
       const F29<Fs> z2 = f29_mul_c<Fs>(y2, w2), z3 = f29_mul_c<Fs>(y3, w3);  // < 2p
-      // outputs < 7p, limbs < 2^31 + 2^30
+      // outputs < 11p, limbs < 2^31 + 2^30
       lds_st<Fs>(sm, plane, i0, f29_nr<Fs>(f29_add<Fs>(y0, z2)));
       lds_st<Fs>(sm, plane, i2, f29_nr<Fs>(f29_sub<Fs>(y0, z2, K::K2)));
       lds_st<Fs>(sm, plane, i1, f29_nr<Fs>(f29_add<Fs>(y1, z3)));

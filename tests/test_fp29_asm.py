@@ -190,9 +190,10 @@ def _f29_consts(field):
     src = open(os.path.join(ROOT, "halo2-aggregation_amd", "csrc", "fp29.hpp")).read()
     body = src[src.index("struct F29Consts<%s>" % field):]
     body = body[:body.index("\n};")]
-    k2 = [int(x, 16) for x in re.search(r"K2\[9\] = \{(.*?)\}", body).group(1).replace("u", "").split(",")]
+    ks = [[int(x, 16) for x in re.search(r"%s\[9\] = \{(.*?)\}" % n, body).group(1).replace("u", "").split(",")]
+          for n in ("K2", "K6")]
     qm = int(re.search(r"QMAGIC = (0x[0-9a-f]+)u", body).group(1), 16)
-    return k2, qm
+    return ks[0], ks[1], qm
 
 
 @pytest.mark.parametrize("field", ["PallasFp", "VestaFp", "Bn254Fr"])
@@ -206,7 +207,7 @@ def test_ntt_operand_bounds(field):
     radix-4 butterfly of the inputs mod p."""
     p = FIELDS[field]
     mul = _functions()[("f29_mul_a", field)]
-    K2, qmagic = _f29_consts(field)
+    K2, K6, qmagic = _f29_consts(field)
     P9 = _limbs(p)
     rinv = pow(1 << 261, -1, p)
 
@@ -215,9 +216,10 @@ def test_ntt_operand_bounds(field):
         assert all(0 <= x < 2 ** 32 for x in r)
         return r
 
-    def sub(a, b):  # a + 2p - b, limb-wise
-        r = [x + k - y for x, k, y in zip(a, K2, b)]
+    def sub(a, b, K=K2):  # a + K - b, limb-wise (K = 2p or 6p)
+        r = [x + k - y for x, k, y in zip(a, K, b)]
         assert all(0 <= x < 2 ** 32 for x in r)
+        assert _value(r) == _value(a) + (2 if K is K2 else 6) * p - _value(b) >= 0
         return r
 
     def norm(a):
@@ -253,13 +255,21 @@ def test_ntt_operand_bounds(field):
 
     rng = random.Random(0x7E7E + len(field))
     edge = [0, 1, p - 1, 2 * p, 3 * p - 1]
-    for t in range(40):
-        xs = [_limbs(edge[(t + k) % len(edge)] if t < 10 else rng.randrange(3 * p)) for k in range(4)]
-        ws = [twiddle(p - 1 if t < 10 else rng.randrange(1, p), (t >> k) & 1) for k in range(3)]
+    one = [x % (1 << 32) for x in _limbs((1 << 261) % p)]  # R261 one: W = 1
+    for t in range(80):
+        first = t % 2 == 1  # stage 0 of the sub-transform: twiddle 1, x1 / x3 unmultiplied
+        xs = [_limbs(edge[(t // 2 + k) % len(edge)] if t < 20 else rng.randrange(3 * p)) for k in range(4)]
+        if t < 20 and first:
+            xs[0], xs[2] = _limbs(0), _limbs(1)  # x1 > x0 + 2p: the case a + 2p - b would break
+        ws = [twiddle(p - 1 if t < 20 else rng.randrange(1, p), (t >> k) & 1) for k in range(3)]
         x0, x1, x2, x3 = xs
-        x1, x3 = mmul(x1, ws[0]), mmul(x3, ws[0])
-        y0, y1 = add(x0, x1), sub(x0, x1)
-        y2, y3 = add(x2, x3), norm(sub(x2, x3))
+        if first:
+            ws[0] = one
+            y1, y3 = sub(x0, x1, K6), norm(sub(x2, x3, K6))
+        else:
+            x1, x3 = mmul(x1, ws[0]), mmul(x3, ws[0])
+            y1, y3 = sub(x0, x1), norm(sub(x2, x3))
+        y0, y2 = add(x0, x1), add(x2, x3)
         assert all(x < 2 ** 30 for x in y2)
         z2, z3 = mmul(y2, ws[1]), mmul(y3, ws[2])
         outs = [reduce3(norm(add(y0, z2))), reduce3(norm(add(y1, z3))), reduce3(norm(sub(y0, z2))),
@@ -270,3 +280,7 @@ def test_ntt_operand_bounds(field):
         b0, b1, b2, b3 = X[0] + a1, X[0] - a1, X[2] + a3, X[2] - a3
         want = [b0 + b2 * W[1], b1 + b3 * W[2], b0 - b2 * W[1], b1 - b3 * W[2]]
         assert [_value(o) % p for o in outs] == [v % p for v in want]
+        # the radix-2 stage 0 of an odd-length sub-transform: u + v, u - v + 6p
+        u, v = xs[0], xs[1]
+        o = [reduce3(norm(add(u, v))), reduce3(norm(sub(u, v, K6)))]
+        assert [_value(x) % p for x in o] == [(X[0] + X[1]) % p, (X[0] - X[1]) % p]
