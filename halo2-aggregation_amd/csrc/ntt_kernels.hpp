@@ -147,12 +147,11 @@ __device__ __forceinline__ F29<Fs> f29_nr(const F29<Fs>& a) {
 // traffic and barriers, 2^20 0.221 -> 0.205 ms; the radix-2 form is retired.)
 template <class Fs>
 __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint32_t tstride,
-                                         const uint32_t* __restrict__ tw) {
+                                         const uint32_t* __restrict__ tw, int t = 0) {
   using K = F29Consts<Fs>;
   const uint32_t plane = 1u << (logL + logC);
   const uint32_t cmask = (1u << logC) - 1;
-  int t = 0;
-  if (logL & 1) {  // stage 0: twiddle 1; v < 3p unmultiplied, so u - v + 6p (< 9p)
+  if (t == 0 && (logL & 1)) {  // stage 0: twiddle 1; v < 3p unmultiplied, so u - v + 6p (< 9p)
     for (uint32_t b = threadIdx.x; b < (plane >> 1); b += kNttThreads) {
       const uint32_t c = b & cmask, j = (b >> logC) << 1;
       const uint32_t ia = (j << logC) | c, ib = ((j + 1) << logC) | c;
@@ -202,6 +201,53 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
   }
 }
 
+// Load phase fused with the first round (saves one LDS round trip and
+// barrier per pass, and the twiddle-1 product of the first radix-4 round):
+// src(i, c) returns input i (natural order, < L) of transform c.  Position
+// 2m / 2m + 1 of the bit-reversed layout holds inputs brev(m) and brev(m) +
+// L/2 (odd logL: the radix-2 stage 0 in registers); positions 4m + q hold
+// brev(m) + {0, L/2, L/4, 3L/4}[q] (even logL: the t = 0 radix-4 unit, W_2 =
+// W_4^0 = 1, W_4^1 = omega^{tstride L/4}).  kfast: lanes walk m fastest (the
+// rows pass: consecutive inputs are contiguous in memory), else c fastest.
+// Returns the stage lds_ntt4 continues from.
+template <class Fs, class Src>
+__device__ __forceinline__ int ntt_load_first(uint32_t* sm, int logL, int logC, uint32_t tstride,
+                                              const uint32_t* __restrict__ tw, bool kfast, Src src) {
+  using K = F29Consts<Fs>;
+  const uint32_t plane = 1u << (logL + logC), L = 1u << logL, C = 1u << logC;
+  if (logL == 0) {
+    for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) lds_st<Fs>(sm, plane, e, src(0u, e));
+    return 0;
+  }
+  if (logL & 1) {
+    const uint32_t nm = L >> 1;
+    for (uint32_t b = threadIdx.x; b < (plane >> 1); b += kNttThreads) {
+      const uint32_t m = kfast ? b & (nm - 1) : b >> logC, c = kfast ? b >> (logL - 1) : b & (C - 1);
+      const uint32_t i = m, pos = ntt_brev(i, logL);  // i < L/2: pos = 2 m'
+      const F29<Fs> u = src(i, c), v = src(i + nm, c);
+      lds_st<Fs>(sm, plane, (pos << logC) | c, f29_nr<Fs>(f29_add<Fs>(u, v)));
+      lds_st<Fs>(sm, plane, ((pos + 1) << logC) | c, f29_nr<Fs>(f29_sub<Fs>(u, v, K::K6)));
+    }
+    return 1;
+  }
+  const uint32_t nm = L >> 2;
+  const F29<Fs> w3 = tw_half<Fs>(tw, (size_t)nm * tstride);  // omega_4
+  for (uint32_t b = threadIdx.x; b < (plane >> 2); b += kNttThreads) {
+    const uint32_t m = kfast ? b & (nm - 1) : b >> logC, c = kfast ? b >> (logL - 2) : b & (C - 1);
+    const uint32_t i = m, pos = ntt_brev(i, logL);  // i < L/4: pos = 4 m'
+    const F29<Fs> x0 = src(i, c), x1 = src(i + 2 * nm, c), x2 = src(i + nm, c), x3 = src(i + 3 * nm, c);
+    // inputs < 3p: y0 < 6p; y1 = x0 - x1 + 6p < 9p; y2 normalised < 6p; y3 normalised < 9p
+    const F29<Fs> y0 = f29_add<Fs>(x0, x1), y1 = f29_sub<Fs>(x0, x1, K::K6);
+    const F29<Fs> y2 = f29_norm<Fs>(f29_add<Fs>(x2, x3)), y3 = f29_norm<Fs>(f29_sub<Fs>(x2, x3, K::K6));
+    const F29<Fs> z3 = f29_mul_c<Fs>(y3, w3);  // < 2p
+    lds_st<Fs>(sm, plane, (pos << logC) | c, f29_nr<Fs>(f29_add<Fs>(y0, y2)));              // < 12p
+    lds_st<Fs>(sm, plane, ((pos + 2) << logC) | c, f29_nr<Fs>(f29_sub<Fs>(y0, y2, K::K6)));  // < 12p
+    lds_st<Fs>(sm, plane, ((pos + 1) << logC) | c, f29_nr<Fs>(f29_add<Fs>(y1, z3)));         // < 11p
+    lds_st<Fs>(sm, plane, ((pos + 3) << logC) | c, f29_nr<Fs>(f29_sub<Fs>(y1, z3, K::K2)));  // < 11p
+  }
+  return 2;
+}
+
 // XCD-aware block order: consecutive logical blocks (adjacent columns / rows,
 // which share 128-B lines) land on the same XCD and its L2.
 __device__ __forceinline__ uint32_t ntt_block(uint32_t nblocks) {
@@ -221,12 +267,11 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, ui
   const uint32_t n2 = 1u << log2, L = 1u << log1, C = 1u << logC, half = 1u << (logn - 1);
   const uint32_t plane = L << logC;
   const uint32_t col0 = ntt_block(n2 >> logC) << logC;
-  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
-    const uint32_t i1 = e >> logC, c = e & (C - 1);
-    lds_st<Fs>(sm, plane, (ntt_brev(i1, log1) << logC) | c, g_ld29<Fs>(in, (size_t)i1 * n2 + col0 + c));
-  }
+  const int t0 = ntt_load_first<Fs>(sm, log1, logC, n2, tw, false, [&](uint32_t i1, uint32_t c) {
+    return g_ld29<Fs>(in, (size_t)i1 * n2 + col0 + c);
+  });
   __syncthreads();
-  lds_ntt4<Fs>(sm, log1, logC, n2, tw);  // root omega^{n2}
+  lds_ntt4<Fs>(sm, log1, logC, n2, tw, t0);  // root omega^{n2}
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t k1 = e >> logC, c = e & (C - 1), i2 = col0 + c;
     F29<Fs> v = lds_ld<Fs>(sm, plane, e);
@@ -256,12 +301,11 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_mid(const uint32_t* __restr
   const uint32_t blk = ntt_block(n1 * groups);
   const uint32_t k1 = blk / groups, col0 = (blk - k1 * groups) << logC;
   const uint32_t* row = in + 8ull * ((size_t)k1 << (loga + logb));
-  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
-    const uint32_t ia = e >> logC, c = e & (C - 1);
-    lds_st<Fs>(sm, plane, (ntt_brev(ia, loga) << logC) | c, g_ld29<Fs>(row, (size_t)ia * nb + col0 + c));
-  }
+  const int t0 = ntt_load_first<Fs>(sm, loga, logC, n1 * nb, tw, false, [&](uint32_t ia, uint32_t c) {
+    return g_ld29<Fs>(row, (size_t)ia * nb + col0 + c);
+  });
   __syncthreads();
-  lds_ntt4<Fs>(sm, loga, logC, n1 * nb, tw);  // root omega^{n1 nb}
+  lds_ntt4<Fs>(sm, loga, logC, n1 * nb, tw, t0);  // root omega^{n1 nb}
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t ka = e >> logC, c = e & (C - 1), ib = col0 + c;
     F29<Fs> v = lds_ld<Fs>(sm, plane, e);
@@ -282,12 +326,11 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_rows(const uint32_t* in, ui
   const uint32_t n1 = 1u << log1, L = 1u << log2, R = 1u << logR;
   const uint32_t plane = L << logR;
   const uint32_t row0 = ntt_block(n1 >> logR) << logR;
-  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
-    const uint32_t r = e >> log2, i2 = e & (L - 1);  // row-contiguous loads
-    lds_st<Fs>(sm, plane, (ntt_brev(i2, log2) << logR) | r, g_ld29<Fs>(in, (size_t)(row0 + r) * L + i2));
-  }
+  const int t0 = ntt_load_first<Fs>(sm, log2, logR, n1, tw, true, [&](uint32_t i2, uint32_t r) {
+    return g_ld29<Fs>(in, (size_t)(row0 + r) * L + i2);  // row-contiguous loads
+  });
   __syncthreads();
-  lds_ntt4<Fs>(sm, log2, logR, n1, tw);  // root omega^{n1}
+  lds_ntt4<Fs>(sm, log2, logR, n1, tw, t0);  // root omega^{n1}
   const F29<Fs> sc = use_scale ? f29_from_r256<Fs>(scale.l) : f29_zero<Fs>();  // Norm, < 2p
   for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
     const uint32_t r = e & (R - 1), k2 = e >> logR;  // adjacent rows -> adjacent outputs

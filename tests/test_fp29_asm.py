@@ -284,3 +284,14 @@ def test_ntt_operand_bounds(field):
         u, v = xs[0], xs[1]
         o = [reduce3(norm(add(u, v))), reduce3(norm(sub(u, v, K6)))]
         assert [_value(x) % p for x in o] == [(X[0] + X[1]) % p, (X[0] - X[1]) % p]
+        # the first radix-4 round fused into the load phase (ntt_load_first):
+        # W_2 = W_4^0 = 1, no product; y2 and y3 normalised, 6p where the
+        # subtrahend is unmultiplied (< 3p) or y2 (< 6p)
+        y0, y1 = add(xs[0], xs[1]), sub(xs[0], xs[1], K6)
+        y2, y3 = norm(add(xs[2], xs[3])), norm(sub(xs[2], xs[3], K6))
+        z3 = mmul(y3, ws[2])
+        outs = [reduce3(norm(add(y0, y2))), reduce3(norm(add(y1, z3))), reduce3(norm(sub(y0, y2, K6))),
+                reduce3(norm(sub(y1, z3)))]
+        b0, b1, b2, b3 = X[0] + X[1], X[0] - X[1], X[2] + X[3], X[2] - X[3]
+        want = [b0 + b2, b1 + b3 * W[2], b0 - b2, b1 - b3 * W[2]]
+        assert [_value(o) % p for o in outs] == [v % p for v in want]
