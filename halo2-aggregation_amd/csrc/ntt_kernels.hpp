@@ -147,7 +147,7 @@ __device__ __forceinline__ F29<Fs> f29_nr(const F29<Fs>& a) {
 // traffic and barriers, 2^20 0.221 -> 0.205 ms; the radix-2 form is retired.)
 template <class Fs>
 __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint32_t tstride,
-                                         const uint32_t* __restrict__ tw, int t = 0) {
+                                         const uint32_t* __restrict__ tw, int t = 0, bool skip_last = false) {
   using K = F29Consts<Fs>;
   const uint32_t plane = 1u << (logL + logC);
   const uint32_t cmask = (1u << logC) - 1;
@@ -162,7 +162,7 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
     __syncthreads();
     t = 1;
   }
-  for (; t + 1 < logL; t += 2) {
+  for (; t + 1 < logL && !(skip_last && t == logL - 2); t += 2) {
     const uint32_t h = 1u << t;
     for (uint32_t b = threadIdx.x; b < (plane >> 2); b += kNttThreads) {
       const uint32_t c = b & cmask, bb = b >> logC;
@@ -248,6 +248,55 @@ __device__ __forceinline__ int ntt_load_first(uint32_t* sm, int logL, int logC, 
   return 2;
 }
 
+// Store phase fused with the last radix-4 round (t = logL - 2 >= 1, h = L/4):
+// the unit on positions j, j + h, j + 2h, j + 3h (j < h) produces outputs
+// j + q h directly, so dst(k, c, v) (the pass's epilogue: inter-pass twiddle
+// or scale, canonical form, global store) takes them from registers instead
+// of a last LDS round trip.  Lanes walk c fastest, as the unfused store does.
+template <class Fs, class Dst>
+__device__ __forceinline__ void ntt_last_store(const uint32_t* sm, int logL, int logC, uint32_t tstride,
+                                               const uint32_t* __restrict__ tw, Dst dst) {
+  using K = F29Consts<Fs>;
+  const uint32_t plane = 1u << (logL + logC), C = 1u << logC, h = 1u << (logL - 2);
+  for (uint32_t b = threadIdx.x; b < (plane >> 2); b += kNttThreads) {
+    const uint32_t c = b & (C - 1), j = b >> logC;  // j < h: lo = j
+    F29<Fs> x0 = lds_ld<Fs>(sm, plane, (j << logC) | c), x1 = lds_ld<Fs>(sm, plane, ((j + h) << logC) | c);
+    F29<Fs> x2 = lds_ld<Fs>(sm, plane, ((j + 2 * h) << logC) | c), x3 = lds_ld<Fs>(sm, plane, ((j + 3 * h) << logC) | c);
+    const F29<Fs> w1 = tw_half<Fs>(tw, (size_t)(j << 1) * tstride);  // W_{2h}^j
+    x1 = f29_mul_c<Fs>(x1, w1);
+    x3 = f29_mul_c<Fs>(x3, w1);
+    const F29<Fs> y0 = f29_add<Fs>(x0, x1), y1 = f29_sub<Fs>(x0, x1, K::K2);
+    const F29<Fs> y2 = f29_add<Fs>(x2, x3), y3 = f29_norm<Fs>(f29_sub<Fs>(x2, x3, K::K2));
+    const F29<Fs> w2 = tw_half<Fs>(tw, (size_t)j * tstride), w3 = tw_half<Fs>(tw, (size_t)(j + h) * tstride);
+    const F29<Fs> z2 = f29_mul_c<Fs>(y2, w2), z3 = f29_mul_c<Fs>(y3, w3);
+    dst(j, c, f29_nr<Fs>(f29_add<Fs>(y0, z2)));
+    dst(j + h, c, f29_nr<Fs>(f29_add<Fs>(y1, z3)));
+    dst(j + 2 * h, c, f29_nr<Fs>(f29_sub<Fs>(y0, z2, K::K2)));
+    dst(j + 3 * h, c, f29_nr<Fs>(f29_sub<Fs>(y1, z3, K::K2)));
+  }
+}
+
+// rounds after the fused load, then the store (with the last round fused
+// when there is one to fuse and its units occupy every thread: with fewer
+// units than threads the epilogue of 4 outputs per unit would run on part of
+// the block)
+// make_dst() builds the epilogue after the rounds, so what it holds (the
+// rows pass's scale) is not live across them (129 instead of 113 VGPRs: 3
+// waves per SIMD, 2^23 rows pass 0.39 -> 0.48 ms)
+template <class Fs, class MakeDst>
+__device__ __forceinline__ void ntt_rounds_store(uint32_t* sm, int logL, int logC, uint32_t tstride,
+                                                 const uint32_t* __restrict__ tw, int t0, MakeDst make_dst) {
+  const bool fuse = logL - 2 >= t0 && logL >= 3 && (1u << (logL + logC - 2)) >= (uint32_t)kNttThreads;
+  lds_ntt4<Fs>(sm, logL, logC, tstride, tw, t0, fuse);
+  auto dst = make_dst();
+  if (fuse) {
+    ntt_last_store<Fs>(sm, logL, logC, tstride, tw, dst);
+    return;
+  }
+  const uint32_t plane = 1u << (logL + logC), C = 1u << logC;
+  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) dst(e >> logC, e & (C - 1), lds_ld<Fs>(sm, plane, e));
+}
+
 // XCD-aware block order: consecutive logical blocks (adjacent columns / rows,
 // which share 128-B lines) land on the same XCD and its L2.
 __device__ __forceinline__ uint32_t ntt_block(uint32_t nblocks) {
@@ -264,21 +313,21 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, ui
                                                           const uint32_t* __restrict__ tw, uint32_t last) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int log2 = logn - log1;
-  const uint32_t n2 = 1u << log2, L = 1u << log1, C = 1u << logC, half = 1u << (logn - 1);
-  const uint32_t plane = L << logC;
+  const uint32_t n2 = 1u << log2, half = 1u << (logn - 1);
   const uint32_t col0 = ntt_block(n2 >> logC) << logC;
   const int t0 = ntt_load_first<Fs>(sm, log1, logC, n2, tw, false, [&](uint32_t i1, uint32_t c) {
     return g_ld29<Fs>(in, (size_t)i1 * n2 + col0 + c);
   });
   __syncthreads();
-  lds_ntt4<Fs>(sm, log1, logC, n2, tw, t0);  // root omega^{n2}
-  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
-    const uint32_t k1 = e >> logC, c = e & (C - 1), i2 = col0 + c;
-    F29<Fs> v = lds_ld<Fs>(sm, plane, e);
-    if (log2 > 0 && i2 && k1) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, i2 * k1, half));  // i2 k1 < n
-    if (last) v = f29_canon<Fs>(v);
-    g_st29<Fs>(out, (size_t)k1 * n2 + i2, v);
-  }
+  // root omega^{n2}
+  ntt_rounds_store<Fs>(sm, log1, logC, n2, tw, t0, [&] {
+    return [&](uint32_t k1, uint32_t c, F29<Fs> v) {
+      const uint32_t i2 = col0 + c;
+      if (log2 > 0 && i2 && k1) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, i2 * k1, half));  // i2 k1 < n
+      if (last) v = f29_canon<Fs>(v);
+      g_st29<Fs>(out, (size_t)k1 * n2 + i2, v);
+    };
+  });
 }
 
 // Three-pass form (n = n1 * na * nb, every factor <= 2^10, for n >= 2^23):
@@ -295,8 +344,7 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_mid(const uint32_t* __restr
                                                          const uint32_t* __restrict__ tw) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int logb = logn - log1 - loga;
-  const uint32_t n1 = 1u << log1, na = 1u << loga, nb = 1u << logb, C = 1u << logC, half = 1u << (logn - 1);
-  const uint32_t plane = na << logC;
+  const uint32_t n1 = 1u << log1, nb = 1u << logb, half = 1u << (logn - 1);
   const uint32_t groups = nb >> logC;  // column groups per row
   const uint32_t blk = ntt_block(n1 * groups);
   const uint32_t k1 = blk / groups, col0 = (blk - k1 * groups) << logC;
@@ -305,13 +353,14 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_mid(const uint32_t* __restr
     return g_ld29<Fs>(row, (size_t)ia * nb + col0 + c);
   });
   __syncthreads();
-  lds_ntt4<Fs>(sm, loga, logC, n1 * nb, tw, t0);  // root omega^{n1 nb}
-  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
-    const uint32_t ka = e >> logC, c = e & (C - 1), ib = col0 + c;
-    F29<Fs> v = lds_ld<Fs>(sm, plane, e);
-    if (ib && ka) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, n1 * ib * ka, half));  // n1 ib ka < n
-    g_st29<Fs>(out, ((size_t)ka * n1 + k1) * nb + ib, v);
-  }
+  // root omega^{n1 nb}
+  ntt_rounds_store<Fs>(sm, loga, logC, n1 * nb, tw, t0, [&] {
+    return [&](uint32_t ka, uint32_t c, F29<Fs> v) {
+      const uint32_t ib = col0 + c;
+      if (ib && ka) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, n1 * ib * ka, half));  // n1 ib ka < n
+      g_st29<Fs>(out, ((size_t)ka * n1 + k1) * nb + ib, v);
+    };
+  });
 }
 
 // pass B: R = 2^logR adjacent rows per block; optional output scale (R256
@@ -323,21 +372,20 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_rows(const uint32_t* in, ui
                                                           uint32_t use_scale) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int log1 = logn - log2;
-  const uint32_t n1 = 1u << log1, L = 1u << log2, R = 1u << logR;
-  const uint32_t plane = L << logR;
+  const uint32_t n1 = 1u << log1, L = 1u << log2;
   const uint32_t row0 = ntt_block(n1 >> logR) << logR;
   const int t0 = ntt_load_first<Fs>(sm, log2, logR, n1, tw, true, [&](uint32_t i2, uint32_t r) {
     return g_ld29<Fs>(in, (size_t)(row0 + r) * L + i2);  // row-contiguous loads
   });
   __syncthreads();
-  lds_ntt4<Fs>(sm, log2, logR, n1, tw, t0);  // root omega^{n1}
-  const F29<Fs> sc = use_scale ? f29_from_r256<Fs>(scale.l) : f29_zero<Fs>();  // Norm, < 2p
-  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) {
-    const uint32_t r = e & (R - 1), k2 = e >> logR;  // adjacent rows -> adjacent outputs
-    F29<Fs> v = lds_ld<Fs>(sm, plane, e);
-    if (use_scale) v = f29_mul_c<Fs>(v, sc);
-    g_st29<Fs>(out, (size_t)(row0 + r) + (size_t)n1 * k2, f29_canon<Fs>(v));
-  }
+  // root omega^{n1}; adjacent rows -> adjacent outputs
+  ntt_rounds_store<Fs>(sm, log2, logR, n1, tw, t0, [&] {
+    const F29<Fs> sc = use_scale ? f29_from_r256<Fs>(scale.l) : f29_zero<Fs>();  // Norm, < 2p
+    return [&, sc](uint32_t k2, uint32_t r, F29<Fs> v) {
+      if (use_scale) v = f29_mul_c<Fs>(v, sc);
+      g_st29<Fs>(out, (size_t)(row0 + r) + (size_t)n1 * k2, f29_canon<Fs>(v));
+    };
+  });
 }
 
 }  // namespace pm

@@ -352,7 +352,9 @@ int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_sca
  * halo2 `best_fft(a, omega, log_n)` [3P] (EvaluationDomain::fft / ifft /
  * coset conversions inside create_proof): in place, natural order in and out,
  * a_k <- sum_j a_j omega^{jk} over the scalar field of `curve` (Montgomery
- * 4 x u64 per element, like pm_msm's scalars).  omega must be a primitive
+ * 4 x u64 per element, like pm_msm's scalars).  Elements, omega and scale are
+ * canonical (< the modulus), as every value of the Rust field types is; the
+ * outputs are canonical.  omega must be a primitive
  * 2^log_n-th root of unity.  scale (may be NULL) multiplies every output:
  * EvaluationDomain::ifft is pm_fft(omega_inv, scale = 1/n).  log_n <= 28
  * (create_proof at k = 23 transforms the extended domain, 2^25); above 2^22
