@@ -368,6 +368,8 @@ int pm_ctx_create(int device, pm_ctx** out) {
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_LOG1")) c->ntt_log1 = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_MAXLOGC")) c->ntt_maxlogc = std::max(0, std::min(4, std::atoi(e)));
+  if (const char* e = std::getenv("PM_NTT_THREADS2")) c->ntt_threads2 = std::atoi(e) == 512 ? 512 : 256;
+  if (const char* e = std::getenv("PM_NTT_THREADS3")) c->ntt_threads3 = std::atoi(e) == 512 ? 512 : 256;
   if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("PM_BITS_SPLIT_K")) c->bits_split_k = std::max(1, std::min(1024, std::atoi(e)));
   if (const char* e = std::getenv("PM_SPIN_WAIT")) c->spin_wait = std::atoi(e) != 0;

@@ -107,15 +107,17 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
     PM_LAUNCH(ctx, "ntt_twiddles", (k_ntt_twiddles<Fs><<<(half + 255) / 256, 256, 0, st>>>(
                                        fearg_from_u64<Fs>(omega), half, (uint32_t*)tw)));
   const FeArg sc = scale ? fearg_from_u64<Fs>(scale) : FeArg{};
+  // threads per block: one / two passes and three passes (A/B: PM_NTT_THREADS2 / 3)
+  const unsigned nt2 = (unsigned)ctx->ntt_threads2, nt3 = (unsigned)ctx->ntt_threads3;
   uint32_t* data = (uint32_t*)d_data;
   if (logn <= (uint32_t)kNttOnePassLog) {
     // one sub-transform in LDS (pass A with a single column, in place)
     const size_t lds = n * kNttLdsBytes;
-    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<1, kNttThreads, lds, st>>>(data, data, (int)logn, (int)logn, 0, tw, scale ? 0u : 1u)));
+    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<1, nt2, lds, st>>>(data, data, (int)logn, (int)logn, 0, tw, scale ? 0u : 1u)));
     if (scale) {
       // scaling rides on a rows pass of length 1 would be wasteful: fold it in
       // with a trivial rows pass of log2 = 0 (one element per row)
-      PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> std::min<uint32_t>(logn, 8)), kNttThreads,
+      PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> std::min<uint32_t>(logn, 8)), nt2,
                                                    ((size_t)1 << std::min<uint32_t>(logn, 8)) * kNttLdsBytes, st>>>(
                                      data, data, (int)logn, 0, (int)std::min<uint32_t>(logn, 8), tw, sc, 1u)));
     }
@@ -126,9 +128,9 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
     if ((rc = ctx->ntt_scratch.ensure(n * 32))) return rc;
     uint32_t* tmp = (uint32_t*)ctx->ntt_scratch.p;
     const size_t ldsA = ((size_t)1 << (log1 + logC)) * kNttLdsBytes, ldsB = ((size_t)1 << (log2 + logR)) * kNttLdsBytes;
-    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)((size_t)1 << (log2 - logC)), kNttThreads, ldsA, st>>>(
+    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)((size_t)1 << (log2 - logC)), nt2, ldsA, st>>>(
                                    data, tmp, (int)logn, log1, logC, tw, 0u)));
-    PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)((size_t)1 << (log1 - logR)), kNttThreads, ldsB, st>>>(
+    PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)((size_t)1 << (log1 - logR)), nt2, ldsB, st>>>(
                                    tmp, data, (int)logn, log2, logR, tw, sc, scale ? 1u : 0u)));
   } else {
     // three passes (k_ntt_kernels.hpp: k_ntt_mid), factors of at most 2^10,
@@ -144,11 +146,11 @@ int ntt_device_impl(Ctx* ctx, int curve, void* d_data, uint32_t logn, const uint
     uint32_t* tmp2 = (uint32_t*)ctx->ntt_scratch2.p;
     const size_t ldsA = ((size_t)1 << (log1 + logC)) * kNttLdsBytes, ldsM = ((size_t)1 << (loga + logM)) * kNttLdsBytes,
                  ldsB = ((size_t)1 << (logb + logR)) * kNttLdsBytes;
-    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)(n >> (log1 + logC)), kNttThreads, ldsA, st>>>(
+    PM_LAUNCH(ctx, "ntt_cols", (k_ntt_cols<Fs><<<(unsigned)(n >> (log1 + logC)), nt3, ldsA, st>>>(
                                    data, tmp, (int)logn, log1, logC, tw, 0u)));
-    PM_LAUNCH(ctx, "ntt_mid", (k_ntt_mid<Fs><<<(unsigned)(n >> (loga + logM)), kNttThreads, ldsM, st>>>(
+    PM_LAUNCH(ctx, "ntt_mid", (k_ntt_mid<Fs><<<(unsigned)(n >> (loga + logM)), nt3, ldsM, st>>>(
                                   tmp, tmp2, (int)logn, log1, loga, logM, tw)));
-    PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> (logb + logR)), kNttThreads, ldsB, st>>>(
+    PM_LAUNCH(ctx, "ntt_rows", (k_ntt_rows<Fs><<<(unsigned)(n >> (logb + logR)), nt3, ldsB, st>>>(
                                    tmp2, data, (int)logn, logb, logR, tw, sc, scale ? 1u : 0u)));
   }
   HIP_TRY(hipStreamSynchronize(st));

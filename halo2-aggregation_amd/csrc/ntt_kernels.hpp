@@ -23,10 +23,9 @@
 
 namespace pm {
 
-#ifndef PM_NTT_THREADS
-#define PM_NTT_THREADS 256
-#endif
-constexpr int kNttThreads = PM_NTT_THREADS;
+// threads per block: chosen per launch by the host (ntt_engine.hpp), at most
+// kNttMaxThreads; the device loops stride by blockDim.x
+constexpr int kNttMaxThreads = 512;
 constexpr int kNttMaxLogL = 12;  // longest sub-transform (2^12 x 36 B = 144 KiB of LDS)
 constexpr size_t kNttLdsBytes = 36;  // LDS bytes per element (9 limb planes)
 
@@ -152,7 +151,7 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
   const uint32_t plane = 1u << (logL + logC);
   const uint32_t cmask = (1u << logC) - 1;
   if (t == 0 && (logL & 1)) {  // stage 0: twiddle 1; v < 3p unmultiplied, so u - v + 6p (< 9p)
-    for (uint32_t b = threadIdx.x; b < (plane >> 1); b += kNttThreads) {
+    for (uint32_t b = threadIdx.x; b < (plane >> 1); b += blockDim.x) {
       const uint32_t c = b & cmask, j = (b >> logC) << 1;
       const uint32_t ia = (j << logC) | c, ib = ((j + 1) << logC) | c;
       const F29<Fs> u = lds_ld<Fs>(sm, plane, ia), v = lds_ld<Fs>(sm, plane, ib);
@@ -164,7 +163,7 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
   }
   for (; t + 1 < logL && !(skip_last && t == logL - 2); t += 2) {
     const uint32_t h = 1u << t;
-    for (uint32_t b = threadIdx.x; b < (plane >> 2); b += kNttThreads) {
+    for (uint32_t b = threadIdx.x; b < (plane >> 2); b += blockDim.x) {
       const uint32_t c = b & cmask, bb = b >> logC;
       const uint32_t lo = bb & (h - 1);
       const uint32_t j = ((bb >> t) << (t + 2)) | lo;
@@ -216,12 +215,12 @@ __device__ __forceinline__ int ntt_load_first(uint32_t* sm, int logL, int logC, 
   using K = F29Consts<Fs>;
   const uint32_t plane = 1u << (logL + logC), L = 1u << logL, C = 1u << logC;
   if (logL == 0) {
-    for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) lds_st<Fs>(sm, plane, e, src(0u, e));
+    for (uint32_t e = threadIdx.x; e < plane; e += blockDim.x) lds_st<Fs>(sm, plane, e, src(0u, e));
     return 0;
   }
   if (logL & 1) {
     const uint32_t nm = L >> 1;
-    for (uint32_t b = threadIdx.x; b < (plane >> 1); b += kNttThreads) {
+    for (uint32_t b = threadIdx.x; b < (plane >> 1); b += blockDim.x) {
       const uint32_t m = kfast ? b & (nm - 1) : b >> logC, c = kfast ? b >> (logL - 1) : b & (C - 1);
       const uint32_t i = m, pos = ntt_brev(i, logL);  // i < L/2: pos = 2 m'
       const F29<Fs> u = src(i, c), v = src(i + nm, c);
@@ -232,7 +231,7 @@ __device__ __forceinline__ int ntt_load_first(uint32_t* sm, int logL, int logC, 
   }
   const uint32_t nm = L >> 2;
   const F29<Fs> w3 = tw_half<Fs>(tw, (size_t)nm * tstride);  // omega_4
-  for (uint32_t b = threadIdx.x; b < (plane >> 2); b += kNttThreads) {
+  for (uint32_t b = threadIdx.x; b < (plane >> 2); b += blockDim.x) {
     const uint32_t m = kfast ? b & (nm - 1) : b >> logC, c = kfast ? b >> (logL - 2) : b & (C - 1);
     const uint32_t i = m, pos = ntt_brev(i, logL);  // i < L/4: pos = 4 m'
     const F29<Fs> x0 = src(i, c), x1 = src(i + 2 * nm, c), x2 = src(i + nm, c), x3 = src(i + 3 * nm, c);
@@ -258,7 +257,7 @@ __device__ __forceinline__ void ntt_last_store(const uint32_t* sm, int logL, int
                                                const uint32_t* __restrict__ tw, Dst dst) {
   using K = F29Consts<Fs>;
   const uint32_t plane = 1u << (logL + logC), C = 1u << logC, h = 1u << (logL - 2);
-  for (uint32_t b = threadIdx.x; b < (plane >> 2); b += kNttThreads) {
+  for (uint32_t b = threadIdx.x; b < (plane >> 2); b += blockDim.x) {
     const uint32_t c = b & (C - 1), j = b >> logC;  // j < h: lo = j
     F29<Fs> x0 = lds_ld<Fs>(sm, plane, (j << logC) | c), x1 = lds_ld<Fs>(sm, plane, ((j + h) << logC) | c);
     F29<Fs> x2 = lds_ld<Fs>(sm, plane, ((j + 2 * h) << logC) | c), x3 = lds_ld<Fs>(sm, plane, ((j + 3 * h) << logC) | c);
@@ -286,7 +285,7 @@ __device__ __forceinline__ void ntt_last_store(const uint32_t* sm, int logL, int
 template <class Fs, class MakeDst>
 __device__ __forceinline__ void ntt_rounds_store(uint32_t* sm, int logL, int logC, uint32_t tstride,
                                                  const uint32_t* __restrict__ tw, int t0, MakeDst make_dst) {
-  const bool fuse = logL - 2 >= t0 && logL >= 3 && (1u << (logL + logC - 2)) >= (uint32_t)kNttThreads;
+  const bool fuse = logL - 2 >= t0 && logL >= 3 && (1u << (logL + logC - 2)) >= blockDim.x;
   lds_ntt4<Fs>(sm, logL, logC, tstride, tw, t0, fuse);
   auto dst = make_dst();
   if (fuse) {
@@ -294,7 +293,7 @@ __device__ __forceinline__ void ntt_rounds_store(uint32_t* sm, int logL, int log
     return;
   }
   const uint32_t plane = 1u << (logL + logC), C = 1u << logC;
-  for (uint32_t e = threadIdx.x; e < plane; e += kNttThreads) dst(e >> logC, e & (C - 1), lds_ld<Fs>(sm, plane, e));
+  for (uint32_t e = threadIdx.x; e < plane; e += blockDim.x) dst(e >> logC, e & (C - 1), lds_ld<Fs>(sm, plane, e));
 }
 
 // XCD-aware block order: consecutive logical blocks (adjacent columns / rows,
@@ -308,7 +307,7 @@ __device__ __forceinline__ uint32_t ntt_block(uint32_t nblocks) {
 // pass A: C = 2^logC adjacent columns per block.  last != 0: this is the
 // whole transform (one pass), so the output is canonicalised.
 template <class Fs>
-__global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, uint32_t* out,  // may alias
+__global__ void __launch_bounds__(kNttMaxThreads) k_ntt_cols(const uint32_t* in, uint32_t* out,  // may alias
                                                           int logn, int log1, int logC,
                                                           const uint32_t* __restrict__ tw, uint32_t last) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -339,7 +338,7 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_cols(const uint32_t* in, ui
 // length nb, root omega^{n1 na}) writes out[k1 + n1 ka + n1 na kb] =
 // out[k1 + n1 k2] with k2 = ka + na kb: the natural order.
 template <class Fs>
-__global__ void __launch_bounds__(kNttThreads) k_ntt_mid(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+__global__ void __launch_bounds__(kNttMaxThreads) k_ntt_mid(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                          int logn, int log1, int loga, int logC,
                                                          const uint32_t* __restrict__ tw) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -366,7 +365,7 @@ __global__ void __launch_bounds__(kNttThreads) k_ntt_mid(const uint32_t* __restr
 // pass B: R = 2^logR adjacent rows per block; optional output scale (R256
 // form, converted once per thread); the output is canonical
 template <class Fs>
-__global__ void __launch_bounds__(kNttThreads) k_ntt_rows(const uint32_t* in, uint32_t* out,  // may alias (log2 = 0)
+__global__ void __launch_bounds__(kNttMaxThreads) k_ntt_rows(const uint32_t* in, uint32_t* out,  // may alias (log2 = 0)
                                                           int logn, int log2, int logR,
                                                           const uint32_t* __restrict__ tw, FeArg scale,
                                                           uint32_t use_scale) {

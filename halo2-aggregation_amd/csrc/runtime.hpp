@@ -185,6 +185,7 @@ struct pm_ctx {
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
   int ntt_log1 = 0;    // three-pass first factor, 0 = auto (A/B: PM_NTT_LOG1 env)
   int ntt_maxlogc = 2; // most columns / rows per block, log2 (A/B: PM_NTT_MAXLOGC env)
+  int ntt_threads2 = 512, ntt_threads3 = 256;  // NTT threads per block, one / two-pass and three-pass forms (A/B: PM_NTT_THREADS2 / 3; profiles/r03/ntt_f29/threads_ab3.jsonl)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)
