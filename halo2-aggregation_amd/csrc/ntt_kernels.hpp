@@ -161,7 +161,15 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
     __syncthreads();
     t = 1;
   }
-  for (; t + 1 < logL && !(skip_last && t == logL - 2); t += 2) {
+  // Lazy reduction: a round whose inputs are < 3p may leave its outputs
+  // normalised but unreduced (< 7p, since the t > 0 unit adds at most 4p);
+  // the next round takes < 7p inputs (products < 7p * 2p, sums < 9p) and
+  // reduces its < 11p outputs.  So rounds alternate, and the last LDS round
+  // reduces when the unfused store phase (canonical form / packing, < 4p)
+  // follows; the fused last round (ntt_last_store) reduces its own outputs.
+  for (int r = 0; t + 1 < logL && !(skip_last && t == logL - 2); t += 2, r++) {
+    const bool next = t + 3 < logL && !(skip_last && t + 2 == logL - 2);
+    const bool red = (r & 1) || (!next && !skip_last) || t == 0;
     const uint32_t h = 1u << t;
     for (uint32_t b = threadIdx.x; b < (plane >> 2); b += blockDim.x) {
       const uint32_t c = b & cmask, bb = b >> logC;
@@ -191,10 +199,18 @@ __device__ __forceinline__ void lds_ntt4(uint32_t* sm, int logL, int logC, uint3
       const F29<Fs> w3 = tw_half<Fs>(tw, (size_t)((lo + h) << (logL - 2 - t)) * tstride);
       const F29<Fs> z2 = f29_mul_c<Fs>(y2, w2), z3 = f29_mul_c<Fs>(y3, w3);  // < 2p
       // outputs < 11p, limbs < 2^31 + 2^30
-      lds_st<Fs>(sm, plane, i0, f29_nr<Fs>(f29_add<Fs>(y0, z2)));
-      lds_st<Fs>(sm, plane, i2, f29_nr<Fs>(f29_sub<Fs>(y0, z2, K::K2)));
-      lds_st<Fs>(sm, plane, i1, f29_nr<Fs>(f29_add<Fs>(y1, z3)));
-      lds_st<Fs>(sm, plane, i3, f29_nr<Fs>(f29_sub<Fs>(y1, z3, K::K2)));
+      F29<Fs> o0 = f29_norm<Fs>(f29_add<Fs>(y0, z2)), o2 = f29_norm<Fs>(f29_sub<Fs>(y0, z2, K::K2));
+      F29<Fs> o1 = f29_norm<Fs>(f29_add<Fs>(y1, z3)), o3 = f29_norm<Fs>(f29_sub<Fs>(y1, z3, K::K2));
+      if (red) {
+        o0 = f29_reduce3<Fs>(o0);
+        o1 = f29_reduce3<Fs>(o1);
+        o2 = f29_reduce3<Fs>(o2);
+        o3 = f29_reduce3<Fs>(o3);
+      }
+      lds_st<Fs>(sm, plane, i0, o0);
+      lds_st<Fs>(sm, plane, i2, o2);
+      lds_st<Fs>(sm, plane, i1, o1);
+      lds_st<Fs>(sm, plane, i3, o3);
     }
     __syncthreads();
   }

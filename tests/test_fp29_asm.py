@@ -295,3 +295,19 @@ def test_ntt_operand_bounds(field):
         b0, b1, b2, b3 = X[0] + X[1], X[0] - X[1], X[2] + X[3], X[2] - X[3]
         want = [b0 + b2, b1 + b3 * W[2], b0 - b2, b1 - b3 * W[2]]
         assert [_value(o) % p for o in outs] == [v % p for v in want]
+        # lazy LDS rounds (lds_ntt4): a round on < 3p inputs leaves its outputs
+        # normalised, < 7p; the next round takes < 7p inputs and reduces
+        lazy_in = [_limbs(rng.randrange(7 * p) if t >= 20 else 7 * p - 1 - k) for k in range(4)]
+        a0, a1, a2, a3 = lazy_in
+        a1, a3 = mmul(a1, ws[0]), mmul(a3, ws[0])
+        e0, e1, e2, e3 = add(a0, a1), sub(a0, a1), add(a2, a3), norm(sub(a2, a3))
+        assert all(x < 2 ** 30 for x in e2)
+        f2, f3 = mmul(e2, ws[1]), mmul(e3, ws[2])
+        lz = [norm(add(e0, f2)), norm(add(e1, f3)), norm(sub(e0, f2)), norm(sub(e1, f3))]
+        assert all(_value(o) < 11 * p and all(x <= M29 for x in o[:8]) for o in lz)
+        assert all(_value(reduce3(o)) < 3 * p for o in lz)
+        # and from < 3p inputs the unreduced outputs stay < 7p
+        g1, g3 = mmul(xs[1], ws[0]), mmul(xs[3], ws[0])
+        h0, h1, h2, h3 = add(xs[0], g1), sub(xs[0], g1), add(xs[2], g3), norm(sub(xs[2], g3))
+        k2, k3 = mmul(h2, ws[1]), mmul(h3, ws[2])
+        assert all(_value(norm(o)) < 7 * p for o in (add(h0, k2), sub(h0, k2), add(h1, k3), sub(h1, k3)))
