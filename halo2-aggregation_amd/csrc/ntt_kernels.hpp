@@ -11,13 +11,15 @@
 //   pass B (k_ntt_rows): for every row k1, the n2-point NTT over the contiguous
 //     row (root omega^{n1}), stored at out[k1 + n1 * k2]  (natural order),
 //     optionally times a scale (ifft: the 1/n divisor).
-// Each sub-transform runs in LDS (structure of arrays: 9 limb planes of the
-// radix-2^29 form, so lane-consecutive elements hit consecutive banks) as a
-// radix-4 DIT on bit-reversed positions.  A workgroup takes C adjacent columns (pass A) or
-// rows (pass B) so its global loads / stores move C x 32 contiguous bytes.
-// All roots come from one table tw[i] = omega^i (R = 2^261 form), i < n/2, built once per
-// (field, omega, log_n) and cached in the context (omega^{n/2} = -1 covers
-// the upper half).
+// Each sub-transform runs as a radix-4 DIT on bit-reversed positions: its
+// first round in registers as the inputs arrive from global memory
+// (ntt_load_first), the middle rounds in LDS (structure of arrays: 9 limb
+// planes of the radix-2^29 form at XOR-swizzled positions, lds_swz), the last
+// round in registers on the way out (ntt_last_store).  A workgroup takes C
+// adjacent columns (pass A) or rows (pass B) so its global loads / stores
+// move C x 32 contiguous bytes.  All roots come from one table tw[i] =
+// omega^i (R = 2^261 form), i < n/2, built once per (field, omega, log_n) and
+// cached in the context (omega^{n/2} = -1 covers the upper half).
 #pragma once
 #include "msm_kernels.hpp"
 
@@ -53,10 +55,11 @@ __device__ __forceinline__ Fe<Fs> fe_of(const FeArg& a) {
 // no per-element conversion is needed.  Bounds (p < 2^254 for Pasta, ~2^253.6
 // for BN254 Fr, so R / p >= 128): LDS holds Norm values < 3p; a twiddle is
 // canonical (< p) or its negation 2p - w (< 2p), both Norm; f29_mul_c of a
-// value < 5p with limbs < 2^30 by a Norm twiddle < 2p is Norm, < 2p
+// value < 9p with limbs < 2^30 by a Norm twiddle < 2p is Norm, < 2p
 // (tests/test_fp29_asm.py::test_ntt_operand_bounds runs these operand shapes
 // through the interpreter with its overflow checks); each radix-4 output
-// (< 11p, limbs < 2^32 - 8) is normalised and reduced to < 3p.  A difference
+// (< 12p, limbs < 2^32 - 8) is normalised and reduced to < 3p, or, in every
+// other LDS round, left normalised at < 7p for the next round to reduce.  A difference
 // adds 2p when its subtrahend is a product (< 2p) and 6p when it is an
 // unmultiplied input (< 3p, the twiddle-1 stage 0), so it never goes negative.  Between
 // passes elements are stored packed but not canonical (< 3p < 2^256); the
