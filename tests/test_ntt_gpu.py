@@ -147,3 +147,30 @@ def test_ntt_errors(gpu_ctx):
         gpu_ctx.fft(9, np.zeros((4, 4), np.uint64), np.zeros(4, np.uint64))
     with pytest.raises(ValueError):
         gpu_ctx.fft(0, np.zeros((3, 4), np.uint64), np.zeros(4, np.uint64))
+
+
+@pytest.mark.parametrize("cid", [0, 1, 2])
+def test_extreme_representations_vs_oracle(gpu_ctx, cid):
+    """Inputs whose Montgomery representations sit at the top of [0, p)
+    (p - 1, p - 2, alternating with 0 and 1, a lone p - 1): the lazy
+    radix-2^29 butterflies see their largest limbs, and the intermediate
+    values between passes land near the top of their < 3p bound.  Two-pass
+    sizes and the forced three-pass form, against the oracle."""
+    os.environ["PM_NTT_PASSES"] = "3"
+    try:
+        ctx3 = H.Context(gpu_ctx.device)
+    finally:
+        del os.environ["PM_NTT_PASSES"]
+    r = P.CURVES[cid].r
+    rinv = pow(P.R_MONT, -1, r)
+    for k, ctx in ((10, gpu_ctx), (13, gpu_ctx), (15, ctx3)):
+        n = 1 << k
+        w = A.domain_omega(r, k)
+        pats = [[r - 1] * n, [0 if j % 2 else r - 1 for j in range(n)], [r - 2 if j % 3 else 1 for j in range(n)],
+                [r - 1 if j == n // 2 + 1 else 0 for j in range(n)]]
+        for pi, reps in enumerate(pats):
+            vals = [x * rinv % r for x in reps]
+            want = N.serial_fft(list(vals), w, k, r)
+            arr = np.array([P.to_limbs(x) for x in reps], dtype=np.uint64).reshape(n, 4)
+            got = ctx.fft(cid, arr, np.array(mont(r, w), np.uint64))
+            assert np.array_equal(got, np.array([mont(r, v) for v in want], dtype=np.uint64).reshape(n, 4)), (k, pi)
