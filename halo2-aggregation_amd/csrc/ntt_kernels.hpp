@@ -97,15 +97,16 @@ __device__ __forceinline__ void g_st29(uint32_t* g, size_t idx, const F29<Fs>& v
 }
 
 // LDS image: 9 limb planes of `plane` words.  Logical position idx sits at
-// word lds_swz(idx) of each plane: bits 0-5 XORed with bits 2-7 and 8-13.
-// Unswizzled, the bit-reversed scatter of the load phase put a wave's 64
-// stores into 1-2 banks (32-way conflicts) and the short-stride radix-4
-// rounds 2-4-way (rocprofv3: SQ_LDS_BANK_CONFLICT 78 % of SQ_LDS_IDX_ACTIVE
-// in k_ntt_rows at 2^20, profiles/r03/ntt_f29/stall_*); a bank model of every
-// access pattern of lds_ntt4 and the load / store phases picked this swizzle
-// (conflict cycles / 9.7).  The map is upper triangular on the bits, so it
-// permutes [0, 2^m) for every plane size 2^m.
-__device__ __forceinline__ uint32_t lds_swz(uint32_t i) { return i ^ (((i >> 2) ^ (i >> 8)) & 63u); }
+// word lds_swz(idx) of each plane: bits 0-5 XORed with bits 2-7, 5-10 and
+// 6-11.  Unswizzled, the bit-reversed scatter of the load phase put a wave's
+// 64 stores into a few banks (up to 32-way conflicts) and the short-stride
+// radix-4 rounds 2-4-way (rocprofv3: SQ_LDS_BANK_CONFLICT 78 % of
+// SQ_LDS_IDX_ACTIVE in k_ntt_rows at 2^20, profiles/r03/ntt_f29/stall_*); a
+// bank model of every access pattern of the fused load, the LDS rounds and the
+// stores (tools/ntt_lds_bank_model.py, 64 banks) picked this swizzle.  The map
+// is upper triangular on the bits, so it permutes [0, 2^m) for every plane
+// size 2^m.
+__device__ __forceinline__ uint32_t lds_swz(uint32_t i) { return i ^ (((i >> 2) ^ (i >> 5) ^ (i >> 6)) & 63u); }
 template <class Fs>
 __device__ __forceinline__ F29<Fs> lds_ld(const uint32_t* sm, uint32_t plane, uint32_t idx) {
   const uint32_t s = lds_swz(idx);

@@ -14,7 +14,7 @@ i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   D=$OUT/s$i
-  LOGN=${LOGN:-20} timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex k_ntt_rows -f csv -d $D -o run -- python3 tools/ntt_timing.py > $D.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $D.log; exit 1; }
+  LOGN=${LOGN:-20} timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex "k_ntt_(cols|mid|rows)" -f csv -d $D -o run -- python3 tools/ntt_timing.py > $D.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $D.log; exit 1; }
   find $D -name '*counter_collection.csv' -exec cp {} $OUT/s$i.csv \;
 done
 python3 - $OUT <<'PY'
@@ -25,8 +25,10 @@ for i in (1, 2, 3):
         rows = list(csv.DictReader(open(f"{out}/s{i}.csv")))
     except FileNotFoundError:
         continue
-    by = collections.defaultdict(list)
+    by = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in rows:
-        by[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    print({k: statistics.median(v) for k, v in by.items()})
+        kn = next((x for x in ("k_ntt_cols", "k_ntt_mid", "k_ntt_rows") if x in r["Kernel_Name"]), "?")
+        by[kn][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for kn, c in sorted(by.items()):
+        print(i, kn, {k: statistics.median(v) for k, v in c.items()})
 PY
