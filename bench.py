@@ -13,7 +13,7 @@ live with HIP events on the context stream over the timed region.  The
 headline runs against the resident SRS bases (their row table, like
 params.g in halo2); `variable_base` is the same MSM from raw bases (non-SRS
 bases, e.g. the verifier's proof commitments) with its own roofline,
-`dropin_pm_msm` the literal pm_msm_ctx drop-in call with host inputs (cold and
+`dropin_pm_msm` the literal pm_msm_ctx drop-in call with host inputs (first, admitting and
 warm), `small_n` its latency against the C port for n = 2^0 .. 2^16.
 `cpu_baseline` times the C restatement of halo2 best_multiexp (oracle/msm_ref.c)
 on the host cores of the same box, on the same inputs, at N=1 on rank 0.
@@ -492,10 +492,12 @@ def run_variable_base(args, ctx, dist, dev, world, curve, d_s, d_b, n, want, nam
 
 def run_dropin(args, curve, S, B, n, want):
     """The literal drop-in call of INTEGRATION.md §2: pm_msm_ctx with host
-    scalars AND host bases on a fresh context.  The first call uploads the
-    bases and builds the resident set (cold); repeated calls with the same
-    base bytes hit the drop-in cache (warm: the scalars' PCIe copy, the
-    content digest of the bases on host threads beside it, and the MSM)."""
+    scalars AND host bases on a fresh context.  The first call with a base
+    set runs the plain pipeline on uploaded bases (first_ms; the set is only
+    remembered), the second admits it (admit_ms: upload + row-table build),
+    later calls with the same base bytes hit the drop-in cache (warm: the
+    scalars' PCIe copy, the keyed digest of the bases on host threads beside
+    it, and the resident MSM)."""
     import numpy as np
 
     import halo2_amd as H
@@ -504,7 +506,10 @@ def run_dropin(args, curve, S, B, n, want):
     try:
         t0 = time.perf_counter()
         first = ctx.msm(curve, S, B)
-        cold = (time.perf_counter() - t0) * 1e3
+        first_ms = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
+        second = ctx.msm(curve, S, B)
+        admit_ms = (time.perf_counter() - t0) * 1e3
         k = max(5, args.steps // 2)
         for _ in range(2):
             ctx.msm(curve, S, B)
@@ -513,9 +518,11 @@ def run_dropin(args, curve, S, B, n, want):
             got = ctx.msm(curve, S, B)
         warm = (time.perf_counter() - t0) * 1e3 / k
         st = ctx.dropin_stats()
-        return {"call": "pm_msm_ctx(curve, host scalars, host bases, n)", "cold_ms": round(cold, 3),
-                "warm_ms_per_msm": round(warm, 4), "warm_Mscalar_s": round(n / (warm * 1e-3) / 1e6, 3),
-                "cache": st, "matches": bool(np.array_equal(first, want) and np.array_equal(got, want))}
+        return {"call": "pm_msm_ctx(curve, host scalars, host bases, n)", "first_ms": round(first_ms, 3),
+                "admit_ms": round(admit_ms, 3), "warm_ms_per_msm": round(warm, 4),
+                "warm_Mscalar_s": round(n / (warm * 1e-3) / 1e6, 3), "cache": st,
+                "matches": bool(np.array_equal(first, want) and np.array_equal(second, want)
+                                and np.array_equal(got, want))}
     finally:
         ctx.close()
 

@@ -62,8 +62,6 @@ pm_ctx::~pm_ctx() {
   (void)hipSetDevice(device);
   dropin_release_all(this);
   delete pool;
-  for (auto& e : copy_ev) (void)hipEventDestroy(e);
-  if (copy_fence) (void)hipEventDestroy(copy_fence);
   for (pm::Buf* b : all_bufs()) b->release();
   for (auto& t : ntt_tw) t.buf.release();
   if (h_pinned) (void)hipHostFree(h_pinned);
@@ -117,22 +115,6 @@ int pm_ctx::ensure_group_events(int n) {
   return PM_OK;
 }
 
-int pm_ctx::ensure_copy_events(int n) {
-  while ((int)copy_ev.size() < n) {
-    hipEvent_t e;
-    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    copy_ev.push_back(e);
-  }
-  return PM_OK;
-}
-
-int pm_ctx::copy_wait_for(hipStream_t st) {
-  if (!copy_fence) HIP_TRY(hipEventCreateWithFlags(&copy_fence, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(copy_fence, st));
-  HIP_TRY(hipStreamWaitEvent(copy_stream, copy_fence, 0));
-  return PM_OK;
-}
-
 // threads for host-side data-parallel work: this process's CPUs, capped by
 // OMP_NUM_THREADS (the GPU pool's 16-CPU share per GPU) and 16
 static int host_threads() {
@@ -147,7 +129,7 @@ static int host_threads() {
 }
 
 pm::HostPool& pm_ctx::host_pool() {
-  if (!pool) pool = new pm::HostPool(pool_threads > 0 ? pool_threads : host_threads());
+  if (!pool) pool = new pm::HostPool(host_threads());
   return *pool;
 }
 
@@ -361,25 +343,14 @@ int pm_ctx_create(int device, pm_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault));
   c->stream = c->own_stream;
   HIP_TRY(hipStreamCreateWithFlags(&c->red_stream, hipStreamNonBlocking));
-  if (const char* e = std::getenv("PM_MINCHUNK")) c->min_chunk = std::atoi(e);
-  if (const char* e = std::getenv("PM_H2D_CHUNKS")) c->h2d_chunks = std::max(1, std::min(64, std::atoi(e)));
-  if (const char* e = std::getenv("PM_POOL_THREADS")) c->pool_threads = std::max(1, std::min(64, std::atoi(e)));
-  if (const char* e = std::getenv("PM_ACC_SPLIT")) c->acc_split = std::atoi(e);
+  pm::digest_key_init(c->dropin_key);
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_LOG1")) c->ntt_log1 = std::atoi(e);
   if (const char* e = std::getenv("PM_NTT_MAXLOGC")) c->ntt_maxlogc = std::max(0, std::min(4, std::atoi(e)));
   if (const char* e = std::getenv("PM_NTT_THREADS2")) c->ntt_threads2 = std::atoi(e) == 512 ? 512 : 256;
   if (const char* e = std::getenv("PM_NTT_THREADS3")) c->ntt_threads3 = std::atoi(e) == 512 ? 512 : 256;
-  if (const char* e = std::getenv("PM_SORT_FB")) c->sort_fb = std::max(0, std::atoi(e));
-  if (const char* e = std::getenv("PM_BITS_SPLIT_K")) c->bits_split_k = std::max(1, std::min(1024, std::atoi(e)));
-  if (const char* e = std::getenv("PM_SPIN_WAIT")) c->spin_wait = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PM_TERMS_COPY")) c->terms_copy = std::atoi(e) != 0;
   if (const char* e = std::getenv("PM_FINE_CACHE_KB")) c->fine_cache_kb = std::max(0, std::min(144, std::atoi(e)));
   if (const char* e = std::getenv("PM_FINE_CHUNK_KB")) c->fine_chunk_kb = std::max(0, std::min(144, std::atoi(e)));
-  if (const char* e = std::getenv("PM_SORT_PPT")) {
-    const int v = std::atoi(e);
-    c->sort_ppt = (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
-  }
   *out = c.release();
   return PM_OK;
 }
@@ -552,7 +523,6 @@ struct pm_bases {
 namespace {
 constexpr size_t kResidentRowsMinN = size_t(1) << 18;
 int resident_rows(size_t n) {
-  if (const char* e = std::getenv("PM_RESIDENT_ROWS")) return std::max(1, std::atoi(e));  // A/B experiments
   if (n < kResidentRowsMinN) return 1;
   // round 3, after the sort changes (profiles/r03/rows_ab/, same box, 3
   // interleaved runs): 8 rows (two bucket sets) win up to 2^20 (2^20
@@ -664,45 +634,67 @@ static int msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const voi
 // halo2 calls best_multiexp with the same SRS bases over and over
 // (commit_lagrange over params.g_lagrange, the commits inside create_proof:
 // examples/simple-example.rs:606,638-640,702).  pm_msm / pm_msm_ctx keep base
-// sets of >= kDropinMinN points resident, keyed by (curve, n, a 64-bit XXH64-
-// style digest of every chunk of the base bytes, folded twice), so a repeated
-// set skips its 64 B/point upload and runs as a resident (row-table) MSM.
-// The digest is computed on the host pool while the scalars cross PCIe; any
-// change of the bytes (same pointer or not) changes the key and re-uploads.
-// The digest is not cryptographic: it guards against stale data, not against
-// a caller forging colliding base sets.
+// sets of >= kDropinMinN points resident, keyed by (curve, n, a keyed 254-bit
+// digest of the base bytes: dropin_digest.hpp, secret key per context), so a
+// repeated set skips its 64 B/point upload and runs as a resident (row-table)
+// MSM.  The digest is computed on the host pool while the scalars cross
+// PCIe; any change of the bytes (same pointer or not) changes the key.
+//  * admission on the second sighting: the first call with a set runs the
+//    plain pipeline on uploaded bases (no row-table build for one-shot sets)
+//    and only remembers the digest;
+//  * memory: least recently used sets are evicted BEFORE a new one is built,
+//    against kDropinEntries and min(kDropinBytes, free device memory /
+//    kDropinFreeDiv); if the build still fails, every set is released and the
+//    build retried once, and if that fails the call runs the plain pipeline.
 namespace {
-constexpr uint64_t kX1 = 0x9E3779B185EBCA87ull, kX2 = 0xC2B2AE3D27D4EB4Full, kX3 = 0x165667B19E3779F9ull,
-                   kX4 = 0x85EBCA77C2B2AE63ull;
-inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-inline uint64_t xround(uint64_t acc, uint64_t w) { return rotl64(acc + w * kX2, 31) * kX1; }
-inline uint64_t xmerge(uint64_t h, uint64_t v) { return (h ^ xround(0, v)) * kX1 + kX4; }
-inline uint64_t xaval(uint64_t h) {
-  h ^= h >> 33;
-  h *= kX2;
-  h ^= h >> 29;
-  h *= kX3;
-  return h ^ (h >> 32);
-}
-// XXH64-style hash of nwords (a multiple of 4) 64-bit words
-uint64_t stripe_hash(const uint64_t* p, size_t nwords, uint64_t seed) {
-  uint64_t v1 = seed + kX1 + kX2, v2 = seed + kX2, v3 = seed, v4 = seed - kX1;
-  for (size_t i = 0; i + 4 <= nwords; i += 4) {
-    v1 = xround(v1, p[i]);
-    v2 = xround(v2, p[i + 1]);
-    v3 = xround(v3, p[i + 2]);
-    v4 = xround(v4, p[i + 3]);
-  }
-  uint64_t h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
-  h = xmerge(xmerge(xmerge(xmerge(h, v1), v2), v3), v4);
-  return xaval(h + nwords * 8);
-}
 constexpr size_t kDigestChunk = size_t(1) << 15;  // points per chunk (2 MiB)
+
+// device bytes of a resident set of n points (bases_upload_locked's layout)
+size_t dropin_bytes(size_t n) {
+  const int rows = resident_rows(n);
+  if (rows <= 1) return std::max<size_t>(64, n * 64);
+  return (size_t)rows * std::max<size_t>(kSortB, (n + kSortB - 1) / kSortB * kSortB) * 64;  // fixed_table's npad
+}
+
+bool same_key(const pm::DropinEntry& e, int curve, size_t n, const uint64_t d[4]) {
+  return e.curve == curve && e.n == n && std::memcmp(e.d, d, sizeof(e.d)) == 0;
+}
 }  // namespace
 
 static void dropin_release_all(pm_ctx* ctx) {
   for (auto& e : ctx->dropin) pm_bases_release(e.b);
   ctx->dropin.clear();
+}
+
+static size_t dropin_total(const pm_ctx* ctx) {
+  size_t s = 0;
+  for (auto& e : ctx->dropin) s += e.bytes;
+  return s;
+}
+
+static void dropin_evict_lru(pm_ctx* ctx) {
+  auto lru = std::min_element(ctx->dropin.begin(), ctx->dropin.end(),
+                              [](const pm::DropinEntry& x, const pm::DropinEntry& y) { return x.last_use < y.last_use; });
+  pm_bases_release(lru->b);
+  ctx->dropin.erase(lru);
+}
+
+// make room for `bytes` more: LRU eviction against the entry count and the
+// memory budget (the fixed cap and a fraction of what the device has free)
+static void dropin_make_room(pm_ctx* ctx, size_t bytes) {
+  size_t free_b = 0, total_b = 0;
+  const bool have_info = hipMemGetInfo(&free_b, &total_b) == hipSuccess;
+  for (;;) {
+    if (ctx->dropin.empty()) return;
+    const size_t held = dropin_total(ctx);
+    size_t budget = kDropinBytes;
+    if (have_info) budget = std::min(budget, (free_b + held) / kDropinFreeDiv);
+    if ((int)ctx->dropin.size() < kDropinEntries && held + bytes <= budget) return;
+    const size_t before = ctx->dropin.size();
+    dropin_evict_lru(ctx);
+    if (have_info) free_b += held - dropin_total(ctx);
+    if (ctx->dropin.size() == before) return;
+  }
 }
 
 static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
@@ -714,21 +706,26 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
   int rc;
   if ((rc = ctx->begin_call())) return rc;
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
-  if (n < kDropinMinN || n > kMaxPoints) {  // small MSMs: both inputs uploaded, plain pipeline
-    if ((rc = ctx->in_bases.ensure(n * 64))) return rc;
-    if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
-    if ((rc = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) return rc;
+  auto plain = [&]() -> int {  // both inputs uploaded, plain pipeline
+    int r;
+    if ((r = ctx->in_bases.ensure(n * 64))) return r;
+    if ((r = ctx->upload_h2d(ctx->in_bases.p, bases, n * 64, ctx->stream))) return r;
     return dispatch_msm_device(ctx, curve, ctx->in_scalars.p, ctx->in_bases.p, n, flags, out);
+  };
+  if (n < kDropinMinN || n > kMaxPoints) {  // small MSMs bypass the cache
+    if ((rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream))) return rc;
+    return plain();
   }
-  // digest of the bases on the pool's workers while this thread copies the scalars
+  // keyed digest of the bases on the pool's workers while this thread copies the scalars
   const size_t nch = (n + kDigestChunk - 1) / kDigestChunk;
-  std::vector<uint64_t> part((nch + 3) & ~size_t(3), 0);
+  std::vector<pm::u128> part(2 * nch);
   pm::HostPool& pool = ctx->host_pool();
   const int nw = std::max(1, pool.size() - 1);
+  const pm::DigestKey& key = ctx->dropin_key;
   auto job = [&](int t, int) {
     for (size_t k = (size_t)(t - 1); k < nch; k += (size_t)nw) {
       const size_t p0 = k * kDigestChunk, p1 = std::min(n, p0 + kDigestChunk);
-      part[k] = stripe_hash(bases + 8 * p0, 8 * (p1 - p0), k);
+      pm::digest_chunk(key, bases + 8 * p0, 8 * (p1 - p0), &part[2 * k]);
     }
   };
   const bool threaded = pool.size() > 1;
@@ -737,11 +734,11 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
   if (threaded) pool.wait();
   else job(1, 1);
   if (copy_rc) return copy_rc;
-  const uint64_t d0 = stripe_hash(part.data(), part.size(), 0x5EEDull + (uint64_t)curve);
-  const uint64_t d1 = stripe_hash(part.data(), part.size(), 0xA11CEull ^ ((uint64_t)n << 8));
+  uint64_t d[4];
+  pm::digest_combine(key, part.data(), nch, d);
   pm_bases* b = nullptr;
   for (auto& e : ctx->dropin)
-    if (e.curve == curve && e.n == n && e.d0 == d0 && e.d1 == d1) {
+    if (same_key(e, curve, n, d)) {
       e.last_use = ++ctx->dropin_clock;
       b = e.b;
       ctx->dropin_hits++;
@@ -749,27 +746,40 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
     }
   if (!b) {
     ctx->dropin_misses++;
-    if ((rc = bases_upload_locked(ctx, curve, bases, true, n, &b))) return rc;
+    auto seen = std::find_if(ctx->dropin_seen.begin(), ctx->dropin_seen.end(),
+                             [&](const pm::DropinEntry& e) { return same_key(e, curve, n, d); });
+    if (seen == ctx->dropin_seen.end()) {  // first sighting: remember it, plain pipeline
+      if ((int)ctx->dropin_seen.size() >= kDropinSeen) ctx->dropin_seen.erase(ctx->dropin_seen.begin());
+      pm::DropinEntry e{curve, n, {d[0], d[1], d[2], d[3]}, nullptr, 0, ++ctx->dropin_clock};
+      ctx->dropin_seen.push_back(e);
+      return plain();
+    }
+    ctx->dropin_seen.erase(seen);
+    dropin_make_room(ctx, dropin_bytes(n));
+    rc = bases_upload_locked(ctx, curve, bases, true, n, &b);
+    if (rc && !ctx->dropin.empty()) {  // out of device memory: release every set and retry once
+      dropin_release_all(ctx);
+      rc = bases_upload_locked(ctx, curve, bases, true, n, &b);
+    }
+    if (rc) return plain();  // the set stays unadmitted; the MSM itself still runs
     size_t bytes = 0;
     pm_bases_info(b, nullptr, nullptr, &bytes);
-    // evict least recently used sets beyond the entry / memory budget
-    auto total = [&] {
-      size_t s = 0;
-      for (auto& e : ctx->dropin) s += e.bytes;
-      return s;
-    };
-    while (!ctx->dropin.empty() &&
-           ((int)ctx->dropin.size() >= kDropinEntries || total() + bytes > kDropinBytes)) {
-      auto lru = std::min_element(ctx->dropin.begin(), ctx->dropin.end(),
-                                  [](const pm::DropinEntry& x, const pm::DropinEntry& y) { return x.last_use < y.last_use; });
-      pm_bases_release(lru->b);
-      ctx->dropin.erase(lru);
-    }
-    ctx->dropin.push_back(pm::DropinEntry{curve, n, d0, d1, b, bytes, ++ctx->dropin_clock});
+    ctx->dropin.push_back(pm::DropinEntry{curve, n, {d[0], d[1], d[2], d[3]}, b, bytes, ++ctx->dropin_clock});
   }
   if (resident_use_table(b, 0, n))
     return curve_ops(curve)->msm_fixed(ctx, b->table, ctx->in_scalars.p, n, flags & ~kBasesR261, out, nullptr);
   return dispatch_msm_device(ctx, curve, ctx->in_scalars.p, b->d, n, flags, out, true);
+}
+
+int pm_ctx_dropin_key_id(pm_ctx* ctx, uint64_t out[2]) {
+  if (!ctx || !out) return set_error(PM_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  pm::Blake2bHost h("pm-dropin-key-id");
+  h.update(&ctx->dropin_key, sizeof(ctx->dropin_key));
+  uint8_t dg[64];
+  h.finalize(dg);
+  std::memcpy(out, dg, 16);
+  return PM_OK;
 }
 
 int pm_ctx_dropin_stats(pm_ctx* ctx, uint64_t* hits, uint64_t* misses, int* entries, size_t* device_bytes) {
@@ -791,6 +801,7 @@ int pm_ctx_dropin_clear(pm_ctx* ctx) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   (void)hipSetDevice(ctx->device);
   dropin_release_all(ctx);
+  ctx->dropin_seen.clear();
   return PM_OK;
 }
 

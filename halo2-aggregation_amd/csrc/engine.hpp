@@ -117,9 +117,7 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result);
 // (pm_msm_resident_batch).  tail == nullptr: run the tail here.
 //
 // h_scalars != nullptr: the scalars are still in (pageable) host memory and
-// d_scalars is their device buffer; the copy goes over the copy stream in
-// chunks, and the histogram pass runs chunk by chunk behind it, so all but
-// the last chunk's histogram overlaps the PCIe transfer.
+// d_scalars is their device buffer; they are copied ahead of the sort.
 template <class Cv>
 int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases, size_t n, uint32_t flags,
                     Xyzz<typename Cv::Base>* result, const pm_fixed_bases* ft = nullptr,
@@ -151,7 +149,6 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // the fixed-base MSM's merged sort rows are W x longer: 4x more coarse bins
   // once they exceed 2^24 entries (2^23, c = 20: FB 11 -> 9, sort 3.4 -> 2.3 ms)
   if (fixed && E > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
-  if (ctx->sort_fb > 0) g.FB = std::min(pl.cmax - 1, ctx->sort_fb);  // PM_SORT_FB: tuning experiments
   g.NCB = (pl.K >> g.FB) + 1;
   // points per thread: blocks of 1024 threads x ppt points, ppt the largest
   // power of two <= 8 that still gives >= 128 blocks (2^20: 8192 points per
@@ -160,7 +157,6 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // 0.16 ms at 2^20; small n keeps enough blocks)
   g.ppt = 1;
   while (g.ppt < kSortPerThread && stride >= (size_t)256 * g.ppt * kSortThreads) g.ppt *= 2;
-  if (ctx->sort_ppt > 0 && !fixed) g.ppt = ctx->sort_ppt;  // PM_SORT_PPT (1, 2, 4, 8): tuning experiments
   g.nblk = (int)((stride + (size_t)g.ppt * kSortThreads - 1) / ((size_t)g.ppt * kSortThreads));
   // The histogram pass is compute-bound per block (Montgomery -> canonical,
   // W signed digits and LDS atomics per scalar); with 8192-point blocks 2^20
@@ -172,7 +168,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // 128 blocks the scan's growth cancels the gain: 2^19 +-0, 2^18 +3-5 us,
   // profiles/r02/hs/ab.txt and profiles/r02/p/ab.txt).
   int hsub = 1;
-  if (ctx->sort_ppt == 0 && g.ppt >= 2 && g.nblk >= 128 && g.nblk < 256) hsub = 2;
+  if (g.ppt >= 2 && g.nblk >= 128 && g.nblk < 256) hsub = 2;
   g.hsub = 1;
   SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
   g.ppt /= hsub;    // histogram geometry
@@ -216,9 +212,10 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // host terms: the reduction kernels store them straight into the pinned
   // slot (mapped; visible to the host once the event below completes), which
   // saves the blit of a D2H copy (~11 us per MSM, profiles/r03/kernel_stats.csv
-  // __amd_rocclr_copyBuffer).  PM_TERMS_COPY=1: the device buffer + copy (A/B).
-  Xyzz<F>* Qd = (Xyzz<F>*)ctx->bitsQ.p;
-  if (!ctx->terms_copy) {
+  // __amd_rocclr_copyBuffer; the copy measured within noise on the headline
+  // and 24 us slower on the variable-base path, profiles/r03/ab/).
+  Xyzz<F>* Qd = nullptr;
+  {
     void* dq = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dq, hslot, 0));
     Qd = (Xyzz<F>*)dq;
@@ -242,43 +239,14 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   }
   const uint32_t canon = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
   if (h_scalars) {
-    // chunks of whole histogram blocks, ~8 MB each (2^20: 4 chunks of 64 blocks)
-    const size_t pts_blk = (size_t)g.ppt * kSortThreads;
-    const int nch = (int)std::max<size_t>(1, std::min<size_t>(ctx->h2d_chunks, n * 32 / kH2DChunkMin));
-    const int bpc = (int)((((n + pts_blk - 1) / pts_blk) + nch - 1) / nch);
-    if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
-    if ((rc = ctx->ensure_copy_events(nch))) return rc;
-    hipEvent_t ta = nullptr, tb = nullptr;  // "h2d" timing: first chunk's start to last chunk's end
-    if (ctx->timed("h2d")) {
-      ta = ctx->next_event();
-      tb = ctx->next_event();
-    }
-    for (int c = 0; c * bpc < g.nblk; c++) {
-      const size_t p0 = std::min(n, (size_t)c * bpc * pts_blk), p1 = std::min(n, (size_t)(c + 1) * bpc * pts_blk);
-      if (p1 > p0) {
-        if (c == 0 && (rc = ctx->copy_wait_for(st))) return rc;  // the buffer's previous reader
-        if (c == 0 && ta) HIP_TRY(hipEventRecord(ta, ctx->copy_stream));
-        HIP_TRY(hipMemcpyAsync((char*)d_scalars + p0 * 32, (const char*)h_scalars + p0 * 32, (p1 - p0) * 32,
-                               hipMemcpyHostToDevice, ctx->copy_stream));
-        HIP_TRY(hipEventRecord(ctx->copy_ev[c], ctx->copy_stream));
-        if (p1 == n && tb) {
-          HIP_TRY(hipEventRecord(tb, ctx->copy_stream));
-          ctx->mark("h2d", ta, tb);
-        }
-        HIP_TRY(hipStreamWaitEvent(st, ctx->copy_ev[c], 0));
-      }
-      SortGeom gc = g;
-      gc.blk0 = c * bpc;
-      const int nb = std::min(bpc, g.nblk - gc.blk0);
-      PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, gc, nb, bh, ctx->digits.p,
-                                                       (uint32_t)stride, (uint32_t)kmerge, st));
-      if (rc) return rc;
-    }
-  } else {
-    PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, g.nblk, bh, ctx->digits.p,
-                                                     (uint32_t)stride, (uint32_t)kmerge, st));
-    if (rc) return rc;
+    // one pageable copy on the context stream ahead of the histogram pass (a
+    // copy in 4 chunks, each chunk's histogram blocks launched behind it,
+    // measured ~0.1 ms slower per 2^20 MSM: round 3, profiles/r03/h2d/)
+    if ((rc = ctx->upload_h2d((void*)d_scalars, h_scalars, n * 32, st))) return rc;
   }
+  PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, g.nblk, bh, ctx->digits.p,
+                                                   (uint32_t)stride, (uint32_t)kmerge, st));
+  if (rc) return rc;
   PM_LAUNCH(ctx, "scan", {
     k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, tiles, bsum);
     k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, tiles, bsum, bofs, nullptr);
@@ -342,7 +310,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // the split stops at ~16 blocks per job (c = 20, 2^19 buckets: 16 -> 0.33
   // ms, 64 -> 0.47 ms; round 3, 16 / Wr against 4, 8, 32, 64 / Wr at 2^19 -
   // 2^22, resident and raw: profiles/r03/ab/bits_split_sweep.jsonl).
-  const int nsplit = std::max(1, std::min(kMaxSplit, ctx->bits_split_k / Wr));
+  const int nsplit = std::max(1, std::min(kMaxSplit, kBitsSplitK / Wr));
   Xyzz<F>* bitsP = nullptr;
   uint32_t* tickets = nullptr;
   if (nsplit > 1) {
@@ -356,7 +324,6 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   PM_LAUNCH(ctx, "bucket_bits",
             (k_bucket_bits<F><<<dim3(NJ, Wr, nsplit), kRedThreads, 0, st>>>(S, T, pl.M1, pl.NB2, Qd, NQ, nsplit,
                                                                              bitsP, tickets)));
-  if (ctx->terms_copy) HIP_TRY(hipMemcpyAsync(hslot, Qd, nQ * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
   hipEvent_t ev = ctx->grp_ev[slot];
   HIP_TRY(hipEventRecord(ev, st));
   MsmTail<F> t;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/pasta_msm.h"
+#include "dropin_digest.hpp"
 
 #include <condition_variable>
 #include <cstring>
@@ -36,17 +37,23 @@ constexpr int kL1 = 4;  // bucket-segment length of k_bucket_seg_q (one quad per
 // caller flags): d_bases already hold the pipeline's R = 2^261 canonical
 // form (resident pm_bases converted at upload), so no per-call conversion
 constexpr uint32_t kBasesR261 = 1u << 30;
-// host scalars (pm_msm_resident, pm_msm_fixed, pm_msm): the copy is split into
-// at most kH2DChunks chunks of >= kH2DChunkMin bytes on the copy stream, and
-// k_sort_hist runs chunk by chunk behind it
-constexpr int kH2DChunks = 1;  // 4 chunks measured ~0.1 ms slower per 2^20 MSM than one copy (round 3, tools/h2d_timing.py)
-constexpr size_t kH2DChunkMin = size_t(4) << 20;
+// k_bucket_bits blocks per job = kBitsSplitK / (bucket sets): the bit sums of
+// few sets (row tables, the fixed-base MSM) are split over more blocks; every
+// extra lane also adds one tree addition (round 3 sweep of 4..64 / Wr at
+// 2^19-2^22, profiles/r03/ab/bits_split_sweep.jsonl: 16 best)
+constexpr int kBitsSplitK = 16;
 // drop-in base cache of pm_msm / pm_msm_ctx (capi.hip): base sets of at least
 // kDropinMinN points are kept resident, keyed by a content digest; at most
 // kDropinEntries sets and kDropinBytes of device memory per context
 constexpr size_t kDropinMinN = size_t(1) << 12;
 constexpr int kDropinEntries = 4;
 constexpr size_t kDropinBytes = size_t(16) << 30;
+// ... and at most this fraction (1/kDropinFreeDiv) of the device memory free
+// at admission, counting the sets already held
+constexpr size_t kDropinFreeDiv = 2;
+// base sets seen once and not admitted: a set becomes resident on its second
+// sighting, so one-shot bases never pay the row-table build
+constexpr int kDropinSeen = 8;
 
 struct Buf {
   void* p = nullptr;
@@ -121,12 +128,13 @@ class HostPool {
   bool stop_ = false;
 };
 
-// resident base set of the drop-in cache (pm_msm): key = (curve, n, digest)
+// resident base set of the drop-in cache (pm_msm): key = (curve, n, keyed
+// digest, dropin_digest.hpp)
 struct DropinEntry {
   int curve;
   size_t n;
-  uint64_t d0, d1;
-  pm_bases* b;
+  uint64_t d[4];
+  pm_bases* b;  // nullptr: seen once, not admitted yet (run through the plain path)
   size_t bytes;
   uint64_t last_use;
 };
@@ -163,30 +171,26 @@ struct pm_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t red_stream = nullptr;  // accumulator side stream (accum_engine.hpp)
-  hipStream_t copy_stream = nullptr; // H2D of host scalars (chunked; pm_msm_resident_batch: the next MSM's)
-  std::vector<hipEvent_t> copy_ev;   // chunk c of the current host-scalar copy has landed
-  hipEvent_t copy_fence = nullptr;   // copy_wait_for: the copy stream waits for the context stream
+  hipStream_t copy_stream = nullptr; // pm_msm_resident_batch: H2D of the next MSM's scalars
   pm::HostPool* pool = nullptr;      // lazily created (drop-in digest)
   std::vector<pm::DropinEntry> dropin;  // drop-in base cache (pm_msm / pm_msm_ctx)
+  std::vector<pm::DropinEntry> dropin_seen;  // digests seen once (b == nullptr), admitted on the second sighting
+  pm::DigestKey dropin_key;             // secret per-context digest key (pm_ctx_create)
   uint64_t dropin_clock = 0;
   uint64_t dropin_hits = 0, dropin_misses = 0;
   hipEvent_t batch_ev[4] = {};       // batch pipelining: copied[2], consumed[2]
   std::vector<hipEvent_t> grp_ev;    // MSM: one per pinned term slot (terms copied)
   int window_c = 0;
   int min_chunk = 0;
-  int h2d_chunks = pm::kH2DChunks;  // host-scalar copy chunks (diagnostics: PM_H2D_CHUNKS env)
-  int pool_threads = 0;             // host pool size, 0 = auto (diagnostics: PM_POOL_THREADS env)  // minimum accumulate slice, 0 = auto (diagnostics: PM_MINCHUNK env)
-  int sort_ppt = 0;   // sort points per thread, 0 = auto (diagnostics: PM_SORT_PPT env, 1/2/4/8)
-  int sort_fb = 0;    // fine bits of the two-level sort, 0 = auto (diagnostics: PM_SORT_FB env)
-  int fine_cache_kb = 0, fine_chunk_kb = 0;  // fine-sort LDS cache / chunk, 0 = auto (PM_FINE_CACHE_KB / _CHUNK_KB)
-  int bits_split_k = 16;    // k_bucket_bits blocks per job = bits_split_k / Wr (PM_BITS_SPLIT_K, A/B)
-  bool spin_wait = false;   // host waits poll their event (PM_SPIN_WAIT=1, A/B; within noise, not default)
-  bool terms_copy = false;  // MSM host terms through a device buffer + D2H copy (PM_TERMS_COPY=1, A/B)
+  // test hooks (tests/test_msm_gpu.py::test_fine_sort_lds_modes forces the
+  // fine sort's LDS modes that only large segments reach): PM_FINE_CACHE_KB /
+  // PM_FINE_CHUNK_KB, 0 = auto
+  int fine_cache_kb = 0, fine_chunk_kb = 0;
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
   int ntt_log1 = 0;    // three-pass first factor, 0 = auto (A/B: PM_NTT_LOG1 env)
   int ntt_maxlogc = 2; // most columns / rows per block, log2 (A/B: PM_NTT_MAXLOGC env)
   int ntt_threads2 = 512, ntt_threads3 = 256;  // NTT threads per block, one / two-pass and three-pass forms (A/B: PM_NTT_THREADS2 / 3; profiles/r03/ntt_f29/threads_ab3.jsonl)
-  int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split, PM_ACC_SPLIT env)
+  int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split)
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)
   bool timed(const char* name) const { return timing && (timing_filter.empty() || timing_filter == name); }
@@ -224,8 +228,6 @@ struct pm_ctx {
   // staging threads round 2 measured, ~38 GB/s, and retired)
   int upload_h2d(void* d, const void* h, size_t bytes, hipStream_t st);
   int ensure_group_events(int n);
-  int ensure_copy_events(int n);
-  int copy_wait_for(hipStream_t st);
   pm::HostPool& host_pool();
   hipEvent_t next_event();
   void mark(const char* name, hipEvent_t a, hipEvent_t b);
@@ -289,19 +291,11 @@ int CachedUpload::put(const std::vector<T>& v, hipStream_t st, size_t pad) {
   return PM_OK;
 }
 
-// Wait for `ev` on the host: the runtime's blocking wait, or (PM_SPIN_WAIT=1)
-// a hipEventQuery poll.  Polling measured within run-to-run noise (2^19-2^22
-// MSM, accumulator, bench; profiles/r03/ab/spin_wait/), so it stays off and
-// leaves the host core to the caller.
-inline int wait_event(const pm_ctx* ctx, hipEvent_t ev) {
-  if (!ctx->spin_wait) {
-    HIP_TRY(hipEventSynchronize(ev));
-    return PM_OK;
-  }
-  hipError_t q;
-  while ((q = hipEventQuery(ev)) == hipErrorNotReady) {
-  }
-  HIP_TRY(q);
+// Wait for `ev` on the host: the runtime's blocking wait (a hipEventQuery
+// poll measured within run-to-run noise and burns a host core, round 3:
+// profiles/r03/ab/spin_wait/).
+inline int wait_event(const pm_ctx*, hipEvent_t ev) {
+  HIP_TRY(hipEventSynchronize(ev));
   return PM_OK;
 }
 }  // namespace pm

@@ -223,6 +223,7 @@ def _load():
         "pm_ctx_dropin_stats": ([_vp, _u64p, _u64p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)],
                                 ctypes.c_int),
         "pm_ctx_dropin_clear": ([_vp], ctypes.c_int),
+        "pm_ctx_dropin_key_id": ([_vp, _u64p], ctypes.c_int),
         "pm_msm": ([ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_msm_ctx": ([_vp, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_msm_device": ([_vp, ctypes.c_int, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
@@ -546,6 +547,13 @@ class Context:
 
     def dropin_clear(self):
         _check(lib().pm_ctx_dropin_clear(self.h))
+
+    def dropin_key_id(self):
+        """pm_ctx_dropin_key_id: a fingerprint (2 x u64) of this context's
+        secret digest key; distinct contexts hold distinct keys."""
+        out = np.zeros(2, dtype=np.uint64)
+        _check(lib().pm_ctx_dropin_key_id(self.h, out.ctypes.data_as(_u64p)))
+        return (int(out[0]), int(out[1]))
 
     def msm(self, curve, coeffs, bases, canonical=False):
         """pm_msm_ctx: host scalars and host bases (the transparent

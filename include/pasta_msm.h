@@ -118,21 +118,31 @@ int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, 
  * computes any n. */
 #define PM_MSM_GPU_MIN_N 4
 /* Same, on an explicit context (host pointers).
- * Drop-in base cache: from 4096 points on, pm_msm / pm_msm_ctx keep each base
- * set they see resident on the device (converted, with the row table from
- * 2^18 points, like pm_bases_upload), keyed by (curve, n, a 64-bit content
- * digest of the base bytes computed on host threads while the scalars are
- * copied).  A repeated set -- halo2's commits against params.g /
- * params.g_lagrange -- then costs only its scalars' transfer; changed bytes
- * (at the same address or not) miss and re-upload.  At most 4 sets / 16 GiB
- * per context, least recently used evicted.  The digest is not
- * cryptographic (it does not defend against forged collisions). */
+ * Drop-in base cache: from 4096 points on, pm_msm / pm_msm_ctx keep the base
+ * sets they see repeatedly resident on the device (converted, with the row
+ * table from 2^18 points, like pm_bases_upload), keyed by (curve, n, a keyed
+ * 254-bit digest of the base bytes computed on host threads while the
+ * scalars are copied).  A set is admitted on its SECOND sighting (the first
+ * call runs the plain pipeline on uploaded bases), so one-shot bases never
+ * pay the resident build; a repeated set -- halo2's commits against params.g
+ * / params.g_lagrange -- then costs only its scalars' transfer.  Changed
+ * bytes (at the same address or not) miss.  The digest is a universal hash
+ * (NH + two polynomial layers over GF(2^127 - 1)) under a secret key drawn
+ * per context from the OS RNG and never returned: a caller cannot construct
+ * two base sets that collide except with probability ~2^-128.  At most 4 sets,
+ * min(16 GiB, half the free device memory) per context, least recently used
+ * evicted before a new set is built; if the build still runs out of memory
+ * every set is released and, failing that, the call runs the plain pipeline. */
 int pm_msm_ctx(pm_ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
                uint32_t flags, uint64_t out[8]);
 /* Drop-in cache counters of ctx (any pointer may be NULL), and a way to
  * release its sets early. */
 int pm_ctx_dropin_stats(pm_ctx* ctx, uint64_t* hits, uint64_t* misses, int* entries, size_t* device_bytes);
 int pm_ctx_dropin_clear(pm_ctx* ctx);
+/* A fingerprint of ctx's secret digest key (16 bytes of BLAKE2b of the key,
+ * personal "pm-dropin-key-id"): distinct contexts hold distinct keys.  It
+ * reveals nothing about the key itself. */
+int pm_ctx_dropin_key_id(pm_ctx* ctx, uint64_t out[2]);
 /* Same, with scalars and bases already in device memory of ctx's device. */
 int pm_msm_device(pm_ctx* ctx, int curve, const void* d_scalars, const void* d_bases, size_t n,
                   uint32_t flags, uint64_t out[8]);

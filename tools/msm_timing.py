@@ -17,7 +17,6 @@ def main():
     curve = int(os.environ.get("CURVE", "0"))
     sizes = [int(x) for x in os.environ.get("LOGN", "16,18,20,22").split(",")]
     cs = [int(x) for x in os.environ.get("WINDOWS", "0").split(",")]
-    gs = [int(x) for x in os.environ.get("PM_SWEEP_GROUPS", "0").split(",")]
     mcs = [int(x) for x in os.environ.get("PM_SWEEP_MINCHUNK", "0").split(",")]
     ctx = H.Context(0)
     nmax = 1 << max(sizes)
@@ -37,9 +36,9 @@ def main():
                 return ctx.msm_resident_device(rb, 0, s.data_ptr(), n)
             return ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
 
-        for c, G, mc in [(c, G, mc) for c in cs for G in gs for mc in mcs]:
+        for c, mc in [(c, mc) for c in cs for mc in mcs]:
             ctx.set_window(c)
-            ctx.set_pipeline(G, mc)
+            ctx.set_pipeline(0, mc)  # one window group (groups > 1 retired)
             ctx.set_timing(False)
             run()
             reps = int(os.environ.get("REPS", "5"))
@@ -52,7 +51,7 @@ def main():
             for _ in range(reps):
                 run()
             ks = {k: round(ctx.kernel_stats(k)[1] / reps, 4) for k in KERNELS}  # per MSM (sum over groups)
-            print(json.dumps({"logn": lg, "c": c, "groups": G, "min_chunk": mc, "resident_rows": rb.rows if rb else 0,
+            print(json.dumps({"logn": lg, "c": c, "min_chunk": mc, "resident_rows": rb.rows if rb else 0,
                               "wall_ms": round(wall * 1e3, 3), "Mscalar_s": round(n / wall / 1e6, 2),
                               "kernels_ms": ks}), flush=True)
         if rb is not None:
