@@ -12,6 +12,7 @@
 #include "engine.hpp"
 #include "selftest.hpp"
 #include "transcript_kernels.hpp"
+#include "proof_kernels.hpp"
 
 namespace pm {
 
@@ -42,9 +43,13 @@ void push_fe(std::vector<uint32_t>& v, const Fe<Fs>& a) {
 template <class Cv>
 int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
                            const void* d_scalars, void* d_ch, void* d_status);
+// canon_ready: the canonical coordinates / scalars the replay hashes are
+// already in ctx->tr_canon (written by k_proof_decode), so k_tr_canon is
+// skipped; keep_status: OR the replay's bits into d_status (the decoder's)
 template <class Cv>
 int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
-                      const void* d_scalars, void* d_ch, void* d_status, hipStream_t st);
+                      const void* d_scalars, void* d_ch, void* d_status, hipStream_t st, bool canon_ready = false,
+                      bool keep_status = false);
 
 // Lanes per item for the latency-bound accumulator kernels: the largest
 // power of two 2^lg <= 2^maxlg that keeps items * 2^lg within about two
@@ -73,7 +78,8 @@ inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
 // with the replay and k_acc_scalars on the reduction stream.
 template <class Cv>
 int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d_points, const void* d_scalars,
-                      void* d_ch, void* d_out, void* d_hout, const uint64_t* vk_repr, void* d_status) {
+                      void* d_ch, void* d_out, void* d_hout, const uint64_t* vk_repr, void* d_status,
+                      bool canon_ready = false, bool keep_status = false) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
@@ -283,7 +289,9 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     side = ctx->red_stream;
     HIP_TRY(hipStreamWaitEvent(side, up, 0));
   }
-  if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side))) return rc;
+  if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side,
+                                             canon_ready, keep_status)))
+    return rc;
   // status: the replay stores bits 0-1 per proof, k_acc_scalars ORs in the
   // denominator bit; without a replay the words start at zero
   if (d_status && !vk_repr) HIP_TRY(hipMemsetAsync(d_status, 0, B * sizeof(uint32_t), side));
@@ -337,7 +345,8 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
 // (B, 7, 4) layout pm_accum_batch reads.
 template <class Cv>
 int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
-                      const void* d_scalars, void* d_ch, void* d_status, hipStream_t st) {
+                      const void* d_scalars, void* d_ch, void* d_status, hipStream_t st, bool canon_ready,
+                      bool keep_status) {
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
   AccLayout L;
@@ -387,11 +396,14 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
   // blocks fit one per CU; larger batches run without the ladder anyway
   const size_t tblocks = (B + kTrSlots - 1) / kTrSlots;
   const bool fence = tblocks <= 256;
-  PM_LAUNCH_ST(ctx, st, "transcript",
-            (k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
-                 (uint32_t)B, L.npts, L.nsc, (const uint32_t*)d_points, (const uint32_t*)d_scalars, cpts, cscs),
-             k_transcript<Cv><<<(unsigned)tblocks, 64, fence ? kAccScalarsLds : 0, st>>>(
-                 hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status)));
+  PM_LAUNCH_ST(ctx, st, "transcript", {
+    if (!canon_ready)
+      k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
+          (uint32_t)B, L.npts, L.nsc, (const uint32_t*)d_points, (const uint32_t*)d_scalars, cpts, cscs);
+    k_transcript<Cv><<<(unsigned)tblocks, 64, fence ? kAccScalarsLds : 0, st>>>(
+        hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status,
+        keep_status ? 1u : 0u);
+  });
   return PM_OK;
 }
 
@@ -399,6 +411,85 @@ template <class Cv>
 int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
                            const void* d_scalars, void* d_ch, void* d_status) {
   return transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, ctx->stream);
+}
+
+// Proof bytes -> the accumulator's inputs (proof_kernels.hpp), then, with
+// vk_repr, the fused transcript replay + accumulator on them.  Byte layout of
+// one proof (the verifier's read order, oracle/proof_bytes.py): the proof
+// points of the accumulator layout after the instance commitments (advice ..
+// h_{d-1}), every scalar, then the W_j.  d_points / d_scalars receive the
+// decoded layout (instance commitments copied from d_inst); d_status gets
+// PM_PROOF_BAD_POINT / _SCALAR per proof (and the replay's bits).
+template <class Cv>
+int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d_proofs, size_t stride,
+                       const void* d_inst, void* d_points, void* d_scalars, void* d_status, const uint64_t* vk_repr,
+                       void* d_ch, void* d_quads, void* d_h) {
+  std::vector<AccQuery> q;
+  AccLayout L;
+  const std::string err = acc_validate(s, q, L, nullptr);
+  if (!err.empty()) return set_error(PM_ERR_ARG, "proof shape: " + err);
+  if (B == 0) return PM_OK;
+  if (B > (1u << 20)) return set_error(PM_ERR_UNSUPPORTED, "proof batch larger than 2^20 proofs");
+  const uint32_t ninst = s->num_instance_columns, npp = L.p_W - ninst + L.nsets;
+  const size_t psize = 32ull * (L.npts - ninst + L.nsc);
+  if (stride < psize || (stride & 3u)) return set_error(PM_ERR_ARG, "proof stride below the proof size or not a multiple of 4");
+  if (stride * B > (size_t(1) << 40)) return set_error(PM_ERR_UNSUPPORTED, "proof batch too large");
+  const int slot = curve_slot<Cv>();
+  int rc;
+  const hipStream_t st = ctx->stream;
+  if (!ctx->sqrt_ready[slot]) {
+    SqrtTab tab;
+    if ((rc = sqrt_tab_build<Cv>(tab))) return rc;
+    if ((rc = ctx->sqrt_tab[slot].ensure(sizeof(SqrtTab)))) return rc;
+    HIP_TRY(hipMemcpy(ctx->sqrt_tab[slot].p, &tab, sizeof(SqrtTab), hipMemcpyHostToDevice));
+    ctx->sqrt_ready[slot] = true;
+  }
+  // (byte offset, destination point) of every point read from the bytes
+  std::vector<uint32_t> map;
+  const uint32_t sc_off = 32u * (L.p_W - ninst);
+  for (uint32_t i = ninst; i < L.p_W; i++) {
+    map.push_back(32u * (i - ninst));
+    map.push_back(i);
+  }
+  for (uint32_t j = 0; j < L.nsets; j++) {
+    map.push_back(sc_off + 32u * L.nsc + 32u * j);
+    map.push_back(L.p_W + j);
+  }
+  if ((rc = ctx->pf_map.put(map, st))) return rc;
+  const size_t ncoord = B * 2 * (size_t)L.npts, nall = ncoord + B * (size_t)L.nsc;
+  if ((rc = ctx->tr_canon.ensure(nall * 32))) return rc;
+  uint32_t* cpts = (uint32_t*)ctx->tr_canon.p;
+  uint32_t* cscs = cpts + 8 * ncoord;
+  HIP_TRY(hipMemsetAsync(d_status, 0, B * sizeof(uint32_t), st));
+  ProofDecodeHdr h{};
+  h.B = (uint32_t)B;
+  h.npts = L.npts;
+  h.nsc = L.nsc;
+  h.ninst = ninst;
+  h.npp = npp;
+  h.sc_off = sc_off;
+  h.stride = (uint32_t)stride;
+  h.nblk_pts = (uint32_t)((B * npp + kDecodeThreads - 1) / kDecodeThreads);
+  const size_t nblk_sc = (B * ((size_t)L.nsc + ninst) + kDecodeThreads - 1) / kDecodeThreads;
+  if (stride > 0xffffffffull) return set_error(PM_ERR_UNSUPPORTED, "proof stride above 4 GiB");
+  PM_LAUNCH(ctx, "proof_decode",
+            (k_proof_decode<Cv><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
+                h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
+                (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
+                cscs, (uint32_t*)d_status)));
+  if (!vk_repr) {
+    HIP_TRY(hipStreamSynchronize(st));
+    ctx->end_call();
+    return PM_OK;
+  }
+  return accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, true);
+}
+
+// the CurveOps entry (no extra parameters)
+template <class Cv>
+int accum_device_entry(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d_points, const void* d_scalars,
+                       void* d_ch, void* d_out, void* d_hout, const uint64_t* vk_repr, void* d_status) {
+  return accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_out, d_hout, vk_repr, d_status);
 }
 
 // vk_repr = from_bytes_wide(Blake2b("Halo2-Verify-Key", ...)) (verifier.rs:347-354)
@@ -426,18 +517,20 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
   extern const CurveOps name;                                                                  \
   const CurveOps name = {&msm_device_to_aff<Cv>, &point_add_impl<typename Cv::Base>,            \
                          &synth_scalars_impl<Cv>, &synth_bases_impl<Cv>,  \
-                         &accum_device_impl<Cv>, &selftest_field_impl<Cv>,           \
+                         &accum_device_entry<Cv>, &selftest_field_impl<Cv>,           \
                          &transcript_device_impl<Cv>, &vk_repr_impl<Cv>,                   \
                          &fixed_table_impl<Cv>, &ntt_device_impl<Cv>, &msm_fixed_to_aff<Cv>,    \
-                         &bases_to29_impl<Cv>, &msm_resident_batch_impl<Cv>};
+                         &bases_to29_impl<Cv>, &msm_resident_batch_impl<Cv>, &proofs_device_impl<Cv>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
   template int msm_device_to_aff<Cv>(Ctx*, const void*, const void*, size_t, uint32_t, uint64_t*, const void*); \
   template int synth_scalars_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, uint32_t, void*);     \
   template int synth_bases_impl<Cv>(Ctx*, uint64_t, uint64_t, uint32_t, void*);                 \
-  template int accum_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, void*, void*, \
-                                     void*, const uint64_t*, void*);                             \
+  template int accum_device_entry<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, const void*, void*, void*, \
+                                      void*, const uint64_t*, void*);                            \
+  template int proofs_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const void*, size_t, const void*, void*, \
+                                      void*, void*, const uint64_t*, void*, void*, void*);       \
   template int selftest_field_impl<Cv>(Ctx*, uint64_t, uint32_t, uint64_t*);                      \
   template int fixed_table_impl<Cv>(Ctx*, const void*, pm_fixed_bases*);                          \
   template int ntt_device_impl<Cv>(Ctx*, int, void*, uint32_t, const uint64_t*, const uint64_t*);  \

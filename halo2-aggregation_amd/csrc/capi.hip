@@ -1214,6 +1214,121 @@ int pm_accum_batch_transcript(pm_ctx* ctx, int curve, const pm_proof_shape* shap
                          out_status, true);
 }
 
+// ------------------------------------------------- proof bytes (read_point / read_scalar)
+int pm_proof_size(const pm_proof_shape* shape, size_t* bytes) {
+  if (!shape || !bytes) return set_error(PM_ERR_ARG, "null argument");
+  uint32_t npts = 0, nsc = 0, ns = 0;
+  int rc = pm_shape_layout(shape, &npts, &nsc, &ns);
+  if (rc) return rc;
+  *bytes = 32ull * (npts - shape->num_instance_columns + nsc);
+  return PM_OK;
+}
+
+int pm_decode_proofs_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_proofs,
+                            size_t stride, const void* d_instance_points, void* d_out_points, void* d_out_scalars,
+                            void* d_out_status) {
+  if (!ctx || !shape || (B && (!d_proofs || !d_out_points || !d_out_scalars || !d_out_status)) ||
+      (B && shape->num_instance_columns && !d_instance_points))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  return ops->proofs(ctx, shape, B, d_proofs, stride, d_instance_points, d_out_points, d_out_scalars, d_out_status,
+                     nullptr, nullptr, nullptr, nullptr);
+}
+
+int pm_accum_batch_proofs_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                                 const uint64_t vk_repr[4], const void* d_proofs, size_t stride,
+                                 const void* d_instance_points, void* d_challenges, void* d_out_quads,
+                                 void* d_out_h_eval, void* d_out_status) {
+  if (!ctx || !shape || !vk_repr || (B && (!d_proofs || !d_challenges || !d_out_quads)) ||
+      (B && shape->num_instance_columns && !d_instance_points))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  uint32_t npts = 0, nsc = 0, ns = 0;
+  int rc = pm_shape_layout(shape, &npts, &nsc, &ns);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (B == 0) return PM_OK;
+  if ((rc = ctx->begin_call())) return rc;
+  // decoded points / scalars (and the status words when the caller passes none) in context scratch
+  const size_t bp = B * npts * 64, bs = B * nsc * 32, bst = B * 4;
+  if ((rc = ctx->pf_io.ensure(bp + bs + bst))) return rc;
+  char* dp = (char*)ctx->pf_io.p;
+  return ops->proofs(ctx, shape, B, d_proofs, stride, d_instance_points, dp, dp + bp,
+                     d_out_status ? d_out_status : dp + bp + bs, vk_repr, d_challenges, d_out_quads, d_out_h_eval);
+}
+
+// Host-buffer variants: proofs | instance points | decoded points | decoded
+// scalars | challenges | quads | h_eval | status in pf_io.
+static int proofs_host(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t* vk_repr,
+                       const uint8_t* proofs, size_t stride, const uint64_t* inst, uint64_t* out_points,
+                       uint64_t* out_scalars, uint64_t* out_challenges, uint64_t* out_quads, uint64_t* out_h_eval,
+                       uint32_t* out_status) {
+  const bool accum = vk_repr != nullptr;
+  if (!ctx || !shape || (B && !proofs) || (B && shape->num_instance_columns && !inst) ||
+      (B && (accum ? !out_quads : (!out_points || !out_scalars))))
+    return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  uint32_t npts = 0, nsc = 0, ns = 0;
+  int rc = pm_shape_layout(shape, &npts, &nsc, &ns);
+  if (rc) return rc;
+  size_t psize = 0;
+  if ((rc = pm_proof_size(shape, &psize))) return rc;
+  if (stride < psize) return set_error(PM_ERR_ARG, "proof stride below the proof size");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (B == 0) return PM_OK;
+  if (B > (1u << 20)) return set_error(PM_ERR_UNSUPPORTED, "proof batch larger than 2^20 proofs");
+  if ((rc = ctx->begin_call())) return rc;
+  const size_t ni = shape->num_instance_columns;
+  const size_t bpf = (B * psize + 255) & ~size_t(255), bin = (B * ni * 64 + 255) & ~size_t(255);
+  const size_t bp = B * npts * 64, bs = B * nsc * 32, bc = B * 7 * 32, bo = B * 4 * 64, bh = B * 32, bst = B * 4;
+  if ((rc = ctx->pf_io.ensure(bpf + bin + bp + bs + bc + bo + bh + bst))) return rc;
+  char* dpf = (char*)ctx->pf_io.p;
+  char* din = dpf + bpf;
+  char* dp = din + bin;
+  char* ds = dp + bp;
+  char* dc = ds + bs;
+  char* dq = dc + bc;
+  char* dh = dq + bo;
+  char* dst = dh + bh;
+  // the proofs packed densely (stride = psize) for the device
+  if (stride == psize) {
+    HIP_TRY(hipMemcpyAsync(dpf, proofs, B * psize, hipMemcpyHostToDevice, ctx->stream));
+  } else {
+    HIP_TRY(hipMemcpy2DAsync(dpf, psize, proofs, stride, psize, B, hipMemcpyHostToDevice, ctx->stream));
+  }
+  if (ni) HIP_TRY(hipMemcpyAsync(din, inst, B * ni * 64, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = ops->proofs(ctx, shape, B, dpf, psize, din, dp, ds, dst, vk_repr, dc, dq, dh))) return rc;
+  if (out_points) HIP_TRY(hipMemcpyAsync(out_points, dp, bp, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_scalars) HIP_TRY(hipMemcpyAsync(out_scalars, ds, bs, hipMemcpyDeviceToHost, ctx->stream));
+  if (accum && out_challenges) HIP_TRY(hipMemcpyAsync(out_challenges, dc, bc, hipMemcpyDeviceToHost, ctx->stream));
+  if (accum) HIP_TRY(hipMemcpyAsync(out_quads, dq, bo, hipMemcpyDeviceToHost, ctx->stream));
+  if (accum && out_h_eval) HIP_TRY(hipMemcpyAsync(out_h_eval, dh, bh, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_status) HIP_TRY(hipMemcpyAsync(out_status, dst, bst, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return PM_OK;
+}
+
+int pm_decode_proofs(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint8_t* proofs,
+                     size_t stride, const uint64_t* instance_points, uint64_t* out_points, uint64_t* out_scalars,
+                     uint32_t* out_status) {
+  return proofs_host(ctx, curve, shape, B, nullptr, proofs, stride, instance_points, out_points, out_scalars, nullptr,
+                     nullptr, nullptr, out_status);
+}
+
+int pm_accum_batch_proofs(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4],
+                          const uint8_t* proofs, size_t stride, const uint64_t* instance_points,
+                          uint64_t* out_challenges, uint64_t* out_quads, uint64_t* out_h_eval, uint32_t* out_status) {
+  if (!vk_repr) return set_error(PM_ERR_ARG, "null argument");
+  return proofs_host(ctx, curve, shape, B, vk_repr, proofs, stride, instance_points, nullptr, nullptr,
+                     out_challenges, out_quads, out_h_eval, out_status);
+}
+
 // Proof batch sharded over several contexts (devices) in one process: proofs
 // are independent, so context k takes the contiguous range
 // [k*per, (k+1)*per) and runs the single-context host entry on it in its own

@@ -200,6 +200,12 @@ struct pm_ctx {
       win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, tr_canon, ntt_scratch2,
       acc_vkpow;
   pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
+  // proof-byte decoder (proof_kernels.hpp): square-root tables per curve
+  // (pm_curve order), the point map of the current shape, host staging
+  pm::Buf sqrt_tab[3];
+  bool sqrt_ready[3] = {false, false, false};
+  pm::CachedUpload pf_map;
+  pm::Buf pf_io;
   // accumulator: powers-of-two tables of the verifying key's points (fixed,
   // sigma, g1), built once per (curve, VK) and reused by every later batch
   std::vector<uint64_t> acc_vkpow_key;
@@ -217,7 +223,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io};
   }
   ~pm_ctx();
   int begin_call();
@@ -265,6 +271,11 @@ struct CurveOps {
   // (ft != nullptr: the resident bases' row table, pm_fixed_bases_create_rows)
   int (*msm_resident_batch)(Ctx* ctx, const void* d_bases29, const pm_fixed_bases* ft, const uint64_t* const* scalars,
                             size_t k, size_t n, uint32_t flags, uint64_t* out);
+  // proof bytes -> decoded points / scalars + status (proof_kernels.hpp); with
+  // vk_repr also the transcript replay + accumulator (pm_accum_batch_proofs*)
+  int (*proofs)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const void* d_proofs, size_t stride,
+                const void* d_inst, void* d_points, void* d_scalars, void* d_status, const uint64_t* vk_repr,
+                void* d_ch, void* d_quads, void* d_h);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

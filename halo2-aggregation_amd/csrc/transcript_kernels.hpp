@@ -289,7 +289,8 @@ template <class Cv>
 __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint32_t* __restrict__ prog,
                                                    const uint32_t* __restrict__ points,
                                                    const uint32_t* __restrict__ scalars,
-                                                   uint32_t* __restrict__ challenges, uint32_t* __restrict__ status) {
+                                                   uint32_t* __restrict__ challenges, uint32_t* __restrict__ status,
+                                                   uint32_t keep_status) {
   using Fs = typename Cv::Scalar;
   __shared__ TrBuf buf;
   const uint32_t slot = threadIdx.x >> 2, q = threadIdx.x & 3;
@@ -371,7 +372,7 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
 #pragma unroll
     for (int i = 0; i < 16; i++) cur[i] = nxt[i];
   }
-  if (status && q == 0) status[b] = st;
+  if (status && q == 0) status[b] = keep_status ? (status[b] | st) : st;
 }
 
 }  // namespace pm

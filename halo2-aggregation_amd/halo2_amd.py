@@ -32,6 +32,9 @@ LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
 # best_multiexp below still runs every n on the GPU: there is no CPU path here.
 MSM_GPU_MIN_N = 4
 ACCUM_CURVES = (PALLAS, VESTA, BN254)
+# per-proof status bits of the proof-byte entries (pm_*_proofs*)
+PROOF_BAD_POINT = 8
+PROOF_BAD_SCALAR = 16
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _vp = ctypes.c_void_p
@@ -279,6 +282,16 @@ def _load():
                                        _u64p, _u64p, _u64p, _u64p, _u64p, _u32p], ctypes.c_int),
         "pm_accum_batch_transcript_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t,
                                               _u64p, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
+        "pm_proof_size": ([ctypes.POINTER(PmProofShape), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "pm_decode_proofs": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, ctypes.c_char_p,
+                              ctypes.c_size_t, _u64p, _u64p, _u64p, _u32p], ctypes.c_int),
+        "pm_decode_proofs_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _vp,
+                                     ctypes.c_size_t, _vp, _vp, _vp, _vp], ctypes.c_int),
+        "pm_accum_batch_proofs": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p,
+                                   ctypes.c_char_p, ctypes.c_size_t, _u64p, _u64p, _u64p, _u64p, _u32p],
+                                  ctypes.c_int),
+        "pm_accum_batch_proofs_device": ([_vp, ctypes.c_int, ctypes.POINTER(PmProofShape), ctypes.c_size_t, _u64p,
+                                          _vp, ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         if not hasattr(L, name) and os.environ.get("PM_LIB"):
@@ -388,6 +401,13 @@ def vk_transcript_repr(curve, pinned: bytes):
     out = np.zeros(4, dtype=np.uint64)
     _check(lib().pm_vk_transcript_repr(curve, pinned, len(pinned), _p(out)))
     return out
+
+
+def proof_size(shape: ProofShape):
+    """pm_proof_size: bytes of one serialized proof of this shape."""
+    n = ctypes.c_size_t(0)
+    _check(lib().pm_proof_size(ctypes.byref(shape.c), ctypes.byref(n)))
+    return n.value
 
 
 def device_count():
@@ -682,6 +702,58 @@ class Context:
         _check(lib().pm_accum_batch_transcript_device(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk),
                                                       _vp(d_points), _vp(d_scalars), _vp(d_challenges),
                                                       _vp(d_quads), _vp(d_h or None), _vp(d_status or None)))
+
+    # ---- proof bytes (pm_*_proofs*): the reference's read_point / read_scalar
+    def _proof_bytes(self, shape: ProofShape, proofs, instance_points):
+        """proofs: (B, stride) u8 (or a list of bytes of equal length);
+        instance_points: (B, num_instance_columns, 8) u64 Montgomery affine."""
+        if isinstance(proofs, (list, tuple)):
+            proofs = np.frombuffer(b"".join(proofs), dtype=np.uint8).reshape(len(proofs), -1)
+        pf = np.ascontiguousarray(proofs, dtype=np.uint8)
+        B = pf.shape[0]
+        ni = shape.c.num_instance_columns
+        inst = np.ascontiguousarray(instance_points if instance_points is not None else np.zeros((B, ni, 8)),
+                                    dtype=np.uint64).reshape(B, ni, 8)
+        return pf, inst, B
+
+    def proof_size(self, shape: ProofShape):
+        return proof_size(shape)
+
+    def decode_proofs(self, shape: ProofShape, proofs, instance_points=None):
+        """pm_decode_proofs -> (points (B, npts, 8), scalars (B, nsc, 4), status (B,))."""
+        pf, inst, B = self._proof_bytes(shape, proofs, instance_points)
+        npts, nsc, _ = shape.layout()
+        pts = np.zeros((B, npts, 8), dtype=np.uint64)
+        scs = np.zeros((B, nsc, 4), dtype=np.uint64)
+        st = np.zeros(B, dtype=np.uint32)
+        _check(lib().pm_decode_proofs(self.h, shape.curve, ctypes.byref(shape.c), B,
+                                      pf.ctypes.data_as(ctypes.c_char_p), pf.shape[1], _p(inst), _p(pts), _p(scs),
+                                      st.ctypes.data_as(_u32p)))
+        return pts, scs, st
+
+    def accum_batch_proofs(self, shape: ProofShape, proofs, instance_points, vk_repr):
+        """pm_accum_batch_proofs -> (quads (B, 4, 8), h_eval (B, 4), challenges (B, 7, 4), status (B,))."""
+        pf, inst, B = self._proof_bytes(shape, proofs, instance_points)
+        vk = np.ascontiguousarray(vk_repr, dtype=np.uint64).reshape(4)
+        ch = np.zeros((B, 7, 4), dtype=np.uint64)
+        quads = np.zeros((B, 4, 8), dtype=np.uint64)
+        hev = np.zeros((B, 4), dtype=np.uint64)
+        st = np.zeros(B, dtype=np.uint32)
+        _check(lib().pm_accum_batch_proofs(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk),
+                                           pf.ctypes.data_as(ctypes.c_char_p), pf.shape[1], _p(inst), _p(ch),
+                                           _p(quads), _p(hev), st.ctypes.data_as(_u32p)))
+        return quads, hev, ch, st
+
+    def decode_proofs_device(self, shape: ProofShape, B, d_proofs, stride, d_inst, d_points, d_scalars, d_status):
+        _check(lib().pm_decode_proofs_device(self.h, shape.curve, ctypes.byref(shape.c), B, _vp(d_proofs), stride,
+                                             _vp(d_inst or None), _vp(d_points), _vp(d_scalars), _vp(d_status)))
+
+    def accum_batch_proofs_device(self, shape: ProofShape, B, vk_repr, d_proofs, stride, d_inst, d_challenges,
+                                  d_quads, d_h=0, d_status=0):
+        vk = np.ascontiguousarray(vk_repr, dtype=np.uint64).reshape(4)
+        _check(lib().pm_accum_batch_proofs_device(self.h, shape.curve, ctypes.byref(shape.c), B, _p(vk),
+                                                  _vp(d_proofs), stride, _vp(d_inst or None), _vp(d_challenges),
+                                                  _vp(d_quads), _vp(d_h or None), _vp(d_status or None)))
 
     def fft(self, curve, values, omega, scale=None):
         """pm_fft: natural-order NTT of values ((2^k, 4) u64 Montgomery) with

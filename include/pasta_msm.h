@@ -44,8 +44,10 @@ enum pm_status {
 /* ABI version: bumped on every change of a signature or of an argument's
  * meaning.  3 = round 3 (pm_ctx_set_stream(ctx, NULL) selects the context's
  * own stream again; the accumulator entries take the trailing out_status
- * argument).  A binding asserts pm_abi_version() == PM_ABI_VERSION at load. */
-#define PM_ABI_VERSION 3
+ * argument); 4 = round 4 (proof-byte entries pm_*_proofs*, the drop-in cache
+ * admits a base set on its second sighting under a keyed digest).  A binding
+ * asserts pm_abi_version() == PM_ABI_VERSION at load. */
+#define PM_ABI_VERSION 4
 
 typedef struct pm_ctx pm_ctx;     /* one device + one HIP stream + workspace */
 typedef struct pm_bases pm_bases; /* device-resident base points (SRS cache) */
@@ -417,6 +419,59 @@ int pm_accum_batch_transcript_device(pm_ctx* ctx, int curve, const pm_proof_shap
                                      const uint64_t vk_repr[4], const void* d_points, const void* d_scalars,
                                      void* d_challenges, void* d_out_quads, void* d_out_h_eval,
                                      void* d_out_status);
+
+/* ---- Proof bytes (SURVEY §8b boundary 2, from the serialized proofs) --------
+ * The reference verifier reads each inner proof from halo2's byte transcript
+ * (Blake2bRead): t.read_point() (src/verifier.rs:370, src/lookup.rs:64-65,96,
+ * src/permutation.rs:67, src/vanishing.rs:67,94, src/multiopen.rs:210) and
+ * t.read_scalar() (src/verifier.rs:443,456,469, src/vanishing.rs:122,
+ * src/permutation.rs:100-107,163, src/lookup.rs:124-128).  These entries take
+ * the proofs as those bytes and do the reads on the device, B proofs at once:
+ *   point  = 32 bytes: canonical little-endian x, bit 255 = parity of the
+ *            canonical y (GroupEncoding::to_bytes of pasta_curves /
+ *            pairing_bn256 [3P]); decompressed with a square root;
+ *   scalar = 32 bytes: canonical little-endian (PrimeField::to_repr).
+ * Byte layout of one proof, pm_proof_size() bytes: the proof points of the
+ * accumulator layout after the instance commitments (advice, per lookup A'
+ * and S', permutation Z_p, per lookup Z, vanishing r, h_0..h_{d-1}), then every
+ * scalar in the accumulator layout, then the multiopen witnesses W_0..W_{S-1}
+ * -- the verifier's read order.  Instance commitments do not travel in the
+ * proof (verifier.rs:312-316 takes them from the instance column); the caller
+ * passes them as affine Montgomery points, B x num_instance_columns x 8 u64.
+ * proofs: B proofs, proof i at byte i * stride (stride >= pm_proof_size; the
+ * device variants need stride % 4 == 0).
+ * Status bits (out_status), where the reference's read fails and it aborts:
+ *   PM_PROOF_BAD_POINT (8)   a point encoding is invalid: x not canonical,
+ *       x^3 + b a non-residue, or the identity (Blake2bRead's common_point
+ *       rejects it);
+ *   PM_PROOF_BAD_SCALAR (16) a scalar encoding is >= r.
+ * Such a proof's decoded slot holds the identity / zero and its quad is
+ * unspecified; the rest of the batch is unaffected. */
+#define PM_PROOF_BAD_POINT 8u
+#define PM_PROOF_BAD_SCALAR 16u
+int pm_proof_size(const pm_proof_shape* shape, size_t* bytes);
+/* Decode only: out_points B x points_per_proof x 8 (instance commitments
+ * copied in), out_scalars B x scalars_per_proof x 4, out_status B (required):
+ * the inputs of pm_accum_batch*. */
+int pm_decode_proofs(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint8_t* proofs,
+                     size_t stride, const uint64_t* instance_points, uint64_t* out_points, uint64_t* out_scalars,
+                     uint32_t* out_status);
+int pm_decode_proofs_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const void* d_proofs,
+                            size_t stride, const void* d_instance_points, void* d_out_points, void* d_out_scalars,
+                            void* d_out_status);
+/* Decode + transcript replay + accumulator in one call (pm_accum_batch_transcript
+ * on the decoded proofs; the decoded points and scalars stay on the device).
+ * out_challenges, out_h_eval and out_status may be NULL; the status words
+ * carry the decoder's bits as well as the replay's and PM_ACCUM_DENOM_ZERO. */
+int pm_accum_batch_proofs(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B, const uint64_t vk_repr[4],
+                          const uint8_t* proofs, size_t stride, const uint64_t* instance_points,
+                          uint64_t* out_challenges, uint64_t* out_quads, uint64_t* out_h_eval, uint32_t* out_status);
+/* Device-buffer variant; d_challenges: B x 7 x 4 caller scratch (receives the
+ * challenges); d_out_h_eval and d_out_status may be NULL. */
+int pm_accum_batch_proofs_device(pm_ctx* ctx, int curve, const pm_proof_shape* shape, size_t B,
+                                 const uint64_t vk_repr[4], const void* d_proofs, size_t stride,
+                                 const void* d_instance_points, void* d_challenges, void* d_out_quads,
+                                 void* d_out_h_eval, void* d_out_status);
 
 #ifdef __cplusplus
 }

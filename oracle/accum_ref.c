@@ -33,6 +33,14 @@
  * this path, src/lib.rs:43-44); pinned by agreement with oracle/accum.py and
  * oracle/transcript.py on every golden case.
  *
+ * Proof bytes (accum_ref_batch_proofs): halo2 Blake2bRead::read_point /
+ * read_scalar [3P] as restated in oracle/proof_bytes.py (the reference's
+ * reads: src/verifier.rs:370,443,456,469, src/lookup.rs:64-65,96,124-128,
+ * src/permutation.rs:67,100-107,163, src/vanishing.rs:67,94,122,
+ * src/multiopen.rs:210): point = canonical x with the y parity in bit 255,
+ * decompressed by a square root (a^((p+1)/4) for BN254, Tonelli-Shanks for
+ * Pasta), scalar = canonical < r; failures set status bits 8 / 16.
+ *
  * Build: oracle/Makefile -> oracle/libmsm_ref.so (with msm_ref.c). */
 #include "ec_ref.h"
 
@@ -727,6 +735,225 @@ int accum_ref_batch(int curve, const pm_proof_shape* s, size_t B, const u64* poi
     jobs[t] = (AccJob){&CURVES[curve], s, &L, points, scalars, challenges, vk_repr, out_challenges, out_quads,
                        out_h_eval, out_status, lo, hi, 0};
     pthread_create(&th[t], NULL, acc_worker, &jobs[t]);
+  }
+  int rc = 0;
+  for (int t = 0; t < num_threads; t++) {
+    pthread_join(th[t], NULL);
+    rc |= jobs[t].rc;
+  }
+  return rc;
+}
+
+/* ------------------------------------------------------- proof bytes */
+enum { ST_BAD_POINT = 8, ST_BAD_SCALAR = 16 };
+
+static void f_pow_words(const Field* F, u64 r[4], const u64 a[4], const u64 e[4]) {
+  u64 acc[4];
+  memcpy(acc, F->one, 32);
+  for (int i = 3; i >= 0; i--)
+    for (int b = 63; b >= 0; b--) {
+      f_mul(F, acc, acc, acc);
+      if ((e[i] >> b) & 1) f_mul(F, acc, acc, a);
+    }
+  memcpy(r, acc, 32);
+}
+static int f_eq(const u64 a[4], const u64 b[4]) { return !memcmp(a, b, 32); }
+static void shr1(u64 a[4]) {
+  for (int i = 0; i < 4; i++) a[i] = (a[i] >> 1) | (i < 3 ? a[i + 1] << 63 : 0);
+}
+/* per-curve constants of the decoder, computed once per batch */
+typedef struct {
+  u64 r2p[4], r2r[4]; /* R^2 mod p, mod r: canonical -> Montgomery */
+  u64 bm[4];          /* b, Montgomery */
+  u64 t[4], th[4];    /* p - 1 = 2^s t; (t - 1) / 2 */
+  u64 c[4];           /* z^t for the first non-residue z */
+  int s;
+} DecCtx;
+static void dec_init(const CurveDef* cv, DecCtx* d) {
+  const Field* F = &cv->fp;
+  u64 r3[4], one[4] = {1, 0, 0, 0}, half[4], mone[4], zc[4] = {2, 0, 0, 0}, z[4], e[4];
+  f_r2r3(F, d->r2p, r3);
+  f_r2r3(&cv->fr, d->r2r, r3);
+  u64 bc[4] = {(u64)cv->b, 0, 0, 0};
+  f_mul(F, d->bm, bc, d->r2p);
+  sub4(d->t, F->p, one);
+  memcpy(half, d->t, 32);
+  shr1(half);
+  d->s = 0;
+  while (!(d->t[0] & 1)) {
+    shr1(d->t);
+    d->s++;
+  }
+  memcpy(d->th, d->t, 32); /* t odd: (t - 1) / 2 = t >> 1 */
+  shr1(d->th);
+  memset(mone, 0, 32);
+  f_sub(F, mone, mone, F->one);
+  for (;; zc[0]++) {
+    f_mul(F, z, zc, d->r2p);
+    f_pow_words(F, e, z, half);
+    if (f_eq(e, mone)) break;
+  }
+  f_pow_words(F, d->c, z, d->t);
+}
+/* y with y^2 = a (Montgomery); 0 if a is a non-residue.  Tonelli-Shanks
+ * (for BN254 Fq, s = 1: y = a^((t+1)/2) = a^((p+1)/4)). */
+static int f_sqrt(const Field* F, const DecCtx* d, u64 y[4], const u64 a[4]) {
+  if (f_is_zero(a)) {
+    memset(y, 0, 32);
+    return 1;
+  }
+  u64 c[4], w[4], x[4], b[4];
+  memcpy(c, d->c, 32);
+  f_pow_words(F, w, a, d->th); /* a^((t-1)/2) */
+  f_mul(F, x, w, a);           /* a^((t+1)/2) */
+  f_mul(F, b, x, w);           /* a^t */
+  int m = d->s;
+  while (!f_eq(b, F->one)) {
+    int i = 0;
+    u64 bb[4];
+    memcpy(bb, b, 32);
+    while (!f_eq(bb, F->one)) {
+      f_mul(F, bb, bb, bb);
+      if (++i == m) return 0; /* b of order 2^m: a non-residue */
+    }
+    u64 g[4];
+    memcpy(g, c, 32);
+    for (int k = 0; k < m - i - 1; k++) f_mul(F, g, g, g);
+    m = i;
+    f_mul(F, c, g, g);
+    f_mul(F, x, x, g);
+    f_mul(F, b, b, c);
+  }
+  memcpy(y, x, 32);
+  return 1;
+}
+static void ld_words(u64 w[4], const uint8_t* p) {
+  for (int i = 0; i < 4; i++) w[i] = ld64(p + 8 * i);
+}
+/* read_point: 1 ok (aff Montgomery), 0 failed (identity written) */
+static int read_point(const CurveDef* cv, const DecCtx* d, const uint8_t* enc, u64* aff) {
+  const Field* F = &cv->fp;
+  u64 x[4];
+  ld_words(x, enc);
+  const int ysign = (int)(x[3] >> 63);
+  x[3] &= 0x7fffffffffffffffull;
+  memset(aff, 0, 64);
+  if (geq(x, F->p)) return 0;
+  if (f_is_zero(x) && !ysign) return 0; /* the identity: common_point fails */
+  u64 xm[4], rhs[4], y[4], yc[4];
+  f_mul(F, xm, x, d->r2p);
+  f_mul(F, rhs, xm, xm);
+  f_mul(F, rhs, rhs, xm);
+  f_add(F, rhs, rhs, d->bm);
+  if (!f_sqrt(F, d, y, rhs)) return 0;
+  from_mont(F, yc, y);
+  if ((int)(yc[0] & 1) != ysign) {
+    u64 zz[4] = {0, 0, 0, 0};
+    f_sub(F, y, zz, y);
+  }
+  memcpy(aff, xm, 32);
+  memcpy(aff + 4, y, 32);
+  return 1;
+}
+static int read_scalar(const Field* Fr, const DecCtx* d, const uint8_t* enc, u64* out) {
+  u64 v[4];
+  ld_words(v, enc);
+  if (geq(v, Fr->p)) {
+    memset(out, 0, 32);
+    return 0;
+  }
+  f_mul(Fr, out, v, d->r2r);
+  return 1;
+}
+/* one proof's bytes (+ instance points) -> the accumulator layout; status bits */
+static uint32_t decode_proof(const CurveDef* cv, const DecCtx* d, const pm_proof_shape* s, const Layout* L,
+                             const uint8_t* pf, const u64* inst, u64* pts, u64* scs) {
+  uint32_t st = 0;
+  const uint32_t ni = s->num_instance_columns;
+  memcpy(pts, inst, (size_t)64 * ni);
+  size_t off = 0;
+  for (uint32_t i = ni; i < L->p_W; i++, off += 32)
+    if (!read_point(cv, d, pf + off, pts + 8 * i)) st |= ST_BAD_POINT;
+  for (uint32_t k = 0; k < L->nsc; k++, off += 32)
+    if (!read_scalar(&cv->fr, d, pf + off, scs + 4 * k)) st |= ST_BAD_SCALAR;
+  for (uint32_t j = 0; j < L->nsets; j++, off += 32)
+    if (!read_point(cv, d, pf + off, pts + 8 * (L->p_W + j))) st |= ST_BAD_POINT;
+  return st;
+}
+
+typedef struct {
+  const CurveDef* cv;
+  const pm_proof_shape* s;
+  const Layout* L;
+  const DecCtx* dec;
+  const uint8_t* proofs;
+  size_t stride;
+  const u64 *inst, *vk;
+  u64 *out_ch, *quads, *hev, *out_pts, *out_scs;
+  uint32_t* status;
+  size_t lo, hi;
+  int rc;
+} PfJob;
+
+static void* pf_worker(void* arg) {
+  PfJob* j = arg;
+  const Layout* L = j->L;
+  u64* pts = malloc((size_t)64 * L->npts);
+  u64* scs = malloc((size_t)32 * (L->nsc ? L->nsc : 1));
+  if (!pts || !scs) {
+    j->rc = -1;
+    free(pts);
+    free(scs);
+    return NULL;
+  }
+  for (size_t b = j->lo; b < j->hi; b++) {
+    uint32_t st = decode_proof(j->cv, j->dec, j->s, L, j->proofs + j->stride * b,
+                               j->inst + (size_t)8 * j->s->num_instance_columns * b, pts, scs);
+    if (j->out_pts) memcpy(j->out_pts + (size_t)8 * L->npts * b, pts, (size_t)64 * L->npts);
+    if (j->out_scs) memcpy(j->out_scs + (size_t)4 * L->nsc * b, scs, (size_t)32 * L->nsc);
+    if (j->quads) {
+      u64 ch[7][4], h[4];
+      st |= replay(j->cv, j->s, L, pts, scs, j->vk, ch);
+      if (j->out_ch) memcpy(j->out_ch + 28 * b, ch, sizeof(ch));
+      const uint32_t a = accum_one(j->cv, j->s, L, pts, scs, ch, j->quads + 32 * b, h);
+      if (a == 0xffffffffu) {
+        j->rc = -1;
+        break;
+      }
+      st |= a;
+      if (j->hev) memcpy(j->hev + 4 * b, h, 32);
+    }
+    if (j->status) j->status[b] = st;
+  }
+  free(pts);
+  free(scs);
+  return NULL;
+}
+
+/* B serialized proofs (stride bytes apart) + instance commitments -> decoded
+ * layout (out_points / out_scalars may be NULL) and, with vk_repr and
+ * out_quads, the replay + accumulator of every proof.  0 on success. */
+int accum_ref_batch_proofs(int curve, const pm_proof_shape* s, size_t B, const uint8_t* proofs, size_t stride,
+                           const u64* inst, const u64* vk_repr, int num_threads, u64* out_points, u64* out_scalars,
+                           u64* out_challenges, u64* out_quads, u64* out_h_eval, uint32_t* out_status) {
+  if (curve < 0 || curve > 2 || !s || num_threads < 1 || (out_quads && !vk_repr)) return -1;
+  Layout L;
+  if (make_layout(s, &L)) return -1;
+  if (B == 0) return 0;
+  if (num_threads > 256) num_threads = 256;
+  if ((size_t)num_threads > B) num_threads = (int)B;
+  pthread_t th[256];
+  PfJob jobs[256];
+  DecCtx dec;
+  dec_init(&CURVES[curve], &dec);
+  const size_t per = (B + num_threads - 1) / num_threads;
+  for (int t = 0; t < num_threads; t++) {
+    size_t lo = per * t, hi = per * (t + 1);
+    if (lo > B) lo = B;
+    if (hi > B) hi = B;
+    jobs[t] = (PfJob){&CURVES[curve], s, &L, &dec, proofs, stride, inst, vk_repr, out_challenges, out_quads, out_h_eval,
+                      out_points, out_scalars, out_status, lo, hi, 0};
+    pthread_create(&th[t], NULL, pf_worker, &jobs[t]);
   }
   int rc = 0;
   for (int t = 0; t < num_threads; t++) {
