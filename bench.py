@@ -19,14 +19,16 @@ warm), `small_n` its latency against the C port for n = 2^0 .. 2^16.
 on the host cores of the same box, on the same inputs, at N=1 on rank 0.
 
 `accumulator` is the second half of the BASELINE metric ("aggregated proofs
-verified/s"): each rank replays the Blake2b transcript of its own B = 256
-synthetic simple-example proofs and runs the batch multiopen accumulator on the
-replayed challenges (pm_accum_batch_transcript_device, SURVEY §8 rows
-a-3..a-9 + §8f-2; BN254, k = 17; weak scaling, proofs are independent),
-followed by an all-gather of the B x 4 accumulator points over RCCL.  Its
-cpu_baseline is the C restatement of the transcript replay + accumulator
-(oracle/accum_ref.c, all host threads) over the GPU's whole batch, with a
-bit-exact check of every proof's challenges, quad and h_eval.
+verified/s"): each rank takes its own B = 256 synthetic simple-example proofs
+as serialized bytes in HBM, decodes them on the device (point decompression,
+canonical checks: halo2's read_point / read_scalar), replays the Blake2b
+transcript and runs the batch multiopen accumulator on the replayed challenges
+(pm_accum_batch_proofs_device, SURVEY §8 rows a-3..a-9 + §8f-2; BN254, k = 17;
+weak scaling, proofs are independent), followed by an all-gather of the B x 4
+accumulator points over RCCL.  Its cpu_baseline is the C restatement of the
+same work from the same bytes (oracle/accum_ref.c, all host threads) over the
+GPU's whole batch, with a bit-exact check of every proof's challenges, quad and
+h_eval.
 """
 import argparse
 import json
@@ -772,7 +774,13 @@ def ntt_cpu_baseline(curve, k, src, w, first, budget_s):
 
 
 def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
-    """Batch multiopen accumulator: B proofs per rank, timed like the MSM leg."""
+    """Batch multiopen accumulator: B proofs per rank, timed like the MSM leg.
+    One step starts from the proofs' BYTES, resident in HBM as halo2's
+    Blake2bWrite serialized them: device decode (read_point decompression /
+    read_scalar checks), transcript replay, scalar block and accumulator quad
+    (pm_accum_batch_proofs_device), then the all-gather of the quads.
+    `from_decoded` times the same batch from already-decoded points (the
+    round-3 boundary, pm_accum_batch_transcript_device) for comparison."""
     import numpy as np
     import torch
 
@@ -782,57 +790,76 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
     curve, B, logn = H.BN254, B or args.accum_batch, logn or args.accum_logn
     shape = Wk.simple_example_shape(ctx, curve, logn)
     batch = Wk.SyntheticBatch(ctx, shape, B, i0=rank * B)
+    batch.to_proof_bytes(shape)
     from sharded import gather_batches
 
     gathered = [torch.zeros_like(batch.quads) for _ in range(world)] if dist else None
 
     def step():
+        batch.run_bytes(ctx, shape)
+        gather_batches(batch.quads, dist, world, gathered)
+
+    def step_decoded():
         batch.run(ctx, shape)
         gather_batches(batch.quads, dist, world, gathered)
 
-    for _ in range(args.warmup):
-        step()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kernels = kernel_breakdown(ctx, step, ("transcript", "acc_ladder", "acc_scalars", "acc_termmul", "acc_sum"))
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms = elapsed * 1e3 / args.steps
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el * 1e3 / args.steps
+
+    ms_dec = timed(step_decoded)
+    quads_dec = batch.quads.clone()
+    ms = timed(step)
+    kernels = kernel_breakdown(ctx, step, ("proof_decode", "transcript", "acc_ladder", "acc_scalars",
+                                            "acc_termmul", "acc_sum"))
     out = {"metric": "aggregated proofs verified/s", "value": round(world * B / (ms * 1e-3), 1), "unit": "proofs/s",
            "ms_per_batch": round(ms, 4), "higher_is_better": True, "scaling": "weak",
            "config": {"workload": f"multiopen_accumulator_simple_example_k{logn}", "curve": "bn254",
-                      "proofs_per_gpu": B, "proofs_total": world * B,
-                      "challenges": "Blake2b transcript replayed on the device (pm_accum_batch_transcript_device)",
-                      "per_proof_work": "transcript replay + scalar block + multiopen accumulator quad (w, zw, f, e) "
-                                        "and h_eval, status checked; the pairing / decider check on the quads is not "
-                                        "part of the reference's verifier circuit either (verifier.rs:739-754 exposes "
-                                        "the quad as instances)",
+                      "proofs_per_gpu": B, "proofs_total": world * B, "proof_bytes": batch.psize,
+                      "input": "serialized proofs in HBM (halo2 Blake2bWrite byte layout) + instance commitments",
+                      "challenges": "Blake2b transcript replayed on the device (pm_accum_batch_proofs_device)",
+                      "per_proof_work": "point decompression (square roots) + canonical checks, transcript replay, "
+                                        "scalar block, multiopen accumulator quad (w, zw, f, e) and h_eval, status "
+                                        "checked; the pairing / decider check on the quads is not part of the "
+                                        "reference's verifier circuit either (verifier.rs:739-754 exposes the quad "
+                                        "as instances)",
                       "parallelism": f"proof-batch x{world} + RCCL all-gather of B x 4 points"},
            "kernels_ms": kernels,
-           "status_nonzero": int((batch.status != 0).sum().item())}
+           "status_nonzero": int((batch.status != 0).sum().item()),
+           "from_decoded": {"ms_per_batch": round(ms_dec, 4), "value": round(world * B / (ms_dec * 1e-3), 1),
+                            "entry": "pm_accum_batch_transcript_device (decoded points / scalars in HBM)",
+                            "quads_match_bytes_path": bool(torch.equal(quads_dec, batch.quads))}}
     if rank == 0:
         host = {k: getattr(batch, k).cpu().numpy().view(np.uint64)
                 for k in ("points", "scalars", "challenges", "quads", "h_eval")}
         host["vk_repr"] = np.asarray(batch.vk_repr, dtype=np.uint64)
+        host["proofs"] = batch.proofs.cpu().numpy()
+        host["inst"] = batch.inst.cpu().numpy().view(np.uint64)
         out["_state"] = (curve, shape, host, B)
     return out
 
 
 def accum_cpu_baseline(curve, shape, host, B, budget_s):
-    """C restatement of the accumulator + transcript replay (oracle/accum_ref.c,
-    all host threads) on the GPU's own batch: bit-exact check of every
-    proof's challenges, quads and h_eval, and throughput over repeated passes
-    of the batch within the budget."""
+    """C restatement of the same work from the same bytes (oracle/accum_ref.c:
+    proof decoding with square roots, transcript replay, accumulator; all host
+    threads) on the GPU's own batch: bit-exact check of every proof's
+    challenges, quads and h_eval, and throughput over repeated passes of the
+    batch within the budget."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -842,20 +869,21 @@ def accum_cpu_baseline(curve, shape, host, B, budget_s):
     reps, t0 = 0, time.perf_counter()
     match = None
     while True:
-        ch, q, h, st = accum_ref.accum_batch(curve, shape.c, host["points"], host["scalars"],
-                                             vk_repr=host["vk_repr"], threads=threads)
+        o = accum_ref.batch_proofs(curve, shape.c, host["proofs"], host["inst"], vk_repr=host["vk_repr"],
+                                   threads=threads)
         if match is None:
-            match = bool(np.array_equal(ch.reshape(host["challenges"].shape), host["challenges"])
-                         and np.array_equal(q.reshape(host["quads"].shape), host["quads"])
-                         and np.array_equal(h.reshape(host["h_eval"].shape), host["h_eval"]) and not st.any())
+            match = bool(np.array_equal(o["challenges"].reshape(host["challenges"].shape), host["challenges"])
+                         and np.array_equal(o["quads"].reshape(host["quads"].shape), host["quads"])
+                         and np.array_equal(o["h_eval"].reshape(host["h_eval"].shape), host["h_eval"])
+                         and not o["status"].any())
         reps += 1
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
     return {"value": round(reps * B / dt, 2), "unit": "proofs/s", "cores": threads, "kind": "port",
             "host": cpu_info(),
-            "sample": f"{reps} x the GPU's batch of {B} proofs through oracle/accum_ref.c (Blake2b replay + "
-                      f"accumulator in C, {threads} threads, {dt:.1f} s)",
+            "sample": f"{reps} x the GPU's batch of {B} serialized proofs through oracle/accum_ref.c (decode + "
+                      f"Blake2b replay + accumulator in C, {threads} threads, {dt:.1f} s)",
             "matches_gpu": match}
 
 

@@ -345,10 +345,6 @@ int pm_ctx_create(int device, pm_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->red_stream, hipStreamNonBlocking));
   pm::digest_key_init(c->dropin_key);
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
-  if (const char* e = std::getenv("PM_NTT_LOG1")) c->ntt_log1 = std::atoi(e);
-  if (const char* e = std::getenv("PM_NTT_MAXLOGC")) c->ntt_maxlogc = std::max(0, std::min(4, std::atoi(e)));
-  if (const char* e = std::getenv("PM_NTT_THREADS2")) c->ntt_threads2 = std::atoi(e) == 512 ? 512 : 256;
-  if (const char* e = std::getenv("PM_NTT_THREADS3")) c->ntt_threads3 = std::atoi(e) == 512 ? 512 : 256;
   if (const char* e = std::getenv("PM_FINE_CACHE_KB")) c->fine_cache_kb = std::max(0, std::min(144, std::atoi(e)));
   if (const char* e = std::getenv("PM_FINE_CHUNK_KB")) c->fine_chunk_kb = std::max(0, std::min(144, std::atoi(e)));
   *out = c.release();

@@ -17,9 +17,10 @@
 // planes of the radix-2^29 form at XOR-swizzled positions, lds_swz), the last
 // round in registers on the way out (ntt_last_store).  A workgroup takes C
 // adjacent columns (pass A) or rows (pass B) so its global loads / stores
-// move C x 32 contiguous bytes.  All roots come from one table tw[i] =
-// omega^i (R = 2^261 form), i < n/2, built once per (field, omega, log_n) and
-// cached in the context (omega^{n/2} = -1 covers the upper half).
+// move C x 32 contiguous bytes.  Roots come from small per-transform tables
+// (R = 2^261 form), built once per (field, omega, log_n) and cached in the
+// context: one segment of L/2 powers per sub-transform, and the inter-pass
+// twiddles as a two-level product (k_ntt_twiddles below).
 #pragma once
 #include "msm_kernels.hpp"
 
@@ -65,20 +66,38 @@ __device__ __forceinline__ Fe<Fs> fe_of(const FeArg& a) {
 // passes elements are stored packed but not canonical (< 3p < 2^256); the
 // last pass canonicalises.
 
-// tw[i] = omega^i 2^261 mod p (canonical, packed) for i < half: one
-// square-and-multiply per entry in the R256 form, then the R261 conversion
+// Twiddle tables (round 4): instead of one flat table tw[i] = omega^i for
+// i < n/2 (512 MiB at 2^25, whose inter-pass gathers went to HBM: pass A
+// fetched 5.2 GB per 2^25 transform, profiles/r03/ntt_pmc/final_ntt25/),
+// each transform keeps small segments, all L2-resident:
+//   * per sub-transform of length L = 2^logL with root omega^step: its L/2
+//     powers (omega^step)^m, read with stride 1 (lds_ntt4 / ntt_load_first /
+//     ntt_last_store take the segment and tstride = 1);
+//   * the inter-pass twiddles omega^e (e < n) as lo[e mod 2^s] * hi[e >> s]
+//     (s = ceil(log n / 2): 2^13 + 2^12 entries at 2^25), one extra product.
+// k_ntt_twiddles fills segment s with omega^{(step_s k) mod n}, k < count_s,
+// by square-and-multiply per entry (R = 2^261 form, canonical, packed).
+constexpr int kNttMaxSegs = 5;
+struct NttSegs {
+  uint32_t off[kNttMaxSegs], count[kNttMaxSegs], step[kNttMaxSegs];
+  uint32_t nseg, logn;
+};
 template <class Fs>
-__global__ void __launch_bounds__(256) k_ntt_twiddles(FeArg omega, uint32_t half, uint32_t* __restrict__ tw) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= half) return;
+__global__ void __launch_bounds__(256) k_ntt_twiddles(FeArg omega, NttSegs sg, uint32_t* __restrict__ tw) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t s = 0;
+  while (s < sg.nseg && i >= sg.count[s]) i -= sg.count[s++];
+  if (s >= sg.nseg) return;
+  const uint64_t nmask = (1ull << sg.logn) - 1;
+  uint64_t e = ((uint64_t)sg.step[s] * i) & nmask;
   Fe<Fs> r = fe_one<Fs>(), b = fe_of<Fs>(omega);
-  for (uint32_t e = i; e; e >>= 1) {
+  for (; e; e >>= 1) {
     if (e & 1) r = fe_mul<Fs>(r, b);
     b = fe_sqr<Fs>(b);
   }
   Fe<Fs> o;
   f29_pack<Fs>(f29_canon<Fs>(f29_from_r256<Fs>(r.l)), o.l);
-  store_fe4<Fs>(reinterpret_cast<uint4*>(tw + 8ull * i), o);
+  store_fe4<Fs>(reinterpret_cast<uint4*>(tw + 8ull * (sg.off[s] + i)), o);
 }
 
 __device__ __forceinline__ uint32_t ntt_brev(uint32_t x, int bits) { return bits ? __brev(x) >> (32 - bits) : 0u; }
@@ -122,16 +141,16 @@ __device__ __forceinline__ void lds_st(uint32_t* sm, uint32_t plane, uint32_t id
   for (int k = 0; k < 9; k++) sm[k * plane + s] = v.l[k];
 }
 
-// twiddle omega^e (R261, Norm): e < half from the table, else its negation
-// (omega^{n/2} = -1) as 2p - w
+// twiddle m of a sub-transform segment (R261, Norm, canonical)
 template <class Fs>
 __device__ __forceinline__ F29<Fs> tw_half(const uint32_t* __restrict__ tw, size_t e) {
   return g_ld29<Fs>(tw, e);
 }
+// inter-pass twiddle omega^e, e < n: lo[e mod 2^s] hi[e >> s] (Norm, < 2p)
 template <class Fs>
-__device__ __forceinline__ F29<Fs> tw_full(const uint32_t* __restrict__ tw, uint32_t e, uint32_t half) {
-  if (e < half) return tw_half<Fs>(tw, e);
-  return f29_norm<Fs>(f29_sub<Fs>(f29_zero<Fs>(), tw_half<Fs>(tw, e - half), F29Consts<Fs>::K2));
+__device__ __forceinline__ F29<Fs> tw_two(const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
+                                          uint32_t e, int s) {
+  return f29_mul_c<Fs>(g_ld29<Fs>(lo, e & ((1u << s) - 1)), g_ld29<Fs>(hi, e >> s));
 }
 
 // lazy sum / difference -> Norm, < 3p
@@ -326,23 +345,26 @@ __device__ __forceinline__ uint32_t ntt_block(uint32_t nblocks) {
 
 // pass A: C = 2^logC adjacent columns per block.  last != 0: this is the
 // whole transform (one pass), so the output is canonicalised.
+// tw: the (omega^{n2})^m segment; lo / hi / s: the inter-pass twiddles
 template <class Fs>
 __global__ void __launch_bounds__(kNttMaxThreads) k_ntt_cols(const uint32_t* in, uint32_t* out,  // may alias
                                                           int logn, int log1, int logC,
-                                                          const uint32_t* __restrict__ tw, uint32_t last) {
+                                                          const uint32_t* __restrict__ tw,
+                                                          const uint32_t* __restrict__ lo,
+                                                          const uint32_t* __restrict__ hi, int s, uint32_t last) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int log2 = logn - log1;
-  const uint32_t n2 = 1u << log2, half = 1u << (logn - 1);
+  const uint32_t n2 = 1u << log2;
   const uint32_t col0 = ntt_block(n2 >> logC) << logC;
-  const int t0 = ntt_load_first<Fs>(sm, log1, logC, n2, tw, false, [&](uint32_t i1, uint32_t c) {
+  const int t0 = ntt_load_first<Fs>(sm, log1, logC, 1, tw, false, [&](uint32_t i1, uint32_t c) {
     return g_ld29<Fs>(in, (size_t)i1 * n2 + col0 + c);
   });
   __syncthreads();
   // root omega^{n2}
-  ntt_rounds_store<Fs>(sm, log1, logC, n2, tw, t0, [&] {
+  ntt_rounds_store<Fs>(sm, log1, logC, 1, tw, t0, [&] {
     return [&](uint32_t k1, uint32_t c, F29<Fs> v) {
       const uint32_t i2 = col0 + c;
-      if (log2 > 0 && i2 && k1) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, i2 * k1, half));  // i2 k1 < n
+      if (log2 > 0 && i2 && k1) v = f29_mul_c<Fs>(v, tw_two<Fs>(lo, hi, i2 * k1, s));  // i2 k1 < n
       if (last) v = f29_canon<Fs>(v);
       g_st29<Fs>(out, (size_t)k1 * n2 + i2, v);
     };
@@ -360,23 +382,25 @@ __global__ void __launch_bounds__(kNttMaxThreads) k_ntt_cols(const uint32_t* in,
 template <class Fs>
 __global__ void __launch_bounds__(kNttMaxThreads) k_ntt_mid(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                          int logn, int log1, int loga, int logC,
-                                                         const uint32_t* __restrict__ tw) {
+                                                         const uint32_t* __restrict__ tw,
+                                                         const uint32_t* __restrict__ lo,
+                                                         const uint32_t* __restrict__ hi, int s) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   const int logb = logn - log1 - loga;
-  const uint32_t n1 = 1u << log1, nb = 1u << logb, half = 1u << (logn - 1);
+  const uint32_t n1 = 1u << log1, nb = 1u << logb;
   const uint32_t groups = nb >> logC;  // column groups per row
   const uint32_t blk = ntt_block(n1 * groups);
   const uint32_t k1 = blk / groups, col0 = (blk - k1 * groups) << logC;
   const uint32_t* row = in + 8ull * ((size_t)k1 << (loga + logb));
-  const int t0 = ntt_load_first<Fs>(sm, loga, logC, n1 * nb, tw, false, [&](uint32_t ia, uint32_t c) {
+  const int t0 = ntt_load_first<Fs>(sm, loga, logC, 1, tw, false, [&](uint32_t ia, uint32_t c) {
     return g_ld29<Fs>(row, (size_t)ia * nb + col0 + c);
   });
   __syncthreads();
-  // root omega^{n1 nb}
-  ntt_rounds_store<Fs>(sm, loga, logC, n1 * nb, tw, t0, [&] {
+  // root omega^{n1 nb} (segment tw)
+  ntt_rounds_store<Fs>(sm, loga, logC, 1, tw, t0, [&] {
     return [&](uint32_t ka, uint32_t c, F29<Fs> v) {
       const uint32_t ib = col0 + c;
-      if (ib && ka) v = f29_mul_c<Fs>(v, tw_full<Fs>(tw, n1 * ib * ka, half));  // n1 ib ka < n
+      if (ib && ka) v = f29_mul_c<Fs>(v, tw_two<Fs>(lo, hi, n1 * ib * ka, s));  // n1 ib ka < n
       g_st29<Fs>(out, ((size_t)ka * n1 + k1) * nb + ib, v);
     };
   });
@@ -393,12 +417,12 @@ __global__ void __launch_bounds__(kNttMaxThreads) k_ntt_rows(const uint32_t* in,
   const int log1 = logn - log2;
   const uint32_t n1 = 1u << log1, L = 1u << log2;
   const uint32_t row0 = ntt_block(n1 >> logR) << logR;
-  const int t0 = ntt_load_first<Fs>(sm, log2, logR, n1, tw, true, [&](uint32_t i2, uint32_t r) {
+  const int t0 = ntt_load_first<Fs>(sm, log2, logR, 1, tw, true, [&](uint32_t i2, uint32_t r) {
     return g_ld29<Fs>(in, (size_t)(row0 + r) * L + i2);  // row-contiguous loads
   });
   __syncthreads();
-  // root omega^{n1}; adjacent rows -> adjacent outputs
-  ntt_rounds_store<Fs>(sm, log2, logR, n1, tw, t0, [&] {
+  // root omega^{n1} (segment tw); adjacent rows -> adjacent outputs
+  ntt_rounds_store<Fs>(sm, log2, logR, 1, tw, t0, [&] {
     const F29<Fs> sc = use_scale ? f29_from_r256<Fs>(scale.l) : f29_zero<Fs>();  // Norm, < 2p
     return [&, sc](uint32_t k2, uint32_t r, F29<Fs> v) {
       if (use_scale) v = f29_mul_c<Fs>(v, sc);

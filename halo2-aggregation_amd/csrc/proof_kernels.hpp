@@ -43,6 +43,7 @@
 #include "curve.hpp"
 #include "fp29.hpp"
 #include "msm_kernels.hpp"
+#include "runtime.hpp"
 
 namespace pm {
 

@@ -186,10 +186,7 @@ struct pm_ctx {
   // fine sort's LDS modes that only large segments reach): PM_FINE_CACHE_KB /
   // PM_FINE_CHUNK_KB, 0 = auto
   int fine_cache_kb = 0, fine_chunk_kb = 0;
-  int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (diagnostics: PM_NTT_PASSES env)
-  int ntt_log1 = 0;    // three-pass first factor, 0 = auto (A/B: PM_NTT_LOG1 env)
-  int ntt_maxlogc = 2; // most columns / rows per block, log2 (A/B: PM_NTT_MAXLOGC env)
-  int ntt_threads2 = 512, ntt_threads3 = 256;  // NTT threads per block, one / two-pass and three-pass forms (A/B: PM_NTT_THREADS2 / 3; profiles/r03/ntt_f29/threads_ab3.jsonl)
+  int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (test hook: PM_NTT_PASSES env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split)
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)
@@ -210,7 +207,7 @@ struct pm_ctx {
   // sigma, g1), built once per (curve, VK) and reused by every later batch
   std::vector<uint64_t> acc_vkpow_key;
   uint64_t acc_vkpow_gen = ~0ull;  // acc_vkpow.gen when the tables were built
-  std::vector<pm::NttTwiddles> ntt_tw;  // cached omega^i tables (pm_fft*)
+  std::vector<pm::NttTwiddles> ntt_tw;  // cached twiddle segments (pm_fft*)
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;  // MSM host terms: two slots (batch pipelining)
   size_t h_pinned_cap = 0;

@@ -103,6 +103,54 @@ class SyntheticBatch:
         ctx.synth_scalars(c, seed ^ 0xC4A1, i0 * 7, B * 7, self.challenges.data_ptr())
         torch.cuda.synchronize()
 
+    def to_proof_bytes(self, shape):
+        """Serialize the batch the way halo2's Blake2bWrite wrote it (the
+        verifier's read order, include/pasta_msm.h "Proof bytes"): proof
+        points compressed (canonical x, y parity in bit 255), scalars
+        canonical, W_j last; instance commitments stay separate.  Host-side,
+        untimed.  Sets self.proofs (B, psize) u8 and self.inst on the device."""
+        import torch
+
+        npts, nsc, nsets = shape.layout()
+        ni = shape.c.num_instance_columns
+        c = shape.curve
+        p, r = BASE_MODULUS[c], H.SCALAR_MODULUS[c]
+        rinv_p, rinv_r = pow(1 << 256, -1, p), pow(1 << 256, -1, r)
+        pts = self.points.cpu().numpy().view(np.uint64)
+        scs = self.scalars.cpu().numpy().view(np.uint64)
+
+        def val(limbs):
+            return int(limbs[0]) | int(limbs[1]) << 64 | int(limbs[2]) << 128 | int(limbs[3]) << 192
+
+        def enc_point(q):
+            x, y = val(q[:4]) * rinv_p % p, val(q[4:]) * rinv_p % p
+            return (x | (y & 1) << 255).to_bytes(32, "little")
+
+        pW = npts - nsets
+        out = bytearray()
+        for b in range(self.B):
+            for i in range(ni, pW):
+                out += enc_point(pts[b, i])
+            for k in range(nsc):
+                out += (val(scs[b, k]) * rinv_r % r).to_bytes(32, "little")
+            for j in range(nsets):
+                out += enc_point(pts[b, pW + j])
+        psize = len(out) // self.B
+        assert psize == H.proof_size(shape)
+        dev = self.points.device
+        self.psize = psize
+        self.proofs = torch.from_numpy(np.frombuffer(bytes(out), dtype=np.uint8).reshape(self.B, psize).copy()).to(dev)
+        self.inst = self.points[:, :ni, :].contiguous()
+        torch.cuda.synchronize()
+
+    def run_bytes(self, ctx, shape):
+        """One batch from its proof bytes: device decode (read_point /
+        read_scalar) + transcript replay + accumulator
+        (pm_accum_batch_proofs_device)."""
+        ctx.accum_batch_proofs_device(shape, self.B, self.vk_repr, self.proofs.data_ptr(), self.psize,
+                                      self.inst.data_ptr(), self.challenges.data_ptr(), self.quads.data_ptr(),
+                                      self.h_eval.data_ptr(), self.status.data_ptr())
+
     def run(self, ctx, shape, transcript=True):
         if transcript:
             ctx.accum_batch_transcript_device(shape, self.B, self.vk_repr, self.points.data_ptr(),

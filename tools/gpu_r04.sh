@@ -6,6 +6,7 @@
 #   quick  headline + accumulator legs only -> bench_quick.json
 #   kt     rocprofv3 --kernel-trace --stats of the headline-only bench
 #   acckt  rocprofv3 --kernel-trace --stats of the accumulator-only bench
+#   micro  tools/microbench_chain (built here beforehand): single-wave step latencies
 set -o pipefail
 TAG=${1:-r04}
 PARTS=${2:-"test smoke bench"}
@@ -43,6 +44,9 @@ for P in $PARTS; do
         $QUICK --logn 10 --accum-b16 1 > $OUT/acckt.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/acckt.log; exit 1; }
       find $OUT/acckt -name '*kernel_stats.csv' -exec cp {} $OUT/acc_kernel_stats.csv \;
       cut -c1-150 $OUT/acc_kernel_stats.csv | head -20 ;;
+    micro)
+      timeout -k 10 300 ./tools/microbench_chain > $OUT/chain_latency.jsonl 2>&1 || { cat $OUT/chain_latency.jsonl; exit 1; }
+      cat $OUT/chain_latency.jsonl ;;
   esac
 done
 echo "== done $(date +%T)"
