@@ -519,10 +519,19 @@ def run_dropin(args, curve, S, B, n, want):
         for _ in range(k):
             got = ctx.msm(curve, S, B)
         warm = (time.perf_counter() - t0) * 1e3 / k
+        # host-side phases of a warm call (separate, untimed calls): the keyed
+        # digest on the pool (start to join) and the scalar copy call beside it
+        ctx.set_timing(True, only="")
+        ctx.reset_stats()
+        for _ in range(3):
+            ctx.msm(curve, S, B)
+        ctx.set_timing(False)
+        phases = {k2: round(ctx.kernel_stats(k2)[1] / 3, 4) for k2 in ("dropin_digest", "dropin_copy_call", "h2d",
+                                                                          "accumulate")}
         st = ctx.dropin_stats()
         return {"call": "pm_msm_ctx(curve, host scalars, host bases, n)", "first_ms": round(first_ms, 3),
                 "admit_ms": round(admit_ms, 3), "warm_ms_per_msm": round(warm, 4),
-                "warm_Mscalar_s": round(n / (warm * 1e-3) / 1e6, 3), "cache": st,
+                "warm_Mscalar_s": round(n / (warm * 1e-3) / 1e6, 3), "warm_phases_ms": phases, "cache": st,
                 "matches": bool(np.array_equal(first, want) and np.array_equal(second, want)
                                 and np.array_equal(got, want))}
     finally:
@@ -827,6 +836,12 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
     ms = timed(step)
     kernels = kernel_breakdown(ctx, step, ("proof_decode", "transcript", "acc_ladder", "acc_scalars",
                                             "acc_termmul", "acc_sum"))
+    npts, nsc, nsets = shape.layout()
+    # MSM terms per proof (accum_engine.hpp): the distinct commitments of f (every
+    # proof point but the W_j, the fixed and sigma commitments: all queried in
+    # the simple-example shape) with the h_i, then W_j for w and zw, and g1 for e
+    nslots = (npts - nsets) + shape.c.num_fixed_columns + shape.c.n_perm_columns
+    T = nslots + 2 * nsets + 1
     out = {"metric": "aggregated proofs verified/s", "value": round(world * B / (ms * 1e-3), 1), "unit": "proofs/s",
            "ms_per_batch": round(ms, 4), "higher_is_better": True, "scaling": "weak",
            "config": {"workload": f"multiopen_accumulator_simple_example_k{logn}", "curve": "bn254",
@@ -840,6 +855,7 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
                                         "as instances)",
                       "parallelism": f"proof-batch x{world} + RCCL all-gather of B x 4 points"},
            "kernels_ms": kernels,
+           "roofline": accum_latency_roofline(B, T, nslots, ms, kernels),
            "status_nonzero": int((batch.status != 0).sum().item()),
            "from_decoded": {"ms_per_batch": round(ms_dec, 4), "value": round(world * B / (ms_dec * 1e-3), 1),
                             "entry": "pm_accum_batch_transcript_device (decoded points / scalars in HBM)",
@@ -852,6 +868,66 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
         host["inst"] = batch.inst.cpu().numpy().view(np.uint64)
         out["_state"] = (curve, shape, host, B)
     return out
+
+
+def accum_latency_roofline(B, T, nslots, ms_batch, kernels, from_bytes=True):
+    """Latency roofline of the accumulator batch (round 4): every kernel on the
+    main stream's critical path is a chain of dependent steps run by lone
+    waves, so its floor is (steps on its longest chain) x (that step's
+    single-wave latency measured in isolation by tools/microbench_chain.hip,
+    profiles/r04/chain_latency.jsonl); the batch floor is the sum over
+    decode -> ladder -> term additions -> sums (the transcript replay and the
+    scalar block run beside the ladder on the side stream and are shorter).
+    Step counts follow the engine's lane rules (accum_engine.hpp):
+      decode   1 square root + 6 products per point lane
+      ladder   127 quad-cooperative Jacobian doublings (k_acc_powers)
+      termadd  ceil(85.3 / S) full XYZZ additions (the mean NAF weight of the
+               two 127-bit GLV halves, dealt over S lanes) + log2(S) butterfly
+      sum      ceil(nslots / (NL/4)) + log2(NL/4) quad-cooperative additions,
+               one quad-cooperative inversion, 5 products
+    frac = floor / measured; per-kernel fractions against the kernels_ms
+    breakdown (HIP events)."""
+    p = os.path.join(ROOT, "profiles", "r04", "chain_latency.jsonl")
+    if not os.path.exists(p):
+        return None
+    lat = {}
+    for line in open(p):
+        line = line.strip()
+        if line.startswith("{"):
+            d = json.loads(line)
+            if "step" in d:
+                lat[d["step"]] = d["us_per_step"]
+    budget = 1024 * 2 * 64
+    nterm = B * T
+    lg = 0
+    while lg < 3 and (nterm << (lg + 1)) <= budget:
+        lg += 1
+    if lg == 3:
+        while lg < 5 and (nterm << (lg + 1)) <= budget // 2:
+            lg += 1
+    S = 1 << lg
+    lgL = 0
+    while lgL < 5 and ((B * 4) << (lgL + 1)) <= 16384:
+        lgL += 1
+    NL = 1 << lgL
+    nq = max(1, NL // 4)
+    floor = {
+        "proof_decode": lat["sqrt_bn254"] + 6 * lat["f29_mul"],
+        "acc_ladder": 127 * lat["ladder_dbl"],
+        "acc_termmul": (-(-85.3 // S) + lg) * lat["xyzz_add"],
+        "acc_sum": (-(-nslots // nq) + (nq.bit_length() - 1)) * lat["xyzz_add_q"] + lat["inv_q"] + 5 * lat["f29_mul"],
+    }
+    if not from_bytes:
+        floor.pop("proof_decode")
+    floor = {k: round(v / 1e3, 4) for k, v in floor.items()}
+    total = round(sum(floor.values()), 4)
+    return {"bound": "latency", "achieved": round(ms_batch, 4), "peak": total, "unit": "ms per batch (critical path)",
+            "frac": round(total / ms_batch, 4), "traffic": None,
+            "floor_ms": floor,
+            "kernel_frac": {k: round(floor[k] / kernels[k], 4) for k in floor if kernels.get(k)},
+            "lanes": {"term_additions_S": S, "sum_lanes_NL": NL},
+            "source": "profiles/r04/chain_latency.jsonl (tools/microbench_chain.hip, one wave per CU); "
+                      "PMC of the same kernels: profiles/r04/pmc_acc/"}
 
 
 def accum_cpu_baseline(curve, shape, host, B, budget_s):

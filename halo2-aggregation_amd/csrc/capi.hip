@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -725,13 +726,25 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
     }
   };
   const bool threaded = pool.size() > 1;
+  const auto t0 = std::chrono::steady_clock::now();
   if (threaded) pool.start(pool.size(), job);
   const int copy_rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream);
+  const auto t1 = std::chrono::steady_clock::now();
   if (threaded) pool.wait();
   else job(1, 1);
   if (copy_rc) return copy_rc;
   uint64_t d[4];
   pm::digest_combine(key, part.data(), nch, d);
+  if (ctx->timing) {  // host-side phases of the drop-in call (bench.py dropin_pm_msm)
+    const auto t2 = std::chrono::steady_clock::now();
+    auto add = [&](const char* k, double ms) {
+      auto& e = ctx->stats[k];
+      e.first += 1;
+      e.second += ms;
+    };
+    add("dropin_copy_call", std::chrono::duration<double, std::milli>(t1 - t0).count());
+    add("dropin_digest", std::chrono::duration<double, std::milli>(t2 - t0).count());
+  }
   pm_bases* b = nullptr;
   for (auto& e : ctx->dropin)
     if (same_key(e, curve, n, d)) {
