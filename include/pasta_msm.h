@@ -371,8 +371,9 @@ int pm_msm_fixed_device(pm_ctx* ctx, const pm_fixed_bases* fb, const void* d_sca
  * EvaluationDomain::ifft is pm_fft(omega_inv, scale = 1/n).  log_n <= 28
  * (create_proof at k = 23 transforms the extended domain, 2^25); above 2^22
  * the transform takes three passes and 2 n x 32 B of context scratch.  The
- * omega^i table (n/2 x 32 B) is cached in the context (4 most recent
- * (curve, log_n, omega)). */
+ * twiddle tables (each sub-transform's root powers and a two-level table of
+ * the inter-pass twiddles, ~0.4 MB at 2^25) are cached in the context (4 most
+ * recent (curve, log_n, omega)). */
 int pm_fft(pm_ctx* ctx, int curve, uint64_t* data, uint32_t log_n, const uint64_t omega[4], const uint64_t* scale);
 int pm_fft_device(pm_ctx* ctx, int curve, void* d_data, uint32_t log_n, const uint64_t omega[4],
                   const uint64_t* scale);
