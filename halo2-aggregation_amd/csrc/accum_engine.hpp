@@ -520,7 +520,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
                          &accum_device_entry<Cv>, &selftest_field_impl<Cv>,           \
                          &transcript_device_impl<Cv>, &vk_repr_impl<Cv>,                   \
                          &fixed_table_impl<Cv>, &ntt_device_impl<Cv>, &msm_fixed_to_aff<Cv>,    \
-                         &bases_to29_impl<Cv>, &msm_resident_batch_impl<Cv>, &proofs_device_impl<Cv>};
+                         &bases_to29_impl<Cv>, &msm_resident_batch_impl<Cv>, &proofs_device_impl<Cv>,    \
+                         &msm_small_impl<Cv>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
@@ -541,5 +542,6 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
                                            size_t, uint32_t, uint64_t*);                             \
   template int transcript_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const uint64_t*, const void*, \
                                           const void*, void*, void*);                            \
+  template int msm_small_impl<Cv>(Ctx*, const void*, bool, const void*, bool, bool, size_t, uint32_t, uint64_t*); \
   PM_OPS_TABLE(Cv, name)                                                                       \
   }

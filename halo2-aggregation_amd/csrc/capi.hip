@@ -66,6 +66,7 @@ pm_ctx::~pm_ctx() {
   for (pm::Buf* b : all_bufs()) b->release();
   for (auto& t : ntt_tw) t.buf.release();
   if (h_pinned) (void)hipHostFree(h_pinned);
+  if (small_pin) (void)hipHostFree(small_pin);
   for (auto& e : ev_pool) (void)hipEventDestroy(e);
   for (auto& e : grp_ev) (void)hipEventDestroy(e);
   for (auto& e : batch_ev)
@@ -190,6 +191,16 @@ int pm_ctx::ensure_pinned(size_t bytes) {
   return PM_OK;
 }
 
+int pm_ctx::ensure_small_pin(size_t bytes) {
+  if (bytes <= small_pin_cap) return PM_OK;
+  if (small_pin) (void)hipHostFree(small_pin);
+  small_pin = nullptr;
+  small_pin_cap = 0;
+  HIP_TRY(hipHostMalloc(&small_pin, bytes, hipHostMallocMapped));
+  small_pin_cap = bytes;
+  return PM_OK;
+}
+
 int pm_ctx::upload_h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
   hipEvent_t ta = nullptr, tb = nullptr;
   if (timed("h2d")) {
@@ -276,6 +287,10 @@ const CurveOps* curve_ops(int curve) {
     default: return nullptr;
   }
 }
+
+// the small-MSM path (msm_small.hpp) takes n <= small_max under the automatic
+// window (an explicit pm_ctx_set_window selects the sorting pipeline)
+bool use_small(const Ctx* ctx, size_t n) { return n <= ctx->small_max && ctx->window_c == 0; }
 
 // pre29: d_b holds resident bases already in the R = 2^261 form (pm_bases);
 // h_s != nullptr: the scalars are still on the host (d_s is their buffer)
@@ -398,6 +413,14 @@ int pm_ctx_set_window(pm_ctx* ctx, int c) {
   return PM_OK;
 }
 
+int pm_ctx_set_small_msm(pm_ctx* ctx, size_t max_n) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  if (max_n > kSmallLimit) return set_error(PM_ERR_ARG, "small-MSM threshold above PM_SMALL_MSM_LIMIT");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->small_max = max_n;
+  return PM_OK;
+}
+
 int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
   if (groups < 0 || min_chunk < 0 || min_chunk > (1 << 20)) return set_error(PM_ERR_ARG, "pipeline setting out of range");
@@ -467,6 +490,7 @@ int pm_msm_device(pm_ctx* ctx, int curve, const void* d_scalars, const void* d_b
   }
   int rc = ctx->begin_call();
   if (rc) return rc;
+  if (use_small(ctx, n)) return curve_ops(curve)->msm_small(ctx, d_scalars, false, d_bases, false, false, n, flags, out);
   return dispatch_msm_device(ctx, curve, d_scalars, d_bases, n, flags, out);
 }
 
@@ -621,6 +645,9 @@ static int msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const voi
     if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
     d_s = ctx->in_scalars.p;
   }
+  if (use_small(ctx, n))  // row 0 of a row table is the bases themselves
+    return curve_ops(b->curve)->msm_small(ctx, scalars, host, (const char*)b->d + offset * 64, false, true, n,
+                                          flags & ~kBasesR261, out);
   const void* h_s = host ? scalars : nullptr;
   if (resident_use_table(b, offset, n))
     return curve_ops(b->curve)->msm_fixed(ctx, b->table, d_s, n, flags & ~kBasesR261, out, h_s);
@@ -702,6 +729,7 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
   }
   int rc;
   if ((rc = ctx->begin_call())) return rc;
+  if (use_small(ctx, n)) return curve_ops(curve)->msm_small(ctx, scalars, true, bases, true, false, n, flags, out);
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
   auto plain = [&]() -> int {  // both inputs uploaded, plain pipeline
     int r;
@@ -1047,6 +1075,29 @@ uint64_t selftest_host_field(uint64_t seed, size_t n) {
     }
   }
   bad += memcmp(&h0, &h1, sizeof(h0)) != 0;
+  // Jacobian chain (jdbl / jadd, the small-MSM Horner) == the XYZZ chain: the
+  // same rational maps, so any (x, y) works; both start from the same point
+  // under a random z (Jacobian (X, Y, z), XYZZ (X, Y, z^2, z^3))
+  auto both = [&](Pt<P>& x, Jac<P>& j) {
+    const E<P> z = fe(), zz = mul<P>(z, z), zzz = mul<P>(zz, z);
+    x = Pt<P>{fe(), fe(), zz, zzz};
+    j = Jac<P>{x.X, x.Y, z};
+  };
+  Pt<P> xa, xg;
+  Jac<P> ja, jg;
+  both(xa, ja);
+  both(xg, jg);
+  for (size_t i = 0; i < 40; i++) {
+    xa = dbl<P, true>(xa);
+    ja = jdbl<P, true>(ja);
+    if (i % 3 == 0) {
+      xa = addp<P, true>(xa, xg);
+      ja = jadd<P, false>(ja, jg);
+    }
+  }
+  const Pt<P> jx = jac_to_xyzz<P, true>(ja);  // equal points: X1 ZZ2 == X2 ZZ1, Y1 ZZZ2 == Y2 ZZZ1
+  const E<P> l1 = mul<P>(xa.X, jx.ZZ), r1 = mul<P>(jx.X, xa.ZZ), l2 = mul<P>(xa.Y, jx.ZZZ), r2 = mul<P>(jx.Y, xa.ZZZ);
+  bad += memcmp(&l1, &r1, 32) != 0 || memcmp(&l2, &r2, 32) != 0 || is_zero(xa.ZZ);
   return bad;
 }
 }  // namespace

@@ -7,11 +7,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
 #include "host_ec.hpp"
 #include "msm_kernels.hpp"
+#include "msm_small.hpp"
 #include "runtime.hpp"
 
 // time a launch on stream `st_` when timing is enabled
@@ -440,6 +442,151 @@ int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint
   int rc = msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, (const uint32_t*)d_b, n, flags, &r, nullptr, nullptr, 0, h_s);
   if (rc) return rc;
   aff_to_u64<F>(xyzz_to_aff<F>(r), out);
+  return PM_OK;
+}
+
+// ------------------------------------------------------ small-MSM path
+// Host Horner over the 33 window sums of msm_small.hpp (Jacobian, X Y Z in
+// the first three coordinates of each slot): 128 doublings, 32 additions.
+template <class F, bool ADX>
+inline host::Pt<F> small_horner(const Xyzz<F>* W) {
+  auto jac = [&](int j) {
+    host::Jac<F> r;
+    std::memcpy(&r, &W[j], sizeof(r));
+    return r;
+  };
+  host::Jac<F> acc = jac(kSmallWin - 1);
+  for (int j = kSmallWin - 2; j >= 0; j--) {
+    for (int k = 0; k < 4; k++) acc = host::jdbl<F, ADX>(acc);
+    acc = host::jadd<F, ADX>(acc, jac(j));
+  }
+  if (host::is_zero(acc.Z)) return host::inf<F>();
+  return host::jac_to_xyzz<F, ADX>(acc);
+}
+template <class F>
+__attribute__((target("bmi2,adx"))) host::Pt<F> small_horner_bmi2(const Xyzz<F>* W) {
+  return small_horner<F, true>(W);
+}
+
+// n <= ctx->small_max: k_small_fused (2n <= 64 terms) or k_small_table +
+// k_small_sum (msm_small.hpp), then the host Horner.  Host inputs are copied
+// into a pinned mapped buffer that the first kernel reads directly (no DMA
+// copy and its launch latency); the 33 window sums land in mapped host
+// memory (no D2H copy), and the host spins on the completion flag the last
+// window raises instead of waiting for the kernel's completion signal
+// (falling back to the stream's event, which also surfaces a failed launch).
+template <class Cv>
+int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases, bool b_host, bool b_r261, size_t n,
+                   uint32_t flags, uint64_t out[8]) {
+  using F = typename Cv::Base;
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  if (n > kSmallLimit) return set_error(PM_ERR_UNSUPPORTED, "small-MSM path: n above its limit");
+  const hipStream_t st = ctx->stream;
+  const uint32_t un = (uint32_t)n, T = 2u * un;
+  const bool fused = T <= (uint32_t)kSmallQuads;
+  // slices per window: up to kSmallSlices blocks of 64 quads (or 256 lanes),
+  // each then adding kq terms serially
+  uint32_t kSmallSlices = 8;
+  if (const char* e = std::getenv("PM_SMALL_SLICES")) kSmallSlices = std::max(1, std::atoi(e));
+  bool lanes = T >= 4096u;
+  if (const char* e = std::getenv("PM_SMALL_LANES")) lanes = std::atoi(e) != 0;
+  const uint32_t per = lanes ? 256u : (uint32_t)kSmallQuads;  // terms per block and round
+  SmallGeom g{};
+  g.n = un;
+  g.canonical = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
+  g.r261 = b_r261 ? 1u : 0u;
+  g.kq = std::max<uint32_t>(1u, (T + per * kSmallSlices - 1) / (per * kSmallSlices));
+  g.ns = (T + per * g.kq - 1) / (per * g.kq);
+  int rc;
+  const uint32_t* ds = (const uint32_t*)scalars;
+  const uint32_t* db = (const uint32_t*)bases;
+  const auto tstage = std::chrono::steady_clock::now();
+  if (s_host || b_host) {
+    const size_t sb = s_host ? n * 32 : 0, bb = b_host ? n * 64 : 0;
+    if ((rc = ctx->ensure_small_pin(sb + bb))) return rc;
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, ctx->small_pin, 0));
+    if (s_host) {
+      std::memcpy(ctx->small_pin, scalars, sb);
+      ds = (const uint32_t*)dp;
+    }
+    if (b_host) {
+      std::memcpy((char*)ctx->small_pin + sb, bases, bb);
+      db = (const uint32_t*)((char*)dp + sb);
+    }
+  }
+  if (ctx->timing) {
+    auto& stt = ctx->stats["small_stage"];  // host copy into the pinned staging buffer
+    stt.first += 1;
+    stt.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tstage).count();
+  }
+  if (!fused) {
+    if ((rc = ctx->small_tab.ensure(n * kSmallMults * sizeof(Xyzz<F>)))) return rc;
+    if ((rc = ctx->small_dig.ensure((size_t)kSmallWin * T))) return rc;
+    if ((rc = ctx->small_part.ensure((size_t)kSmallWin * g.ns * sizeof(Xyzz<F>)))) return rc;
+  }
+  // counters (self-resetting; zero fresh allocations): a ticket per window, the done count
+  const size_t old_cap = ctx->small_tk.cap;
+  if ((rc = ctx->small_tk.ensure((kSmallWin + 1) * 4))) return rc;
+  if (ctx->small_tk.cap != old_cap) HIP_TRY(hipMemsetAsync(ctx->small_tk.p, 0, ctx->small_tk.cap, st));
+  uint32_t* tickets = (uint32_t*)ctx->small_tk.p;
+  if ((rc = ctx->ensure_pinned(kSmallWin * sizeof(Xyzz<F>) + 64))) return rc;
+  if ((rc = ctx->ensure_group_events(1))) return rc;
+  Xyzz<F>* hW = (Xyzz<F>*)ctx->h_pinned;
+  volatile uint32_t* hflag = (volatile uint32_t*)(hW + kSmallWin);
+  *hflag = 0;
+  const uint32_t seq = ++ctx->small_seq ? ctx->small_seq : ++ctx->small_seq;
+  void* dW = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&dW, hW, 0));
+  uint32_t* dflag = (uint32_t*)((Xyzz<F>*)dW + kSmallWin);
+  if (fused) {
+    PM_LAUNCH(ctx, "small_fused",
+              (k_small_fused<Cv><<<kSmallWin, 256, 0, st>>>(g, ds, db, (Xyzz<F>*)dW, tickets + kSmallWin, dflag, seq)));
+  } else {
+    Xyzz<F>* tab = (Xyzz<F>*)ctx->small_tab.p;
+    int8_t* dig = (int8_t*)ctx->small_dig.p;
+    PM_LAUNCH(ctx, "small_table",
+              (k_small_table<Cv><<<(un + kSmallTabPts - 1) / kSmallTabPts, 256, 0, st>>>(g, ds, db, tab, dig)));
+    if (lanes)
+      PM_LAUNCH(ctx, "small_sum",
+                (k_small_sum_lanes<Cv><<<dim3(g.ns, kSmallWin), 256, 0, st>>>(
+                    g, tab, dig, (Xyzz<F>*)ctx->small_part.p, tickets, (Xyzz<F>*)dW, tickets + kSmallWin, dflag, seq)));
+    else
+      PM_LAUNCH(ctx, "small_sum",
+                (k_small_sum<Cv><<<dim3(g.ns, kSmallWin), 256, 0, st>>>(g, tab, dig, (Xyzz<F>*)ctx->small_part.p,
+                                                                         tickets, (Xyzz<F>*)dW, tickets + kSmallWin,
+                                                                         dflag, seq)));
+  }
+  hipEvent_t ev = ctx->grp_ev[0];
+  HIP_TRY(hipEventRecord(ev, st));
+  if (ctx->timing) {  // the timed launches' events must complete (end_call)
+    if ((rc = wait_event(ctx, ev))) return rc;
+  } else {
+    for (uint32_t it = 1;; it++) {
+      if (__atomic_load_n((const uint32_t*)hflag, __ATOMIC_ACQUIRE) == seq) break;
+      if ((it & 1023u) == 0) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) {
+          if (*hflag != seq) return set_error(PM_ERR_HIP, "small MSM: kernels finished without the completion flag");
+          break;
+        }
+        if (q != hipErrorNotReady) return set_error(PM_ERR_HIP, std::string("small MSM: ") + hipGetErrorString(q));
+      }
+      __builtin_ia32_pause();
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const host::Pt<F> r = host_has_bmi2() ? small_horner_bmi2<F>(hW) : small_horner<F, false>(hW);
+  if (ctx->timing) {
+    auto& stt = ctx->stats["host_tail"];
+    stt.first += 1;
+    stt.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  ctx->end_call();
+  aff_to_u64<F>(xyzz_to_aff<F>(host::to_dev<F>(r)), out);
   return PM_OK;
 }
 

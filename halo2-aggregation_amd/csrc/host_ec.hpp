@@ -75,13 +75,12 @@ inline E<P> sub(const E<P>& a, const E<P>& b) {
     t[i] = (uint64_t)x;
     br = (uint64_t)(x >> 64) & 1;
   }
-  if (br) {
-    uint64_t c = 0;
-    for (int i = 0; i < 4; i++) {
-      u128 s = (u128)t[i] + F64<P>::mod(i) + c;
-      t[i] = (uint64_t)s;
-      c = (uint64_t)(s >> 64);
-    }
+  const uint64_t m = 0 - br;  // add p back on a borrow, branch-free (the sign is data-dependent)
+  uint64_t c = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 s = (u128)t[i] + (F64<P>::mod(i) & m) + c;
+    t[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
   }
   E<P> r;
   memcpy(r.v, t, 32);
@@ -238,6 +237,76 @@ inline Pt<P> addp(const Pt<P>& p, const Pt<P>& q) {
   r.Y = sub(mulv<P, ADX>(R, sub(Q, r.X)), mulv<P, ADX>(S1, PPP));
   r.ZZ = mulv<P, ADX>(mulv<P, ADX>(p.ZZ, q.ZZ), PP);
   r.ZZZ = mulv<P, ADX>(mulv<P, ADX>(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+// Jacobian (x = X / Z^2, y = Y / Z^3; Z == 0 is the identity) for pure
+// doubling chains: dbl-2009-l (a = 0) is 2M + 5S against XYZZ's 6M + 3S, and
+// the small-MSM Horner (engine.hpp small_horner) spends 128 of its 161 group
+// operations doubling.  Additions: add-2007-bl (11M + 5S).
+template <class P>
+struct Jac {
+  E<P> X, Y, Z;
+};
+
+template <class P, bool ADX = false>
+inline Jac<P> jdbl(const Jac<P>& p) {
+  if (is_zero(p.Z)) return p;  // (no y = 0 points: every group here has odd order)
+  const E<P> A = mulv<P, ADX>(p.X, p.X);
+  const E<P> B = mulv<P, ADX>(p.Y, p.Y);
+  const E<P> YZ = mulv<P, ADX>(p.Y, p.Z);
+  const E<P> C = mulv<P, ADX>(B, B);
+  const E<P> xb = add(p.X, B);
+  const E<P> t = mulv<P, ADX>(xb, xb);
+  const E<P> u = sub(t, add(A, C));
+  const E<P> D = add(u, u);
+  const E<P> Ee = add(add(A, A), A);
+  const E<P> F = mulv<P, ADX>(Ee, Ee);
+  Jac<P> r;
+  r.X = sub(F, add(D, D));
+  const E<P> C2 = add(C, C), C4 = add(C2, C2);
+  r.Y = sub(mulv<P, ADX>(Ee, sub(D, r.X)), add(C4, C4));
+  r.Z = add(YZ, YZ);
+  return r;
+}
+
+template <class P, bool ADX = false>
+inline Jac<P> jadd(const Jac<P>& p, const Jac<P>& q) {
+  if (is_zero(q.Z)) return p;
+  if (is_zero(p.Z)) return q;
+  const E<P> Z1Z1 = mulv<P, ADX>(p.Z, p.Z), Z2Z2 = mulv<P, ADX>(q.Z, q.Z);
+  const E<P> U1 = mulv<P, ADX>(p.X, Z2Z2), U2 = mulv<P, ADX>(q.X, Z1Z1);
+  const E<P> S1 = mulv<P, ADX>(mulv<P, ADX>(p.Y, q.Z), Z2Z2);
+  const E<P> S2 = mulv<P, ADX>(mulv<P, ADX>(q.Y, p.Z), Z1Z1);
+  const E<P> H = sub(U2, U1), Rh = sub(S2, S1);
+  if (is_zero(H)) {
+    if (is_zero(Rh)) return jdbl<P, ADX>(p);
+    Jac<P> o;
+    memset(&o, 0, sizeof(o));
+    return o;
+  }
+  const E<P> H2 = add(H, H);
+  const E<P> I = mulv<P, ADX>(H2, H2);
+  const E<P> J = mulv<P, ADX>(H, I);
+  const E<P> r = add(Rh, Rh);
+  const E<P> V = mulv<P, ADX>(U1, I);
+  Jac<P> o;
+  o.X = sub(sub(mulv<P, ADX>(r, r), J), add(V, V));
+  const E<P> SJ = mulv<P, ADX>(S1, J);
+  o.Y = sub(mulv<P, ADX>(r, sub(V, o.X)), add(SJ, SJ));
+  const E<P> zs = add(p.Z, q.Z);
+  o.Z = mulv<P, ADX>(sub(mulv<P, ADX>(zs, zs), add(Z1Z1, Z2Z2)), H);
+  return o;
+}
+
+// Jacobian -> XYZZ (ZZ = Z^2, ZZZ = Z^3)
+template <class P, bool ADX = false>
+inline Pt<P> jac_to_xyzz(const Jac<P>& p) {
+  Pt<P> r;
+  r.X = p.X;
+  r.Y = p.Y;
+  r.ZZ = mulv<P, ADX>(p.Z, p.Z);
+  r.ZZZ = mulv<P, ADX>(r.ZZ, p.Z);
   return r;
 }
 

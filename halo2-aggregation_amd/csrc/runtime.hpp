@@ -54,6 +54,11 @@ constexpr size_t kDropinFreeDiv = 2;
 // base sets seen once and not admitted: a set becomes resident on its second
 // sighting, so one-shot bases never pay the row-table build
 constexpr int kDropinSeen = 8;
+// small-MSM path (msm_small.hpp): pm_msm* calls with n <= ctx->small_max (and
+// the automatic window) run the two-launch table + window-sum kernels instead
+// of the sorting pipeline; kSmallLimit bounds pm_ctx_set_small_msm
+constexpr size_t kSmallMaxN = PM_SMALL_MSM_DEFAULT;
+constexpr size_t kSmallLimit = PM_SMALL_MSM_LIMIT;
 
 struct Buf {
   void* p = nullptr;
@@ -195,7 +200,7 @@ struct pm_ctx {
   // workspace
   pm::Buf in_scalars, in_scalars2, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
       win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, tr_canon, ntt_scratch2,
-      acc_vkpow;
+      acc_vkpow, small_tab, small_dig, small_part, small_tk;
   pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
   // proof-byte decoder (proof_kernels.hpp): square-root tables per curve
   // (pm_curve order), the point map of the current shape, host staging
@@ -211,6 +216,10 @@ struct pm_ctx {
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;  // MSM host terms: two slots (batch pipelining)
   size_t h_pinned_cap = 0;
+  size_t small_max = pm::kSmallMaxN;  // small-MSM path threshold (pm_ctx_set_small_msm)
+  void* small_pin = nullptr;          // small-MSM host inputs, pinned + mapped (read by k_small_table)
+  size_t small_pin_cap = 0;
+  uint32_t small_seq = 0;             // completion-flag value of the last small MSM
   // timing
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -220,12 +229,13 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &small_tab, &small_dig, &small_part, &small_tk};
   }
   ~pm_ctx();
   int begin_call();
   int end_call();
   int ensure_pinned(size_t bytes);
+  int ensure_small_pin(size_t bytes);
   // host -> device copy of a caller buffer on `st` (one pageable
   // hipMemcpyAsync: ~52 GB/s for 32 MB on MI355X, faster than the pinned
   // staging threads round 2 measured, ~38 GB/s, and retired)
@@ -273,6 +283,10 @@ struct CurveOps {
   int (*proofs)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const void* d_proofs, size_t stride,
                 const void* d_inst, void* d_points, void* d_scalars, void* d_status, const uint64_t* vk_repr,
                 void* d_ch, void* d_quads, void* d_h);
+  // small-MSM path (msm_small.hpp); s_host / b_host: the input is in host
+  // memory; b_r261: bases in the resident R = 2^261 form
+  int (*msm_small)(Ctx* ctx, const void* scalars, bool s_host, const void* bases, bool b_host, bool b_r261, size_t n,
+                   uint32_t flags, uint64_t out[8]);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

@@ -31,6 +31,10 @@ LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
 # multiexp (a pm_msm call's fixed latency loses there).
 # best_multiexp below still runs every n on the GPU: there is no CPU path here.
 MSM_GPU_MIN_N = 4
+# PM_SMALL_MSM_DEFAULT / PM_SMALL_MSM_LIMIT: the small-MSM path's default and
+# largest threshold (pm_ctx_set_small_msm)
+SMALL_MSM_DEFAULT = 4096
+SMALL_MSM_LIMIT = 65536
 ACCUM_CURVES = (PALLAS, VESTA, BN254)
 # per-proof status bits of the proof-byte entries (pm_*_proofs*)
 PROOF_BAD_POINT = 8
@@ -216,6 +220,7 @@ def _load():
         "pm_ctx_set_stream": ([_vp, _vp], ctypes.c_int),
         "pm_ctx_use_own_stream": ([_vp], ctypes.c_int),
         "pm_ctx_set_window": ([_vp, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_small_msm": ([_vp, ctypes.c_size_t], ctypes.c_int),
         "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_split": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_glv": ([_vp, ctypes.c_int], ctypes.c_int),
@@ -528,6 +533,11 @@ class Context:
 
     def set_window(self, c):
         _check(lib().pm_ctx_set_window(self.h, c))
+
+    def set_small_msm(self, max_n):
+        """MSMs of at most max_n terms (automatic window) take the small-MSM
+        path (table + window-sum kernels, 33-window host Horner); 0 = never."""
+        _check(lib().pm_ctx_set_small_msm(self.h, max_n))
 
     def set_pipeline(self, groups=0, min_chunk=0):
         """Minimum accumulate slice per lane (0 = automatic); groups must be

@@ -84,6 +84,15 @@ int pm_ctx_set_window(pm_ctx* ctx, int c);
  * `groups` must be 0 or 1: pipelined window groups measured slower on MI355X
  * and were retired (PM_ERR_UNSUPPORTED for groups > 1). */
 int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk);
+/* Small-MSM path: MSM calls (pm_msm*, pm_msm_device, pm_msm_resident*) of at
+ * most max_n terms under the automatic window run two launches -- a table of
+ * [1..8] P_i with the GLV-split 4-bit digits, then per-window sums -- and a
+ * 33-window host Horner instead of the sorting pipeline.  Default
+ * PM_SMALL_MSM_DEFAULT, 0 disables it, at most PM_SMALL_MSM_LIMIT.  Results do
+ * not depend on it. */
+#define PM_SMALL_MSM_DEFAULT 4096
+#define PM_SMALL_MSM_LIMIT 65536
+int pm_ctx_set_small_msm(pm_ctx* ctx, size_t max_n);
 /* Retired: the GLV-mode variable-base MSM measured slower on MI355X
  * (DESIGN.md §7).  enable == 0 succeeds, anything else returns
  * PM_ERR_UNSUPPORTED.  Kept so older bindings still link. */

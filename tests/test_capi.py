@@ -46,6 +46,15 @@ def test_crossover_threshold_is_one_number():
     assert int(h.group(1)) == int(doc.group(1)) == H.MSM_GPU_MIN_N
 
 
+def test_small_msm_constants():
+    """The small-MSM path's default threshold and limit: header == Python."""
+    src = open(H.HEADER_PATH).read()
+    d = re.search(r"#define PM_SMALL_MSM_DEFAULT (\d+)", src)
+    lim = re.search(r"#define PM_SMALL_MSM_LIMIT (\d+)", src)
+    assert d and lim
+    assert (int(d.group(1)), int(lim.group(1))) == (H.SMALL_MSM_DEFAULT, H.SMALL_MSM_LIMIT)
+
+
 def test_last_error_is_thread_local_string():
     assert isinstance(H.lib().pm_last_error(), bytes)
 
