@@ -521,7 +521,7 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
                          &transcript_device_impl<Cv>, &vk_repr_impl<Cv>,                   \
                          &fixed_table_impl<Cv>, &ntt_device_impl<Cv>, &msm_fixed_to_aff<Cv>,    \
                          &bases_to29_impl<Cv>, &msm_resident_batch_impl<Cv>, &proofs_device_impl<Cv>,    \
-                         &msm_small_impl<Cv>};
+                         &msm_start_impl<Cv>, &msm_finish_impl<Cv>, &msm_small_impl<Cv>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
@@ -542,6 +542,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
                                            size_t, uint32_t, uint64_t*);                             \
   template int transcript_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const uint64_t*, const void*, \
                                           const void*, void*, void*);                            \
+  template int msm_start_impl<Cv>(Ctx*, const pm_fixed_bases*, const void*, const void*, size_t, uint32_t, void*); \
+  template int msm_finish_impl<Cv>(Ctx*, const void*, uint64_t*);                                \
   template int msm_small_impl<Cv>(Ctx*, const void*, bool, const void*, bool, bool, size_t, uint32_t, uint64_t*); \
   PM_OPS_TABLE(Cv, name)                                                                       \
   }

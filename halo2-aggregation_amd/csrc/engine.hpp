@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 
 #include "host_ec.hpp"
@@ -445,6 +446,26 @@ int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint
   return PM_OK;
 }
 
+// the two halves of a resident-bases MSM (CurveOps::msm_start / msm_finish)
+template <class Cv>
+int msm_start_impl(Ctx* ctx, const pm_fixed_bases* ft, const void* d_bases29, const void* d_s, size_t n,
+                   uint32_t flags, void* tail) {
+  using F = typename Cv::Base;
+  static_assert(sizeof(MsmTail<F>) <= kTailBytes, "tail storage");
+  MsmTail<F>* t = new (tail) MsmTail<F>();
+  return msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, (const uint32_t*)d_bases29, n,
+                             ft ? flags & ~kBasesR261 : flags | kBasesR261, nullptr, ft, t, 0, nullptr);
+}
+template <class Cv>
+int msm_finish_impl(Ctx* ctx, const void* tail, uint64_t out[8]) {
+  using F = typename Cv::Base;
+  Xyzz<F> r;
+  if (int rc = msm_tail<F>(ctx, *(const MsmTail<F>*)tail, &r)) return rc;
+  ctx->end_call();
+  aff_to_u64<F>(xyzz_to_aff<F>(r), out);
+  return PM_OK;
+}
+
 // ------------------------------------------------------ small-MSM path
 // Host Horner over the 33 window sums of msm_small.hpp (Jacobian, X Y Z in
 // the first three coordinates of each slot): 128 doublings, 32 additions.
@@ -487,12 +508,13 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   const hipStream_t st = ctx->stream;
   const uint32_t un = (uint32_t)n, T = 2u * un;
   const bool fused = T <= (uint32_t)kSmallQuads;
-  // slices per window: up to kSmallSlices blocks of 64 quads (or 256 lanes),
-  // each then adding kq terms serially
-  uint32_t kSmallSlices = 8;
-  if (const char* e = std::getenv("PM_SMALL_SLICES")) kSmallSlices = std::max(1, std::atoi(e));
-  bool lanes = T >= 4096u;
-  if (const char* e = std::getenv("PM_SMALL_LANES")) lanes = std::atoi(e) != 0;
+  // slices per window: up to kSmallSlices blocks of 64 quads (or, from 4096
+  // terms, 256 lanes with one-lane additions), each adding kq terms serially.
+  // Measured (profiles/r04/small/ab.jsonl, n = 256 .. 8192, quads / lanes x
+  // 4 .. 32 slices): 8 slices best at every size, lanes ahead from n = 2048
+  // (121 vs 132 us; 4096: 138 vs 167 us), even at 1024.
+  constexpr uint32_t kSmallSlices = 8;
+  const bool lanes = T >= 4096u;
   const uint32_t per = lanes ? 256u : (uint32_t)kSmallQuads;  // terms per block and round
   SmallGeom g{};
   g.n = un;
@@ -548,8 +570,9 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   } else {
     Xyzz<F>* tab = (Xyzz<F>*)ctx->small_tab.p;
     int8_t* dig = (int8_t*)ctx->small_dig.p;
+    const uint32_t nb_tab = (un + kSmallTabPts - 1) / kSmallTabPts, nb_dig = (un + 255) / 256;
     PM_LAUNCH(ctx, "small_table",
-              (k_small_table<Cv><<<(un + kSmallTabPts - 1) / kSmallTabPts, 256, 0, st>>>(g, ds, db, tab, dig)));
+              (k_small_table<Cv><<<nb_tab + nb_dig, 256, 0, st>>>(g, nb_tab, ds, db, tab, dig)));
     if (lanes)
       PM_LAUNCH(ctx, "small_sum",
                 (k_small_sum_lanes<Cv><<<dim3(g.ns, kSmallWin), 256, 0, st>>>(
@@ -562,6 +585,8 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   }
   hipEvent_t ev = ctx->grp_ev[0];
   HIP_TRY(hipEventRecord(ev, st));
+  // the flag instead of the event: 66.5 / 80.3 / 138.8 us against 71.9 /
+  // 86.4 / 144.5 at n = 1 / 32 / 4096 (profiles/r04/small/flag_vs_event.txt)
   if (ctx->timing) {  // the timed launches' events must complete (end_call)
     if ((rc = wait_event(ctx, ev))) return rc;
   } else {

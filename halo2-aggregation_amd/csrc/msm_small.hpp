@@ -7,10 +7,11 @@
 // dwarfs the work.  Here:
 //   k_small_table   per base P_i: the multiples [1..8] P_i (XYZZ, R = 2^261,
 //                   one quad per point per wave: [2]P; [4]P, [3]P; [8]P, [6]P,
-//                   [5]P, [7]P -- three levels of quad-cooperative operations)
-//                   and, from the scalar, the GLV halves k = k1 + lambda k2
-//                   (|k_h| < 2^127, glv.hpp) recoded into 33 signed 4-bit
-//                   digits in [-8, 8] each (the half's sign folded in)
+//                   [5]P, [7]P -- three levels of quad-cooperative operations);
+//                   in separate blocks of the same launch, from the scalar,
+//                   the GLV halves k = k1 + lambda k2 (|k_h| < 2^127,
+//                   glv.hpp) recoded into 33 signed 4-bit digits in [-8, 8]
+//                   each (the half's sign folded in)
 //   k_small_sum     block (s, j): window j's sum over terms [s kq 64, (s+1) kq
 //                   64) of the 2n (point, half) terms: each of 64 quads adds
 //                   kq selected table entries (phi(P) = (beta X, Y, ZZ, ZZZ),
@@ -98,8 +99,8 @@ __device__ __forceinline__ Fe<Fs> fe_reduce_full(Fe<Fs> k) {
 }
 
 // one GLV half (< 2^127, 4 words) -> 33 signed digits d_w in [-8, 8],
-// sum_w d_w 16^w = k; lane q of the quad stores the digits w = q mod 4
-__device__ __forceinline__ void small_recode(const uint32_t* k, bool neg, int8_t* dst, size_t stride, uint32_t q) {
+// sum_w d_w 16^w = k, stored at dst[w * stride]
+__device__ __forceinline__ void small_recode(const uint32_t* k, bool neg, int8_t* dst, size_t stride) {
   uint32_t carry = 0;
 #pragma unroll
   for (int w = 0; w < kSmallWin; w++) {
@@ -108,22 +109,46 @@ __device__ __forceinline__ void small_recode(const uint32_t* k, bool neg, int8_t
     carry = v >= 8u ? 1u : 0u;
     int d = (int)v - (carry ? 16 : 0);
     if (neg) d = -d;
-    if ((uint32_t)(w & 3) == q) dst[(size_t)w * stride] = (int8_t)d;
+    dst[(size_t)w * stride] = (int8_t)d;
   }
 }
 
+// blocks [0, nb_tab): the table, one quad per base per wave, 16 bases per
+// block; blocks [nb_tab, ...): the digits, one lane per scalar (kept out of
+// the table blocks, where the split's ~5 us held every level's barrier)
 template <class Cv>
-__global__ void __launch_bounds__(256) k_small_table(SmallGeom g, const uint32_t* __restrict__ scalars,
+__global__ void __launch_bounds__(256) k_small_table(SmallGeom g, uint32_t nb_tab, const uint32_t* __restrict__ scalars,
                                                      const uint32_t* __restrict__ bases,
                                                      Xyzz<typename Cv::Base>* __restrict__ tab,
                                                      int8_t* __restrict__ digits) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   __shared__ uint32_t s_m[3][kSmallTabPts][kSmallPt];  // [2]P, [3]P, [4]P
+  if (blockIdx.x >= nb_tab) {  // digits of scalar i (zero for an identity base)
+    const uint32_t i = (blockIdx.x - nb_tab) * blockDim.x + threadIdx.x;
+    if (i >= g.n) return;
+    const size_t T = 2ull * g.n;
+    int8_t* dst = digits + 2ull * i;
+    const uint4* p = reinterpret_cast<const uint4*>(bases + 16ull * i);
+    const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    const bool ident = ((a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w) | (c.x | c.y | c.z | c.w | d.x | d.y | d.z | d.w)) == 0;
+    if (ident) {
+      for (int w = 0; w < kSmallWin; w++) dst[(size_t)w * T] = dst[(size_t)w * T + 1] = 0;
+      return;
+    }
+    Fe<Fs> k = load_canonical<Fs>(scalars, i, g.canonical);
+    if (g.canonical) k = fe_reduce_full<Fs>(k);
+    uint32_t k1[6], k2[6];
+    bool n1, n2;
+    glv_split<Cv, true>(k, k1, k2, n1, n2);
+    small_recode(k1, n1, dst, T);
+    small_recode(k2, n2, dst + 1, T);
+    return;
+  }
   const uint32_t wave = threadIdx.x >> 6, v = (threadIdx.x >> 2) & (kSmallTabPts - 1), q = threadIdx.x & 3u;
   const uint32_t i = blockIdx.x * kSmallTabPts + v;
   const bool valid = i < g.n;
-  // base i: the identity (all-zero bytes) gets an all-identity table and zero digits
+  // base i: the identity (all-zero bytes) gets an all-identity table
   F29<F> x = f29_zero<F>(), y = f29_zero<F>();
   bool ident = true;
   if (valid) {
@@ -143,21 +168,6 @@ __global__ void __launch_bounds__(256) k_small_table(SmallGeom g, const uint32_t
   const F29<F> one = f29_const<F>(F29Consts<F>::ONE);
   const Xyzz29<F> M1 = ident ? xyzz29_inf<F>() : Xyzz29<F>{x, y, one, one};
   Xyzz<F>* row = tab + (size_t)i * kSmallMults;
-  if (wave == 1 && valid) {  // the digits, beside wave 0's first doubling
-    const size_t T = 2ull * g.n;
-    int8_t* dst = digits + 2ull * i;
-    if (ident) {
-      for (int w = (int)q; w < kSmallWin; w += 4) dst[(size_t)w * T] = dst[(size_t)w * T + 1] = 0;
-    } else {
-      Fe<Fs> k = load_canonical<Fs>(scalars, i, g.canonical);
-      if (g.canonical) k = fe_reduce_full<Fs>(k);
-      uint32_t k1[6], k2[6];
-      bool n1, n2;
-      glv_split<Cv, true>(k, k1, k2, n1, n2);
-      small_recode(k1, n1, dst, T, q);
-      small_recode(k2, n2, dst + 1, T, q);
-    }
-  }
   // level 1: [2]P
   if (wave == 0) {
     const Xyzz29<F> M2 = xyzz29_dbl_q<F>(M1);
@@ -252,12 +262,16 @@ __device__ __forceinline__ void small_finish(Xyzz<F>* out, uint32_t j, const Xyz
 // [4] + [2], [7] = [8] - [1]) -- four operations, against the table kernel's
 // three levels plus a launch and a round trip through memory -- then the
 // LDS tree.  The GLV split and recoding run per quad (only digit j is kept).
-template <class Cv>
+// TRACE (tools/microbench_small.hip only): thread 0 of block 0 records the
+// real-time clock at each phase boundary into tr[0..7]
+template <class Cv, bool TRACE = false>
 __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t* __restrict__ scalars,
                                                      const uint32_t* __restrict__ bases,
                                                      Xyzz<typename Cv::Base>* __restrict__ out,
                                                      uint32_t* __restrict__ done, uint32_t* __restrict__ flag,
-                                                     uint32_t seq) {
+                                                     uint32_t seq, uint64_t* __restrict__ tr = nullptr) {
+  const bool rec = TRACE && blockIdx.x == 0 && threadIdx.x == 0;
+  if (rec) tr[0] = wall_clock64();
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   using K = F29Consts<F>;
@@ -280,12 +294,16 @@ __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t
       x = f29_from_r256<F>(wx);
       y = f29_from_r256<F>(wy);
     }
+    if (h) x = f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), x);  // phi(P): independent of the split below
+    if (rec) tr[1] = wall_clock64() + (x.l[0] & 0u);
     if (!ident) {
       Fe<Fs> k = load_canonical<Fs>(scalars, i, g.canonical);
       if (g.canonical) k = fe_reduce_full<Fs>(k);
+      if (rec) tr[2] = wall_clock64() + (k.l[0] & 0u);
       uint32_t k1[6], k2[6];
       bool n1, n2;
       glv_split<Cv, true>(k, k1, k2, n1, n2);
+      if (rec) tr[3] = wall_clock64() + (k1[0] & 0u);
       const uint32_t* kh = h ? k2 : k1;
       uint32_t carry = 0;
 #pragma unroll
@@ -298,12 +316,17 @@ __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t
       if (h ? n2 : n1) d = -d;
     }
   }
+  if (rec) tr[4] = wall_clock64() + ((uint32_t)d & 0u);
   if (d != 0) {  // quad-uniform
+    // [d] (+-phi^h P) = [|d|] of the base with phi (above) and the sign
+    // applied first: no product after the chain
+    if (d < 0) y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), y, K::K6)));
     const F29<F> one = f29_const<F>(K::ONE);
     const Xyzz29<F> P1{x, y, one, one};
     const Xyzz29<F> P2 = xyzz29_dbl_q<F>(P1);
     const Xyzz29<F> P4 = xyzz29_dbl_q<F>(P2);
     const Xyzz29<F> P8 = xyzz29_dbl_q<F>(P4);
+    if (rec) tr[5] = wall_clock64() + (P8.X.l[0] & 0u);
     const uint32_t m = (uint32_t)(d < 0 ? -d : d);
     // [m] = A + B: (P1, -), (P2, -), (P2, P1), (P4, -), (P4, P1), (P4, P2), (P8, -P1), (P8, -)
     const Xyzz29<F> A = xyzz29_pick<F>(m == 1, P1, xyzz29_pick<F>(m <= 3, P2, xyzz29_pick<F>(m <= 6, P4, P8)));
@@ -311,11 +334,12 @@ __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t
     if (m == 7) B.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), B.Y, K::K6)));
     B = xyzz29_pick<F>(m == 3 || (m >= 5 && m <= 7), B, xyzz29_inf<F>());
     acc = xyzz29_add_q<F>(A, B);
-    if (h) acc.X = f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), acc.X);  // phi
-    if (d < 0) acc.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), acc.Y, K::K6)));
   }
+  if (rec) tr[6] = wall_clock64() + (acc.X.l[0] & 0u);
   acc = small_tree<F>(s_p, acc, v, q, small_pow2(T));
+  if (rec) tr[7] = wall_clock64() + (acc.X.l[0] & 0u);
   if (v == 0) small_finish<F>(out, j, acc, q, done, flag, seq);
+  if (rec) tr[8] = wall_clock64();
 }
 
 // table entry of term t with digit d != 0: [|d|] P_i, phi'd for the second

@@ -57,6 +57,7 @@ constexpr int kDropinSeen = 8;
 // small-MSM path (msm_small.hpp): pm_msm* calls with n <= ctx->small_max (and
 // the automatic window) run the two-launch table + window-sum kernels instead
 // of the sorting pipeline; kSmallLimit bounds pm_ctx_set_small_msm
+constexpr size_t kTailBytes = 128;  // opaque MsmTail storage (CurveOps::msm_start)
 constexpr size_t kSmallMaxN = PM_SMALL_MSM_DEFAULT;
 constexpr size_t kSmallLimit = PM_SMALL_MSM_LIMIT;
 
@@ -142,6 +143,7 @@ struct DropinEntry {
   pm_bases* b;  // nullptr: seen once, not admitted yet (run through the plain path)
   size_t bytes;
   uint64_t last_use;
+  uint64_t quick = 0;  // keyed hash of the first and last 8 points: picks the set to start speculatively
 };
 
 }  // namespace pm
@@ -183,6 +185,7 @@ struct pm_ctx {
   pm::DigestKey dropin_key;             // secret per-context digest key (pm_ctx_create)
   uint64_t dropin_clock = 0;
   uint64_t dropin_hits = 0, dropin_misses = 0;
+  uint64_t dropin_spec_hits = 0, dropin_spec_misses = 0;  // speculative starts kept / drained
   hipEvent_t batch_ev[4] = {};       // batch pipelining: copied[2], consumed[2]
   std::vector<hipEvent_t> grp_ev;    // MSM: one per pinned term slot (terms copied)
   int window_c = 0;
@@ -283,6 +286,13 @@ struct CurveOps {
   int (*proofs)(Ctx* ctx, const pm_proof_shape* shape, size_t B, const void* d_proofs, size_t stride,
                 const void* d_inst, void* d_points, void* d_scalars, void* d_status, const uint64_t* vk_repr,
                 void* d_ch, void* d_quads, void* d_h);
+  // resident-bases MSM in two halves (the drop-in cache's speculative start):
+  // msm_start enqueues the device pipeline on ctx->stream (ft: the row table,
+  // else d_bases29 in the R = 2^261 form) and fills the opaque tail;
+  // msm_finish waits for it and runs the host Horner
+  int (*msm_start)(Ctx* ctx, const pm_fixed_bases* ft, const void* d_bases29, const void* d_scalars, size_t n,
+                   uint32_t flags, void* tail);
+  int (*msm_finish)(Ctx* ctx, const void* tail, uint64_t out[8]);
   // small-MSM path (msm_small.hpp); s_host / b_host: the input is in host
   // memory; b_r261: bases in the resident R = 2^261 form
   int (*msm_small)(Ctx* ctx, const void* scalars, bool s_host, const void* bases, bool b_host, bool b_r261, size_t n,

@@ -27,10 +27,10 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "pasta_msm.h")
 PALLAS, VESTA, BN254 = 0, 1, 2
 SCALARS_CANONICAL = 1
 LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
-# PM_MSM_GPU_MIN_N: below this many terms the Rust shim keeps halo2's CPU
-# multiexp (a pm_msm call's fixed latency loses there).
-# best_multiexp below still runs every n on the GPU: there is no CPU path here.
-MSM_GPU_MIN_N = 4
+# PM_MSM_GPU_MIN_N: below this many terms the Rust shim would keep halo2's CPU
+# multiexp; with the small-MSM path the GPU wins from one
+# term.  best_multiexp below runs every n on the GPU: there is no CPU path here.
+MSM_GPU_MIN_N = 1
 # PM_SMALL_MSM_DEFAULT / PM_SMALL_MSM_LIMIT: the small-MSM path's default and
 # largest threshold (pm_ctx_set_small_msm)
 SMALL_MSM_DEFAULT = 4096
@@ -230,6 +230,7 @@ def _load():
         "pm_ctx_reset_stats": ([_vp], ctypes.c_int),
         "pm_ctx_dropin_stats": ([_vp, _u64p, _u64p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)],
                                 ctypes.c_int),
+        "pm_ctx_dropin_spec_stats": ([_vp, _u64p, _u64p], ctypes.c_int),
         "pm_ctx_dropin_clear": ([_vp], ctypes.c_int),
         "pm_ctx_dropin_key_id": ([_vp, _u64p], ctypes.c_int),
         "pm_msm": ([ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
@@ -574,6 +575,12 @@ class Context:
         _check(lib().pm_ctx_dropin_stats(self.h, ctypes.byref(hi), ctypes.byref(mi), ctypes.byref(en),
                                          ctypes.byref(by)))
         return {"hits": hi.value, "misses": mi.value, "entries": en.value, "device_bytes": by.value}
+
+    def dropin_spec_stats(self):
+        """pm_ctx_dropin_spec_stats -> (kept, drained) speculative starts."""
+        k, d = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().pm_ctx_dropin_spec_stats(self.h, ctypes.byref(k), ctypes.byref(d)))
+        return k.value, d.value
 
     def dropin_clear(self):
         _check(lib().pm_ctx_dropin_clear(self.h))

@@ -121,13 +121,12 @@ int pm_ctx_reset_stats(pm_ctx* ctx);
  * it into C::Curve with `to_curve()`.  n == 0 yields the identity. */
 int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
            uint64_t out[8]);
-/* Below this many terms a pm_msm call (~230-300 us of launches, copies and the
- * host Horner whatever n is up to 2^8) is slower than halo2's CPU multiexp
- * (serial for so few terms); the Rust shim keeps the CPU path there
- * (measured on MI355X + EPYC, 16 threads: bench.py small_n,
- * 1-2 terms CPU, from 4 terms the GPU call).  pm_msm itself
- * computes any n. */
-#define PM_MSM_GPU_MIN_N 4
+/* Below this many terms the Rust shim would keep halo2's CPU multiexp.  Since
+ * the small-MSM path (round 4: ~67 us at one term, ~81 us at 32, ~140 us at
+ * 4096) every n >= 1 is faster on the GPU than halo2's multiexp on 16 host
+ * threads (~150 us at one term, ~700 us at 32: bench.py small_n, DESIGN.md
+ * §12), so the threshold is 1.  pm_msm itself computes any n. */
+#define PM_MSM_GPU_MIN_N 1
 /* Same, on an explicit context (host pointers).
  * Drop-in base cache: from 4096 points on, pm_msm / pm_msm_ctx keep the base
  * sets they see repeatedly resident on the device (converted, with the row
@@ -143,13 +142,21 @@ int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, 
  * two base sets that collide except with probability ~2^-128.  At most 4 sets,
  * min(16 GiB, half the free device memory) per context, least recently used
  * evicted before a new set is built; if the build still runs out of memory
- * every set is released and, failing that, the call runs the plain pipeline. */
+ * every set is released and, failing that, the call runs the plain pipeline.
+ * A warm call starts the MSM of the set a cheap keyed hash of its first and
+ * last 8 points predicts right behind the scalar copy, while the full digest
+ * is still being computed; the result is returned only if the digest then
+ * names that same set (else the speculative MSM is drained and the call
+ * proceeds as a miss).  n <= the small-MSM threshold bypasses the cache. */
 int pm_msm_ctx(pm_ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
                uint32_t flags, uint64_t out[8]);
 /* Drop-in cache counters of ctx (any pointer may be NULL), and a way to
  * release its sets early. */
 int pm_ctx_dropin_stats(pm_ctx* ctx, uint64_t* hits, uint64_t* misses, int* entries, size_t* device_bytes);
 int pm_ctx_dropin_clear(pm_ctx* ctx);
+/* Speculative starts of pm_msm_ctx: kept (the digest confirmed the predicted
+ * set) and drained (it named another set or none). */
+int pm_ctx_dropin_spec_stats(pm_ctx* ctx, uint64_t* kept, uint64_t* drained);
 /* A fingerprint of ctx's secret digest key (16 bytes of BLAKE2b of the key,
  * personal "pm-dropin-key-id"): distinct contexts hold distinct keys.  It
  * reveals nothing about the key itself. */

@@ -379,6 +379,18 @@ def test_dropin_base_cache(curve):
         assert st["misses"] == 4 and st["entries"] == 2 and st["hits"] == 1
         assert np.array_equal(ctx.msm(curve, S[:n], Bn), want2)
         assert ctx.dropin_stats()["hits"] == 2
+        # warm hits start the predicted set's MSM behind the scalar copy
+        kept, drained = ctx.dropin_spec_stats()
+        assert kept >= 2 and drained == 0
+        # a change the prediction cannot see (a middle base: the first and
+        # last 8 points are equal): the predicted set's MSM starts, the full
+        # digest names no set, the speculative result is dropped
+        Bm = Bn.copy()
+        Bm[n // 2] = B[n + 7]
+        wm = msm_ref.best_multiexp(curve, S[:n], Bm)
+        assert np.array_equal(ctx.msm(curve, S[:n], Bm), wm)
+        assert ctx.dropin_spec_stats() == (kept, 1)
+        assert ctx.dropin_stats()["hits"] == 2
         # small MSMs bypass the cache
         ctx.msm(curve, S[:100], B[:100])
         assert ctx.dropin_stats()["entries"] == 2
