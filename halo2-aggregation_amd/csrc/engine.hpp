@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
+#include <memory>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -377,12 +380,106 @@ __attribute__((target("bmi2,adx"))) void horner_steps_bmi2(host::Pt<F>& hacc, in
   }
 }
 
+// Host tail with many bucket sets (Wr >= kTailSplitSets: the variable-base
+// MSM's 16 windows): the one Horner over 256 positions costs ~256 additions
+// on one core (0.157 ms at 2^20, profiles/r04/bench_r04b.json; split: 0.072
+// ms, bench_r04d.json).  With the 4-row tables' 4 sets the split measured
+// slower (2^22: 0.047 against 0.040 ms), so it starts at 8 sets.
+// Instead each set's V_w = sum_b 2^{rel_b} Q_{w,b} (rel_b < cmax) is a short
+// Horner on a pool thread, and the caller runs the outer Horner
+// sum_w 2^{o_w} V_w from the top set down in Jacobian form (host_ec.hpp jdbl),
+// waiting for each V_w only when the chain reaches it.
+constexpr int kTailSplitSets = 8;
+template <class F, bool ADX>
+host::Pt<F> tail_set(const MsmTail<F>& t, int w) {
+  // terms of set w by descending relative position: bit sums b + log2 L1,
+  // the top bucket at cmax - 1, the T partials at 0
+  host::Pt<F> acc = host::inf<F>();
+  int q = t.cmax - 1;
+  if (t.NB2 - 1 + t.log2L1 > q) q = t.NB2 - 1 + t.log2L1;
+  const Xyzz<F>* Q = t.hQ + (size_t)w * t.NQ;
+  for (; q >= 0; q--) {
+    acc = host::dbl<F, ADX>(acc);
+    const int b = q - t.log2L1;
+    if (b >= 0 && b < t.NB2) acc = host::addp<F, ADX>(acc, host::from_dev<F>(Q[b]));
+    if (q == t.cmax - 1) acc = host::addp<F, ADX>(acc, host::from_dev<F>(Q[t.NQ - 1]));
+    if (q == 0)
+      for (int b2 = t.NB2; b2 < t.NQ - 1; b2++) acc = host::addp<F, ADX>(acc, host::from_dev<F>(Q[b2]));
+  }
+  return acc;
+}
+template <class F, bool ADX>
+host::Pt<F> tail_split(Ctx* ctx, const MsmTail<F>& t) {
+  const int Wr = t.Wr;
+  std::vector<host::Pt<F>> V((size_t)Wr);
+  std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[(size_t)Wr]);
+  for (int w = 0; w < Wr; w++) ready[w].store(0, std::memory_order_relaxed);
+  HostPool& pool = ctx->host_pool();
+  const int nt = std::min(pool.size(), Wr);
+  // the caller takes the top set, the workers the rest round-robin from the top
+  auto job = [&](int th, int n) {
+    for (int w = Wr - 1 - th; w >= 0; w -= n) {
+      V[(size_t)w] = tail_set<F, ADX>(t, w);
+      ready[w].store(1, std::memory_order_release);
+    }
+  };
+  if (nt > 1) pool.start(nt, job);
+  // the caller's share (th = 0): the top set now, the rest (only when the
+  // pool is smaller than Wr) when the chain below reaches them
+  V[(size_t)Wr - 1] = tail_set<F, ADX>(t, Wr - 1);
+  ready[Wr - 1].store(1, std::memory_order_release);
+  auto jac = [](const host::Pt<F>& p) {  // XYZZ (ZZ^3 = ZZZ^2) -> Jacobian (X ZZ^2, Y ZZZ^2, ZZZ)
+    host::Jac<F> r;
+    if (host::is_zero(p.ZZ)) {
+      std::memset(&r, 0, sizeof(r));
+      return r;
+    }
+    r.X = host::mulv<F, ADX>(p.X, host::mulv<F, ADX>(p.ZZ, p.ZZ));
+    r.Y = host::mulv<F, ADX>(p.Y, host::mulv<F, ADX>(p.ZZZ, p.ZZZ));
+    r.Z = p.ZZZ;
+    return r;
+  };
+  host::Jac<F> acc = jac(V[(size_t)Wr - 1]);
+  for (int w = Wr - 2; w >= 0; w--) {
+    const int width = t.base + (w < t.extra ? 1 : 0);  // o_{w+1} - o_w
+    for (int k = 0; k < width; k++) acc = host::jdbl<F, ADX>(acc);
+    if (nt <= 1 || (Wr - 1 - w) % nt == 0) {  // the caller's own set
+      if (!ready[w].load(std::memory_order_acquire)) {
+        V[(size_t)w] = tail_set<F, ADX>(t, w);
+        ready[w].store(1, std::memory_order_release);
+      }
+    }
+    while (!ready[w].load(std::memory_order_acquire)) __builtin_ia32_pause();
+    acc = host::jadd<F, ADX>(acc, jac(V[(size_t)w]));
+  }
+  if (nt > 1) pool.wait();
+  if (host::is_zero(acc.Z)) return host::inf<F>();
+  return host::jac_to_xyzz<F, ADX>(acc);
+}
+template <class F>
+__attribute__((target("bmi2,adx"))) host::Pt<F> tail_split_bmi2(Ctx* ctx, const MsmTail<F>& t) {
+  return tail_split<F, true>(ctx, t);
+}
+
 // Host tail: sum_w 2^{o_w} (sum_b 2^{b + log2 L1} G_{w,b} + sum T_w + K B_{w,K})
-// as one Horner over absolute bit positions q (host_ec.hpp).
+// as one Horner over absolute bit positions q (host_ec.hpp), or split by set
+// (tail_split) when there are many sets.
 template <class F>
 int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
   if (t.empty) {
     *result = xyzz_inf<F>();
+    return PM_OK;
+  }
+  if (t.Wr >= kTailSplitSets) {
+    if (int rc = wait_event(ctx, t.ev)) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    const host::Pt<F> r = host_has_bmi2() ? tail_split_bmi2<F>(ctx, t) : tail_split<F, false>(ctx, t);
+    if (ctx->timing) {
+      auto& stt = ctx->stats["host_tail"];
+      stt.first += 1;
+      stt.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    *result = host::to_dev<F>(r);
     return PM_OK;
   }
   // the terms as (position, index) sorted by descending position: one flat

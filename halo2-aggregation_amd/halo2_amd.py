@@ -33,7 +33,7 @@ LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
 MSM_GPU_MIN_N = 1
 # PM_SMALL_MSM_DEFAULT / PM_SMALL_MSM_LIMIT: the small-MSM path's default and
 # largest threshold (pm_ctx_set_small_msm)
-SMALL_MSM_DEFAULT = 4096
+SMALL_MSM_DEFAULT = 16384
 SMALL_MSM_LIMIT = 65536
 ACCUM_CURVES = (PALLAS, VESTA, BN254)
 # per-proof status bits of the proof-byte entries (pm_*_proofs*)

@@ -90,7 +90,7 @@ int pm_ctx_set_pipeline(pm_ctx* ctx, int groups, int min_chunk);
  * 33-window host Horner instead of the sorting pipeline.  Default
  * PM_SMALL_MSM_DEFAULT, 0 disables it, at most PM_SMALL_MSM_LIMIT.  Results do
  * not depend on it. */
-#define PM_SMALL_MSM_DEFAULT 4096
+#define PM_SMALL_MSM_DEFAULT 16384
 #define PM_SMALL_MSM_LIMIT 65536
 int pm_ctx_set_small_msm(pm_ctx* ctx, size_t max_n);
 /* Retired: the GLV-mode variable-base MSM measured slower on MI355X
@@ -128,7 +128,8 @@ int pm_msm(int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, 
  * §12), so the threshold is 1.  pm_msm itself computes any n. */
 #define PM_MSM_GPU_MIN_N 1
 /* Same, on an explicit context (host pointers).
- * Drop-in base cache: from 4096 points on, pm_msm / pm_msm_ctx keep the base
+ * Drop-in base cache: from 4096 points on (and above the small-MSM threshold,
+ * PM_SMALL_MSM_DEFAULT by default), pm_msm / pm_msm_ctx keep the base
  * sets they see repeatedly resident on the device (converted, with the row
  * table from 2^18 points, like pm_bases_upload), keyed by (curve, n, a keyed
  * 254-bit digest of the base bytes computed on host threads while the
