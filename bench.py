@@ -253,7 +253,7 @@ def main():
             "data": "synthetic (SplitMix64 scalars in [0,r), bases [a_i]G generated on device)",
             "config": leg["config"],
             "kernels_ms": leg["kernels_ms"],
-            "roofline": leg["roofline"],
+            "roofline": leg.get("roofline"),  # absent only when --logn puts the leg on the small-MSM path
         }
         for k in ("variable_base", "host_scalars", "dropin_pm_msm", "small_n"):
             if k in leg:
@@ -499,7 +499,9 @@ def run_dropin(args, curve, S, B, n, want):
     remembered), the second admits it (admit_ms: upload + row-table build),
     later calls with the same base bytes hit the drop-in cache (warm: the
     scalars' PCIe copy, the keyed digest of the bases on host threads beside
-    it, and the resident MSM)."""
+    it, and the resident MSM, started speculatively behind the copy for the
+    set the first and last 8 points predict, kept once the digest confirms
+    it: speculation = pm_ctx_dropin_spec_stats)."""
     import numpy as np
 
     import halo2_amd as H
@@ -529,9 +531,11 @@ def run_dropin(args, curve, S, B, n, want):
         phases = {k2: round(ctx.kernel_stats(k2)[1] / 3, 4) for k2 in ("dropin_digest", "dropin_copy_call", "h2d",
                                                                           "accumulate")}
         st = ctx.dropin_stats()
+        kept, drained = ctx.dropin_spec_stats()
         return {"call": "pm_msm_ctx(curve, host scalars, host bases, n)", "first_ms": round(first_ms, 3),
                 "admit_ms": round(admit_ms, 3), "warm_ms_per_msm": round(warm, 4),
                 "warm_Mscalar_s": round(n / (warm * 1e-3) / 1e6, 3), "warm_phases_ms": phases, "cache": st,
+                "speculation": {"kept": kept, "drained": drained},
                 "matches": bool(np.array_equal(first, want) and np.array_equal(second, want)
                                 and np.array_equal(got, want))}
     finally:
@@ -598,7 +602,9 @@ def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
         cnt, h2d_ms = ctx.kernel_stats("h2d")
         h2d = h2d_ms / max(1, cnt)
         res[label] = {"ms_per_msm": round(el * 1e3 / k, 4), "Mscalar_s": round(n / (el / k) / 1e6, 3),
-                      "scalar_h2d_ms": round(h2d, 4), "scalar_h2d_GBps": round(32 * n / (h2d * 1e-3) / 1e9, 2),
+                      "scalar_h2d_ms": round(h2d, 4),
+                      # no h2d events on the small-MSM path (its kernel reads pinned host memory)
+                      "scalar_h2d_GBps": round(32 * n / (h2d * 1e-3) / 1e9, 2) if h2d > 0 else None,
                       "matches": bool(np.array_equal(np.asarray(got), np.asarray(want)))}
     # the prover's commit of many polynomials: K MSMs per call
     # (pm_msm_resident_batch), the scalar copy of MSM j+1 and the host tail of

@@ -692,7 +692,11 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
       if ((it & 1023u) == 0) {
         const hipError_t q = hipEventQuery(ev);
         if (q == hipSuccess) {
-          if (*hflag != seq) return set_error(PM_ERR_HIP, "small MSM: kernels finished without the completion flag");
+          if (*hflag != seq) {  // counters left inconsistent by an earlier failure: reset them for the next call
+            (void)hipMemsetAsync(ctx->small_tk.p, 0, ctx->small_tk.cap, st);
+            (void)hipStreamSynchronize(st);
+            return set_error(PM_ERR_HIP, "small MSM: kernels finished without the completion flag");
+          }
           break;
         }
         if (q != hipErrorNotReady) return set_error(PM_ERR_HIP, std::string("small MSM: ") + hipGetErrorString(q));

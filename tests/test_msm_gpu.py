@@ -462,3 +462,34 @@ def test_headline_path_vs_c_port(gpu_ctx, logn, rows):
             assert ctx.dropin_stats()["hits"] == 1
         finally:
             ctx.close()
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_split_host_tail_pool_sizes(threads):
+    """The host tail split by bucket set (>= 8 sets: the variable-base MSM's
+    16 windows) with a pool smaller than the set count: 1 thread computes
+    every set inline in the chain, 3 threads leave the caller several sets.
+    Run in a child process (the pool size is read from OMP_NUM_THREADS when a
+    context first uses it) against the C port."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path[:0] = [{os.path.join(root, 'halo2-aggregation_amd')!r}, {os.path.join(root, 'oracle')!r}]\n"
+        "import halo2_amd as H, msm_ref, pasta as P\n"
+        "n = (1 << 16) + 5\n"
+        "S = msm_ref.synth_scalars(1, P.SEED_SCALARS ^ 0x77, 0, n, threads=4)\n"
+        "B = msm_ref.synth_bases(1, P.SEED_BASES ^ 0x77, 0, n, threads=4)\n"
+        "ctx = H.Context(0)\n"
+        "got = ctx.msm(1, S, B)\n"
+        "assert np.array_equal(got, msm_ref.best_multiexp(1, S, B, threads=4))\n"
+        "ctx.set_window(5)\n"
+        "assert np.array_equal(ctx.msm(1, S[:3000], B[:3000]), msm_ref.best_multiexp(1, S[:3000], B[:3000], threads=4))\n"
+        "ctx.close()\n"
+        "print('ok')\n")
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

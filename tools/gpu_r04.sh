@@ -41,7 +41,7 @@ for P in $PARTS; do
       cut -c1-150 $OUT/kernel_stats.csv | head -14 ;;
     acckt)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/acckt -o run -- python3 bench.py --no-cpu \
-        $QUICK --logn 10 --accum-b16 1 > $OUT/acckt.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/acckt.log; exit 1; }
+        $QUICK --logn 15 --accum-b16 1 > $OUT/acckt.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/acckt.log; exit 1; }
       find $OUT/acckt -name '*kernel_stats.csv' -exec cp {} $OUT/acc_kernel_stats.csv \;
       cut -c1-150 $OUT/acc_kernel_stats.csv | head -20 ;;
     micro)
