@@ -118,7 +118,14 @@ def test_vs_c_oracle(gpu_ctx, curve, n):
     got = gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n)
     S = s.cpu().numpy().view(np.uint64)
     B = b.cpu().numpy().view(np.uint64)
-    assert np.array_equal(got, msm_ref.best_multiexp(curve, S, B))
+    want = msm_ref.best_multiexp(curve, S, B)
+    assert np.array_equal(got, want)
+    if n <= H.SMALL_MSM_DEFAULT:  # that ran the small-MSM path: the sorting pipeline too
+        gpu_ctx.set_small_msm(0)
+        try:
+            assert np.array_equal(gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), n), want)
+        finally:
+            gpu_ctx.set_small_msm(H.SMALL_MSM_DEFAULT)
 
 
 @pytest.mark.parametrize("curve,logn", [(0, 20), (0, 22), (1, 22)])
