@@ -604,7 +604,7 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   if (n > kSmallLimit) return set_error(PM_ERR_UNSUPPORTED, "small-MSM path: n above its limit");
   const hipStream_t st = ctx->stream;
   const uint32_t un = (uint32_t)n, T = 2u * un;
-  const bool fused = T <= (uint32_t)kSmallQuads;
+  const bool fused = un <= kSmallFusedN;
   // slices per window: up to kSmallSlices blocks of 64 quads (or, from 4096
   // terms, 256 lanes with one-lane additions), each adding kq terms serially.
   // Measured (profiles/r04/small/ab.jsonl, n = 256 .. 8192, quads / lanes x
@@ -619,6 +619,10 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   g.r261 = b_r261 ? 1u : 0u;
   g.kq = std::max<uint32_t>(1u, (T + per * kSmallSlices - 1) / (per * kSmallSlices));
   g.ns = (T + per * g.kq - 1) / (per * g.kq);
+  if (fused) {  // one term per quad: 64 per slice
+    g.kq = 1;
+    g.ns = (T + kSmallQuads - 1) / kSmallQuads;
+  }
   int rc;
   const uint32_t* ds = (const uint32_t*)scalars;
   const uint32_t* db = (const uint32_t*)bases;
@@ -645,8 +649,8 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   if (!fused) {
     if ((rc = ctx->small_tab.ensure(n * kSmallMults * sizeof(Xyzz<F>)))) return rc;
     if ((rc = ctx->small_dig.ensure((size_t)kSmallWin * T))) return rc;
-    if ((rc = ctx->small_part.ensure((size_t)kSmallWin * g.ns * sizeof(Xyzz<F>)))) return rc;
   }
+  if ((rc = ctx->small_part.ensure((size_t)kSmallWin * g.ns * sizeof(Xyzz<F>)))) return rc;
   // counters (self-resetting; zero fresh allocations): a ticket per window, the done count
   const size_t old_cap = ctx->small_tk.cap;
   if ((rc = ctx->small_tk.ensure((kSmallWin + 1) * 4))) return rc;
@@ -663,7 +667,9 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   uint32_t* dflag = (uint32_t*)((Xyzz<F>*)dW + kSmallWin);
   if (fused) {
     PM_LAUNCH(ctx, "small_fused",
-              (k_small_fused<Cv><<<kSmallWin, 256, 0, st>>>(g, ds, db, (Xyzz<F>*)dW, tickets + kSmallWin, dflag, seq)));
+              (k_small_fused<Cv><<<dim3(g.ns, kSmallWin), 256, 0, st>>>(g, ds, db, (Xyzz<F>*)ctx->small_part.p,
+                                                                         tickets, (Xyzz<F>*)dW, tickets + kSmallWin,
+                                                                         dflag, seq)));
   } else {
     Xyzz<F>* tab = (Xyzz<F>*)ctx->small_tab.p;
     int8_t* dig = (int8_t*)ctx->small_dig.p;

@@ -37,6 +37,11 @@ constexpr int kSmallMults = 8;         // table entries per base: [1..8] P
 constexpr int kSmallTabPts = 16;       // k_small_table: bases per block (one per quad of each wave)
 constexpr int kSmallQuads = 64;        // k_small_sum: quads per block
 constexpr int kSmallPt = 36;           // an unpacked Xyzz29 in LDS (u32 words)
+// k_small_fused up to here (one slice per window).  Several slices per window
+// (one term per quad, the last block folding) measured slower than table + sum
+// from 64 points on (64 / 128 / 256: 86.6-87.1 / 92.3-93.1 / 95.1-100.8 us
+// against 83.4 / 89.0 / 95.1; profiles/r04/small/fused_ab.jsonl)
+constexpr uint32_t kSmallFusedN = 32;
 
 struct SmallGeom {
   uint32_t n;          // bases
@@ -256,7 +261,47 @@ __device__ __forceinline__ void small_finish(Xyzz<F>* out, uint32_t j, const Xyz
   }
 }
 
-// n <= 32 (2n <= 64 terms): one launch, block j = window j, one quad per term.
+// table entry of term t with digit d != 0: [|d|] P_i, phi'd for the second
+// GLV half (t odd), negated for d < 0
+template <class Cv>
+__device__ __forceinline__ Xyzz29<typename Cv::Base> small_term(const Xyzz<typename Cv::Base>* __restrict__ tab,
+                                                                 uint32_t t, int d) {
+  using F = typename Cv::Base;
+  using K = F29Consts<F>;
+  Xyzz29<F> P = load_xyzz29<F>(&tab[(size_t)(t >> 1) * kSmallMults + (uint32_t)(d < 0 ? -d : d) - 1u]);
+  if (t & 1u) P.X = f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), P.X);  // phi(P), X < 2p
+  if (d < 0) P.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), P.Y, K::K6)));  // < 3p
+  return P;
+}
+
+// after the block's tree (quad 0 holds slice s's sum of window j): with one
+// slice, finish window j; else park the partial, and the last slice's block
+// (atomic ticket) folds the ns partials and finishes it
+template <class F>
+__device__ __forceinline__ void small_fold(const SmallGeom& g, uint32_t (*s_p)[kSmallPt], uint32_t* last,
+                                           Xyzz29<F> acc, uint32_t s, uint32_t j, uint32_t v, uint32_t q,
+                                           Xyzz<F>* __restrict__ part, uint32_t* __restrict__ tickets,
+                                           Xyzz<F>* __restrict__ out, uint32_t* done, uint32_t* flag, uint32_t seq) {
+  if (g.ns > 1) {
+    if (v == 0) {
+      store_xyzz29_q<F>(&part[(size_t)j * g.ns + s], acc, q);
+      __threadfence();
+      if (q == 0) *last = atomicAdd(&tickets[j], 1u) == g.ns - 1u;
+    }
+    __syncthreads();
+    if (!*last) return;
+    __threadfence();
+    acc = xyzz29_inf<F>();
+    for (uint32_t u = v; u < g.ns; u += kSmallQuads) acc = xyzz29_add_q<F>(acc, load_xyzz29<F>(&part[(size_t)j * g.ns + u]));
+    acc = small_tree<F>(s_p, acc, v, q, small_pow2(g.ns < (uint32_t)kSmallQuads ? g.ns : (uint32_t)kSmallQuads));
+    if (v == 0 && q == 0) tickets[j] = 0;  // ready for the next MSM
+  }
+  if (v == 0) small_finish<F>(out, j, acc, q, done, flag, seq);
+}
+
+// Up to kSmallFusedN points: one launch, block (s, j) = slice s of window j,
+// one quad per term (64 terms per slice; several slices are folded by the
+// last block of the window, small_fold).
 // The quad builds its own term [d] (+-phi^h P) from the affine base: [2]P,
 // [4]P, [8]P and at most one addition ([3] = [2] + [1], [5] = [4] + [1], [6] =
 // [4] + [2], [7] = [8] - [1]) -- four operations, against the table kernel's
@@ -267,21 +312,24 @@ __device__ __forceinline__ void small_finish(Xyzz<F>* out, uint32_t j, const Xyz
 template <class Cv, bool TRACE = false>
 __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t* __restrict__ scalars,
                                                      const uint32_t* __restrict__ bases,
+                                                     Xyzz<typename Cv::Base>* __restrict__ part,
+                                                     uint32_t* __restrict__ tickets,
                                                      Xyzz<typename Cv::Base>* __restrict__ out,
                                                      uint32_t* __restrict__ done, uint32_t* __restrict__ flag,
                                                      uint32_t seq, uint64_t* __restrict__ tr = nullptr) {
-  const bool rec = TRACE && blockIdx.x == 0 && threadIdx.x == 0;
+  const bool rec = TRACE && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
   if (rec) tr[0] = wall_clock64();
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   using K = F29Consts<F>;
   __shared__ uint32_t s_p[kSmallQuads][kSmallPt];
-  const uint32_t j = blockIdx.x, v = threadIdx.x >> 2, q = threadIdx.x & 3u;
-  const uint32_t T = 2u * g.n, i = v >> 1, h = v & 1u;
+  __shared__ uint32_t last;
+  const uint32_t s = blockIdx.x, j = blockIdx.y, v = threadIdx.x >> 2, q = threadIdx.x & 3u;
+  const uint32_t T = 2u * g.n, t = s * kSmallQuads + v, i = t >> 1, h = t & 1u;
   Xyzz29<F> acc = xyzz29_inf<F>();
   int d = 0;
   F29<F> x = f29_zero<F>(), y = f29_zero<F>();
-  if (v < T) {
+  if (t < T) {
     const uint4* p = reinterpret_cast<const uint4*>(bases + 16ull * i);
     const uint4 a = p[0], b = p[1], c = p[2], e = p[3];
     const bool ident = ((a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w) | (c.x | c.y | c.z | c.w | e.x | e.y | e.z | e.w)) == 0;
@@ -336,48 +384,11 @@ __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t
     acc = xyzz29_add_q<F>(A, B);
   }
   if (rec) tr[6] = wall_clock64() + (acc.X.l[0] & 0u);
-  acc = small_tree<F>(s_p, acc, v, q, small_pow2(T));
+  const uint32_t active = T - s * kSmallQuads >= (uint32_t)kSmallQuads ? (uint32_t)kSmallQuads : T - s * kSmallQuads;
+  acc = small_tree<F>(s_p, acc, v, q, small_pow2(active));
   if (rec) tr[7] = wall_clock64() + (acc.X.l[0] & 0u);
-  if (v == 0) small_finish<F>(out, j, acc, q, done, flag, seq);
+  small_fold<F>(g, s_p, &last, acc, s, j, v, q, part, tickets, out, done, flag, seq);
   if (rec) tr[8] = wall_clock64();
-}
-
-// table entry of term t with digit d != 0: [|d|] P_i, phi'd for the second
-// GLV half (t odd), negated for d < 0
-template <class Cv>
-__device__ __forceinline__ Xyzz29<typename Cv::Base> small_term(const Xyzz<typename Cv::Base>* __restrict__ tab,
-                                                                 uint32_t t, int d) {
-  using F = typename Cv::Base;
-  using K = F29Consts<F>;
-  Xyzz29<F> P = load_xyzz29<F>(&tab[(size_t)(t >> 1) * kSmallMults + (uint32_t)(d < 0 ? -d : d) - 1u]);
-  if (t & 1u) P.X = f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), P.X);  // phi(P), X < 2p
-  if (d < 0) P.Y = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), P.Y, K::K6)));  // < 3p
-  return P;
-}
-
-// after the block's tree (quad 0 holds slice s's sum of window j): with one
-// slice, finish window j; else park the partial, and the last slice's block
-// (atomic ticket) folds the ns partials and finishes it
-template <class F>
-__device__ __forceinline__ void small_fold(const SmallGeom& g, uint32_t (*s_p)[kSmallPt], uint32_t* last,
-                                           Xyzz29<F> acc, uint32_t s, uint32_t j, uint32_t v, uint32_t q,
-                                           Xyzz<F>* __restrict__ part, uint32_t* __restrict__ tickets,
-                                           Xyzz<F>* __restrict__ out, uint32_t* done, uint32_t* flag, uint32_t seq) {
-  if (g.ns > 1) {
-    if (v == 0) {
-      store_xyzz29_q<F>(&part[(size_t)j * g.ns + s], acc, q);
-      __threadfence();
-      if (q == 0) *last = atomicAdd(&tickets[j], 1u) == g.ns - 1u;
-    }
-    __syncthreads();
-    if (!*last) return;
-    __threadfence();
-    acc = xyzz29_inf<F>();
-    for (uint32_t u = v; u < g.ns; u += kSmallQuads) acc = xyzz29_add_q<F>(acc, load_xyzz29<F>(&part[(size_t)j * g.ns + u]));
-    acc = small_tree<F>(s_p, acc, v, q, small_pow2(g.ns < (uint32_t)kSmallQuads ? g.ns : (uint32_t)kSmallQuads));
-    if (v == 0 && q == 0) tickets[j] = 0;  // ready for the next MSM
-  }
-  if (v == 0) small_finish<F>(out, j, acc, q, done, flag, seq);
 }
 
 // block (s, j), quads: quad v adds terms t0 + r 64 + v, r < kq (quad-

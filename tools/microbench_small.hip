@@ -47,8 +47,8 @@ int main() {
     double acc[8] = {0};
     const int reps = 20;
     for (int r = 0; r < reps + 2; r++) {
-      k_small_fused<Cv, true><<<kSmallWin, 256>>>(g, host ? dhs : ds, host ? dhb : db, out, done, flag,
-                                                  (uint32_t)r + 1, tr);
+      k_small_fused<Cv, true><<<dim3(1, kSmallWin), 256>>>(g, host ? dhs : ds, host ? dhb : db, nullptr, nullptr, out,
+                                                           done, flag, (uint32_t)r + 1, tr);
       (void)hipDeviceSynchronize();
       if (r >= 2)
         for (int k = 0; k < 8; k++) acc[k] += (double)(tr[k + 1] - tr[k]) * 0.01;  // 100 MHz ticks -> us
