@@ -146,6 +146,15 @@ def load_pmc_traffic(workload, launches_per_msm):
     return None
 
 
+def load_ntt_valu(workload):
+    """Integer-VALU fractions of the NTT passes from the committed SQ counters
+    (profiles/pmc_ntt.json "valu", tools/ntt_valu.py)."""
+    p = os.path.join(ROOT, "profiles", "pmc_ntt.json")
+    if os.path.exists(p):
+        return json.load(open(p)).get("workloads", {}).get(workload, {}).get("valu")
+    return None
+
+
 def load_ntt_traffic(workload):
     """HBM bytes per NTT (all passes) from the committed PMC passes
     (profiles/pmc_ntt.json: one entry per workload)."""
@@ -756,7 +765,10 @@ def run_ntt(args, ctx, dist, dev, world, k=None, keep_state=True):
                         "traffic": load_ntt_traffic(f"ntt_bn254_2^{k}"),
                         "note": "achieved = 64 B/element (read + write once) over all passes' kernel time; "
                                 "traffic = PMC FETCH+WRITE of all passes (profiles/pmc_ntt.json); the NTT is "
-                                "VALU-bound (n/2 log n Montgomery products)"}}
+                                "VALU-bound (n/2 log n Montgomery products): valu_int"}}
+    valu = load_ntt_valu(f"ntt_bn254_2^{k}")
+    if valu:
+        out["roofline"]["valu_int"] = valu
     if src is not None:
         out["_state"] = (curve, k, src, w, first)
     return out
