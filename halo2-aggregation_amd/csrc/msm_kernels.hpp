@@ -17,16 +17,14 @@
 //                   sorted list, summing consecutive same-bucket points with
 //                   XYZZ mixed additions (load-balanced regardless of the
 //                   bucket-size distribution).      [VALU-int bound, dominant]
-//   5. k_fixup_short folds the slice-boundary partial sums into their bucket
-//                   (chains queued by k_accumulate; k_fixup_long: block tree
-//                   for buckets spanning many slices; k_fixup: fixed-base).
-//   6. k_bucket_seg segment sums: S_j = sum B, T_j = sum i*B (L1 wide).
-//   7. k_bucket_bits per window: G_b = sum_{j: bit b of j} S_j and sum T_j via
-//                   LDS tree reductions (parallel form of sum_j j*S_j).
-//   8. k_bits_combine folds pairs of bit sums (Q = G_2j + 2 G_2j+1) and
-//                   converts them to the Rust R = 2^256 layout.
+//   5. k_bucket_seg_q folds each bucket's slice-boundary chain and forms the
+//                   segment sums of L1 = 4 buckets: S_j = sum B, T_j = sum i*B.
+//   6. k_bucket_bits per bucket set: G_b = sum_{j: bit b of j} S_j and
+//                   partial sums of T_j via LDS tree reductions (parallel form
+//                   of sum_j j*S_j), converted to the Rust R = 2^256 layout as
+//                   host terms.
 // The host (host_ec.hpp) then evaluates sum_w 2^{o_w} (sum T + L1 * sum_b 2^b
-// G_b) as one Horner over absolute bit positions.
+// G_b + K B_K) as one Horner over absolute bit positions.
 #pragma once
 #include "coop29.hpp"
 #include "curve29.hpp"

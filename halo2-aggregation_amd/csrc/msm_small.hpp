@@ -331,7 +331,9 @@ __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t
   F29<F> x = f29_zero<F>(), y = f29_zero<F>();
   if (t < T) {
     const uint4* p = reinterpret_cast<const uint4*>(bases + 16ull * i);
-    const uint4 a = p[0], b = p[1], c = p[2], e = p[3];
+    const uint4* sp = reinterpret_cast<const uint4*>(scalars + 8ull * i);
+    // the scalar's loads go out with the base's (one host-memory round trip, not two)
+    const uint4 a = p[0], b = p[1], c = p[2], e = p[3], s0 = sp[0], s1 = sp[1];
     const bool ident = ((a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w) | (c.x | c.y | c.z | c.w | e.x | e.y | e.z | e.w)) == 0;
     const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     const uint32_t wy[8] = {c.x, c.y, c.z, c.w, e.x, e.y, e.z, e.w};
@@ -345,8 +347,11 @@ __global__ void __launch_bounds__(256) k_small_fused(SmallGeom g, const uint32_t
     if (h) x = f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), x);  // phi(P): independent of the split below
     if (rec) tr[1] = wall_clock64() + (x.l[0] & 0u);
     if (!ident) {
-      Fe<Fs> k = load_canonical<Fs>(scalars, i, g.canonical);
-      if (g.canonical) k = fe_reduce_full<Fs>(k);
+      Fe<Fs> k;
+      const uint32_t kw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+      for (int w = 0; w < 8; w++) k.l[w] = kw[w];
+      k = g.canonical ? fe_reduce_full<Fs>(k) : fe_from_mont<Fs>(k);
       if (rec) tr[2] = wall_clock64() + (k.l[0] & 0u);
       uint32_t k1[6], k2[6];
       bool n1, n2;
