@@ -42,48 +42,78 @@ inline bool is_zero(const E<P>& a) {
   return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0;
 }
 
+// Field elements are canonical (< p) on entry and exit.  Every modulus here
+// is below 2^255, so a sum of two never carries out of 4 words and one
+// conditional subtraction reduces it.  Add / sub / the products' final step
+// are branch-free add/adc (sub/sbb) chains with cmov: the u128 forms GCC
+// emitted spilled through the stack (~7-10 ns per add on the container's
+// Xeon, tools/host_field_bench.cpp).
 template <class P>
-inline E<P> sub_p_if(const uint64_t t[4], uint64_t hi) {
-  uint64_t d[4], br = 0;
-  for (int i = 0; i < 4; i++) {
-    u128 x = (u128)t[i] - F64<P>::mod(i) - br;
-    d[i] = (uint64_t)x;
-    br = (uint64_t)(x >> 64) & 1;
-  }
+struct PMod {
+  static constexpr uint64_t v[4] = {F64<P>::mod(0), F64<P>::mod(1), F64<P>::mod(2), F64<P>::mod(3)};
+};
+
+// t < 2p -> t mod p
+template <class P>
+inline E<P> reduce_once(uint64_t t0, uint64_t t1, uint64_t t2, uint64_t t3) {
+  uint64_t d0 = t0, d1 = t1, d2 = t2, d3 = t3;
+  asm("subq %[p0], %[d0]\n\t"
+      "sbbq %[p1], %[d1]\n\t"
+      "sbbq %[p2], %[d2]\n\t"
+      "sbbq %[p3], %[d3]\n\t"
+      "cmovcq %[t0], %[d0]\n\t"
+      "cmovcq %[t1], %[d1]\n\t"
+      "cmovcq %[t2], %[d2]\n\t"
+      "cmovcq %[t3], %[d3]"
+      : [d0] "+&r"(d0), [d1] "+&r"(d1), [d2] "+&r"(d2), [d3] "+&r"(d3)
+      : [t0] "r"(t0), [t1] "r"(t1), [t2] "r"(t2), [t3] "r"(t3), [p0] "m"(PMod<P>::v[0]), [p1] "m"(PMod<P>::v[1]),
+        [p2] "m"(PMod<P>::v[2]), [p3] "m"(PMod<P>::v[3])
+      : "cc");
   E<P> r;
-  const bool take = hi || !br;
-  for (int i = 0; i < 4; i++) r.v[i] = take ? d[i] : t[i];
+  r.v[0] = d0;
+  r.v[1] = d1;
+  r.v[2] = d2;
+  r.v[3] = d3;
   return r;
 }
 
 template <class P>
 inline E<P> add(const E<P>& a, const E<P>& b) {
-  uint64_t t[4], c = 0;
-  for (int i = 0; i < 4; i++) {
-    u128 s = (u128)a.v[i] + b.v[i] + c;
-    t[i] = (uint64_t)s;
-    c = (uint64_t)(s >> 64);
-  }
-  return sub_p_if<P>(t, c);
+  uint64_t t0 = a.v[0], t1 = a.v[1], t2 = a.v[2], t3 = a.v[3];
+  asm("addq %[b0], %[t0]\n\t"
+      "adcq %[b1], %[t1]\n\t"
+      "adcq %[b2], %[t2]\n\t"
+      "adcq %[b3], %[t3]"
+      : [t0] "+r"(t0), [t1] "+r"(t1), [t2] "+r"(t2), [t3] "+r"(t3)
+      : [b0] "rm"(b.v[0]), [b1] "rm"(b.v[1]), [b2] "rm"(b.v[2]), [b3] "rm"(b.v[3])
+      : "cc");
+  return reduce_once<P>(t0, t1, t2, t3);
 }
 
 template <class P>
 inline E<P> sub(const E<P>& a, const E<P>& b) {
-  uint64_t t[4], br = 0;
-  for (int i = 0; i < 4; i++) {
-    u128 x = (u128)a.v[i] - b.v[i] - br;
-    t[i] = (uint64_t)x;
-    br = (uint64_t)(x >> 64) & 1;
-  }
-  const uint64_t m = 0 - br;  // add p back on a borrow, branch-free (the sign is data-dependent)
-  uint64_t c = 0;
-  for (int i = 0; i < 4; i++) {
-    u128 s = (u128)t[i] + (F64<P>::mod(i) & m) + c;
-    t[i] = (uint64_t)s;
-    c = (uint64_t)(s >> 64);
-  }
+  uint64_t t0 = a.v[0], t1 = a.v[1], t2 = a.v[2], t3 = a.v[3], m;
+  asm("subq %[b0], %[t0]\n\t"
+      "sbbq %[b1], %[t1]\n\t"
+      "sbbq %[b2], %[t2]\n\t"
+      "sbbq %[b3], %[t3]\n\t"
+      "sbbq %[m], %[m]"  // m = 0 - borrow: add p back on a borrow, branch-free
+      : [t0] "+r"(t0), [t1] "+r"(t1), [t2] "+r"(t2), [t3] "+r"(t3), [m] "=&r"(m)
+      : [b0] "rm"(b.v[0]), [b1] "rm"(b.v[1]), [b2] "rm"(b.v[2]), [b3] "rm"(b.v[3])
+      : "cc");
+  const uint64_t q0 = PMod<P>::v[0] & m, q1 = PMod<P>::v[1] & m, q2 = PMod<P>::v[2] & m, q3 = PMod<P>::v[3] & m;
+  asm("addq %[q0], %[t0]\n\t"
+      "adcq %[q1], %[t1]\n\t"
+      "adcq %[q2], %[t2]\n\t"
+      "adcq %[q3], %[t3]"
+      : [t0] "+r"(t0), [t1] "+r"(t1), [t2] "+r"(t2), [t3] "+r"(t3)
+      : [q0] "r"(q0), [q1] "r"(q1), [q2] "r"(q2), [q3] "r"(q3)
+      : "cc");
   E<P> r;
-  memcpy(r.v, t, 32);
+  r.v[0] = t0;
+  r.v[1] = t1;
+  r.v[2] = t2;
+  r.v[3] = t3;
   return r;
 }
 
@@ -94,7 +124,7 @@ template <class P>
 inline E<P> mul(const E<P>& a, const E<P>& b) {
   constexpr uint64_t INV = F64<P>::inv();
   constexpr uint64_t p0 = F64<P>::mod(0), p1 = F64<P>::mod(1), p2 = F64<P>::mod(2), p3 = F64<P>::mod(3);
-  static_assert(p3 < (1ull << 63) - 1, "no-carry CIOS needs a spare top bit");
+  static_assert(p3 < (1ull << 63) - 1, "no-carry CIOS (and the carry-free add) need a spare top bit");
   uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   for (int i = 0; i < 4; i++) {
     const uint64_t bi = b.v[i];
@@ -120,8 +150,7 @@ inline E<P> mul(const E<P>& a, const E<P>& b) {
     C >>= 64;
     t3 = (uint64_t)C + (uint64_t)A;
   }
-  const uint64_t t[4] = {t0, t1, t2, t3};
-  return sub_p_if<P>(t, 0);
+  return reduce_once<P>(t0, t1, t2, t3);
 }
 
 // The same product with BMI2 / ADX: CIOS, every round one mulx row of a b_i
@@ -176,8 +205,7 @@ inline E<P> mul_adx(const E<P>& a, const E<P>& b) {
           [p0] "m"(PM[0]), [p1] "m"(PM[1]), [p2] "m"(PM[2]), [p3] "m"(PM[3]), [inv] "m"(INV)
         : "rax", "rdx", "cc");
   }
-  const uint64_t t[4] = {t0, t1, t2, t3};
-  return sub_p_if<P>(t, 0);
+  return reduce_once<P>(t0, t1, t2, t3);
 }
 
 template <class P>

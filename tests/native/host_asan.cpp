@@ -83,6 +83,20 @@ static Fe<P> to_fe(const host::E<P>& e) {
 // host 64-bit Montgomery == the 32-bit library product; inversion round trip
 template <class P>
 static void field_checks(int n) {
+  // the asm add / sub (host_ec.hpp) against the 32-bit library, at the edges
+  // (0, 1, p - 1, p - 2) and on random canonical values
+  host::E<P> pm1, pm2, zero, one;
+  for (int k = 0; k < 4; k++) pm1.v[k] = host::F64<P>::mod(k), zero.v[k] = 0, one.v[k] = 0;
+  pm1.v[0] -= 1;
+  pm2 = pm1;
+  pm2.v[0] -= 1;
+  one.v[0] = 1;
+  const host::E<P> edge[4] = {zero, one, pm1, pm2};
+  for (int i = 0; i < 16 + n; i++) {
+    const host::E<P> a = i < 16 ? edge[i & 3] : rnd_fe<P>(), b = i < 16 ? edge[i >> 2] : rnd_fe<P>();
+    CHECK(std::memcmp(to_fe<P>(host::add<P>(a, b)).l, fe_add<P>(to_fe<P>(a), to_fe<P>(b)).l, 32) == 0);
+    CHECK(std::memcmp(to_fe<P>(host::sub<P>(a, b)).l, fe_sub<P>(to_fe<P>(a), to_fe<P>(b)).l, 32) == 0);
+  }
   for (int i = 0; i < n; i++) {
     const host::E<P> a = rnd_fe<P>(), b = rnd_fe<P>();
     const host::E<P> x = host::mul<P>(a, b);
