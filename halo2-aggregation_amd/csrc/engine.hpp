@@ -408,26 +408,35 @@ host::Pt<F> tail_set(const MsmTail<F>& t, int w) {
   }
   return acc;
 }
+// Sets are claimed, not assigned: a worker takes the next unclaimed set from
+// the top (shared counter + per-set claim), and the caller computes a set
+// itself when the chain reaches it unclaimed -- so a worker that wakes late
+// (condition-variable wake-ups take ~10-20 us) delays nothing; the caller
+// waits only for a set already in progress on a worker.
 template <class F, bool ADX>
 host::Pt<F> tail_split(Ctx* ctx, const MsmTail<F>& t) {
   const int Wr = t.Wr;
   std::vector<host::Pt<F>> V((size_t)Wr);
-  std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[(size_t)Wr]);
-  for (int w = 0; w < Wr; w++) ready[w].store(0, std::memory_order_relaxed);
+  std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[(size_t)Wr]);  // 0 free, 1 claimed, 2 ready
+  for (int w = 0; w < Wr; w++) state[w].store(0, std::memory_order_relaxed);
+  std::atomic<int> next(Wr - 2);
+  auto run = [&](int w) {
+    V[(size_t)w] = tail_set<F, ADX>(t, w);
+    state[w].store(2, std::memory_order_release);
+  };
+  auto claim = [&](int w) {
+    int z = 0;
+    return state[w].compare_exchange_strong(z, 1, std::memory_order_acq_rel);
+  };
   HostPool& pool = ctx->host_pool();
   const int nt = std::min(pool.size(), Wr);
-  // the caller takes the top set, the workers the rest round-robin from the top
-  auto job = [&](int th, int n) {
-    for (int w = Wr - 1 - th; w >= 0; w -= n) {
-      V[(size_t)w] = tail_set<F, ADX>(t, w);
-      ready[w].store(1, std::memory_order_release);
-    }
+  auto job = [&](int, int) {
+    for (int w = next.fetch_sub(1, std::memory_order_relaxed); w >= 0; w = next.fetch_sub(1, std::memory_order_relaxed))
+      if (claim(w)) run(w);
   };
   if (nt > 1) pool.start(nt, job);
-  // the caller's share (th = 0): the top set now, the rest (only when the
-  // pool is smaller than Wr) when the chain below reaches them
-  V[(size_t)Wr - 1] = tail_set<F, ADX>(t, Wr - 1);
-  ready[Wr - 1].store(1, std::memory_order_release);
+  state[Wr - 1].store(1, std::memory_order_relaxed);
+  run(Wr - 1);  // the caller: the top set now, then the outer chain
   auto jac = [](const host::Pt<F>& p) {  // XYZZ (ZZ^3 = ZZZ^2) -> Jacobian (X ZZ^2, Y ZZZ^2, ZZZ)
     host::Jac<F> r;
     if (host::is_zero(p.ZZ)) {
@@ -443,13 +452,8 @@ host::Pt<F> tail_split(Ctx* ctx, const MsmTail<F>& t) {
   for (int w = Wr - 2; w >= 0; w--) {
     const int width = t.base + (w < t.extra ? 1 : 0);  // o_{w+1} - o_w
     for (int k = 0; k < width; k++) acc = host::jdbl<F, ADX>(acc);
-    if (nt <= 1 || (Wr - 1 - w) % nt == 0) {  // the caller's own set
-      if (!ready[w].load(std::memory_order_acquire)) {
-        V[(size_t)w] = tail_set<F, ADX>(t, w);
-        ready[w].store(1, std::memory_order_release);
-      }
-    }
-    while (!ready[w].load(std::memory_order_acquire)) __builtin_ia32_pause();
+    if (claim(w)) run(w);
+    while (state[w].load(std::memory_order_acquire) != 2) __builtin_ia32_pause();
     acc = host::jadd<F, ADX>(acc, jac(V[(size_t)w]));
   }
   if (nt > 1) pool.wait();
