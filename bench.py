@@ -167,6 +167,45 @@ def load_ntt_traffic(workload):
     return None
 
 
+class HostCollectives:
+    """PM_BENCH_SHARE_GPU=1: a rehearsal of the N-rank flow on a one-GPU box
+    (every leg's collectives, barriers and rank-0 output with world > 1).  All
+    ranks run on device 0 -- RCCL refuses two ranks on one device -- and the
+    collectives go through gloo on host copies of the device tensors.  The
+    numbers of such a run say nothing about scaling; only the driver's
+    multi-GPU runs (RCCL over xGMI) do."""
+
+    def __init__(self, d, torch):
+        self.d, self.torch, self.ReduceOp = d, torch, d.ReduceOp
+
+    class _Done:
+        def wait(self):
+            return None
+
+    def barrier(self):
+        self.d.barrier()
+
+    def all_reduce(self, t, op=None):
+        c = t.cpu()
+        self.d.all_reduce(c, op=self.d.ReduceOp.SUM if op is None else op)
+        t.copy_(c)
+
+    def all_gather(self, out_list, t):
+        parts = [self.torch.empty_like(t, device="cpu") for _ in out_list]
+        self.d.all_gather(parts, t.cpu())
+        for dst, src in zip(out_list, parts):
+            dst.copy_(src)
+
+    def all_gather_into_tensor(self, out, t, async_op=False):
+        parts = [self.torch.empty_like(t, device="cpu") for _ in range(self.d.get_world_size())]
+        self.d.all_gather(parts, t.cpu())
+        out.copy_(self.torch.cat(parts).to(out.device))
+        return self._Done() if async_op else None
+
+    def destroy_process_group(self):
+        self.d.destroy_process_group()
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -184,11 +223,18 @@ def main():
     import halo2_amd as H
     from sharded import combine_partials, shard_range, split_range
 
+    share = world > 1 and os.environ.get("PM_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0  # rehearsal: every rank on device 0 (see HostCollectives)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+            dist = HostCollectives(dist, torch)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     n = 1 << args.logn
     curve = H.PALLAS

@@ -21,10 +21,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_per_rank, q):
+def _worker(rank, world, port, n_per_rank, q, host_collectives=False):
     import sys
 
-    for p in (os.path.join(ROOT, "halo2-aggregation_amd"), os.path.join(ROOT, "oracle")):
+    for p in (ROOT, os.path.join(ROOT, "halo2-aggregation_amd"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
     import torch
     import torch.distributed as dist
@@ -36,6 +36,13 @@ def _worker(rank, world, port, n_per_rank, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if host_collectives:  # bench.py's PM_BENCH_SHARE_GPU rehearsal wrapper
+        import bench
+
+        dist = bench.HostCollectives(dist, torch)
+        t = torch.tensor([rank + 1.0])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        assert t.item() == world
     i0, n = shard_range(rank, world, n_per_rank)
     S = msm_ref.synth_scalars(0, P.SEED_SCALARS, i0, n, threads=2)
     B = msm_ref.synth_bases(0, P.SEED_BASES, i0, n, threads=2)
@@ -54,8 +61,8 @@ def _worker(rank, world, port, n_per_rank, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_msm_gloo(world):
+@pytest.mark.parametrize("world,host_collectives", [(2, False), (3, False), (2, True)])
+def test_sharded_msm_gloo(world, host_collectives):
     import msm_ref
     import pasta as P
 
@@ -63,7 +70,8 @@ def test_sharded_msm_gloo(world):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per_rank, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per_rank, q, host_collectives))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=240) for _ in range(world)]
