@@ -15,6 +15,7 @@
 #include <sched.h>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/pasta_msm.h"
@@ -23,6 +24,7 @@
 #include "msm_kernels.hpp"
 #include "runtime.hpp"
 #include "blake2b.hpp"
+#include "engine.hpp"
 
 using namespace pm;
 
@@ -1141,8 +1143,51 @@ uint64_t selftest_host_field(uint64_t seed, size_t n) {
     }
   }
   const Pt<P> jx = jac_to_xyzz<P, true>(ja);  // equal points: X1 ZZ2 == X2 ZZ1, Y1 ZZZ2 == Y2 ZZZ1
-  const E<P> l1 = mul<P>(xa.X, jx.ZZ), r1 = mul<P>(jx.X, xa.ZZ), l2 = mul<P>(xa.Y, jx.ZZZ), r2 = mul<P>(jx.Y, xa.ZZZ);
-  bad += memcmp(&l1, &r1, 32) != 0 || memcmp(&l2, &r2, 32) != 0 || is_zero(xa.ZZ);
+  auto same = [&](const Pt<P>& u, const Pt<P>& v) {
+    const E<P> l1 = mul<P>(u.X, v.ZZ), r1 = mul<P>(v.X, u.ZZ), l2 = mul<P>(u.Y, v.ZZZ), r2 = mul<P>(v.Y, u.ZZZ);
+    return memcmp(&l1, &r1, 32) == 0 && memcmp(&l2, &r2, 32) == 0 && !is_zero(u.ZZ) && !is_zero(v.ZZ);
+  };
+  bad += !same(xa, jx);
+  // the split host tail (sets claimed by pool threads, engine.hpp tail_split)
+  // == the single Horner (tail_terms / tail_run) on the variable-base
+  // geometry (16 sets of 16 bits), with identity terms among random ones, on
+  // pools of 1, 3 and 16 threads
+  {
+    pm::MsmTail<P> t;
+    t.Wr = 16;
+    t.NB2 = 13;
+    t.NQ = t.NB2 + pm::kTJobs + 1;
+    t.base = 16;
+    t.extra = 0;
+    t.log2L1 = 2;
+    t.cmax = 16;
+    t.empty = false;
+    // terms on the curve (the group law is associative only there, and the
+    // two forms add the terms in different orders): multiples of the
+    // generator by a random double-and-add walk, each under a random z
+    auto e_of = [](const pm::Fe<P>& f) {
+      E<P> e;
+      for (int k = 0; k < 4; k++) e.v[k] = (uint64_t)f.l[2 * k] | ((uint64_t)f.l[2 * k + 1] << 32);
+      return e;
+    };
+    const pm::Fe<P> one = pm::fe_one<P>();
+    const bool pasta = !std::is_same<P, pm::Bn254Fq>::value;  // generators (-1, 2) / (1, 2)
+    const Pt<P> G{e_of(pasta ? pm::fe_neg<P>(one) : one), e_of(pm::fe_add<P>(one, one)), e_of(one), e_of(one)};
+    std::vector<pm::Xyzz<P>> Q((size_t)t.Wr * t.NQ);
+    Pt<P> cur = G;
+    for (size_t k = 0; k < Q.size(); k++) {
+      cur = (rnd() & 1) ? dbl<P, true>(cur) : addp<P, true>(cur, G);
+      const E<P> z = fe(), zz = mul<P>(z, z), zzz = mul<P>(zz, z);
+      const Pt<P> x{mul<P>(cur.X, zz), mul<P>(cur.Y, zzz), mul<P>(cur.ZZ, zz), mul<P>(cur.ZZZ, zzz)};
+      Q[k] = to_dev<P>(k % 37 == 5 || is_zero(z) ? inf<P>() : x);
+    }
+    t.hQ = Q.data();
+    const Pt<P> want = pm::tail_run<P>(t, pm::tail_terms<P>(t));
+    for (int th : {1, 3, 16}) {
+      pm::HostPool pool(th);
+      bad += !same(pm::tail_split_bmi2<P>(pool, t), want);
+    }
+  }
   return bad;
 }
 }  // namespace

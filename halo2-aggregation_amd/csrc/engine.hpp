@@ -414,7 +414,7 @@ host::Pt<F> tail_set(const MsmTail<F>& t, int w) {
 // (condition-variable wake-ups take ~10-20 us) delays nothing; the caller
 // waits only for a set already in progress on a worker.
 template <class F, bool ADX>
-host::Pt<F> tail_split(Ctx* ctx, const MsmTail<F>& t) {
+host::Pt<F> tail_split(HostPool& pool, const MsmTail<F>& t) {
   const int Wr = t.Wr;
   std::vector<host::Pt<F>> V((size_t)Wr);
   std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[(size_t)Wr]);  // 0 free, 1 claimed, 2 ready
@@ -428,7 +428,6 @@ host::Pt<F> tail_split(Ctx* ctx, const MsmTail<F>& t) {
     int z = 0;
     return state[w].compare_exchange_strong(z, 1, std::memory_order_acq_rel);
   };
-  HostPool& pool = ctx->host_pool();
   const int nt = std::min(pool.size(), Wr);
   auto job = [&](int, int) {
     for (int w = next.fetch_sub(1, std::memory_order_relaxed); w >= 0; w = next.fetch_sub(1, std::memory_order_relaxed))
@@ -461,8 +460,39 @@ host::Pt<F> tail_split(Ctx* ctx, const MsmTail<F>& t) {
   return host::jac_to_xyzz<F, ADX>(acc);
 }
 template <class F>
-__attribute__((target("bmi2,adx"))) host::Pt<F> tail_split_bmi2(Ctx* ctx, const MsmTail<F>& t) {
-  return tail_split<F, true>(ctx, t);
+__attribute__((target("bmi2,adx"))) host::Pt<F> tail_split_bmi2(HostPool& pool, const MsmTail<F>& t) {
+  return tail_split<F, true>(pool, t);
+}
+
+// The single Horner over absolute bit positions (fewer than kTailSplitSets
+// sets): tail_terms lists the terms as (position, index) sorted by descending
+// position, one flat array (a vector per position cost ~270 allocations per
+// call; msm_tail builds it while the kernels still run), tail_run evaluates.
+template <class F>
+std::vector<std::pair<int, int>> tail_terms(const MsmTail<F>& t) {
+  std::vector<std::pair<int, int>> terms;
+  terms.reserve((size_t)t.Wr * t.NQ);
+  for (int w = 0; w < t.Wr; w++) {
+    const int o = w * t.base + std::min(w, t.extra);  // w < Wr: set w's offset
+    for (int b = 0; b < t.NQ; b++) {
+      const int q = b < t.NB2 ? o + b + t.log2L1 : b < t.NQ - 1 ? o : o + t.cmax - 1;
+      terms.emplace_back(q, w * t.NQ + b);
+    }
+  }
+  std::sort(terms.begin(), terms.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+    return a.first > b.first || (a.first == b.first && a.second < b.second);
+  });
+  return terms;
+}
+template <class F>
+host::Pt<F> tail_run(const MsmTail<F>& t, const std::vector<std::pair<int, int>>& terms) {
+  host::Pt<F> hacc = host::inf<F>();
+  const int q = terms.front().first;
+  if (host_has_bmi2())
+    horner_steps_bmi2<F>(hacc, q, terms.data(), terms.size(), t.hQ);
+  else
+    horner_steps<F>(hacc, q, terms.data(), terms.size(), t.hQ);
+  return hacc;
 }
 
 // Host tail: sum_w 2^{o_w} (sum_b 2^{b + log2 L1} G_{w,b} + sum T_w + K B_{w,K})
@@ -477,7 +507,8 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
   if (t.Wr >= kTailSplitSets) {
     if (int rc = wait_event(ctx, t.ev)) return rc;
     const auto t0 = std::chrono::steady_clock::now();
-    const host::Pt<F> r = host_has_bmi2() ? tail_split_bmi2<F>(ctx, t) : tail_split<F, false>(ctx, t);
+    const host::Pt<F> r = host_has_bmi2() ? tail_split_bmi2<F>(ctx->host_pool(), t)
+                                          : tail_split<F, false>(ctx->host_pool(), t);
     if (ctx->timing) {
       auto& stt = ctx->stats["host_tail"];
       stt.first += 1;
@@ -486,28 +517,10 @@ int msm_tail(Ctx* ctx, const MsmTail<F>& t, Xyzz<F>* result) {
     *result = host::to_dev<F>(r);
     return PM_OK;
   }
-  // the terms as (position, index) sorted by descending position: one flat
-  // array (a vector per position cost ~270 allocations per call)
-  std::vector<std::pair<int, int>> terms;
-  terms.reserve((size_t)t.Wr * t.NQ);
-  for (int w = 0; w < t.Wr; w++) {
-    const int o = w * t.base + std::min(w, t.extra);  // w < Wr: set w's offset
-    for (int b = 0; b < t.NQ; b++) {
-      const int q = b < t.NB2 ? o + b + t.log2L1 : b < t.NQ - 1 ? o : o + t.cmax - 1;
-      terms.emplace_back(q, w * t.NQ + b);
-    }
-  }
-  std::sort(terms.begin(), terms.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
-    return a.first > b.first || (a.first == b.first && a.second < b.second);
-  });
+  const std::vector<std::pair<int, int>> terms = tail_terms<F>(t);
   if (int rc = wait_event(ctx, t.ev)) return rc;
   const auto t0 = std::chrono::steady_clock::now();
-  host::Pt<F> hacc = host::inf<F>();
-  const int q = terms.front().first;
-  if (host_has_bmi2())
-    horner_steps_bmi2<F>(hacc, q, terms.data(), terms.size(), t.hQ);
-  else
-    horner_steps<F>(hacc, q, terms.data(), terms.size(), t.hQ);
+  const host::Pt<F> hacc = tail_run<F>(t, terms);
   if (ctx->timing) {
     auto& stt = ctx->stats["host_tail"];
     stt.first += 1;

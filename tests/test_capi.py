@@ -93,7 +93,9 @@ def test_device_code_has_every_launched_kernel():
 @pytest.mark.parametrize("curve", [0, 1, 2])
 def test_host_tail_adx_product(curve):
     """CPU: the host Horner tail's mulx/adcx/adox Montgomery product (and the
-    doubling / addition chain built on it) equals the portable product."""
+    doubling / addition chain built on it) equals the portable product, the
+    Jacobian chain the XYZZ chain, and the split tail (sets claimed by pool
+    threads, 1 / 3 / 16 of them) the single Horner on random terms."""
     got = H.selftest_host(curve, seed=0xC0FFEE + curve, n=20000)
     if got is None:
         pytest.skip("CPU without BMI2/ADX")
