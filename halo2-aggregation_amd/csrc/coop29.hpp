@@ -90,44 +90,59 @@ __device__ __forceinline__ Jac29<F> jac29_dbl_q(const Jac29<F>& p) {
   return r;
 }
 
-// jac29_dbl_q plus the storage form of the new point, on lanes that idle in
-// the last two levels: L2 lane 3 squares Z3 (-> zz, lane 3), L3 lane 0
-// multiplies beta X3 and lane 3 ZZ Z3 (-> ext).  Only lanes 1 and 2 compute
-// E (D - X3), so only they hold Y3 afterwards; lanes 0 and 3 never read Y
-// (their L1 product is X X) and keep a bounded dummy there.  Outputs on the
-// owning lanes: X3 (all), Y3 (1, 2), ZZ3 < 2p (3), ZZZ3 < 2p (3), beta X3 < 2p
-// (0).  Same chain length as jac29_dbl_q.
+// The a = 0 doubling of k_acc_powers plus the storage form of the new point.
+// dbl-2009-l's values, with every linear combination that can be a product
+// turned into one (one quad level costs one product on every lane, whatever
+// each lane multiplies, while the linear steps run on all 4 lanes in series):
+//   L1  lane 1 B = Y Y, lane 2 Y Z, lane 3 E = (3X) X   (lane 0 idles)
+//   L2  lane 0 4C = (4B) B, lane 1 D = (4X) B (= 2((X + B)^2 - A - C)),
+//       lane 2 F = E E, lane 3 ZZ3 = Z3 Z3
+//   L3  lanes 1, 2 E (D - X3), lane 0 beta X3, lane 3 ZZZ3 = ZZ3 Z3
+// X3 = F - 2D, Y3 = E (D - X3) - 2 (4C), Z3 = 2 Y Z.  Against the
+// squaring form (A, (X + B)^2 and C as squares, D, E and 8C from additions
+// with a normalisation and a reduction each) this drops ~220 instructions of
+// the ~610 between the products, for a product instead of a square at L2.
+// Bounds (fp29.hpp: operand limbs a_i b_j <= 2^60, a b < R p): X, Y Norm < 3p,
+// Z < 4p with limbs < 2^30 (Z3 is not normalised: it only enters products);
+// 3X, 4X, 4B have limbs < 2^31 against a Norm partner; the products are
+// <= 27 p^2.  X3 = F + 8p - 2D < 10p, Y3 = E w + 8p - 8C < 10p before the
+// reduction (Norm, < 3p after it).  Only lanes 1 and 2 compute E (D - X3),
+// so only they hold Y3 afterwards; lanes 0 and 3 never read Y and keep a
+// bounded dummy there.  Outputs on the owning lanes: X3 (all), Y3 (1, 2),
+// ZZ3 < 2p (3), ZZZ3 < 2p (3), beta X3 < 2p (0).
 template <class F>
 __device__ __forceinline__ Jac29<F> jac29_dbl_q_ext(const Jac29<F>& p, const F29<F>& beta, F29<F>& zz,
                                                     F29<F>& ext) {
   using K = F29Consts<F>;
   const uint32_t q = quad_id();
-  const uint32_t m12 = (q == 1u || q == 2u) ? ~0u : 0u, m2 = q == 2u ? ~0u : 0u;
+  const uint32_t m0 = q == 0u ? ~0u : 0u, m01 = q < 2u ? ~0u : 0u, m12 = (q == 1u || q == 2u) ? ~0u : 0u;
+  const uint32_t m2 = q == 2u ? ~0u : 0u, m3 = q == 3u ? ~0u : 0u;
+  // L1 operands: (X, X) / (Y, Y) / (Y, Z) / (3X, X)
   F29<F> o1a, o1b;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
-    o1a.l[i] = bsel(m12, p.Y.l[i], p.X.l[i]);
-    o1b.l[i] = bsel(m2, p.Z.l[i], o1a.l[i]);
+    o1a.l[i] = bsel(m12, p.Y.l[i], bsel(m3, p.X.l[i] * 3u, p.X.l[i]));
+    o1b.l[i] = bsel(m2, p.Z.l[i], bsel(m12, p.Y.l[i], p.X.l[i]));
   }
   const F29<F> r1 = f29_mul_c<F>(o1a, o1b);
-  const F29<F> A = qbc<0, F>(r1), B = qbc<1, F>(r1), YZ = qbc<2, F>(r1);
+  const F29<F> B = qbc<1, F>(r1), YZ = qbc<2, F>(r1), E = qbc<3, F>(r1);
   Jac29<F> r;
-  r.Z = f29_norm<F>(f29_add<F>(YZ, YZ));                                   // < 4p
-  const F29<F> t = f29_norm<F>(f29_add<F>(p.X, B));
-  const F29<F> E = f29_norm<F>(f29_add<F>(f29_add<F>(A, A), A));
-  const F29<F> r2 = f29_sqr_c<F>(qsel<F>(q, B, t, E, r.Z));
-  const F29<F> C = qbc<0, F>(r2), s = qbc<1, F>(r2), FF = qbc<2, F>(r2);
+  r.Z = f29_add<F>(YZ, YZ);  // < 4p, limbs < 2^30
+  // L2 operands: (4B, B) / (4X, B) / (E, E) / (Z3, Z3)
+  F29<F> o2a, o2b;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t ez = bsel(m2, E.l[i], r.Z.l[i]);
+    o2a.l[i] = bsel(m01, bsel(m0, B.l[i], p.X.l[i]) << 2, ez);
+    o2b.l[i] = bsel(m01, B.l[i], ez);
+  }
+  const F29<F> r2 = f29_mul_c<F>(o2a, o2b);
   zz = r2;
-  const F29<F> u = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(s, f29_add<F>(A, C), K::K8x3)));
-  const F29<F> D = f29_reduce3<F>(f29_norm<F>(f29_add<F>(u, u)));
+  const F29<F> C4 = qbc<0, F>(r2), D = qbc<1, F>(r2), FF = qbc<2, F>(r2);
   r.X = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(FF, f29_add<F>(D, D), K::K8x3)));
   const F29<F> w = f29_sub<F>(D, r.X, K::K6);
-  F29<F> C8 = C;
-#pragma unroll
-  for (int i = 0; i < 9; i++) C8.l[i] = C.l[i] << 3;
-  C8 = f29_reduce3<F>(f29_norm<F>(C8));
-  // operands (beta, X3) / (E, w) / (E, w) / (ZZ3, Z3): two selects per limb
-  const uint32_t m0 = q == 0u ? ~0u : 0u, m3 = q == 3u ? ~0u : 0u;
+  const F29<F> C8 = f29_add<F>(C4, C4);  // limbs < 2^30 <= K8x3's
+  // L3 operands: (beta, X3) / (E, w) / (E, w) / (ZZ3, Z3)
   F29<F> o3a, o3b;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
