@@ -924,6 +924,8 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
            "from_decoded": {"ms_per_batch": round(ms_dec, 4), "value": round(world * B / (ms_dec * 1e-3), 1),
                             "entry": "pm_accum_batch_transcript_device (decoded points / scalars in HBM)",
                             "quads_match_bytes_path": bool(torch.equal(quads_dec, batch.quads))}}
+    if world == 1:
+        out["two_in_flight"] = accum_two_in_flight(args, ctx, shape, batch, B)
     if rank == 0:
         host = {k: getattr(batch, k).cpu().numpy().view(np.uint64)
                 for k in ("points", "scalars", "challenges", "quads", "h_eval")}
@@ -932,6 +934,53 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
         host["inst"] = batch.inst.cpu().numpy().view(np.uint64)
         out["_state"] = (curve, shape, host, B)
     return out
+
+
+def accum_two_in_flight(args, ctx, shape, batch, B):
+    """Two batches in flight: a second context (its own HIP streams and
+    workspace) runs another B proofs from bytes on a second host thread
+    while `ctx` runs `batch`.  One batch is a set of latency-bound chains
+    that leave most SIMDs idle; the pair's combined rate
+    is the throughput of a stream of batches.  Reported beside the
+    one-batch `value`, which stays the headline."""
+    import threading
+
+    import torch
+
+    import halo2_amd as H
+    import workloads as Wk
+
+    ctx2 = H.Context(0)
+    b2 = Wk.SyntheticBatch(ctx2, shape, B, seed=0xACD)
+    b2.to_proof_bytes(shape)
+    b2.run_bytes(ctx2, shape)
+    torch.cuda.synchronize()
+    refs = [batch.quads.clone(), b2.quads.clone()]
+    errs = []
+
+    def loop(c, b):
+        try:
+            for _ in range(args.warmup + args.steps):
+                b.run_bytes(c, shape)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=loop, args=cb) for cb in ((ctx, batch), (ctx2, b2))]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    n = 2 * (args.warmup + args.steps)
+    ok = not errs and all(torch.equal(r, b.quads) for r, b in zip(refs, (batch, b2)))
+    ok = ok and int((batch.status != 0).sum().item()) == 0 and int((b2.status != 0).sum().item()) == 0
+    del ctx2
+    return {"value": round(n * B / el, 1), "unit": "proofs/s", "ms_per_batch": round(el * 1e3 / n, 4),
+            "batches": n, "how": "2 contexts x 2 host threads, each looping pm_accum_batch_proofs_device on its "
+                                 "own batch of B proofs from bytes (warmup included in the timed loop)",
+            "quads_match_single_runs": ok, "errors": errs}
 
 
 def accum_latency_roofline(B, T, nslots, ms_batch, kernels, from_bytes=True):
