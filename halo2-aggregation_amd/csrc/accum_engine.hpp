@@ -7,6 +7,7 @@
 // src/multiopen.rs:271-509).
 #pragma once
 #include <vector>
+#include <hip/hip_ext.h>
 
 #include "accum_kernels.hpp"
 #include "engine.hpp"
@@ -79,7 +80,7 @@ inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
 template <class Cv>
 int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d_points, const void* d_scalars,
                       void* d_ch, void* d_out, void* d_hout, const uint64_t* vk_repr, void* d_status,
-                      bool canon_ready = false, bool keep_status = false) {
+                      bool canon_ready = false, bool keep_status = false, hipEvent_t inputs_ready = nullptr) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
@@ -270,10 +271,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     key.push_back((uint64_t)F::MOD[1] << 32 | F::MOD[2]);  // the curve (its base field)
     const bool vk_current = ctx->acc_vkpow_gen == ctx->acc_vkpow.gen && ctx->acc_vkpow_key == key;
     const uint32_t nvk_build = vk_current ? 0u : (uint32_t)nvk;
-    up = ctx->next_event();
+    // inputs_ready: the proof decode's own completion event (proof-bytes
+    // entry), so no marker sits between the decode and the ladder
+    up = inputs_ready ? inputs_ready : ctx->next_event();
     sc_done = ctx->next_event();
     if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
-    HIP_TRY(hipEventRecord(up, st));
+    if (!inputs_ready) HIP_TRY(hipEventRecord(up, st));
     if (nprf + nvk_build > 0)
       PM_LAUNCH(ctx, "acc_ladder",
                 (k_acc_powers<Cv><<<(unsigned)((4 * (nprf + nvk_build) + 255) / 256), 256, kAccLadderFence, st>>>(
@@ -323,13 +326,18 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // (profiles/r01_s4/accum_sum_lanes.jsonl).
   uint32_t lgL = 0;
   while (lgL < 5 && ((size_t)B * 4 << (lgL + 1)) <= kAccSumLanes) lgL++;
-  PM_LAUNCH(ctx, "acc_sum",
-            (k_acc_sum<Cv><<<(unsigned)((B * 4 * (1u << lgL) + 63) / 64), 64, 0, st>>>(h, dpart, lgL,
-                                                                                      (uint32_t*)d_out)));
   {
     hipEvent_t done = ctx->next_event();
     if (!done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
-    HIP_TRY(hipEventRecord(done, st));
+    const unsigned nblk = (unsigned)((B * 4 * (1u << lgL) + 63) / 64);
+    if (ctx->timing) {
+      PM_LAUNCH(ctx, "acc_sum", (k_acc_sum<Cv><<<nblk, 64, 0, st>>>(h, dpart, lgL, (uint32_t*)d_out)));
+      HIP_TRY(hipEventRecord(done, st));
+    } else {  // the completion event rides on the dispatch (no marker packet behind it)
+      hipExtLaunchKernelGGL(k_acc_sum<Cv>, dim3(nblk), dim3(64), 0, st, nullptr, done, 0, h, dpart, lgL,
+                            (uint32_t*)d_out);
+      HIP_TRY(hipGetLastError());
+    }
     if (int rc = wait_event(ctx, done)) return rc;
   }
   if (!built_key.empty()) {
@@ -472,17 +480,32 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   h.nblk_pts = (uint32_t)((B * npp + kDecodeThreads - 1) / kDecodeThreads);
   const size_t nblk_sc = (B * ((size_t)L.nsc + ninst) + kDecodeThreads - 1) / kDecodeThreads;
   if (stride > 0xffffffffull) return set_error(PM_ERR_UNSUPPORTED, "proof stride above 4 GiB");
-  PM_LAUNCH(ctx, "proof_decode",
-            (k_proof_decode<Cv><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
-                h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
-                (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
-                cscs, (uint32_t*)d_status)));
+  // untimed calls launch the decode with its completion event attached to the
+  // dispatch (hipExtLaunchKernel): the side stream waits on it, and the ladder
+  // follows the decode directly instead of behind an event-record marker
+  hipEvent_t dec_done = nullptr;
+  if (vk_repr && !ctx->timing) {
+    dec_done = ctx->next_event();
+    if (!dec_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+    hipExtLaunchKernelGGL(k_proof_decode<Cv>, dim3((unsigned)(h.nblk_pts + nblk_sc)), dim3(kDecodeThreads), 0, st,
+                          nullptr, dec_done, 0, h, (const SqrtTab*)ctx->sqrt_tab[slot].p,
+                          (const uint32_t*)ctx->pf_map.buf.p, (const uint32_t*)d_proofs, (const uint32_t*)d_inst,
+                          (uint32_t*)d_points, (uint32_t*)d_scalars, cpts, cscs, (uint32_t*)d_status);
+    HIP_TRY(hipGetLastError());
+  } else {
+    PM_LAUNCH(ctx, "proof_decode",
+              (k_proof_decode<Cv><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
+                  h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
+                  (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
+                  cscs, (uint32_t*)d_status)));
+  }
   if (!vk_repr) {
     HIP_TRY(hipStreamSynchronize(st));
     ctx->end_call();
     return PM_OK;
   }
-  return accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, true);
+  return accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, true,
+                               dec_done);
 }
 
 // the CurveOps entry (no extra parameters)
