@@ -46,11 +46,12 @@ int transcript_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const ui
                            const void* d_scalars, void* d_ch, void* d_status);
 // canon_ready: the canonical coordinates / scalars the replay hashes are
 // already in ctx->tr_canon (written by k_proof_decode), so k_tr_canon is
-// skipped; keep_status: OR the replay's bits into d_status (the decoder's)
+// skipped; dflags: the decoder's per-proof flags, OR-ed into d_status by the
+// replay, which clears them
 template <class Cv>
 int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
                       const void* d_scalars, void* d_ch, void* d_status, hipStream_t st, bool canon_ready = false,
-                      bool keep_status = false);
+                      uint32_t* dflags = nullptr);
 
 // Lanes per item for the latency-bound accumulator kernels: the largest
 // power of two 2^lg <= 2^maxlg that keeps items * 2^lg within about two
@@ -80,7 +81,7 @@ inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
 template <class Cv>
 int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d_points, const void* d_scalars,
                       void* d_ch, void* d_out, void* d_hout, const uint64_t* vk_repr, void* d_status,
-                      bool canon_ready = false, bool keep_status = false, hipEvent_t inputs_ready = nullptr) {
+                      bool canon_ready = false, uint32_t* dflags = nullptr, hipEvent_t inputs_ready = nullptr) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
@@ -293,7 +294,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     HIP_TRY(hipStreamWaitEvent(side, up, 0));
   }
   if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side,
-                                             canon_ready, keep_status)))
+                                             canon_ready, dflags)))
     return rc;
   // status: the replay stores bits 0-1 per proof, k_acc_scalars ORs in the
   // denominator bit; without a replay the words start at zero
@@ -354,7 +355,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
 template <class Cv>
 int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
                       const void* d_scalars, void* d_ch, void* d_status, hipStream_t st, bool canon_ready,
-                      bool keep_status) {
+                      uint32_t* dflags) {
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
   AccLayout L;
@@ -409,8 +410,7 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
       k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
           (uint32_t)B, L.npts, L.nsc, (const uint32_t*)d_points, (const uint32_t*)d_scalars, cpts, cscs);
     k_transcript<Cv><<<(unsigned)tblocks, 64, fence ? kAccScalarsLds : 0, st>>>(
-        hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status,
-        keep_status ? 1u : 0u);
+        hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status, dflags);
   });
   return PM_OK;
 }
@@ -468,7 +468,21 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   if ((rc = ctx->tr_canon.ensure(nall * 32))) return rc;
   uint32_t* cpts = (uint32_t*)ctx->tr_canon.p;
   uint32_t* cscs = cpts + 8 * ncoord;
-  HIP_TRY(hipMemsetAsync(d_status, 0, B * sizeof(uint32_t), st));
+  // decode flags: straight into the caller's status words (zeroed first) when
+  // only decoding; with the replay, into a per-context word per proof that
+  // k_transcript folds into the status and clears, so no memset precedes the
+  // decode (a failed call leaves them dirty: cleared on the next call)
+  uint32_t* dflags = (uint32_t*)d_status;
+  if (vk_repr) {
+    const size_t old_cap = ctx->pf_flags.cap;
+    if ((rc = ctx->pf_flags.ensure(B * sizeof(uint32_t)))) return rc;
+    if (ctx->pf_flags.cap != old_cap || ctx->pf_flags_dirty)
+      HIP_TRY(hipMemsetAsync(ctx->pf_flags.p, 0, ctx->pf_flags.cap, st));
+    ctx->pf_flags_dirty = true;
+    dflags = (uint32_t*)ctx->pf_flags.p;
+  } else {
+    HIP_TRY(hipMemsetAsync(d_status, 0, B * sizeof(uint32_t), st));
+  }
   ProofDecodeHdr h{};
   h.B = (uint32_t)B;
   h.npts = L.npts;
@@ -490,22 +504,24 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     hipExtLaunchKernelGGL(k_proof_decode<Cv>, dim3((unsigned)(h.nblk_pts + nblk_sc)), dim3(kDecodeThreads), 0, st,
                           nullptr, dec_done, 0, h, (const SqrtTab*)ctx->sqrt_tab[slot].p,
                           (const uint32_t*)ctx->pf_map.buf.p, (const uint32_t*)d_proofs, (const uint32_t*)d_inst,
-                          (uint32_t*)d_points, (uint32_t*)d_scalars, cpts, cscs, (uint32_t*)d_status);
+                          (uint32_t*)d_points, (uint32_t*)d_scalars, cpts, cscs, dflags);
     HIP_TRY(hipGetLastError());
   } else {
     PM_LAUNCH(ctx, "proof_decode",
               (k_proof_decode<Cv><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
                   h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
                   (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
-                  cscs, (uint32_t*)d_status)));
+                  cscs, dflags)));
   }
   if (!vk_repr) {
     HIP_TRY(hipStreamSynchronize(st));
     ctx->end_call();
     return PM_OK;
   }
-  return accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, true,
-                               dec_done);
+  rc = accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, dflags,
+                             dec_done);
+  if (rc == PM_OK) ctx->pf_flags_dirty = false;  // k_transcript has cleared every word
+  return rc;
 }
 
 // the CurveOps entry (no extra parameters)

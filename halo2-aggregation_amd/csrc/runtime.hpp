@@ -211,6 +211,8 @@ struct pm_ctx {
   bool sqrt_ready[3] = {false, false, false};
   pm::CachedUpload pf_map;
   pm::Buf pf_io;
+  pm::Buf pf_flags;            // proof-decode flags per proof (cleared by k_transcript)
+  bool pf_flags_dirty = false;  // a call failed between the decode and the replay
   // accumulator: powers-of-two tables of the verifying key's points (fixed,
   // sigma, g1), built once per (curve, VK) and reused by every later batch
   std::vector<uint64_t> acc_vkpow_key;
@@ -232,7 +234,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &small_tab, &small_dig, &small_part, &small_tk};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &pf_flags, &small_tab, &small_dig, &small_part, &small_tk};
   }
   ~pm_ctx();
   int begin_call();

@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
                                                    const uint32_t* __restrict__ points,
                                                    const uint32_t* __restrict__ scalars,
                                                    uint32_t* __restrict__ challenges, uint32_t* __restrict__ status,
-                                                   uint32_t keep_status) {
+                                                   uint32_t* __restrict__ dflags) {
   using Fs = typename Cv::Scalar;
   __shared__ TrBuf buf;
   const uint32_t slot = threadIdx.x >> 2, q = threadIdx.x & 3;
@@ -372,7 +372,15 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
 #pragma unroll
     for (int i = 0; i < 16; i++) cur[i] = nxt[i];
   }
-  if (status && q == 0) status[b] = keep_status ? (status[b] | st) : st;
+  // dflags: the proof decode's flags of this batch (proof-bytes entry), taken
+  // into the status word and cleared for the next batch
+  if (q == 0) {
+    if (dflags) {
+      st |= dflags[b];
+      dflags[b] = 0;
+    }
+    if (status) status[b] = st;
+  }
 }
 
 }  // namespace pm
