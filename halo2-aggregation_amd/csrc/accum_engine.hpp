@@ -229,6 +229,10 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   if ((rc = ctx->acc_prog.put(prog, st))) return rc;
   if ((rc = ctx->acc_const.put(cst, st, 32))) return rc;
   if ((rc = ctx->acc_vk.put(vk, st))) return rc;
+  // a shape / VK / constants change re-sends these behind the caller's
+  // inputs_ready point on st: the side stream must then wait for the copies
+  // too, not only for the decode (k_acc_scalars reads dprog and acc_const)
+  if (ctx->acc_prog.sent || ctx->acc_const.sent || ctx->acc_vk.sent) inputs_ready = nullptr;
   if ((rc = ctx->acc_coef.ensure((size_t)B * T * 32))) return rc;
   if ((rc = ctx->acc_part.ensure((size_t)B * T * sizeof(Xyzz<F>)))) return rc;
   const uint32_t* dprog = (const uint32_t*)ctx->acc_prog.buf.p;

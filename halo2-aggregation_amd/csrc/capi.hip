@@ -198,7 +198,9 @@ int pm_ctx::ensure_small_pin(size_t bytes) {
   if (small_pin) (void)hipHostFree(small_pin);
   small_pin = nullptr;
   small_pin_cap = 0;
-  HIP_TRY(hipHostMalloc(&small_pin, bytes, hipHostMallocMapped));
+  // coherent (fine-grained) whatever HIP_HOST_COHERENT says: the host spins on
+  // the completion flag and window sums the kernel writes here mid-launch
+  HIP_TRY(hipHostMalloc(&small_pin, bytes, hipHostMallocMapped | hipHostMallocCoherent));
   small_pin_cap = bytes;
   return PM_OK;
 }
@@ -361,7 +363,11 @@ int pm_ctx_create(int device, pm_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault));
   c->stream = c->own_stream;
   HIP_TRY(hipStreamCreateWithFlags(&c->red_stream, hipStreamNonBlocking));
-  pm::digest_key_init(c->dropin_key);
+  try {  // std::random_device may throw when no entropy source is available
+    pm::digest_key_init(c->dropin_key);
+  } catch (const std::exception& e) {
+    return set_error(PM_ERR_HIP, std::string("drop-in cache key: no entropy source: ") + e.what());
+  }
   if (const char* e = std::getenv("PM_NTT_PASSES")) c->ntt_passes = std::atoi(e);
   if (const char* e = std::getenv("PM_FINE_CACHE_KB")) c->fine_cache_kb = std::max(0, std::min(144, std::atoi(e)));
   if (const char* e = std::getenv("PM_FINE_CHUNK_KB")) c->fine_chunk_kb = std::max(0, std::min(144, std::atoi(e)));
@@ -835,9 +841,14 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
     rc = bases_upload_locked(ctx, curve, bases, true, n, &b);
     if (rc && !ctx->dropin.empty()) {  // out of device memory: release every set and retry once
       dropin_release_all(ctx);
+      ctx->dropin_oom_flushes++;
       rc = bases_upload_locked(ctx, curve, bases, true, n, &b);
     }
-    if (rc) return plain();  // the set stays unadmitted; the MSM itself still runs
+    if (rc) {  // the set stays unadmitted; the MSM itself still runs (and succeeds without a stale message)
+      ctx->dropin_failed_builds++;
+      pm::g_last_error.clear();
+      return plain();
+    }
     size_t bytes = 0;
     pm_bases_info(b, nullptr, nullptr, &bytes);
     ctx->dropin.push_back(pm::DropinEntry{curve, n, {d[0], d[1], d[2], d[3]}, b, bytes, ++ctx->dropin_clock, quick});
@@ -877,6 +888,14 @@ int pm_ctx_dropin_spec_stats(pm_ctx* ctx, uint64_t* kept, uint64_t* drained) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (kept) *kept = ctx->dropin_spec_hits;
   if (drained) *drained = ctx->dropin_spec_misses;
+  return PM_OK;
+}
+
+int pm_ctx_dropin_oom_stats(pm_ctx* ctx, uint64_t* flushes, uint64_t* failed_builds) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (flushes) *flushes = ctx->dropin_oom_flushes;
+  if (failed_builds) *failed_builds = ctx->dropin_failed_builds;
   return PM_OK;
 }
 

@@ -76,6 +76,7 @@ struct CachedUpload {
   Buf buf;
   std::vector<uint8_t> host;
   uint64_t gen_at_upload = ~0ull;
+  bool sent = false;  // the last put() queued a copy (false: the device copy was current)
   template <class T>
   int put(const std::vector<T>& v, hipStream_t st, size_t pad = 0);
 };
@@ -186,6 +187,7 @@ struct pm_ctx {
   uint64_t dropin_clock = 0;
   uint64_t dropin_hits = 0, dropin_misses = 0;
   uint64_t dropin_spec_hits = 0, dropin_spec_misses = 0;  // speculative starts kept / drained
+  uint64_t dropin_oom_flushes = 0, dropin_failed_builds = 0;  // out-of-memory: whole cache released / set not admitted
   hipEvent_t batch_ev[4] = {};       // batch pipelining: copied[2], consumed[2]
   std::vector<hipEvent_t> grp_ev;    // MSM: one per pinned term slot (terms copied)
   int window_c = 0;
@@ -316,10 +318,12 @@ template <class T>
 int CachedUpload::put(const std::vector<T>& v, hipStream_t st, size_t pad) {
   const size_t bytes = v.size() * sizeof(T);
   int rc;
+  sent = false;
   if ((rc = buf.ensure(bytes + pad))) return rc;
   if (buf.gen == gen_at_upload && host.size() == bytes && (bytes == 0 || memcmp(host.data(), v.data(), bytes) == 0))
     return PM_OK;
   if (bytes) HIP_TRY(hipMemcpyAsync(buf.p, v.data(), bytes, hipMemcpyHostToDevice, st));
+  sent = bytes != 0;
   host.assign((const uint8_t*)v.data(), (const uint8_t*)v.data() + bytes);
   gen_at_upload = buf.gen;
   return PM_OK;

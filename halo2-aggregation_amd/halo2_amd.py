@@ -231,6 +231,7 @@ def _load():
         "pm_ctx_dropin_stats": ([_vp, _u64p, _u64p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)],
                                 ctypes.c_int),
         "pm_ctx_dropin_spec_stats": ([_vp, _u64p, _u64p], ctypes.c_int),
+        "pm_ctx_dropin_oom_stats": ([_vp, _u64p, _u64p], ctypes.c_int),
         "pm_ctx_dropin_clear": ([_vp], ctypes.c_int),
         "pm_ctx_dropin_key_id": ([_vp, _u64p], ctypes.c_int),
         "pm_msm": ([ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
@@ -581,6 +582,13 @@ class Context:
         k, d = ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib().pm_ctx_dropin_spec_stats(self.h, ctypes.byref(k), ctypes.byref(d)))
         return k.value, d.value
+
+    def dropin_oom_stats(self):
+        """pm_ctx_dropin_oom_stats -> (flushes, failed_builds): out-of-memory
+        events of the drop-in cache."""
+        f, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().pm_ctx_dropin_oom_stats(self.h, ctypes.byref(f), ctypes.byref(b)))
+        return f.value, b.value
 
     def dropin_clear(self):
         _check(lib().pm_ctx_dropin_clear(self.h))

@@ -158,6 +158,10 @@ int pm_ctx_dropin_clear(pm_ctx* ctx);
 /* Speculative starts of pm_msm_ctx: kept (the digest confirmed the predicted
  * set) and drained (it named another set or none). */
 int pm_ctx_dropin_spec_stats(pm_ctx* ctx, uint64_t* kept, uint64_t* drained);
+/* Out-of-memory events of the drop-in cache: *flushes = builds that failed
+ * and released every cached set before their one retry, *failed_builds =
+ * sets left unadmitted (that call ran the plain pipeline and succeeded). */
+int pm_ctx_dropin_oom_stats(pm_ctx* ctx, uint64_t* flushes, uint64_t* failed_builds);
 /* A fingerprint of ctx's secret digest key (16 bytes of BLAKE2b of the key,
  * personal "pm-dropin-key-id"): distinct contexts hold distinct keys.  It
  * reveals nothing about the key itself. */

@@ -398,6 +398,7 @@ def test_dropin_base_cache(curve):
         assert np.array_equal(ctx.msm(curve, S[:n], Bm), wm)
         assert ctx.dropin_spec_stats() == (kept, 1)
         assert ctx.dropin_stats()["hits"] == 2
+        assert ctx.dropin_oom_stats() == (0, 0)   # no out-of-memory event at these sizes
         # small MSMs bypass the cache
         ctx.msm(curve, S[:100], B[:100])
         assert ctx.dropin_stats()["entries"] == 2

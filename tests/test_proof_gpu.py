@@ -205,3 +205,31 @@ def test_device_entries_and_stride(gpu_ctx):
     with pytest.raises(H.PmError):   # stride below the proof size
         gpu_ctx.decode_proofs_device(ps, 21, dpf.data_ptr(), psize - 4, din.data_ptr(), dp.data_ptr(),
                                      ds.data_ptr(), dst.data_ptr())
+
+
+def test_alternating_shapes_one_context():
+    """on one untimed context, batches from proof bytes that
+    alternate between two shapes and two VKs re-send the program / constants /
+    VK words behind the decode; each result must still equal the fused
+    transcript entry on the decoded inputs, computed on a second context (a
+    stale read would see the previous shape's program words)."""
+    ctx = H.Context(0)
+    cases = []
+    for i, (cid, shape) in enumerate([(2, "simple"), (2, "rich"), (0, "simple"), (2, "simple")]):
+        C, sh, proofs = U.make_case(cid, shape, 11 + i, 12, 0xA17 + 31 * i)
+        ps = U.to_product_shape(cid, sh)
+        ni = sh.num_instance_columns
+        vk = np.array(A.to_limbs_mont(C.r, T.vk_repr(C.r, b"alt-%d" % i)), dtype=np.uint64)
+        datas = [PB.serialize(C, sh, pf) for pf in proofs]
+        inst = np.array([[P.point_to_limbs(C, q) for q in pf.points[:ni]] for pf in proofs], dtype=np.uint64)
+        pts, scs, _ = A.pack_proofs(C, sh, proofs)
+        cases.append((ps, datas, inst, vk, pts, scs))
+    want = []
+    ref = H.Context(0)
+    for ps, datas, inst, vk, pts, scs in cases:
+        want.append(ref.accum_batch_transcript(ps, pts, scs, vk))
+    for rep in range(3):
+        for (ps, datas, inst, vk, _, _), w in zip(cases, want):
+            q, h, ch, st = ctx.accum_batch_proofs(ps, datas, inst, vk)
+            assert not st.any()
+            assert np.array_equal(q, w[0]) and np.array_equal(h, w[1]) and np.array_equal(ch, w[2]), rep
