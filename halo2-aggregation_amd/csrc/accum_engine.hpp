@@ -549,6 +549,7 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
 }  // namespace pm
 
 #include "ntt_engine.hpp"  // uses fe_from_u64 above
+#include "msm_many.hpp"
 
 // Explicit instantiations are visible to both compilation passes, so the
 // device pass instantiates every kernel the host driver launches; the op
@@ -564,7 +565,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
                          &transcript_device_impl<Cv>, &vk_repr_impl<Cv>,                   \
                          &fixed_table_impl<Cv>, &ntt_device_impl<Cv>, &msm_fixed_to_aff<Cv>,    \
                          &bases_to29_impl<Cv>, &msm_resident_batch_impl<Cv>, &proofs_device_impl<Cv>,    \
-                         &msm_start_impl<Cv>, &msm_finish_impl<Cv>, &msm_small_impl<Cv>};
+                         &msm_start_impl<Cv>, &msm_finish_impl<Cv>, &msm_small_impl<Cv>,         \
+                         &many_table_impl<Cv>, &msm_many_impl<Cv>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \
@@ -588,5 +590,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
   template int msm_start_impl<Cv>(Ctx*, const pm_fixed_bases*, const void*, const void*, size_t, uint32_t, void*); \
   template int msm_finish_impl<Cv>(Ctx*, const void*, uint64_t*);                                \
   template int msm_small_impl<Cv>(Ctx*, const void*, bool, const void*, bool, bool, size_t, uint32_t, uint64_t*); \
+  template int many_table_impl<Cv>(Ctx*, const void*, size_t, ManyTable*);                       \
+  template int msm_many_impl<Cv>(Ctx*, const ManyTable*, size_t, const size_t*, const size_t*, const void*, bool, \
+                                 uint32_t, uint64_t*);                                           \
   PM_OPS_TABLE(Cv, name)                                                                       \
   }

@@ -188,7 +188,9 @@ int pm_ctx::ensure_pinned(size_t bytes) {
   if (h_pinned) (void)hipHostFree(h_pinned);
   h_pinned = nullptr;
   h_pinned_cap = 0;
-  HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocMapped));
+  // coherent: the small-MSM path's window sums and completion flag live here
+  // and are read by the host while the kernel still runs
+  HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocMapped | hipHostMallocCoherent));
   h_pinned_cap = bytes;
   return PM_OK;
 }
@@ -547,6 +549,9 @@ struct pm_bases {
   size_t n;
   void* d;                 // row 0 (64 B per point)
   pm_fixed_bases* table;   // rows > 1: the same memory as a row table, or nullptr
+  // multiples table of pm_msm_resident_many* (msm_many.hpp), built on demand
+  mutable pm::ManyTable many;
+  mutable std::mutex many_mu;
 };
 
 namespace {
@@ -631,6 +636,7 @@ int pm_bases_release(pm_bases* b) {
   if (!b) return PM_OK;
   (void)hipSetDevice(b->device);
   (void)hipFree(b->d);  // the row table's memory when there is one
+  if (b->many.d) (void)hipFree(b->many.d);
   delete b->table;
   delete b;
   return PM_OK;
@@ -660,6 +666,97 @@ static int msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const voi
   if (resident_use_table(b, offset, n))
     return curve_ops(b->curve)->msm_fixed(ctx, b->table, d_s, n, flags & ~kBasesR261, out, h_s);
   return dispatch_msm_device(ctx, b->curve, d_s, (const char*)b->d + offset * 64, n, flags, out, true, h_s);
+}
+
+// ------------------------------------- many short MSMs (pm_msm_resident_many)
+namespace {
+// the multiples table covers the first n bases (grown to a power of two,
+// at least 64, at most the set); the caller holds ctx->mu and b->many_mu
+int many_ensure(pm_ctx* ctx, const pm_bases* b, size_t need) {
+  if (b->many.d && b->many.n >= need) return PM_OK;
+  size_t n = 64;
+  while (n < need) n <<= 1;
+  n = std::max(need, std::min({n, b->n, pm::kManyTabCap / pm::many_bytes_per_base(4)}));
+  return curve_ops(b->curve)->many_table(ctx, b->d, n, &b->many);
+}
+}  // namespace
+
+static int msm_many(pm_ctx* ctx, const pm_bases* b, size_t B, const size_t* n, const size_t* offsets,
+                    const void* scalars, bool host, uint32_t flags, uint64_t* out) {
+  if (!ctx || !b || (B && (!n || !out))) return set_error(PM_ERR_ARG, "null argument");
+  if (b->device != ctx->device) return set_error(PM_ERR_ARG, "bases live on another device");
+  if (B > (size_t(1) << 20)) return set_error(PM_ERR_UNSUPPORTED, "more than 2^20 MSMs in one call");
+  size_t need = 0, total = 0;
+  for (size_t i = 0; i < B; i++) {
+    const size_t o = offsets ? offsets[i] : 0;
+    if (o > b->n || n[i] > b->n - o) return set_error(PM_ERR_ARG, "an MSM window exceeds the resident bases");
+    if (n[i]) need = std::max(need, o + n[i]);
+    total += n[i];
+  }
+  if (total && !scalars) return set_error(PM_ERR_ARG, "null scalars");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  if (need * pm::many_bytes_per_base(4) > pm::kManyTabCap) {
+    // a prefix too long for a table: one resident MSM per entry (same results)
+    size_t s0 = 0;
+    for (size_t i = 0; i < B; i++) {
+      const void* si = (const char*)scalars + s0 * 32;
+      const size_t o = offsets ? offsets[i] : 0;
+      if (n[i] == 0) std::memset(out + 8 * i, 0, 64);
+      else if (use_small(ctx, n[i]))
+        rc = curve_ops(b->curve)->msm_small(ctx, si, host, (const char*)b->d + o * 64, false, true, n[i],
+                                            flags & ~kBasesR261, out + 8 * i);
+      else {
+        const void* d_s = si;
+        if (host) {
+          if ((rc = ctx->in_scalars.ensure(n[i] * 32))) return rc;
+          d_s = ctx->in_scalars.p;
+        }
+        rc = dispatch_msm_device(ctx, b->curve, d_s, (const char*)b->d + o * 64, n[i], flags, out + 8 * i, true,
+                                 host ? si : nullptr);
+      }
+      if (rc) return rc;
+      if ((rc = ctx->begin_call())) return rc;
+      s0 += n[i];
+    }
+    return PM_OK;
+  }
+  std::lock_guard<std::mutex> lt(b->many_mu);
+  if (need && (rc = many_ensure(ctx, b, need))) return rc;
+  return curve_ops(b->curve)->msm_many(ctx, &b->many, B, n, offsets, scalars, host, flags, out);
+}
+
+int pm_msm_resident_many(pm_ctx* ctx, const pm_bases* bases, size_t B, const size_t* n, const size_t* offsets,
+                         const uint64_t* scalars, uint32_t flags, uint64_t* out) {
+  return msm_many(ctx, bases, B, n, offsets, scalars, true, flags, out);
+}
+
+int pm_msm_resident_many_device(pm_ctx* ctx, const pm_bases* bases, size_t B, const size_t* n, const size_t* offsets,
+                                const void* d_scalars, uint32_t flags, uint64_t* out) {
+  return msm_many(ctx, bases, B, n, offsets, d_scalars, false, flags, out);
+}
+
+int pm_bases_many_prepare(pm_ctx* ctx, const pm_bases* bases, size_t max_n) {
+  if (!ctx || !bases) return set_error(PM_ERR_ARG, "null argument");
+  if (bases->device != ctx->device) return set_error(PM_ERR_ARG, "bases live on another device");
+  if (max_n > bases->n) return set_error(PM_ERR_ARG, "prefix exceeds the resident bases");
+  if (max_n * pm::many_bytes_per_base(4) > pm::kManyTabCap)
+    return set_error(PM_ERR_UNSUPPORTED, "prefix too long for a multiples table");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = ctx->begin_call();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lt(bases->many_mu);
+  return max_n ? many_ensure(ctx, bases, max_n) : PM_OK;
+}
+
+int pm_bases_many_info(const pm_bases* bases, size_t* n, int* window, size_t* device_bytes) {
+  if (!bases) return set_error(PM_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lt(bases->many_mu);
+  if (n) *n = bases->many.d ? bases->many.n : 0;
+  if (window) *window = bases->many.d ? (int)bases->many.c : 0;
+  if (device_bytes) *device_bytes = bases->many.d ? bases->many.n * pm::many_bytes_per_base(bases->many.c) : 0;
+  return PM_OK;
 }
 
 // ------------------------------------------------ drop-in base cache (pm_msm)

@@ -163,6 +163,29 @@ struct pm_fixed_bases {
 };
 
 namespace pm {
+// multiples table of a resident base set (msm_many.hpp): entry (i, w, m) =
+// [m 2^{c w}] P_i, m = 1 .. H = 2^(c-1), w < W, XYZZ R = 2^261 (128 B), for
+// the first n bases; built on demand by pm_msm_resident_many* /
+// pm_bases_many_prepare and owned by the pm_bases
+struct ManyTable {
+  void* d = nullptr;
+  size_t n = 0;
+  uint32_t c = 0, W = 0, H = 0;
+};
+// geometry for a prefix of n bases: the widest window (fewest additions per
+// scalar, W(c) of them) whose table fits kManyTabBudget; c = 4 up to the hard
+// cap, beyond it pm_msm_resident_many falls back to one resident MSM each.
+// W(c): signed digits in [-(2^(c-1) - 1), 2^(c-1)] of a scalar < 2^255 need a
+// carry window only when c divides 255.
+constexpr size_t kManyTabBudget = size_t(2) << 30;
+constexpr size_t kManyTabCap = size_t(8) << 30;
+inline uint32_t many_windows(uint32_t c) { return 255u % c == 0 ? 255u / c + 1u : (255u + c - 1u) / c; }
+inline size_t many_bytes_per_base(uint32_t c) { return (size_t)many_windows(c) << (c - 1) << 7; }
+inline uint32_t many_pick_c(size_t n) {
+  for (uint32_t c = 8; c > 4; c--)
+    if (n * many_bytes_per_base(c) <= kManyTabBudget) return c;
+  return 4;
+}
 constexpr size_t kNttTwiddleSlots = 4;
 constexpr uint32_t kNttMaxLog = 28;  // pm_fft: three passes above 2^22; BN254 Fr has 2-adicity 28
 struct NttTwiddles {
@@ -207,6 +230,7 @@ struct pm_ctx {
       win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, tr_canon, ntt_scratch2,
       acc_vkpow, small_tab, small_dig, small_part, small_tk;
   pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
+  pm::CachedUpload many_prog;  // pm_msm_resident_many*: job + MSM tables
   // proof-byte decoder (proof_kernels.hpp): square-root tables per curve
   // (pm_curve order), the point map of the current shape, host staging
   pm::Buf sqrt_tab[3];
@@ -236,7 +260,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &pf_flags, &small_tab, &small_dig, &small_part, &small_tk};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &pf_flags, &small_tab, &small_dig, &small_part, &small_tk, &many_prog.buf};
   }
   ~pm_ctx();
   int begin_call();
@@ -301,6 +325,11 @@ struct CurveOps {
   // memory; b_r261: bases in the resident R = 2^261 form
   int (*msm_small)(Ctx* ctx, const void* scalars, bool s_host, const void* bases, bool b_host, bool b_r261, size_t n,
                    uint32_t flags, uint64_t out[8]);
+  // many short MSMs against resident bases (msm_many.hpp): build / grow the
+  // multiples table of the first n bases, and the batched sum
+  int (*many_table)(Ctx* ctx, const void* d_bases29, size_t n, ManyTable* t);
+  int (*msm_many)(Ctx* ctx, const ManyTable* t, size_t B, const size_t* n, const size_t* off, const void* scalars,
+                  bool s_host, uint32_t flags, uint64_t* out);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

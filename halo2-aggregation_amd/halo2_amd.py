@@ -42,6 +42,7 @@ PROOF_BAD_SCALAR = 16
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _vp = ctypes.c_void_p
+_szp = ctypes.POINTER(ctypes.c_size_t)
 
 
 class PmError(RuntimeError):
@@ -251,6 +252,12 @@ def _load():
                                    ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
         "pm_msm_resident": ([_vp, _vp, ctypes.c_size_t, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p],
                             ctypes.c_int),
+        "pm_msm_resident_many": ([_vp, _vp, ctypes.c_size_t, _szp, _szp, _u64p, ctypes.c_uint32, _u64p],
+                                 ctypes.c_int),
+        "pm_msm_resident_many_device": ([_vp, _vp, ctypes.c_size_t, _szp, _szp, _vp, ctypes.c_uint32, _u64p],
+                                        ctypes.c_int),
+        "pm_bases_many_prepare": ([_vp, _vp, ctypes.c_size_t], ctypes.c_int),
+        "pm_bases_many_info": ([_vp, _szp, ctypes.POINTER(ctypes.c_int), _szp], ctypes.c_int),
         "pm_point_add": ([ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
         "pm_selftest_field": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_selftest_host": ([ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, _u64p], ctypes.c_int),
@@ -441,6 +448,13 @@ class Bases:
         nn, rr, bb = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_size_t()
         _check(lib().pm_bases_info(h, ctypes.byref(nn), ctypes.byref(rr), ctypes.byref(bb)))
         self.rows, self.device_bytes = rr.value, bb.value  # rows of [2^{256 j / rows}] P kept at upload
+
+    def many_info(self):
+        """pm_bases_many_info -> (prefix n, window c, device bytes) of the
+        multiples table (zeros before the first pm_msm_resident_many)."""
+        nn, cc, bb = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_size_t()
+        _check(lib().pm_bases_many_info(self.h, ctypes.byref(nn), ctypes.byref(cc), ctypes.byref(bb)))
+        return nn.value, cc.value, bb.value
 
     def release(self):
         if self.h:
@@ -636,6 +650,37 @@ class Context:
         _check(lib().pm_msm_resident_batch(self.h, bases.h, offset, ptrs, len(arrs), n,
                                            SCALARS_CANONICAL if canonical else 0, _p(out)))
         return out
+
+    def _many_args(self, n, offsets):
+        nn = np.ascontiguousarray(np.asarray(n, dtype=np.uint64).reshape(-1))
+        oo = None if offsets is None else np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64).reshape(-1))
+        if oo is not None and oo.shape != nn.shape:
+            raise ValueError("offsets and n differ in length")
+        szp = lambda a: None if a is None else a.ctypes.data_as(_szp)  # noqa: E731
+        return nn, oo, szp(nn), szp(oo)
+
+    def msm_resident_many(self, bases: Bases, n, scalars, offsets=None, canonical=False):
+        """pm_msm_resident_many: B = len(n) short MSMs against resident bases,
+        MSM i over the next n[i] rows of `scalars` (sum(n) x 4 u64) and bases
+        [offsets[i], offsets[i] + n[i]) (offsets None: 0); returns (B, 8) u64."""
+        nn, oo, pn, po = self._many_args(n, offsets)
+        s = _as_u64(scalars, 4) if int(nn.sum()) else np.zeros((1, 4), dtype=np.uint64)
+        if int(nn.sum()) and s.shape[0] != int(nn.sum()):
+            raise ValueError("scalars must hold sum(n) rows")
+        out = np.zeros((nn.shape[0], 8), dtype=np.uint64)
+        _check(lib().pm_msm_resident_many(self.h, bases.h, nn.shape[0], pn, po, _p(s),
+                                          SCALARS_CANONICAL if canonical else 0, _p(out)))
+        return out
+
+    def msm_resident_many_device(self, bases: Bases, n, d_scalars, offsets=None, canonical=False):
+        nn, oo, pn, po = self._many_args(n, offsets)
+        out = np.zeros((nn.shape[0], 8), dtype=np.uint64)
+        _check(lib().pm_msm_resident_many_device(self.h, bases.h, nn.shape[0], pn, po, _vp(d_scalars),
+                                                 SCALARS_CANONICAL if canonical else 0, _p(out)))
+        return out
+
+    def bases_many_prepare(self, bases: Bases, max_n):
+        _check(lib().pm_bases_many_prepare(self.h, bases.h, max_n))
 
     def set_h2d_threads(self, threads):
         """Retired pinned staging: only threads=0 is accepted."""

@@ -206,6 +206,29 @@ int pm_msm_resident_device(pm_ctx* ctx, const pm_bases* b, size_t offset, const 
  * tail overlaps them too.  Same results as k pm_msm_resident calls. */
 int pm_msm_resident_batch(pm_ctx* ctx, const pm_bases* b, size_t offset, const uint64_t* const* scalars,
                           size_t k, size_t n, uint32_t flags, uint64_t* out);
+/* B independent short MSMs against one resident base set in one launch --
+ * the aggregator's per-proof instance commitments
+ * params_verifier.commit_lagrange(public_inputs)
+ * (examples/simple-example.rs:632-641; verifier.rs:200-225, 312-316 take them
+ * as the instance column's commitment), i.e. B calls of
+ * best_multiexp(public_inputs_i, g_lagrange[0..n_i]):
+ *   out[i] = sum_{t < n[i]} s_i[t] P[offsets[i] + t]   (8 u64 affine each)
+ * with s_i the next n[i] scalars of `scalars` (concatenated, n x 4 u64 in
+ * the pm_msm scalar form and flags).  offsets == NULL: every MSM starts at
+ * base 0 (commit_lagrange).  n[i] == 0 gives the identity (0, 0).
+ * The first call that reaches a base beyond the set's multiples table builds
+ * it (entry (i, w, m) = [m 2^{c w}] P_i: 2^(c-1) x W(c) x 128 B per base, c = 8
+ * for up to 4096 bases, narrower windows for longer prefixes, at most 8 GiB);
+ * prefixes beyond that cap run one resident MSM per entry (same results).
+ * pm_bases_many_prepare builds the table for [0, max_n) ahead of time;
+ * pm_bases_many_info reports its prefix, window and bytes (0 when none).
+ * Same results as B pm_msm_resident calls. */
+int pm_msm_resident_many(pm_ctx* ctx, const pm_bases* b, size_t B, const size_t* n, const size_t* offsets,
+                         const uint64_t* scalars, uint32_t flags, uint64_t* out);
+int pm_msm_resident_many_device(pm_ctx* ctx, const pm_bases* b, size_t B, const size_t* n, const size_t* offsets,
+                                const void* d_scalars, uint32_t flags, uint64_t* out);
+int pm_bases_many_prepare(pm_ctx* ctx, const pm_bases* b, size_t max_n);
+int pm_bases_many_info(const pm_bases* b, size_t* n, int* window, size_t* device_bytes);
 /* Retired: host inputs are copied with one pageable hipMemcpyAsync, which
  * measured faster on MI355X than pinned staging threads (~52 vs ~38 GB/s for
  * 32 MB).  threads == 0 succeeds, threads > 0 returns PM_ERR_UNSUPPORTED. */
