@@ -68,6 +68,11 @@ def parse():
     ap.add_argument("--strong-logn", type=int, default=22,
                     help="strong-scaling leg: a fixed 2^k Vesta MSM split over the ranks (SURVEY config 4); 0 = skip")
     ap.add_argument("--small-n", type=int, default=1, help="drop-in latency curve n = 2^0..2^16 vs the C port (1/0)")
+    ap.add_argument("--inst-batch", type=int, default=256,
+                    help="instance-commitment leg: proofs per GPU (pm_msm_resident_many, 0 = skip)")
+    ap.add_argument("--inst-npub", type=int, default=1, help="public inputs per proof (simple-example: 1)")
+    ap.add_argument("--accum-b32", type=int, default=1,
+                    help="config 5's per-rank share: 32 proofs at k = 17 per GPU (1/0)")
     ap.add_argument("--accum-b16", type=int, default=1,
                     help="also time BASELINE config 3: 16 simple-example proofs at k = 14 per GPU (1) or skip (0)")
     ap.add_argument("--dry-run", action="store_true",
@@ -299,6 +304,10 @@ def main():
     accum = run_accumulator(args, ctx, dist, dev, rank, world) if args.accum_batch > 0 else None
     # BASELINE config 3: 16 simple-example proofs at k = 14 per GPU
     accum16 = run_accumulator(args, ctx, dist, dev, rank, world, B=16, logn=14) if args.accum_b16 else None
+    # BASELINE config 5 on 8 GPUs: 256 proofs = 32 per rank (the per-rank slice)
+    accum32 = run_accumulator(args, ctx, dist, dev, rank, world, B=32, logn=17, light=True) \
+        if args.accum_b32 else None
+    inst = run_instance_commitments(args, ctx, dist, dev, rank, world) if args.inst_batch > 0 else None
 
     if rank == 0:
         out = {
@@ -343,6 +352,11 @@ def main():
             else:
                 accum16.pop("_state", None)
             out["accumulator_b16_k14"] = accum16
+        if accum32 is not None:
+            accum32.pop("_state", None)
+            out["accumulator_b32_k17"] = accum32
+        if inst is not None:
+            out["instance_commitments"] = inst
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -846,7 +860,7 @@ def ntt_cpu_baseline(curve, k, src, w, first, budget_s):
             "matches_gpu": match}
 
 
-def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
+def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None, light=False):
     """Batch multiopen accumulator: B proofs per rank, timed like the MSM leg.
     One step starts from the proofs' BYTES, resident in HBM as halo2's
     Blake2bWrite serialized them: device decode (read_point decompression /
@@ -924,15 +938,104 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None):
            "from_decoded": {"ms_per_batch": round(ms_dec, 4), "value": round(world * B / (ms_dec * 1e-3), 1),
                             "entry": "pm_accum_batch_transcript_device (decoded points / scalars in HBM)",
                             "quads_match_bytes_path": bool(torch.equal(quads_dec, batch.quads))}}
-    if world == 1:
+    if world == 1 and not light:
         out["two_in_flight"] = accum_two_in_flight(args, ctx, shape, batch, B)
-    if rank == 0:
+    if rank == 0 and not light:
         host = {k: getattr(batch, k).cpu().numpy().view(np.uint64)
                 for k in ("points", "scalars", "challenges", "quads", "h_eval")}
         host["vk_repr"] = np.asarray(batch.vk_repr, dtype=np.uint64)
         host["proofs"] = batch.proofs.cpu().numpy()
         host["inst"] = batch.inst.cpu().numpy().view(np.uint64)
         out["_state"] = (curve, shape, host, B)
+    return out
+
+
+def run_instance_commitments(args, ctx, dist, dev, rank, world, logn=17):
+    """Per-proof instance commitments (examples/simple-example.rs:632-641:
+    params_verifier.commit_lagrange(public_inputs), the instance column the
+    verifier reads, src/verifier.rs:200-225, 312-316) for B proofs per rank
+    with `--inst-npub` public inputs each, against a resident g_lagrange of
+    2^logn synthetic bases (BN254, the reference's curve): ONE
+    pm_msm_resident_many_device call per step.  Beside it: the same B MSMs
+    as B pm_msm_resident_device calls (the per-proof loop it replaces, timed
+    once, bit-exact check), and `with_accumulator`: the instance commitments
+    then the accumulator batch from proof bytes fed with them (aggregated
+    proofs verified/s counting the commitments)."""
+    import numpy as np
+    import torch
+
+    import halo2_amd as H
+    import workloads as Wk
+
+    curve, B, npub = H.BN254, args.inst_batch, args.inst_npub
+    nb = 1 << logn
+    d_b = torch.empty((nb, 8), dtype=torch.int64, device=dev)
+    ctx.synth_bases(curve, SEED_BASES ^ 0x1A6, 0, nb, d_b.data_ptr())
+    d_s = torch.empty((B * npub, 4), dtype=torch.int64, device=dev)
+    ctx.synth_scalars(curve, SEED_SCALARS ^ 0x1A6, rank * B * npub, B * npub, d_s.data_ptr())
+    torch.cuda.synchronize()
+    bases = ctx.upload_bases(curve, d_bases=d_b.data_ptr(), n=nb)
+    n = [npub] * B
+    t0 = time.perf_counter()
+    res = ctx.msm_resident_many_device(bases, n, d_s.data_ptr())
+    build_ms = (time.perf_counter() - t0) * 1e3
+    pre, c, tbytes = bases.many_info()
+
+    def step():
+        ctx.msm_resident_many_device(bases, n, d_s.data_ptr())
+
+    ms = timed_steps(step, args.steps, args.warmup, dist, dev)[0] * 1e3 / args.steps
+    # the loop it replaces: one resident MSM per proof
+    loop = []
+    t0 = time.perf_counter()
+    for i in range(B):
+        loop.append(ctx.msm_resident_device(bases, 0, d_s.data_ptr() + 32 * npub * i, npub))
+    ms_loop = (time.perf_counter() - t0) * 1e3
+    match_loop = bool(np.array_equal(np.array(loop), res))
+    out = {"value": round(world * B / (ms * 1e-3), 1), "unit": "instance commitments/s", "ms_per_batch": round(ms, 4),
+           "higher_is_better": True, "scaling": "weak",
+           "config": {"workload": f"commit_lagrange_b{B}_npub{npub}", "curve": "bn254", "proofs_per_gpu": B,
+                      "public_inputs_per_proof": npub, "g_lagrange": nb, "entry": "pm_msm_resident_many_device",
+                      "table": {"prefix": pre, "window_bits": c, "device_bytes": tbytes,
+                                "first_call_ms_with_build": round(build_ms, 3)}},
+           "per_proof_loop": {"ms_per_batch": round(ms_loop, 4), "entry": "B x pm_msm_resident_device",
+                              "matches": match_loop},
+           "speedup_vs_loop": round(ms_loop / ms, 1)}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import msm_ref
+
+        hb = d_b[:npub].cpu().numpy().view(np.uint64)
+        hs = d_s.cpu().numpy().view(np.uint64)
+        threads = cpu_threads()
+        t0 = time.perf_counter()
+        ok, k = True, 0
+        while k < B and time.perf_counter() - t0 < 3.0:
+            ok &= bool(np.array_equal(msm_ref.best_multiexp(curve, hs[k * npub:(k + 1) * npub], hb, threads=1),
+                                      res[k]))
+            k += 1
+        el = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(k / el, 1), "unit": "instance commitments/s", "cores": 1,
+                               "kind": "port", "sample": f"{k} of the {B} MSMs, oracle/msm_ref.c best_multiexp, "
+                                                         "one thread each (independent MSMs: x cores for a pool)",
+                               "matches": ok}
+    # the batch accumulator fed with these commitments (proof bytes in HBM)
+    shape = Wk.simple_example_shape(ctx, curve, logn)
+    batch = Wk.SyntheticBatch(ctx, shape, B, i0=rank * B, seed=0x1A7)
+    batch.to_proof_bytes(shape)
+
+    def step_acc():
+        q = ctx.msm_resident_many_device(bases, n, d_s.data_ptr())
+        batch.inst.copy_(torch.from_numpy(q.view(np.int64)).reshape(B, 1, 8), non_blocking=False)
+        batch.run_bytes(ctx, shape)
+
+    ms_acc = timed_steps(step_acc, args.steps, args.warmup, dist, dev)[0] * 1e3 / args.steps
+    out["with_accumulator"] = {"value": round(world * B / (ms_acc * 1e-3), 1), "unit": "proofs/s",
+                               "ms_per_batch": round(ms_acc, 4),
+                               "how": "pm_msm_resident_many_device -> H2D of the B commitments -> "
+                                      "pm_accum_batch_proofs_device from proof bytes",
+                               "status_nonzero": int((batch.status != 0).sum().item())}
+    bases.release()
     return out
 
 
