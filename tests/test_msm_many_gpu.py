@@ -97,8 +97,9 @@ def test_device_entry_and_table_growth():
 
     ctx = H.Context(0)
     curve = 2
-    S, B = _inputs(curve, 2048, 0x99)
-    bases = ctx.upload_bases(curve, B[:2048])
+    S, B = _inputs(curve, 4096, 0x99)
+    B = B[:2048]
+    bases = ctx.upload_bases(curve, B)
     assert bases.many_info() == (0, 0, 0)
     n = [1] * 64
     got = ctx.msm_resident_many(bases, n, S[:64])

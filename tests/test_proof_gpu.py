@@ -233,3 +233,32 @@ def test_alternating_shapes_one_context():
             q, h, ch, st = ctx.accum_batch_proofs(ps, datas, inst, vk)
             assert not st.any()
             assert np.array_equal(q, w[0]) and np.array_equal(h, w[1]) and np.array_equal(ch, w[2]), rep
+
+
+def test_bn254_hand_derived_edges(gpu_ctx):
+    """The hand-derived BN254 G1 encodings of tests/test_proof_bytes_oracle.py
+    (generator, its negation, x = 0 with and without the sign bit, x = p - 1
+    with both parities, a non-residue x, x = p) through the device decoder:
+    each in the first point slot of its own proof."""
+    from test_proof_bytes_oracle import BN254_EDGE, bn254_edge_bytes
+
+    cid = 2
+    C, sh, proofs = U.make_case(cid, "simple", 10, len(BN254_EDGE), 0xED6E)
+    ps = U.to_product_shape(cid, sh)
+    items = PB.proof_items(sh)
+    j = next(k for k, (kind, _) in enumerate(items) if kind == "pt")
+    slot = items[j][1]
+    ni = sh.num_instance_columns
+    datas = []
+    for pf, ((x, sign), _) in zip(proofs, BN254_EDGE):
+        d = bytearray(PB.serialize(C, sh, pf))
+        d[32 * j:32 * j + 32] = bn254_edge_bytes(x, sign)
+        datas.append(bytes(d))
+    inst = np.array([[P.point_to_limbs(C, q) for q in pf.points[:ni]] for pf in proofs], dtype=np.uint64)
+    pts, _, st = gpu_ctx.decode_proofs(ps, datas, inst)
+    for b, (_, want) in enumerate(BN254_EDGE):
+        if want is None:
+            assert st[b] & H.PROOF_BAD_POINT, b
+        else:
+            assert st[b] == 0, b
+            assert P.limbs_to_point(C, [int(v) for v in pts[b, slot]]) == want, b
