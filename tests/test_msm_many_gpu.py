@@ -126,7 +126,7 @@ def test_pipeline_order_independent(gpu_ctx):
     """The same MSMs in another order (and split over two calls) give the
     same points: no state leaks between MSMs or calls."""
     curve = 1
-    S, B = _inputs(curve, 600, 0x1234)
+    S, B = _inputs(curve, 1000, 0x1234)
     bases = gpu_ctx.upload_bases(curve, B[:256])
     n = [1, 5, 17, 64, 1, 2, 100, 3] * 4
     offs = [(7 * i) % 100 for i in range(len(n))]

@@ -1,0 +1,97 @@
+// microbench_slice.hip -- single-wave latency of the row-sliced Montgomery
+// product (slice29.hpp) against the one-lane product (fp29.hpp f29_mul_c),
+// and their agreement: one wave per block, each of its four rows (sliced) or
+// lanes (one-lane) iterating x <- x y; the final x of every chain is compared
+// (canonical) between the two forms on the host.
+// Output: one JSON line per field: us per product for each form, mismatches.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o tools/microbench_slice tools/microbench_slice.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "../halo2-aggregation_amd/csrc/slice29.hpp"
+using namespace pm;
+
+template <class F>
+__device__ void seed(uint32_t t, F29<F>& x, F29<F>& y) {
+  for (int i = 0; i < 9; i++) {
+    x.l[i] = (t * 7919u + i * 977u + 12345u) & kM29;
+    y.l[i] = (t * 104729u + i * 131u + 777u) & kM29;
+  }
+  x.l[8] &= 0xfffff;
+  y.l[8] &= 0xfffff;
+}
+
+// chain id = blockIdx.x * 4 + row
+template <class F>
+__global__ void __launch_bounds__(64) k_slice(uint32_t* out, uint64_t* clk, int iters) {
+  const uint32_t row = threadIdx.x >> 4, id = blockIdx.x * 4 + row;
+  F29<F> x0, y0;
+  seed<F>(id, x0, y0);
+  const SConst<F> k = SConst<F>::make();
+  S29<F> x = s29_from<F>(x0), y = s29_from<F>(y0);
+  const uint64_t t0 = wall_clock64();
+  for (int i = 0; i < iters; i++) x = s29_mul<F>(x, y, k);
+  const F29<F> r = f29_canon<F>(f29_reduce3<F>(s29_to<F>(s29_norm_exact<F>(x))));
+  const uint64_t t1 = wall_clock64() + (r.l[0] & 0u);
+  if (s_lane() == 0)
+    for (int i = 0; i < 9; i++) out[id * 9 + i] = r.l[i];
+  if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
+}
+
+template <class F>
+__global__ void __launch_bounds__(64) k_lane(uint32_t* out, uint64_t* clk, int iters) {
+  const uint32_t id = blockIdx.x * 64 + threadIdx.x;
+  F29<F> x, y;
+  seed<F>(id, x, y);
+  const uint64_t t0 = wall_clock64();
+  for (int i = 0; i < iters; i++) x = f29_mul_c<F>(x, y);
+  const F29<F> r = f29_canon<F>(f29_reduce3<F>(x));
+  const uint64_t t1 = wall_clock64() + (r.l[0] & 0u);
+  for (int i = 0; i < 9; i++) out[id * 9 + i] = r.l[i];
+  if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
+}
+
+template <class F>
+void run(const char* name) {
+  const int iters = 2000, blocks = 64;  // 256 sliced chains, 4096 one-lane chains
+  uint32_t *d_s, *d_l;
+  uint64_t *c_s, *c_l;
+  hipMalloc(&d_s, blocks * 4 * 9 * 4);
+  hipMalloc(&d_l, blocks * 64 * 9 * 4);
+  hipMalloc(&c_s, blocks * 8);
+  hipMalloc(&c_l, blocks * 8);
+  for (int rep = 0; rep < 2; rep++) {
+    k_slice<F><<<blocks, 64>>>(d_s, c_s, iters);
+    k_lane<F><<<blocks, 64>>>(d_l, c_l, iters);
+  }
+  hipDeviceSynchronize();
+  std::vector<uint32_t> hs(blocks * 4 * 9), hl(blocks * 64 * 9);
+  std::vector<uint64_t> cs(blocks), cl(blocks);
+  hipMemcpy(hs.data(), d_s, hs.size() * 4, hipMemcpyDeviceToHost);
+  hipMemcpy(hl.data(), d_l, hl.size() * 4, hipMemcpyDeviceToHost);
+  hipMemcpy(cs.data(), c_s, blocks * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(cl.data(), c_l, blocks * 8, hipMemcpyDeviceToHost);
+  int bad = 0;
+  for (int id = 0; id < blocks * 4; id++)
+    for (int i = 0; i < 9; i++) bad += hs[id * 9 + i] != hl[id * 9 + i];
+  double s = 0, l = 0;
+  for (int b = 0; b < blocks; b++) {
+    s += cs[b];
+    l += cl[b];
+  }
+  // wall_clock64 runs at 100 MHz
+  printf("{\"field\": \"%s\", \"sliced_us_per_mul\": %.4f, \"lane_us_per_mul\": %.4f, \"mismatches\": %d}\n", name,
+         s / blocks * 0.01 / iters, l / blocks * 0.01 / iters, bad);
+  hipFree(d_s);
+  hipFree(d_l);
+  hipFree(c_s);
+  hipFree(c_l);
+}
+
+int main() {
+  run<Bn254Fq>("bn254_fq");
+  run<PallasFp>("pallas_fp");
+  return 0;
+}
