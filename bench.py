@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--inst-npub", type=int, default=1, help="public inputs per proof (simple-example: 1)")
     ap.add_argument("--accum-b32", type=int, default=1,
                     help="config 5's per-rank share: 32 proofs at k = 17 per GPU (1/0)")
+    ap.add_argument("--accum-large", type=int, default=4096,
+                    help="throughput leg: one batch of this many proofs per GPU in ONE call (0 = skip)")
     ap.add_argument("--accum-b16", type=int, default=1,
                     help="also time BASELINE config 3: 16 simple-example proofs at k = 14 per GPU (1) or skip (0)")
     ap.add_argument("--dry-run", action="store_true",
@@ -308,6 +310,10 @@ def main():
     accum32 = run_accumulator(args, ctx, dist, dev, rank, world, B=32, logn=17, light=True) \
         if args.accum_b32 else None
     inst = run_instance_commitments(args, ctx, dist, dev, rank, world) if args.inst_batch > 0 else None
+    # many proofs in one pm_accum_batch_proofs_device call (the stream of a
+    # busy aggregator): the batch fills the GPU instead of a latency chain
+    accum_large = run_accumulator(args, ctx, dist, dev, rank, world, B=args.accum_large, logn=17, light=True) \
+        if args.accum_large else None
 
     if rank == 0:
         out = {
@@ -357,6 +363,9 @@ def main():
             out["accumulator_b32_k17"] = accum32
         if inst is not None:
             out["instance_commitments"] = inst
+        if accum_large is not None:
+            accum_large.pop("_state", None)
+            out[f"accumulator_b{args.accum_large}"] = accum_large
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -940,6 +949,16 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None, light=
                             "quads_match_bytes_path": bool(torch.equal(quads_dec, batch.quads))}}
     if world == 1 and not light:
         out["two_in_flight"] = accum_two_in_flight(args, ctx, shape, batch, B)
+    if B > 256:  # its first 256 proofs as a batch of their own: the same quads
+        sub = 256
+        q = torch.empty((sub, 4, 8), dtype=torch.int64, device=dev)
+        hh = torch.empty((sub, 4), dtype=torch.int64, device=dev)
+        cc = torch.empty((sub, 7, 4), dtype=torch.int64, device=dev)
+        ss = torch.empty((sub,), dtype=torch.int32, device=dev)
+        ctx.accum_batch_proofs_device(shape, sub, batch.vk_repr, batch.proofs.data_ptr(), batch.psize,
+                                      batch.inst.data_ptr(), cc.data_ptr(), q.data_ptr(), hh.data_ptr(), ss.data_ptr())
+        torch.cuda.synchronize()
+        out["matches_b256_subbatch"] = bool(torch.equal(q, batch.quads[:sub]) and torch.equal(hh, batch.h_eval[:sub]))
     if rank == 0 and not light:
         host = {k: getattr(batch, k).cpu().numpy().view(np.uint64)
                 for k in ("points", "scalars", "challenges", "quads", "h_eval")}

@@ -68,6 +68,9 @@ constexpr size_t kAccScalarsLds = 128 * 1024;
 // a SIMD with a ladder wave doubled k_acc_scalars (0.14 -> 0.27 ms at
 // B = 256).
 constexpr size_t kAccLadderFence = 40 * 1024;
+// row-sliced ladder (k_acc_powers_s) up to this many chains: one wave each,
+// at most one per SIMD of the 1024 (the fence allows 4 blocks per CU)
+constexpr size_t kAccSlicedChains = 1024;
 static_assert(kAccScalarsLds + kAccLadderFence > 160 * 1024, "the fence must not fit beside k_acc_scalars");
 inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
   uint32_t lg = 0;
@@ -282,9 +285,18 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     sc_done = ctx->next_event();
     if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     if (!inputs_ready) HIP_TRY(hipEventRecord(up, st));
-    if (nprf + nvk_build > 0)
+    // few chains: one row-sliced wave per chain (slice29.hpp, ~2x shorter
+    // steps while the waves fit one per SIMD); more: a quad per chain
+    const size_t chains = nprf + nvk_build;
+    const bool sliced = ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1 : chains <= kAccSlicedChains;
+    if (chains > 0 && sliced)
       PM_LAUNCH(ctx, "acc_ladder",
-                (k_acc_powers<Cv><<<(unsigned)((4 * (nprf + nvk_build) + 255) / 256), 256, kAccLadderFence, st>>>(
+                (k_acc_powers_s<Cv><<<(unsigned)chains, 64, kAccLadderFence, st>>>(
+                    h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
+                    (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
+    else if (chains > 0)
+      PM_LAUNCH(ctx, "acc_ladder",
+                (k_acc_powers<Cv><<<(unsigned)((4 * chains + 255) / 256), 256, kAccLadderFence, st>>>(
                     h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
                     (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
     if (!vk_current) {

@@ -21,6 +21,7 @@
 #include "msm_kernels.hpp"
 #include "curve29.hpp"
 #include "coop29.hpp"
+#include "slice29.hpp"
 #include "glv.hpp"
 
 namespace pm {
@@ -494,6 +495,103 @@ __global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* 
     F29<F> zz, ext;
     cur = jac29_dbl_q_ext<F>(cur, beta, zz, ext);
     pow_store<F>(out + j * kPowPoint, ps, cur, zz, ext);
+  }
+}
+
+// k_acc_powers_s: the same tables, one WAVE per (proof, term) chain with
+// row-sliced field elements (slice29.hpp: an element is one VGPR across a
+// 16-lane row, a product ~0.27 us instead of ~0.42 one-lane).  For few
+// chains (config 3's 16 proofs, config 5's 32-proof rank slices: one wave per
+// SIMD or less), where jac29_dbl_q_ext's quads leave most lanes idle.  The
+// four rows take the quad's four lanes' roles, level by level:
+//   L1  row 1 B = Y Y, row 2 Y Z, row 3 E = (3X) X            (row 0 idles)
+//   L2  row 0 4C = (4B) B, row 1 D = (4X) B, row 2 F = E E, row 3 ZZ3 = Z3 Z3
+//   L3  row 0 beta X3, rows 1, 2 E (D - X3), row 3 ZZZ3 = ZZ3 Z3
+// with the results other rows need gathered by ds_bpermute, and the same
+// values (the same integers: every step is the same Montgomery product,
+// reduction and normalisation) as k_acc_powers stores.  Each row's lanes 0-8
+// store one limb each: coordinate c of position j is 9 consecutive words.
+template <class Cv>
+__global__ void __launch_bounds__(64) k_acc_powers_s(AccumHdr h, const uint32_t* __restrict__ prog,
+                                                   const uint32_t* __restrict__ points,
+                                                   const uint32_t* __restrict__ vk, uint32_t nvk,
+                                                   uint4* __restrict__ pw, uint4* __restrict__ pwv) {
+  using F = typename Cv::Base;
+  using K = F29Consts<F>;
+  const uint32_t g = blockIdx.x;
+  const uint32_t nprf = h.B * h.Tp;
+  if (g >= nprf + nvk) return;
+  const uint32_t* pp;
+  uint4* out;
+  if (g < nprf) {
+    const uint32_t b = g / h.Tp, tp = g - b * h.Tp;
+    pp = points + 16ull * ((size_t)h.npts * b + prog[h.p_psrc + tp]);
+    out = pw + (size_t)g * kPowPos * kPowPoint;
+  } else {
+    pp = vk + 16ull * (g - nprf);
+    out = pwv + (size_t)(g - nprf) * kPowPos * kPowPoint;
+  }
+  const uint32_t row = s_rowid(), l = s_lane();
+  const bool limb = l < 9u;
+  uint32_t* o32 = reinterpret_cast<uint32_t*>(out) + l;  // + position * kPowPoint * 4 + coordinate * 12
+  constexpr uint32_t kPosW = kPowPoint * 4, kCoordW = kPowWords * 4;
+  // store sites of the two stores per position (kPowCoord - 1 = the junk slot)
+  const uint32_t site1 = (row == 0 ? 0u : row == 1 ? 1u : row == 3 ? 2u : 5u) * kCoordW;
+  const uint32_t site2 = (row == 0 ? 4u : row == 3 ? 3u : 5u) * kCoordW;
+  const SConst<F> k = SConst<F>::make();
+  const Aff<F> P = load_aff<F>(pp);
+  if (aff_is_inf<F>(P)) {  // the identity (ZZ = 0) at every power, as k_acc_powers stores it
+    const uint32_t v1 = row == 3 ? 0u : k.one;
+    for (uint32_t j = 0; j < kPowPos; j++)
+      if (limb) {
+        o32[j * kPosW + site1] = v1;
+        o32[j * kPosW + site2] = k.one;
+      }
+    return;
+  }
+  const uint32_t m0 = row == 0 ? ~0u : 0u, m1 = row == 1 ? ~0u : 0u, m2 = row == 2 ? ~0u : 0u,
+                 m3 = row == 3 ? ~0u : 0u;
+  const S29<F> beta{s_limbs(Glv<Cv>::BETA29)};
+  S29<F> X = s29_from<F>(f29_canon<F>(f29_from_r256<F>(P.x.l)));
+  S29<F> Y = s29_from<F>(f29_canon<F>(f29_from_r256<F>(P.y.l)));
+  S29<F> Z{k.one};
+  {  // position 0: (x, y, 1, 1, beta x)
+    const S29<F> bx = s29_norm_exact<F>(s29_mul<F>(beta, X, k));
+    if (limb) {
+      o32[site1] = bsel(m0, X.v, bsel(m1, Y.v, k.one));
+      o32[site2] = bsel(m0, bx.v, k.one);
+    }
+  }
+  for (uint32_t j = 1; j < kPowPos; j++) {
+    // L1: (X, X) / (Y, Y) / (Y, Z) / (3X, X)
+    const uint32_t a1 = bsel(m1 | m2, Y.v, bsel(m3, X.v * 3u, X.v));
+    const uint32_t b1 = bsel(m2, Z.v, bsel(m1, Y.v, X.v));
+    const uint32_t r1 = s29_mul<F>(S29<F>{a1}, S29<F>{b1}, k).v;
+    const uint32_t B = s_row<1>(r1), YZ = s_row<2>(r1), E = s_row<3>(r1);
+    const uint32_t Z3 = YZ + YZ;  // < 4p, limbs <= 2^30
+    // L2: (4B, B) / (4X, B) / (E, E) / (Z3, Z3)
+    const uint32_t a2 = bsel(m0, B << 2, bsel(m1, X.v << 2, bsel(m2, E, Z3)));
+    const uint32_t b2 = bsel(m0 | m1, B, bsel(m2, E, Z3));
+    const uint32_t r2 = s29_mul<F>(S29<F>{a2}, S29<F>{b2}, k).v;
+    const uint32_t C4 = s_row<0>(r2), D = s_row<1>(r2), FF = s_row<2>(r2);
+    const S29<F> X3 = s29_reduce3<F>(s29_norm<F>(S29<F>{FF + k.k8x3 - (D + D)}), k.p);
+    const uint32_t w = D + k.k6 - X3.v;  // < 9p, limbs < 2^31
+    // L3: (beta, X3) / (E, w) / (E, w) / (ZZ3, Z3)
+    const uint32_t a3 = bsel(m0, beta.v, bsel(m3, r2, E));
+    const uint32_t b3 = bsel(m0, X3.v, bsel(m3, Z3, w));
+    const uint32_t r3 = s29_mul<F>(S29<F>{a3}, S29<F>{b3}, k).v;
+    const S29<F> Y3r = s29_reduce3<F>(s29_norm<F>(S29<F>{r3 + k.k8x3 - (C4 + C4)}), k.p);  // rows 1, 2
+    const uint32_t Y3 = s_row<1>(Y3r.v);
+    // stores: X3 (row 0), Y3 (row 1), ZZ3 (row 3) | beta X3 (row 0), ZZZ3 (row 3)
+    const uint32_t v1 = s29_norm_exact<F>(S29<F>{bsel(m0, X3.v, bsel(m1, Y3, r2))}).v;
+    const uint32_t v2 = s29_norm_exact<F>(S29<F>{r3}).v;
+    if (limb) {
+      o32[j * kPosW + site1] = v1;
+      o32[j * kPosW + site2] = v2;
+    }
+    X = X3;
+    Y = S29<F>{Y3};
+    Z = S29<F>{Z3};
   }
 }
 

@@ -407,6 +407,14 @@ int pm_ctx_set_glv(pm_ctx* ctx, int enable) {
   return PM_OK;
 }
 
+int pm_ctx_set_accum_ladder(pm_ctx* ctx, int mode) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  if (mode < -1 || mode > 1) return set_error(PM_ERR_ARG, "accum ladder mode out of range (-1 auto, 0 quads, 1 sliced)");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->acc_ladder = mode;
+  return PM_OK;
+}
+
 int pm_ctx_set_accum_split(pm_ctx* ctx, int lg_lanes) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
   if (lg_lanes < -1 || lg_lanes > 5) return set_error(PM_ERR_ARG, "accum split out of range (-1 auto, 0..5)");

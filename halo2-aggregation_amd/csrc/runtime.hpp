@@ -221,6 +221,7 @@ struct pm_ctx {
   int fine_cache_kb = 0, fine_chunk_kb = 0;
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (test hook: PM_NTT_PASSES env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split)
+  int acc_ladder = -1; // powers-table chains: 0 quads, 1 row-sliced waves, -1 = auto (pm_ctx_set_accum_ladder)
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)
   bool timed(const char* name) const { return timing && (timing_filter.empty() || timing_filter == name); }

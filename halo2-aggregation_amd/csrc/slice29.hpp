@@ -74,11 +74,12 @@ __device__ __forceinline__ uint32_t s_limbs(const uint32_t (&c)[9]) {
 template <class F>
 struct SConst {
   uint32_t pnz;  // p_l for 1 <= l <= 8, 0 in lane 0 and lanes 9..15
-  uint32_t k6, k8x3, k2, one;
+  uint32_t p, k6, k8x3, k2, one;
   __device__ static SConst make() {
     using K = F29Consts<F>;
     SConst c;
-    c.pnz = s_lane() == 0 ? 0u : s_limbs(K::P);
+    c.p = s_limbs(K::P);
+    c.pnz = s_lane() == 0 ? 0u : c.p;
     c.k6 = s_limbs(K::K6);
     c.k8x3 = s_limbs(K::K8x3);
     c.k2 = s_limbs(K::K2);
@@ -176,5 +177,35 @@ __device__ __forceinline__ S29<F> s29_norm_exact(S29<F> a) {
   while (__builtin_amdgcn_ballot_w64(t > kM29 && s_lane() < 8u)) t = (t & kM29) + rshr1(t >> 29);
   return S29<F>{t};
 }
+
+// Norm-ish a (limbs <= 2^29 + small, value < 16p) -> exact Norm, < 3p:
+// v - q p with q = floor(v_8 / (p_8 + 1)) (f29_reduce3's quotient), then
+// signed carry rounds until every limb is in [0, 2^29) (the top lane keeps its
+// carries: the value is non-negative, so it ends non-negative)
+template <class F>
+__device__ __forceinline__ S29<F> s29_norm_exact(S29<F> a);
+template <class F>
+__device__ __forceinline__ S29<F> s29_reduce3(S29<F> a_in, uint32_t pl) {
+  using K = F29Consts<F>;
+  const S29<F> a = s29_norm_exact<F>(a_in);  // the quotient from the exact top limb (f29_reduce3's q)
+  const uint32_t q = (uint32_t)(((uint64_t)rbc32<8>(a.v) * K::QMAGIC) >> 40);
+  const bool low = s_lane() < 8u;
+  const int64_t t0 = (int64_t)a.v - (int64_t)q * pl;  // > -2^34 (the top lane's fits 32 bits)
+  const int32_t hi0 = low ? (int32_t)(t0 >> 29) : 0;
+  int32_t t = (int32_t)(low ? (uint32_t)t0 & kM29 : (uint32_t)t0) + (int32_t)rshr1((uint32_t)hi0);
+  auto bad = [&](int32_t x) { return low && (x < 0 || x > (int32_t)kM29); };
+  while (__builtin_amdgcn_ballot_w64(bad(t))) {
+    const int32_t hi = low ? t >> 29 : 0;
+    t = (low ? (int32_t)((uint32_t)t & kM29) : t) + (int32_t)rshr1((uint32_t)hi);
+  }
+  return S29<F>{(uint32_t)t};
+}
+
+// value of row K (lanes 16 K .. 16 K + 15) in every row (ds_bpermute)
+template <int K>
+__device__ __forceinline__ uint32_t s_row(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((((uint32_t)K << 4) | s_lane()) << 2), (int)v);
+}
+__device__ __forceinline__ uint32_t s_rowid() { return (threadIdx.x >> 4) & 3u; }
 
 }  // namespace pm

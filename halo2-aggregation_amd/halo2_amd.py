@@ -224,6 +224,7 @@ def _load():
         "pm_ctx_set_small_msm": ([_vp, ctypes.c_size_t], ctypes.c_int),
         "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_split": ([_vp, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_accum_ladder": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_glv": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing_filter": ([_vp, ctypes.c_char_p], ctypes.c_int),
@@ -563,6 +564,10 @@ class Context:
     def set_glv(self, enable=True):
         """Retired GLV mode: only enable=False is accepted."""
         _check(lib().pm_ctx_set_glv(self.h, 1 if enable else 0))
+
+    def set_accum_ladder(self, mode=-1):
+        """pm_ctx_set_accum_ladder: 0 quads, 1 row-sliced waves, -1 auto."""
+        _check(lib().pm_ctx_set_accum_ladder(self.h, mode))
 
     def set_accum_split(self, lg_lanes=-1):
         """Accumulator: 2^lg_lanes lanes (bit segments) per MSM term, 0..5 (-1 = automatic)."""

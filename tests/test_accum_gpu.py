@@ -53,6 +53,29 @@ def test_split_ladder_widths(gpu_ctx, lg):
         gpu_ctx.set_accum_split(-1)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_ladder_modes(gpu_ctx, mode):
+    """Both forms of the powers-of-two table chains (0: a quad of lanes per
+    chain, k_acc_powers; 1: a row-sliced wave per chain, k_acc_powers_s)
+    reproduce the golden vectors (identity and W_1 = -W_0 edge cases) and
+    random proofs of both shapes on every curve; with the VK tables rebuilt
+    by the mode under test (a fresh context)."""
+    ctx = H.Context(0)
+    ctx.set_accum_ladder(mode)
+    test_golden_accumulator(ctx)
+    for cid in (0, 1, 2):
+        for shape in ("simple", "rich"):
+            C, sh, proofs = U.make_case(cid, shape, 12, 6, 0x1ADD + 13 * cid + mode)
+            ps = U.to_product_shape(cid, sh)
+            pts, scs, chs = A.pack_proofs(C, sh, proofs)
+            quads, h = ctx.accum_batch(ps, pts, scs, chs)
+            for b in (0, 5):
+                q, hh = A.pack_result(C, A.accumulate_msm(C, sh, proofs[b]))
+                assert np.array_equal(h[b], hh) and np.array_equal(quads[b], q), (cid, shape, b)
+    with pytest.raises(H.PmError):
+        ctx.set_accum_ladder(2)
+
+
 @pytest.mark.parametrize("cid", [0, 1, 2])
 @pytest.mark.parametrize("shape", ["simple", "rich"])
 def test_random_proofs_vs_oracle(gpu_ctx, cid, shape):

@@ -262,3 +262,45 @@ def test_bn254_hand_derived_edges(gpu_ctx):
         else:
             assert st[b] == 0, b
             assert P.limbs_to_point(C, [int(v) for v in pts[b, slot]]) == want, b
+
+
+def test_large_batch_vs_c_port():
+    """A 1000-proof batch from bytes (simple-example shape, BN254, k = 17: the
+    one-lane term-product path above the table budget) in ONE
+    pm_accum_batch_proofs_device call, against oracle/accum_ref.c on the same
+    bytes (decode + Blake2b replay + accumulator): every challenge, quad and
+    h_eval; and its first 256 proofs as a batch of their own give the same
+    quads (no cross-proof state)."""
+    import torch
+
+    import accum_ref
+    import workloads as Wk
+
+    ctx = H.Context(0)
+    B = 1000
+    shape = Wk.simple_example_shape(ctx, H.BN254, 17)
+    batch = Wk.SyntheticBatch(ctx, shape, B, seed=0xB16)
+    batch.to_proof_bytes(shape)
+    batch.run_bytes(ctx, shape)
+    torch.cuda.synchronize()
+    proofs = batch.proofs.cpu().numpy()
+    inst = batch.inst.cpu().numpy().view(np.uint64)
+    o = accum_ref.batch_proofs(H.BN254, shape.c, proofs, inst, vk_repr=np.asarray(batch.vk_repr, dtype=np.uint64),
+                               threads=8)
+    ch = batch.challenges.cpu().numpy().view(np.uint64)
+    quads = batch.quads.cpu().numpy().view(np.uint64)
+    hev = batch.h_eval.cpu().numpy().view(np.uint64)
+    assert not o["status"].any() and not batch.status.cpu().numpy().any()
+    assert np.array_equal(o["challenges"].reshape(ch.shape), ch)
+    assert np.array_equal(o["quads"].reshape(quads.shape), quads)
+    assert np.array_equal(o["h_eval"].reshape(hev.shape), hev)
+    sub = 256
+    dev = batch.proofs.device
+    q = torch.empty((sub, 4, 8), dtype=torch.int64, device=dev)
+    h = torch.empty((sub, 4), dtype=torch.int64, device=dev)
+    c = torch.empty((sub, 7, 4), dtype=torch.int64, device=dev)
+    st = torch.empty((sub,), dtype=torch.int32, device=dev)
+    ctx.accum_batch_proofs_device(shape, sub, batch.vk_repr, batch.proofs.data_ptr(), batch.psize,
+                                  batch.inst.data_ptr(), c.data_ptr(), q.data_ptr(), h.data_ptr(), st.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(q, batch.quads[:sub]) and torch.equal(h, batch.h_eval[:sub])
