@@ -71,6 +71,9 @@ constexpr size_t kAccLadderFence = 40 * 1024;
 // row-sliced ladder (k_acc_powers_s) up to this many chains: one wave each,
 // at most one per SIMD of the 1024 (the fence allows 4 blocks per CU)
 constexpr size_t kAccSlicedChains = 1024;
+// row-sliced square roots (k_proof_decode<Cv, true>) up to this many points
+// (four per wave: 1024 waves)
+constexpr size_t kDecodeSlicedPoints = 4096;
 static_assert(kAccScalarsLds + kAccLadderFence > 160 * 1024, "the fence must not fit beside k_acc_scalars");
 inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
   uint32_t lg = 0;
@@ -467,6 +470,7 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     if ((rc = ctx->sqrt_tab[slot].ensure(sizeof(SqrtTab)))) return rc;
     HIP_TRY(hipMemcpy(ctx->sqrt_tab[slot].p, &tab, sizeof(SqrtTab), hipMemcpyHostToDevice));
     ctx->sqrt_ready[slot] = true;
+    ctx->sqrt_tab_ts[slot] = tab.ts != 0;
   }
   // (byte offset, destination point) of every point read from the bytes
   std::vector<uint32_t> map;
@@ -507,7 +511,12 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   h.npp = npp;
   h.sc_off = sc_off;
   h.stride = (uint32_t)stride;
-  h.nblk_pts = (uint32_t)((B * npp + kDecodeThreads - 1) / kDecodeThreads);
+  // few points on a p = 3 mod 4 curve: one point per row, the square root
+  // row-sliced (k_proof_decode<Cv, true>); up to ~one wave per SIMD
+  const bool sliced = !ctx->sqrt_tab_ts[slot] && (ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1
+                                                                         : B * npp <= kDecodeSlicedPoints);
+  const uint32_t per_blk = sliced ? kDecodeThreads / 16 : kDecodeThreads;
+  h.nblk_pts = (uint32_t)((B * npp + per_blk - 1) / per_blk);
   const size_t nblk_sc = (B * ((size_t)L.nsc + ninst) + kDecodeThreads - 1) / kDecodeThreads;
   if (stride > 0xffffffffull) return set_error(PM_ERR_UNSUPPORTED, "proof stride above 4 GiB");
   // untimed calls launch the decode with its completion event attached to the
@@ -517,14 +526,21 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   if (vk_repr && !ctx->timing) {
     dec_done = ctx->next_event();
     if (!dec_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
-    hipExtLaunchKernelGGL(k_proof_decode<Cv>, dim3((unsigned)(h.nblk_pts + nblk_sc)), dim3(kDecodeThreads), 0, st,
+    auto kern = sliced ? k_proof_decode<Cv, true> : k_proof_decode<Cv, false>;
+    hipExtLaunchKernelGGL(kern, dim3((unsigned)(h.nblk_pts + nblk_sc)), dim3(kDecodeThreads), 0, st,
                           nullptr, dec_done, 0, h, (const SqrtTab*)ctx->sqrt_tab[slot].p,
                           (const uint32_t*)ctx->pf_map.buf.p, (const uint32_t*)d_proofs, (const uint32_t*)d_inst,
                           (uint32_t*)d_points, (uint32_t*)d_scalars, cpts, cscs, dflags);
     HIP_TRY(hipGetLastError());
+  } else if (sliced) {
+    PM_LAUNCH(ctx, "proof_decode",
+              (k_proof_decode<Cv, true><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
+                  h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
+                  (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
+                  cscs, dflags)));
   } else {
     PM_LAUNCH(ctx, "proof_decode",
-              (k_proof_decode<Cv><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
+              (k_proof_decode<Cv, false><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
                   h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
                   (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
                   cscs, dflags)));

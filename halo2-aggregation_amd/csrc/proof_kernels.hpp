@@ -43,6 +43,7 @@
 #include "curve.hpp"
 #include "fp29.hpp"
 #include "msm_kernels.hpp"
+#include "slice29.hpp"
 #include "runtime.hpp"
 
 namespace pm {
@@ -248,6 +249,31 @@ __device__ F29<F> sqrt_pow(const SqrtTab& T, const F29<F>& a, uint32_t* odd, uin
   return acc;
 }
 
+// sqrt_pow with row-sliced elements (slice29.hpp: one element per 16-lane
+// row, a product ~0.27 us instead of ~0.42): the odd powers stay in eight
+// VGPRs, the schedule is the same for every row (one exponent per curve).
+template <class F>
+__device__ S29<F> sqrt_pow_s(const SqrtTab& T, S29<F> a, const SConst<F>& k) {
+  const S29<F> a2 = s29_mul<F>(a, a, k);
+  S29<F> odd[kSqrtWin];
+  odd[0] = a;
+#pragma unroll
+  for (int i = 1; i < kSqrtWin; i++) odd[i] = s29_mul<F>(odd[i - 1], a2, k);
+  auto pick = [&](uint32_t idx) {
+    uint32_t v = odd[0].v;
+#pragma unroll
+    for (int i = 1; i < kSqrtWin; i++) v = idx == (uint32_t)i ? odd[i].v : v;
+    return S29<F>{v};
+  };
+  S29<F> acc = pick(T.sched[0] & 0xffu);
+  for (uint32_t j = 1; j < T.nsched; j++) {
+    const uint32_t s = T.sched[j];
+    for (uint32_t q = s >> 8; q; q--) acc = s29_mul<F>(acc, acc, k);
+    if ((s & 0xffu) != 0xffu) acc = s29_mul<F>(acc, pick(s & 0xffu), k);
+  }
+  return acc;
+}
+
 // 8-bit discrete log of v (canonical R261, a power of G3) in the sorted LDS keys
 __device__ __forceinline__ uint32_t sqrt_dlog(const uint32_t* klo, const uint32_t* khi, const uint32_t* kidx,
                                               const uint32_t l0, const uint32_t l1, bool& ok) {
@@ -265,15 +291,23 @@ __device__ __forceinline__ uint32_t sqrt_dlog(const uint32_t* klo, const uint32_
 }
 
 // y with y^2 = a (a Norm < 3p, R261); false when a is a non-residue
-template <class F>
+// SLICED: the rows of the wave each decode one point (all 16 lanes of a row
+// hold the same a), and the exponentiation runs row-sliced (p = 3 mod 4 only:
+// the caller checks T.ts == 0)
+template <class F, bool SLICED = false>
 __device__ bool f29_sqrt(const SqrtTab& T, const F29<F>& a_in, F29<F>& y, uint32_t* odd, uint32_t ls,
                          const uint32_t* klo, const uint32_t* khi, const uint32_t* kidx) {
   const F29<F> a = f29_canon<F>(f29_reduce3<F>(a_in));
+  F29<F> w;
+  if constexpr (SLICED) {  // every row runs the chain (a zero a gives y = 0 below too)
+    const SConst<F> k = SConst<F>::make();
+    w = s29_to<F>(s29_norm_exact<F>(sqrt_pow_s<F>(T, s29_from<F>(a), k)));
+  }
   if (f29_is_zero_exact<F>(a)) {
     y = a;
     return true;
   }
-  const F29<F> w = sqrt_pow<F>(T, a, odd, ls);
+  if constexpr (!SLICED) w = sqrt_pow<F>(T, a, odd, ls);
   bool ok = true;
   if (!T.ts) {
     y = w;
@@ -326,7 +360,10 @@ struct ProofDecodeHdr {
 // Blocks after: one lane per scalar, then per instance commitment.
 constexpr int kDecodeThreads = 64;
 
-template <class Cv>
+// SLICED (p = 3 mod 4 curves, few points): one point per 16-lane row, the
+// square root's exponentiation row-sliced (sqrt_pow_s); every lane of a row
+// runs the rest of the point's code redundantly and lane 0 stores.
+template <class Cv, bool SLICED = false>
 __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
     ProofDecodeHdr h, const SqrtTab* __restrict__ tabp, const uint32_t* __restrict__ pt_map,
     const uint32_t* __restrict__ proofs, const uint32_t* __restrict__ inst, uint32_t* __restrict__ points,
@@ -339,7 +376,7 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
   const SqrtTab& T = *tabp;
   const uint32_t lane = threadIdx.x;
   if (blockIdx.x < h.nblk_pts) {
-    if (T.ts) {
+    if (!SLICED && T.ts) {
       for (uint32_t i = lane; i < 256; i += kDecodeThreads) {
         s_klo[i] = T.key_lo[i];
         s_khi[i] = T.key_hi[i];
@@ -347,8 +384,10 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
       }
       __syncthreads();
     }
-    const size_t e = (size_t)blockIdx.x * kDecodeThreads + lane;
-    if (e >= (size_t)h.B * h.npp) return;
+    const size_t e = SLICED ? (size_t)blockIdx.x * (kDecodeThreads / 16) + (lane >> 4)
+                            : (size_t)blockIdx.x * kDecodeThreads + lane;
+    if (e >= (size_t)h.B * h.npp) return;  // whole rows when SLICED
+    const bool writer = !SLICED || (lane & 15u) == 0u;
     const uint32_t b = (uint32_t)(e / h.npp), j = (uint32_t)(e % h.npp);
     const uint32_t off = pt_map[2 * j], dst = pt_map[2 * j + 1];
     const uint32_t* src = proofs + ((size_t)b * h.stride + off) / 4;
@@ -367,7 +406,7 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
       const F29<F> X = f29_mul_c<F>(f29_unpack<F>(w), f29_ld<F>(T.r2));  // R261
       const F29<F> rhs = f29_norm<F>(f29_add<F>(f29_mul_c<F>(f29_sqr_c<F>(X), X), f29_ld<F>(T.b)));
       F29<F> Y;
-      ok = f29_sqrt<F>(T, rhs, Y, s_odd + lane, kDecodeThreads, s_klo, s_khi, s_kidx);
+      ok = f29_sqrt<F, SLICED>(T, rhs, Y, s_odd + lane, kDecodeThreads, s_klo, s_khi, s_kidx);
       if (ok) {
         F29<F> one = f29_zero<F>();
         one.l[0] = 1;
@@ -384,6 +423,7 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
         f29_pack<F>(y, yc);
       }
     }
+    if (!writer) return;
     if (!ok) atomicOr(&status[b], kProofBadPoint);
     const size_t pi = (size_t)b * h.npts + dst;
     uint4* po = reinterpret_cast<uint4*>(points + 16 * pi);

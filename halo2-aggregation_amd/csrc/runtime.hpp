@@ -236,6 +236,7 @@ struct pm_ctx {
   // (pm_curve order), the point map of the current shape, host staging
   pm::Buf sqrt_tab[3];
   bool sqrt_ready[3] = {false, false, false};
+  bool sqrt_tab_ts[3] = {false, false, false};  // the curve's root needs the Tonelli-Shanks windows (Pasta)
   pm::CachedUpload pf_map;
   pm::Buf pf_io;
   pm::Buf pf_flags;            // proof-decode flags per proof (cleared by k_transcript)

@@ -99,11 +99,16 @@ def test_decode_vs_oracle(gpu_ctx, cid, shape):
     assert np.array_equal(pts[:27], p0) and np.array_equal(scs[:27], s0)
 
 
-@pytest.mark.parametrize("cid", [0, 1, 2])
-def test_decode_many_points(gpu_ctx, cid):
+@pytest.mark.parametrize("cid,mode", [(0, -1), (1, -1), (2, -1), (2, 0), (2, 1)])
+def test_decode_many_points(gpu_ctx, cid, mode):
     """Decompression of 2000 random curve points and their negations (random
     square roots in both Tonelli-Shanks windows / the (p+1)/4 power), plus
-    random x (about half non-residues): every output against the oracle."""
+    random x (about half non-residues): every output against the oracle.
+    BN254 also with each square-root form forced (mode 0: one lane per point;
+    1: one row-sliced row per point, k_proof_decode<Cv, true>)."""
+    if mode >= 0:
+        gpu_ctx = H.Context(0)
+        gpu_ctx.set_accum_ladder(mode)
     C = P.CURVES[cid]
     rng = random.Random(0x5027 + cid)
     sh = A.synth_vk_points(C, U.SHAPES["simple"](C, 10), seed=0x11)
