@@ -42,9 +42,13 @@ template <int J>
 __device__ __forceinline__ uint32_t rbc32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + J, 0xF, 0xF, false);
 }
-template <int J>
-__device__ __forceinline__ uint64_t rbc64(uint64_t v) {
-  return (uint64_t)__builtin_amdgcn_update_dpp((long)v, (long)v, 0x150 + J, 0xF, 0xF, false);
+// 64-bit broadcast of lane 0 into a fresh register (the builtin ties its
+// destination to an "old" operand and copies it first); the s_nop covers the
+// VALU-write -> DPP-read hazard the compiler does not see through the asm
+__device__ __forceinline__ uint64_t rbc64_0(uint64_t v) {
+  uint64_t r;
+  asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v));
+  return r;
 }
 // lane l <- lane l + 1 (lane 15 <- 0)
 __device__ __forceinline__ uint32_t rshl1(uint32_t v) {
@@ -118,7 +122,7 @@ template <class F, int J>
 __device__ __forceinline__ void s29_step(uint32_t a, uint32_t b, uint32_t pnz, uint64_t& T, uint64_t& c) {
   using K = F29Consts<F>;
   T += (uint64_t)a * rbc32<J>(b);
-  const uint64_t t = rbc64<0>(T) + c;
+  const uint64_t t = rbc64_0(T) + c;
   uint32_t m;
   if constexpr (K::INV == kM29) m = (0u - (uint32_t)t) & kM29;
   else m = ((uint32_t)t * K::INV) & kM29;
