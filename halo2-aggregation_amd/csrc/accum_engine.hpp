@@ -69,8 +69,14 @@ constexpr size_t kAccScalarsLds = 128 * 1024;
 // B = 256).
 constexpr size_t kAccLadderFence = 40 * 1024;
 // row-sliced ladder (k_acc_powers_s) up to this many chains: one wave each,
-// at most one per SIMD of the 1024 (the fence allows 4 blocks per CU)
-constexpr size_t kAccSlicedChains = 1024;
+// four per block and one block per CU (kAccSlicedFence), leaving CUs for the
+// side stream's transcript / k_acc_scalars blocks (which a ladder block on
+// every CU kept waiting until the ladder ended: B = 16 transcript 0.10 ->
+// 0.27 ms with 64-thread ladder blocks, profiles/r05/ladder_ab/)
+constexpr size_t kAccSlicedChains = 800;
+constexpr size_t kAccSlicedFence = 84 * 1024;
+static_assert(2 * kAccSlicedFence > 160 * 1024 && kAccSlicedFence + kAccScalarsLds > 160 * 1024,
+              "one sliced ladder block per CU, no side-stream block beside it");
 // row-sliced square roots (k_proof_decode<Cv, true>) up to this many points
 // (four per wave: 1024 waves)
 constexpr size_t kDecodeSlicedPoints = 4096;
@@ -294,7 +300,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     const bool sliced = ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1 : chains <= kAccSlicedChains;
     if (chains > 0 && sliced)
       PM_LAUNCH(ctx, "acc_ladder",
-                (k_acc_powers_s<Cv><<<(unsigned)chains, 64, kAccLadderFence, st>>>(
+                (k_acc_powers_s<Cv><<<(unsigned)((chains + 3) / 4), 256, kAccSlicedFence, st>>>(
                     h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
                     (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
     else if (chains > 0)

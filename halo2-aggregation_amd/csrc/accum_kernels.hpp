@@ -511,14 +511,18 @@ __global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* 
 // values (the same integers: every step is the same Montgomery product,
 // reduction and normalisation) as k_acc_powers stores.  Each row's lanes 0-8
 // store one limb each: coordinate c of position j is 9 consecutive words.
+// Blocks of four waves (four chains: one wave per SIMD of a CU), each with an
+// LDS fence that keeps a second ladder block and every side-stream block
+// (transcript, k_acc_scalars) off its CU.  Waves only talk inside themselves
+// (DPP, ds_bpermute, ballot), so a wave past the last chain just exits.
 template <class Cv>
-__global__ void __launch_bounds__(64) k_acc_powers_s(AccumHdr h, const uint32_t* __restrict__ prog,
-                                                   const uint32_t* __restrict__ points,
-                                                   const uint32_t* __restrict__ vk, uint32_t nvk,
-                                                   uint4* __restrict__ pw, uint4* __restrict__ pwv) {
+__global__ void __launch_bounds__(256) k_acc_powers_s(AccumHdr h, const uint32_t* __restrict__ prog,
+                                                    const uint32_t* __restrict__ points,
+                                                    const uint32_t* __restrict__ vk, uint32_t nvk,
+                                                    uint4* __restrict__ pw, uint4* __restrict__ pwv) {
   using F = typename Cv::Base;
   using K = F29Consts<F>;
-  const uint32_t g = blockIdx.x;
+  const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
   const uint32_t nprf = h.B * h.Tp;
   if (g >= nprf + nvk) return;
   const uint32_t* pp;

@@ -105,7 +105,8 @@ int pm_ctx_set_accum_split(pm_ctx* ctx, int lg_lanes);
 /* Batch accumulator: how the powers-of-two table chains run (mode 0: a quad
  * of lanes per chain; 1: one wave per chain with row-sliced field elements,
  * shorter steps while the chains fit one wave per SIMD; -1 = automatic: 1 for
- * up to 1024 chains).  Results do not depend on it. */
+ * up to 800 chains, and the proof decoder's square roots row-sliced for up
+ * to 4096 points on BN254).  Results do not depend on it. */
 int pm_ctx_set_accum_ladder(pm_ctx* ctx, int mode);
 /* Per-kernel HIP-event timing on the context stream (for bench/profiling).
  * Every event pair costs ~10 us of stream time on MI355X, so a timed region
