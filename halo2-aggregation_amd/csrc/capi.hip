@@ -801,6 +801,8 @@ bool same_key(const pm::DropinEntry& e, int curve, size_t n, const uint64_t d[4]
 static void dropin_release_all(pm_ctx* ctx) {
   for (auto& e : ctx->dropin) pm_bases_release(e.b);
   ctx->dropin.clear();
+  for (auto& e : ctx->dropin_small) pm_bases_release(e.b);
+  ctx->dropin_small.clear();
 }
 
 static size_t dropin_total(const pm_ctx* ctx) {
@@ -834,6 +836,71 @@ static void dropin_make_room(pm_ctx* ctx, size_t bytes) {
   }
 }
 
+// Small sets (the small-MSM path's sizes): a repeated set -- halo2's
+// commit_lagrange of a few public inputs against the first bases of
+// g_lagrange, examples/simple-example.rs:632-641 -- is kept resident with a
+// multiples table after its second sighting and then runs as ONE short MSM of
+// pm_msm_resident_many (no doublings, no host Horner); first sightings and
+// sets that do not fit run the small-MSM path on the host inputs.  The keyed
+// digest of a small set is cheap (at most 1 MiB of bases).
+static int dropin_small_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
+                            uint32_t flags, uint64_t out[8]) {
+  const CurveOps* ops = curve_ops(curve);
+  auto small = [&]() { return ops->msm_small(ctx, scalars, true, bases, true, false, n, flags, out); };
+  const size_t tbytes = n * pm::many_bytes_per_base(pm::many_pick_c(n));
+  if (n * 64 > (size_t(1) << 20) || tbytes > pm::kDropinSmallBytes / 2) return small();
+  pm::u128 part[2];
+  pm::digest_chunk(ctx->dropin_key, bases, 8 * n, part);
+  uint64_t d[4];
+  pm::digest_combine(ctx->dropin_key, part, 1, d);
+  pm_bases* b = nullptr;
+  for (auto& e : ctx->dropin_small)
+    if (same_key(e, curve, n, d)) {
+      e.last_use = ++ctx->dropin_clock;
+      b = e.b;
+      break;
+    }
+  if (!b) {
+    auto seen = std::find_if(ctx->dropin_small_seen.begin(), ctx->dropin_small_seen.end(),
+                             [&](const pm::DropinEntry& e) { return same_key(e, curve, n, d); });
+    if (seen == ctx->dropin_small_seen.end()) {  // first sighting
+      if ((int)ctx->dropin_small_seen.size() >= kDropinSeen) ctx->dropin_small_seen.erase(ctx->dropin_small_seen.begin());
+      ctx->dropin_small_seen.push_back(pm::DropinEntry{curve, n, {d[0], d[1], d[2], d[3]}, nullptr, 0, ++ctx->dropin_clock});
+      return small();
+    }
+    ctx->dropin_small_seen.erase(seen);
+    // LRU room against the entry count and the byte budget
+    for (;;) {
+      size_t held = 0;
+      for (auto& e : ctx->dropin_small) held += e.bytes;
+      if ((int)ctx->dropin_small.size() < kDropinSmallEntries && held + tbytes + 64 * n <= pm::kDropinSmallBytes) break;
+      auto lru = std::min_element(ctx->dropin_small.begin(), ctx->dropin_small.end(),
+                                  [](const pm::DropinEntry& x, const pm::DropinEntry& y) { return x.last_use < y.last_use; });
+      pm_bases_release(lru->b);
+      ctx->dropin_small.erase(lru);
+    }
+    int rc = bases_upload_locked(ctx, curve, bases, true, n, &b);
+    if (!rc) {
+      std::lock_guard<std::mutex> lt(b->many_mu);
+      rc = ops->many_table(ctx, b->d, n, &b->many);
+    }
+    if (rc) {  // not admitted (e.g. out of memory): the small path still computes it
+      if (b) pm_bases_release(b);
+      pm::g_last_error.clear();
+      if ((rc = ctx->begin_call())) return rc;
+      return small();
+    }
+    ctx->dropin_small_admits++;
+    ctx->dropin_small.push_back(pm::DropinEntry{curve, n, {d[0], d[1], d[2], d[3]}, b, tbytes + 64 * n,
+                                                ++ctx->dropin_clock});
+    if (int r = ctx->begin_call()) return r;
+  } else {
+    ctx->dropin_small_hits++;
+  }
+  std::lock_guard<std::mutex> lt(b->many_mu);
+  return ops->msm_many(ctx, &b->many, 1, &n, nullptr, scalars, true, flags, out);
+}
+
 static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n, uint32_t flags,
                       uint64_t out[8]) {
   if (n == 0) {
@@ -842,7 +909,7 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
   }
   int rc;
   if ((rc = ctx->begin_call())) return rc;
-  if (use_small(ctx, n)) return curve_ops(curve)->msm_small(ctx, scalars, true, bases, true, false, n, flags, out);
+  if (use_small(ctx, n)) return dropin_small_msm(ctx, curve, scalars, bases, n, flags, out);
   if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
   auto plain = [&]() -> int {  // both inputs uploaded, plain pipeline
     int r;
@@ -1010,6 +1077,21 @@ int pm_ctx_dropin_clear(pm_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   dropin_release_all(ctx);
   ctx->dropin_seen.clear();
+  ctx->dropin_small_seen.clear();
+  return PM_OK;
+}
+
+int pm_ctx_dropin_small_stats(pm_ctx* ctx, uint64_t* hits, uint64_t* admitted, int* entries, size_t* device_bytes) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (hits) *hits = ctx->dropin_small_hits;
+  if (admitted) *admitted = ctx->dropin_small_admits;
+  if (entries) *entries = (int)ctx->dropin_small.size();
+  if (device_bytes) {
+    size_t t = 0;
+    for (auto& e : ctx->dropin_small) t += e.bytes;
+    *device_bytes = t;
+  }
   return PM_OK;
 }
 

@@ -54,6 +54,10 @@ constexpr size_t kDropinFreeDiv = 2;
 // base sets seen once and not admitted: a set becomes resident on its second
 // sighting, so one-shot bases never pay the row-table build
 constexpr int kDropinSeen = 8;
+// small drop-in sets (multiples tables): at most this many, and this many
+// bytes of tables, per context
+constexpr int kDropinSmallEntries = 8;
+constexpr size_t kDropinSmallBytes = size_t(4) << 30;
 // small-MSM path (msm_small.hpp): pm_msm* calls with n <= ctx->small_max (and
 // the automatic window) run the two-launch table + window-sum kernels instead
 // of the sorting pipeline; kSmallLimit bounds pm_ctx_set_small_msm
@@ -206,6 +210,11 @@ struct pm_ctx {
   pm::HostPool* pool = nullptr;      // lazily created (drop-in digest)
   std::vector<pm::DropinEntry> dropin;  // drop-in base cache (pm_msm / pm_msm_ctx)
   std::vector<pm::DropinEntry> dropin_seen;  // digests seen once (b == nullptr), admitted on the second sighting
+  // small sets (n <= small_max, below kDropinMinN): resident with a multiples
+  // table (msm_many.hpp) after their second sighting, run as one-MSM
+  // pm_msm_resident_many calls
+  std::vector<pm::DropinEntry> dropin_small, dropin_small_seen;
+  uint64_t dropin_small_hits = 0, dropin_small_admits = 0;
   pm::DigestKey dropin_key;             // secret per-context digest key (pm_ctx_create)
   uint64_t dropin_clock = 0;
   uint64_t dropin_hits = 0, dropin_misses = 0;

@@ -234,6 +234,7 @@ def _load():
                                 ctypes.c_int),
         "pm_ctx_dropin_spec_stats": ([_vp, _u64p, _u64p], ctypes.c_int),
         "pm_ctx_dropin_oom_stats": ([_vp, _u64p, _u64p], ctypes.c_int),
+        "pm_ctx_dropin_small_stats": ([_vp, _u64p, _u64p, ctypes.POINTER(ctypes.c_int), _szp], ctypes.c_int),
         "pm_ctx_dropin_clear": ([_vp], ctypes.c_int),
         "pm_ctx_dropin_key_id": ([_vp, _u64p], ctypes.c_int),
         "pm_msm": ([ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p], ctypes.c_int),
@@ -608,6 +609,13 @@ class Context:
         f, b = ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib().pm_ctx_dropin_oom_stats(self.h, ctypes.byref(f), ctypes.byref(b)))
         return f.value, b.value
+
+    def dropin_small_stats(self):
+        """pm_ctx_dropin_small_stats -> dict(hits, admitted, entries, device_bytes)."""
+        h, a, e, b = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_size_t()
+        _check(lib().pm_ctx_dropin_small_stats(self.h, ctypes.byref(h), ctypes.byref(a), ctypes.byref(e),
+                                               ctypes.byref(b)))
+        return {"hits": h.value, "admitted": a.value, "entries": e.value, "device_bytes": b.value}
 
     def dropin_clear(self):
         _check(lib().pm_ctx_dropin_clear(self.h))

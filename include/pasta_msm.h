@@ -168,6 +168,13 @@ int pm_ctx_dropin_spec_stats(pm_ctx* ctx, uint64_t* kept, uint64_t* drained);
  * and released every cached set before their one retry, *failed_builds =
  * sets left unadmitted (that call ran the plain pipeline and succeeded). */
 int pm_ctx_dropin_oom_stats(pm_ctx* ctx, uint64_t* flushes, uint64_t* failed_builds);
+/* The drop-in cache's small sets (n up to the small-MSM threshold, at most
+ * 1 MiB of bases): a set seen twice is kept resident with a multiples table
+ * (pm_msm_resident_many's) and later calls with it run as one short MSM of
+ * that path; at most 8 sets and 4 GiB per context, LRU; pm_ctx_dropin_clear
+ * releases them too.  *hits = calls served from a kept set, *admitted = sets
+ * admitted so far, *entries / *device_bytes = what is held now. */
+int pm_ctx_dropin_small_stats(pm_ctx* ctx, uint64_t* hits, uint64_t* admitted, int* entries, size_t* device_bytes);
 /* A fingerprint of ctx's secret digest key (16 bytes of BLAKE2b of the key,
  * personal "pm-dropin-key-id"): distinct contexts hold distinct keys.  It
  * reveals nothing about the key itself. */

@@ -176,3 +176,36 @@ def test_larger_threshold_sizes(gpu_ctx):
             assert np.array_equal(gpu_ctx.msm(2, S[:n], B[:n]), want), n
     finally:
         gpu_ctx.set_small_msm(H.SMALL_MSM_DEFAULT)
+
+
+@pytest.mark.parametrize("curve", [0, 2])
+def test_small_set_dropin_cache(curve):
+    """A small base set seen twice is kept resident with a multiples table
+    and later pm_msm calls with it run as one short MSM of the many-MSM path:
+    every call (first sighting on the small path, admission, hits, a base
+    changed in place, new scalars each time) against the C port."""
+    ctx = H.Context(0)
+    try:
+        S, B = _inputs(curve, 8192, 0x5A5 + curve)
+        admitted = 0
+        for n in (1, 5, 32, 300, 4096):
+            b = np.ascontiguousarray(B[:n])
+            for k in range(4):
+                s = np.ascontiguousarray(S[k:k + n])
+                want = msm_ref.best_multiexp(curve, s, b, threads=4)
+                assert np.array_equal(ctx.msm(curve, s, b), want), (n, k)
+            admitted += 1
+            st = ctx.dropin_small_stats()
+            assert st["admitted"] == admitted and st["entries"] == min(admitted, 8), (n, st)
+        assert ctx.dropin_small_stats()["hits"] == 2 * 5
+        # a base changed in place: a new key (first sighting, small path), still exact
+        b = np.ascontiguousarray(B[:32]).copy()
+        b[7] = B[100]
+        s = np.ascontiguousarray(S[:32])
+        assert np.array_equal(ctx.msm(curve, s, b), msm_ref.best_multiexp(curve, s, b, threads=4))
+        assert ctx.dropin_small_stats()["hits"] == 10
+        assert ctx.dropin_stats()["entries"] == 0   # the large-set cache is untouched
+        ctx.dropin_clear()
+        assert ctx.dropin_small_stats()["entries"] == 0
+    finally:
+        ctx.close()
