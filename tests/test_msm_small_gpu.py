@@ -29,8 +29,10 @@ def _inputs(curve, n, seed=0x5A11):
 
 
 def _ran_small(ctx):
+    """the small-MSM kernels ran, or (a base set seen twice: the drop-in
+    cache's small sets) the many-MSM sum"""
     two = ctx.kernel_stats("small_table")[0] > 0 and ctx.kernel_stats("small_sum")[0] > 0
-    return two or ctx.kernel_stats("small_fused")[0] > 0
+    return two or ctx.kernel_stats("small_fused")[0] > 0 or ctx.kernel_stats("many_sum")[0] > 0
 
 
 def test_golden_vectors_both_paths(golden, gpu_ctx):
