@@ -843,12 +843,16 @@ static void dropin_make_room(pm_ctx* ctx, size_t bytes) {
 // pm_msm_resident_many (no doublings, no host Horner); first sightings and
 // sets that do not fit run the small-MSM path on the host inputs.  The keyed
 // digest of a small set is cheap (at most 1 MiB of bases).
+// up to this many points (measured, profiles/r05/small_n_cache.json: a kept
+// set against the small-MSM path 38 vs 66 us at n = 1, 63 vs 73 at 32, 82 vs
+// 93 at 512, 107 vs 106 at 1024, 174 vs 139 at 4096)
+constexpr size_t kDropinSmallMaxN = 512;
 static int dropin_small_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
                             uint32_t flags, uint64_t out[8]) {
   const CurveOps* ops = curve_ops(curve);
   auto small = [&]() { return ops->msm_small(ctx, scalars, true, bases, true, false, n, flags, out); };
   const size_t tbytes = n * pm::many_bytes_per_base(pm::many_pick_c(n));
-  if (n * 64 > (size_t(1) << 20) || tbytes > pm::kDropinSmallBytes / 2) return small();
+  if (n > kDropinSmallMaxN || tbytes > pm::kDropinSmallBytes / 2) return small();
   pm::u128 part[2];
   pm::digest_chunk(ctx->dropin_key, bases, 8 * n, part);
   uint64_t d[4];

@@ -168,8 +168,8 @@ int pm_ctx_dropin_spec_stats(pm_ctx* ctx, uint64_t* kept, uint64_t* drained);
  * and released every cached set before their one retry, *failed_builds =
  * sets left unadmitted (that call ran the plain pipeline and succeeded). */
 int pm_ctx_dropin_oom_stats(pm_ctx* ctx, uint64_t* flushes, uint64_t* failed_builds);
-/* The drop-in cache's small sets (n up to the small-MSM threshold, at most
- * 1 MiB of bases): a set seen twice is kept resident with a multiples table
+/* The drop-in cache's small sets (1 <= n <= 512, where the many-MSM path
+ * beats the small-MSM path): a set seen twice is kept resident with a multiples table
  * (pm_msm_resident_many's) and later calls with it run as one short MSM of
  * that path; at most 8 sets and 4 GiB per context, LRU; pm_ctx_dropin_clear
  * releases them too.  *hits = calls served from a kept set, *admitted = sets

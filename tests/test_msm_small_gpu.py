@@ -190,7 +190,7 @@ def test_small_set_dropin_cache(curve):
     try:
         S, B = _inputs(curve, 8192, 0x5A5 + curve)
         admitted = 0
-        for n in (1, 5, 32, 300, 4096):
+        for n in (1, 5, 32, 300, 512):
             b = np.ascontiguousarray(B[:n])
             for k in range(4):
                 s = np.ascontiguousarray(S[k:k + n])
@@ -207,6 +207,12 @@ def test_small_set_dropin_cache(curve):
         assert np.array_equal(ctx.msm(curve, s, b), msm_ref.best_multiexp(curve, s, b, threads=4))
         assert ctx.dropin_small_stats()["hits"] == 10
         assert ctx.dropin_stats()["entries"] == 0   # the large-set cache is untouched
+        # above the small-set limit: the small-MSM path, never kept
+        b = np.ascontiguousarray(B[:1000])
+        for k in range(3):
+            s = np.ascontiguousarray(S[k:k + 1000])
+            assert np.array_equal(ctx.msm(curve, s, b), msm_ref.best_multiexp(curve, s, b, threads=4))
+        assert ctx.dropin_small_stats()["admitted"] == 5
         ctx.dropin_clear()
         assert ctx.dropin_small_stats()["entries"] == 0
     finally:
