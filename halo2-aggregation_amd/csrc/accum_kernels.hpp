@@ -521,7 +521,6 @@ __global__ void __launch_bounds__(256) k_acc_powers_s(AccumHdr h, const uint32_t
                                                     const uint32_t* __restrict__ vk, uint32_t nvk,
                                                     uint4* __restrict__ pw, uint4* __restrict__ pwv) {
   using F = typename Cv::Base;
-  using K = F29Consts<F>;
   const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
   const uint32_t nprf = h.B * h.Tp;
   if (g >= nprf + nvk) return;

@@ -196,12 +196,55 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_madd_signed(const Xyzz29<F>& acc, co
   r.ZZZ = f29_mul_c<F>(acc.ZZZ, PPP);
   return r;
 }
-// The exceptional cases of xyzz29_madd_signed (r = its output for a
+// Round 5 form of the same step (k_accumulate): X kept lazy (< 9p, reduced
+// only when the bucket is stored) and the differences P = U2 - X1 and
+// D = Q - X3 left as signed limbs (|limb| < 2^29) feeding the signed-operand
+// products of fp29_asm.hpp (v_mad_i64_i32 columns), so neither is offset by
+// a multiple of p nor normalised: two normalisations, two 9-limb constant
+// adds and the reduce3 of X3 less per addition.  Bounds (p < 2^254.3,
+// R = 2^261 > 128p; tests/test_fp29_asm.py::test_lazy_bucket_addition runs
+// this sequence through the column interpreter at the extremes):
+//   X1 < 9p, Y1 < 3p, ZZ1, ZZZ1 < 2p;  P in (-9p, 2p);  R in (3p, 10p)
+//   PP = P^2 < 1.75p;  PPP = P PP in (0.86p, 2.03p] (2 pR added);  Q < 1.14p
+//   X3 = R^2 + 8p - PPP - 2Q in (3.7p, 8.92p);  D in (-8.92p, 1.14p)
+//   Y3 = R D - Y1 PPP in (0.25p, 2.1p];  ZZ3, ZZZ3 < 2p.
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_madd_lazy(const Xyzz29<F>& acc, const F29<F>& x2, const F29<F>& y2,
+                                                      uint32_t negm) {
+  using K = F29Consts<F>;
+  const F29<F> U2 = f29_mul_c<F>(x2, acc.ZZ);   // < 2p
+  const F29<F> S2 = f29_mul_c<F>(y2, acc.ZZZ);  // < 2p
+  F29<F> P, R, D;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    P.l[i] = U2.l[i] - acc.X.l[i];
+    R.l[i] = K::K8x3[i] + ((S2.l[i] ^ negm) - negm) - acc.Y.l[i];
+  }
+  R = f29_norm<F>(R);
+  const F29<F> PP = f29_sqr_sa_a<F>(P);
+  const F29<F> PPP = f29_mul_sa_a<F>(P, PP);
+  const F29<F> Q = f29_mul_c<F>(acc.X, PP);
+  Xyzz29<F> r;
+  r.X = f29_norm<F>(f29_sub<F>(f29_sqr_c<F>(R), f29_add<F>(PPP, f29_add<F>(Q, Q)), K::K8x3));
+#pragma unroll
+  for (int i = 0; i < 9; i++) D.l[i] = Q.l[i] - r.X.l[i];
+  r.Y = f29_mul2n_sb_a<F>(R, D, acc.Y, PPP);
+  r.ZZ = f29_mul_c<F>(acc.ZZ, PP);
+  r.ZZZ = f29_mul_c<F>(acc.ZZZ, PPP);
+  return r;
+}
+// the stored form of a lazy accumulator (X < 3p, as every bucket consumer expects)
+template <class F>
+__device__ __forceinline__ Xyzz29<F> xyzz29_settle(const Xyzz29<F>& a) {
+  return Xyzz29<F>{f29_reduce3<F>(a.X), a.Y, a.ZZ, a.ZZZ};
+}
+
+// The exceptional cases of xyzz29_madd_signed / _lazy (r = its output for a
 // non-empty acc).  Returns true when the sum is O.
 template <class F>
 __device__ __forceinline__ bool xyzz29_madd_fix(Xyzz29<F>& r, const F29<F>& x2, const F29<F>& y2, uint32_t negm) {
   if (!f29_is_zero_mod<F>(r.ZZ)) return false;
-  if (!f29_is_zero_mod<F>(r.X)) {
+  if (!f29_is_zero_mod<F>(f29_reduce3<F>(r.X))) {  // lazy X3 < 9p
     r.ZZ = f29_zero<F>();
     return true;
   }

@@ -701,7 +701,7 @@ __global__ void __launch_bounds__(256, PM_ACC_WAVES) k_accumulate(const uint32_t
       // the next bucket's end is loaded before the store, so its use waits
       // for the load only (vmcnt counts stores too)
       const uint32_t nb = offsets[gb + 2];
-      store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc);
+      store_xyzz29<F>(owned ? &buckets[gb] : &head[t], xyzz29_settle<F>(acc));
       fresh = true;
       acc.ZZ = f29_zero<F>();
       gb++;
@@ -724,7 +724,7 @@ __global__ void __launch_bounds__(256, PM_ACC_WAVES) k_accumulate(const uint32_t
     // identity base (0, 0): y = 0 holds for no point of odd order
     if (f29_is_zero_exact<F>(y)) continue;
     const uint32_t negm = 0u - (ccode >> 31);  // kNegBit
-    Xyzz29<F> r = xyzz29_madd_signed<F>(acc, x, y, negm);
+    Xyzz29<F> r = xyzz29_madd_lazy<F>(acc, x, y, negm);
     // ZZ3 = 0 mod p only when acc = +-point: the filter almost never hits,
     // and the wave-uniform branch keeps the exact check off the hot path
     const bool hit = !fresh && f29_zero_filter<F>(r.ZZ);
@@ -740,7 +740,7 @@ __global__ void __launch_bounds__(256, PM_ACC_WAVES) k_accumulate(const uint32_t
     }
     acc = r;
   }
-  store_xyzz29<F>(owned ? &buckets[gb] : &head[t], acc);
+  store_xyzz29<F>(owned ? &buckets[gb] : &head[t], xyzz29_settle<F>(acc));
 }
 
 // Base conversion (once per MSM): Rust-layout R = 2^256 Montgomery -> the

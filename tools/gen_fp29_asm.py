@@ -78,41 +78,47 @@ def opnd(ins, c, e):
     return "%%%d" % (len(ins) + 1)
 
 
-def statement(k, sq, P):
-    """asm text and input list of statement k (acc is %0, the carry sink %1)."""
+def statement(k, sq, P, sa=False, kp=None):
+    """asm text and input list of statement k (acc is %0, the carry sink %1).
+    sa: the operand a has signed limbs (two's complement, |a_i| < 2^29): its
+    products are v_mad_i64_i32 and the columns signed (arithmetic carries);
+    kp: the multiple of p R added to the result (default: 1 subtractive, 0
+    additive)."""
     ins, body = [], []
     sub = P[0] == 1
+    if kp is None:
+        kp = 1 if sub else 0
 
     def mad(x, y):
         body.append("v_mad_u64_u32 %%0, %%1, %s, %s, %%0" % (x, y))
+
+    def omad(x, y):  # operand product: signed when a is
+        body.append("v_mad_%s %%0, %%1, %s, %s, %%0" % ("i64_i32" if sa else "u64_u32", x, y))
 
     if k >= 10:
         # dummy input: orders the C extraction of the previous output limb
         # before this statement (else the compiler copies acc with v_mov_b64)
         opnd(ins, "v", "r.l[%d]" % (k - 10))
     if k > 0:
-        if sub:
-            body.append("v_ashrrev_i64 %0, 29, %0")
-            if k >= 9:
-                pr_add(body, ins, k, P, 1)  # + p R
-        else:
-            if k - 1 < 9:
-                mad(opnd(ins, "v", "m[%d]" % (k - 1)), const(ins, P[0]))
-            body.append("v_lshrrev_b64 %0, 29, %0")
+        if not sub and k - 1 < 9:
+            mad(opnd(ins, "v", "m[%d]" % (k - 1)), const(ins, P[0]))
+        body.append("v_ashrrev_i64 %0, 29, %0" if sub or sa else "v_lshrrev_b64 %0, 29, %0")
+        if kp and k >= 9:
+            pr_add(body, ins, k, P, kp)  # + kp p R
     if k < 17:
         if not sq:
             for i in range(9):
                 j = k - i
                 if 0 <= j < 9:
-                    mad(opnd(ins, "v", "a.l[%d]" % i), opnd(ins, "v", "b.l[%d]" % j))
+                    omad(opnd(ins, "v", "a.l[%d]" % i), opnd(ins, "v", "b.l[%d]" % j))
         else:
             for i in range(9):
                 j = k - i
                 if i < j < 9:
-                    mad(opnd(ins, "v", "d[%d]" % i), opnd(ins, "v", "a.l[%d]" % j))
+                    omad(opnd(ins, "v", "d[%d]" % i), opnd(ins, "v", "a.l[%d]" % j))
             if k % 2 == 0 and k // 2 < 9:
                 x = opnd(ins, "v", "a.l[%d]" % (k // 2))
-                mad(x, x)
+                omad(x, x)
         for i in range(9):
             j = k - i
             if i < k and 1 <= j < 9 and P[j] != 0:
@@ -124,7 +130,7 @@ def statement(k, sq, P):
     return body, ins
 
 
-def statement2(k, P, neg=False):
+def statement2(k, P, neg=False, sb=False):
     """f29_mul2_a, column k: statement A = carry-in + the a b terms, statement B
     = the u v terms + the reduction terms (one statement would exceed the
     inline-asm operand limit).
@@ -137,7 +143,7 @@ def statement2(k, P, neg=False):
     routines use (u v < 6 p^2 < R p / 16)."""
     insA, bodyA, insB, bodyB = [], [], [], []
     sub = P[0] == 1
-    signed = sub or neg
+    signed = sub or neg or sb
     kp = (2 if sub else 1) if neg else (1 if sub else 0)  # multiple of p R added
 
     def mad(body, x, y):
@@ -155,7 +161,11 @@ def statement2(k, P, neg=False):
         for i in range(9):
             j = k - i
             if 0 <= j < 9:
-                mad(bodyA, opnd(insA, "v", "a.l[%d]" % i), opnd(insA, "v", "b.l[%d]" % j))
+                if sb:  # b signed (f29_mul2n_sb_a)
+                    bodyA.append("v_mad_i64_i32 %%0, %%1, %s, %s, %%0" % (opnd(insA, "v", "a.l[%d]" % i),
+                                                                          opnd(insA, "v", "b.l[%d]" % j)))
+                else:
+                    mad(bodyA, opnd(insA, "v", "a.l[%d]" % i), opnd(insA, "v", "b.l[%d]" % j))
                 if neg:
                     bodyB.append("v_mad_i64_i32 %%0, %%1, %s, %s, %%0" % (opnd(insB, "v", "u.l[%d]" % i),
                                                                           opnd(insB, "v", "nv[%d]" % j)))
@@ -172,15 +182,16 @@ def statement2(k, P, neg=False):
     return [(bodyA, insA), (bodyB, insB)]
 
 
-def gen_fn2(field, neg=False):
+def gen_fn2(field, neg=False, sb=False):
     """(a b + u v) 2^-261 mod p with ONE Montgomery reduction (sum of products);
-    neg: (a b - u v) 2^-261 (f29_mul2n_a)."""
+    neg: (a b - u v) 2^-261 (f29_mul2n_a); sb: b with signed limbs
+    (f29_mul2n_sb_a, neg only)."""
     p = FIELDS[field]
     P = limbs(p)
     inv = (-pow(p, -1, 1 << 29)) % (1 << 29)
     sub = P[0] == 1
     kp = (2 if sub else 1) if neg else (1 if sub else 0)
-    name = "f29_mul2n_a" if neg else "f29_mul2_a"
+    name = "f29_mul2n_sb_a" if sb else "f29_mul2n_a" if neg else "f29_mul2_a"
     L = []
     L.append("template <>\n__device__ __forceinline__ F29<%s> %s<%s>(const F29<%s>& a, const F29<%s>& b, "
              "const F29<%s>& u, const F29<%s>& v) {" % (field, name, field, field, field, field, field))
@@ -188,7 +199,7 @@ def gen_fn2(field, neg=False):
     if neg:
         L.append("  uint32_t nv[9];\n#pragma unroll\n  for (int i = 0; i < 9; i++) nv[i] = 0u - v.l[i];")
     for k in range(17):
-        for body, ins in statement2(k, P, neg):
+        for body, ins in statement2(k, P, neg, sb):
             if not body:
                 continue
             text = "\\n\\t".join(body)
@@ -210,10 +221,14 @@ def gen_fn2(field, neg=False):
     return "\n".join(L)
 
 
-def gen_fn(name, field, sq):
+def gen_fn(name, field, sq, sa=False):
+    """sa: a with signed limbs; the product then gets p R more (subtractive 2,
+    additive 1) unless it is a square (never negative)."""
     p = FIELDS[field]
     P = limbs(p)
     inv = (-pow(p, -1, 1 << 29)) % (1 << 29)
+    sub = P[0] == 1
+    kp = (1 if sub else 0) + (1 if sa and not sq else 0)
     L = []
     args = "const F29<%s>& a" % field + ("" if sq else ", const F29<%s>& b" % field)
     L.append("template <>\n__device__ __forceinline__ F29<%s> %s<%s>(%s) {" % (field, name, field, args))
@@ -221,7 +236,7 @@ def gen_fn(name, field, sq):
     if sq:
         L.append("  uint32_t d[8];\n#pragma unroll\n  for (int i = 0; i < 8; i++) d[i] = a.l[i] << 1;")
     for k in range(17):
-        body, ins = statement(k, sq, P)
+        body, ins = statement(k, sq, P, sa, kp)
         text = "\\n\\t".join(body)
         L.append('  asm("%s"\n      : "+v"(acc), "=&s"(c)\n      : %s);'
                  % (text, ", ".join('"%s"(%s)' % ce for ce in ins)))
@@ -234,8 +249,8 @@ def gen_fn(name, field, sq):
                 L.append("  m[%d] = ((uint32_t)acc * %du) & kM29;" % (k, inv))
         else:
             L.append("  r.l[%d] = (uint32_t)acc & kM29;" % (k - 9))
-    if P[0] == 1:
-        L.append("  r.l[8] = (uint32_t)((int64_t)acc >> 29) + %du;\n  (void)c;\n  return r;\n}\n" % P[8])
+    if sub or sa:
+        L.append("  r.l[8] = (uint32_t)((int64_t)acc >> 29) + %du;\n  (void)c;\n  return r;\n}\n" % (kp * P[8]))
     else:
         L.append("  r.l[8] = (uint32_t)(acc >> 29);\n  (void)c;\n  return r;\n}\n")
     return "\n".join(L)
@@ -250,12 +265,20 @@ def main():
            "template <class P>\n__device__ F29<P> f29_mul2_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, "
            "const F29<P>& v);",
            "template <class P>\n__device__ F29<P> f29_mul2n_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, "
+           "const F29<P>& v);",
+           "template <class P>\n__device__ F29<P> f29_mul_sa_a(const F29<P>& a, const F29<P>& b);",
+           "template <class P>\n__device__ F29<P> f29_sqr_sa_a(const F29<P>& a);",
+           "template <class P>\n__device__ F29<P> f29_mul2n_sb_a(const F29<P>& a, const F29<P>& b, const F29<P>& u, "
            "const F29<P>& v);", ""]
     for f in FIELDS:
         out.append(gen_fn("f29_mul_a", f, False))
         out.append(gen_fn("f29_sqr_a", f, True))
         out.append(gen_fn2(f))
         out.append(gen_fn2(f, neg=True))
+    for f in ("PallasFp", "VestaFp", "Bn254Fq"):  # the MSM base fields (k_accumulate)
+        out.append(gen_fn("f29_mul_sa_a", f, False, sa=True))
+        out.append(gen_fn("f29_sqr_sa_a", f, True, sa=True))
+        out.append(gen_fn2(f, neg=True, sb=True))
     out.append("}  // namespace pm")
     print("\n".join(out))
 
