@@ -1,5 +1,6 @@
 // Host build of csrc/inv_bgcd.hpp for tests/test_inv_bgcd.py: reads lines
-// "<field> <y as 64 hex digits, big endian>" and prints bg_inverse(y) and
+// "<field> <y as 64 hex digits, big endian>" and prints bg_inverse(y),
+// sg_inverse(y) (safegcd) and
 // fe_inv_bgcd(y) (y read as a Montgomery element) as 64 hex digits each,
 // plus fe_inv(y) (Fermat) for the Montgomery form, and fe_redc(y) = y R^-1.
 #include <cstdio>
@@ -24,9 +25,12 @@ static void emit(const uint32_t w[8]) {
 
 template <class P>
 static void run(const uint32_t y[8]) {
-  uint32_t r[8];
+  uint32_t r[8], r2[8];
   bg_inverse<P>(y, r);
+  sg_inverse<P>(y, r2);
   emit(r);
+  printf(" ");
+  emit(r2);
   printf(" ");
   Fe<P> a;
   for (int i = 0; i < 8; i++) a.l[i] = y[i];

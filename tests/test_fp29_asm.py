@@ -43,14 +43,17 @@ def _run(body, a, b=None, u=None, v=None):
             return env[mm.group(1)][int(mm.group(2))]
         return int(expr.rstrip("ul"))
 
-    stmts = re.findall(r'asm\("(.*?)"\s*:\s*"\+v"\(acc\), "=&s"\(c\)\s*:\s*(.*?)\);|^  (?!asm)([^\n]*?);$', body, re.S | re.M)
+    stmts = re.findall(r'asm\("(.*?)"\s*:\s*"(?:\+|=&)v"\(acc\), "=&s"\(c\)\s*:\s*(.*?)\);|^  (?!asm)([^\n]*?);$', body,
+                       re.S | re.M)
     for text, ins, cline in stmts:
         if text:
             ops = [val(x.split("(", 1)[1][:-1]) for x in re.findall(r'"[vs]"\([^)]*\)', ins)]
             for ins_text in text.split("\\n\\t"):
                 f = [x.strip() for x in ins_text.replace(",", " ").split()]
                 if f[0] in ("v_mad_u64_u32", "v_mad_i64_i32"):
-                    assert f[1] == "%0" and f[2] == "%1" and f[5] == "%0"
+                    assert f[1] == "%0" and f[2] == "%1" and f[5] in ("%0", "0")
+                    if f[5] == "0":  # a product's first multiply-add: acc starts from 0
+                        acc = 0
                     x = ops[int(f[3][1:]) - 2] if f[3].startswith("%") else int(f[3])
                     y = ops[int(f[4][1:]) - 2] if f[4].startswith("%") else int(f[4])
                     if f[0] == "v_mad_i64_i32":  # signed 32 x 32 + signed 64
@@ -98,7 +101,7 @@ def _run(body, a, b=None, u=None, v=None):
             top = (acc >> 29) + int(re.search(r"\+ (\d+)u", c).group(1))
             assert 0 <= top < 2 ** 32
             env["r.l"][8] = top
-        elif not re.fullmatch(r"F29<\w+> r|uint32_t (m|d|nv)\[\d\]|uint64_t acc = 0, c|\(void\)c|return r", c):
+        elif not re.fullmatch(r"F29<\w+> r|uint32_t (m|d|nv)\[\d\]|uint64_t acc, c|\(void\)c|return r", c):
             raise AssertionError("unhandled line: " + c)
     return env["r.l"]
 

@@ -1,5 +1,6 @@
-"""CPU: csrc/inv_bgcd.hpp (Pornin's optimized binary GCD, used by the
-latency-bound device kernels in place of Fermat inversions) built for the host
+"""CPU: csrc/inv_bgcd.hpp (Pornin's optimized binary GCD and the
+variable-time safegcd, used by the latency-bound device kernels in place of
+Fermat inversions) built for the host
 with g++ and checked against Python's pow(y, -1, p) and the library's Fermat
 fe_inv, on random and edge inputs for all four fields."""
 import os
@@ -40,8 +41,9 @@ def test_inverse_matches_python(exe):
     rows = out.split("\n")[:-1]
     assert len(rows) == len(want)
     for line, row, (inv, inv_m) in zip(lines, rows, want):
-        got, got_m, fermat, redc = (int(x, 16) for x in row.split())
+        got, got_sg, got_m, fermat, redc = (int(x, 16) for x in row.split())
         assert got == inv, line
+        assert got_sg == inv, line  # safegcd (sg_inverse)
         assert got_m == inv_m == fermat, line
         f, y = line.split()
         p = FIELDS[f]

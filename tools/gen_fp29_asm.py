@@ -182,6 +182,17 @@ def statement2(k, P, neg=False, sb=False):
     return [(bodyA, insA), (bodyB, insB)]
 
 
+def asm_stmt(body, ins, first):
+    """One inline-asm statement.  The product's first multiply-add starts the
+    accumulator from the inline constant 0 (acc an early-clobber output), so
+    no v_mov_b64 zeroes it."""
+    if first:
+        assert body[0].endswith(", %0")
+        body = [body[0][:-len("%0")] + "0"] + body[1:]
+    return '  asm("%s"\n      : "%s"(acc), "=&s"(c)\n      : %s);' % (
+        "\\n\\t".join(body), "=&v" if first else "+v", ", ".join('"%s"(%s)' % ce for ce in ins))
+
+
 def gen_fn2(field, neg=False, sb=False):
     """(a b + u v) 2^-261 mod p with ONE Montgomery reduction (sum of products);
     neg: (a b - u v) 2^-261 (f29_mul2n_a); sb: b with signed limbs
@@ -195,16 +206,16 @@ def gen_fn2(field, neg=False, sb=False):
     L = []
     L.append("template <>\n__device__ __forceinline__ F29<%s> %s<%s>(const F29<%s>& a, const F29<%s>& b, "
              "const F29<%s>& u, const F29<%s>& v) {" % (field, name, field, field, field, field, field))
-    L.append("  F29<%s> r;\n  uint32_t m[9];\n  uint64_t acc = 0, c;" % field)
+    L.append("  F29<%s> r;\n  uint32_t m[9];\n  uint64_t acc, c;" % field)
     if neg:
         L.append("  uint32_t nv[9];\n#pragma unroll\n  for (int i = 0; i < 9; i++) nv[i] = 0u - v.l[i];")
+    first = True
     for k in range(17):
         for body, ins in statement2(k, P, neg, sb):
             if not body:
                 continue
-            text = "\\n\\t".join(body)
-            L.append('  asm("%s"\n      : "+v"(acc), "=&s"(c)\n      : %s);'
-                     % (text, ", ".join('"%s"(%s)' % ce for ce in ins)))
+            L.append(asm_stmt(body, ins, first))
+            first = False
         if k < 9:
             if P[0] == 1:
                 L.append("  m[%d] = (uint32_t)acc & kM29;" % k)
@@ -232,14 +243,12 @@ def gen_fn(name, field, sq, sa=False):
     L = []
     args = "const F29<%s>& a" % field + ("" if sq else ", const F29<%s>& b" % field)
     L.append("template <>\n__device__ __forceinline__ F29<%s> %s<%s>(%s) {" % (field, name, field, args))
-    L.append("  F29<%s> r;\n  uint32_t m[9];\n  uint64_t acc = 0, c;" % field)
+    L.append("  F29<%s> r;\n  uint32_t m[9];\n  uint64_t acc, c;" % field)
     if sq:
         L.append("  uint32_t d[8];\n#pragma unroll\n  for (int i = 0; i < 8; i++) d[i] = a.l[i] << 1;")
     for k in range(17):
         body, ins = statement(k, sq, P, sa, kp)
-        text = "\\n\\t".join(body)
-        L.append('  asm("%s"\n      : "+v"(acc), "=&s"(c)\n      : %s);'
-                 % (text, ", ".join('"%s"(%s)' % ce for ce in ins)))
+        L.append(asm_stmt(body, ins, k == 0))
         if k < 9:
             if P[0] == 1:
                 L.append("  m[%d] = (uint32_t)acc & kM29;" % k)

@@ -53,23 +53,82 @@ __global__ void __launch_bounds__(64) k_lane(uint32_t* out, uint64_t* clk, int i
   if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
 }
 
-// inversion latency: one lane per input (bg_inverse on the VALU), or one
+// inversion latency: one lane per input (bg_inverse on the VALU), one
 // wave per input with wave-uniform operands (the compiler keeps the whole
-// binary GCD on the scalar unit)
-template <class F, bool W>
+// binary GCD on the scalar unit), or one lane per input with the
+// variable-time safegcd (sg_inverse; lanes of a wave run the longest lane's
+// loop counts)
+template <class F, bool W, bool SG = false>
 __global__ void __launch_bounds__(64) k_inv(const uint32_t* in, uint32_t* out, uint64_t* clk, int reps) {
   const uint32_t id = W ? blockIdx.x : blockIdx.x * 64 + threadIdx.x;
   uint32_t y[8], o[8];
   for (int i = 0; i < 8; i++) y[i] = W ? __builtin_amdgcn_readfirstlane(in[id * 8 + i]) : in[id * 8 + i];
   const uint64_t t0 = wall_clock64();
   for (int r = 0; r < reps; r++) {
-    bg_inverse<F>(y, o);
+    if (SG) sg_inverse<F>(y, o);
+    else bg_inverse<F>(y, o);
     for (int i = 0; i < 8; i++) y[i] = o[i];
   }
   const uint64_t t1 = wall_clock64() + (o[0] & 0u);
   if (!W || threadIdx.x == 0)
     for (int i = 0; i < 8; i++) out[id * 8 + i] = o[i];
   if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
+}
+
+// quad-cooperative forms: the 4 lanes of a quad invert the same input
+template <class F, bool SG>
+__global__ void __launch_bounds__(64) k_invq(const uint32_t* in, uint32_t* out, uint64_t* clk, int reps) {
+  const uint32_t id = blockIdx.x * 16 + (threadIdx.x >> 2);
+  uint32_t y[8], o[8];
+  for (int i = 0; i < 8; i++) y[i] = in[id * 8 + i];
+  const uint64_t t0 = wall_clock64();
+  for (int r = 0; r < reps; r++) {
+    if (SG) sg_inverse_q<F>(y, o);
+    else bg_inverse_q<F>(y, o);
+    for (int i = 0; i < 8; i++) y[i] = o[i];
+  }
+  const uint64_t t1 = wall_clock64() + (o[0] & 0u);
+  if ((threadIdx.x & 3) == 0)
+    for (int i = 0; i < 8; i++) out[id * 8 + i] = o[i];
+  if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
+}
+
+template <class F>
+void run_invq(const char* name) {
+  const int n = 256, reps = 20;
+  std::vector<uint32_t> h(n * 8);
+  uint64_t s = 0x243F6A8885A308D3ull;
+  for (auto& w : h) {
+    s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+    w = (uint32_t)s;
+  }
+  for (int i = 0; i < n; i++) h[i * 8 + 7] &= 0x0fffffff;
+  uint32_t *d_in, *d_a, *d_b;
+  uint64_t *c_a, *c_b;
+  (void)hipMalloc(&d_in, n * 32);
+  (void)hipMalloc(&d_a, n * 32);
+  (void)hipMalloc(&d_b, n * 32);
+  (void)hipMalloc(&c_a, n * 8);
+  (void)hipMalloc(&c_b, n * 8);
+  (void)hipMemcpy(d_in, h.data(), n * 32, hipMemcpyHostToDevice);
+  for (int rep = 0; rep < 2; rep++) {
+    k_invq<F, false><<<n / 16, 64>>>(d_in, d_a, c_a, reps);
+    k_invq<F, true><<<n / 16, 64>>>(d_in, d_b, c_b, reps);
+  }
+  (void)hipDeviceSynchronize();
+  std::vector<uint32_t> a(n * 8), b(n * 8);
+  std::vector<uint64_t> ca(n / 16), cb(n / 16);
+  (void)hipMemcpy(a.data(), d_a, n * 32, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(b.data(), d_b, n * 32, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(ca.data(), c_a, ca.size() * 8, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(cb.data(), c_b, cb.size() * 8, hipMemcpyDeviceToHost);
+  int bad = 0;
+  for (int i = 0; i < n * 8; i++) bad += a[i] != b[i];
+  double sa = 0, sb = 0;
+  for (auto v : ca) sa += v;
+  for (auto v : cb) sb += v;
+  printf("{\"field\": \"%s\", \"inv_quad_bgcd_us\": %.3f, \"inv_quad_safegcd_us\": %.3f, \"mismatches\": %d}\n", name,
+         sa / ca.size() * 0.01 / reps, sb / cb.size() * 0.01 / reps, bad);
 }
 
 template <class F>
@@ -82,32 +141,42 @@ void run_inv(const char* name) {
     w = (uint32_t)s;
   }
   for (int i = 0; i < n; i++) h[i * 8 + 7] &= 0x0fffffff;  // < 2^252 < p
-  uint32_t *d_in, *d_a, *d_b;
-  uint64_t *c_a, *c_b;
+  uint32_t *d_in, *d_a, *d_b, *d_c;
+  uint64_t *c_a, *c_b, *c_c;
   hipMalloc(&d_in, n * 32);
   hipMalloc(&d_a, n * 32);
   hipMalloc(&d_b, n * 32);
+  hipMalloc(&d_c, n * 32);
   hipMalloc(&c_a, n * 8);
   hipMalloc(&c_b, n * 8);
+  hipMalloc(&c_c, n * 8);
   hipMemcpy(d_in, h.data(), n * 32, hipMemcpyHostToDevice);
   for (int rep = 0; rep < 2; rep++) {
     k_inv<F, false><<<n / 64, 64>>>(d_in, d_a, c_a, reps);
     k_inv<F, true><<<n, 64>>>(d_in, d_b, c_b, reps);
+    k_inv<F, false, true><<<n / 64, 64>>>(d_in, d_c, c_c, reps);
   }
   hipDeviceSynchronize();
-  std::vector<uint32_t> a(n * 8), b(n * 8);
-  std::vector<uint64_t> ca(n / 64), cb(n);
+  std::vector<uint32_t> a(n * 8), b(n * 8), c(n * 8);
+  std::vector<uint64_t> ca(n / 64), cb(n), cc(n / 64);
   hipMemcpy(a.data(), d_a, n * 32, hipMemcpyDeviceToHost);
   hipMemcpy(b.data(), d_b, n * 32, hipMemcpyDeviceToHost);
+  hipMemcpy(c.data(), d_c, n * 32, hipMemcpyDeviceToHost);
   hipMemcpy(ca.data(), c_a, ca.size() * 8, hipMemcpyDeviceToHost);
   hipMemcpy(cb.data(), c_b, cb.size() * 8, hipMemcpyDeviceToHost);
-  int bad = 0;
-  for (int i = 0; i < n * 8; i++) bad += a[i] != b[i];
-  double sa = 0, sb = 0;
+  hipMemcpy(cc.data(), c_c, cc.size() * 8, hipMemcpyDeviceToHost);
+  int bad = 0, bad_sg = 0;
+  for (int i = 0; i < n * 8; i++) {
+    bad += a[i] != b[i];
+    bad_sg += a[i] != c[i];
+  }
+  double sa = 0, sb = 0, sc = 0;
   for (auto v : ca) sa += v;
   for (auto v : cb) sb += v;
-  printf("{\"field\": \"%s\", \"inv_lane_us\": %.3f, \"inv_wave_scalar_us\": %.3f, \"mismatches\": %d}\n", name,
-         sa / ca.size() * 0.01 / reps, sb / cb.size() * 0.01 / reps, bad);
+  for (auto v : cc) sc += v;
+  printf("{\"field\": \"%s\", \"inv_lane_us\": %.3f, \"inv_wave_scalar_us\": %.3f, \"inv_safegcd_lane_us\": %.3f, "
+         "\"mismatches\": %d, \"safegcd_mismatches\": %d}\n",
+         name, sa / ca.size() * 0.01 / reps, sb / cb.size() * 0.01 / reps, sc / cc.size() * 0.01 / reps, bad, bad_sg);
 }
 
 template <class F>
@@ -152,5 +221,7 @@ int main() {
   run<PallasFp>("pallas_fp");
   run_inv<Bn254Fq>("bn254_fq");
   run_inv<PallasFp>("pallas_fp");
+  run_invq<Bn254Fq>("bn254_fq");
+  run_invq<PallasFp>("pallas_fp");
   return 0;
 }
