@@ -223,13 +223,28 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     acc = fe_mul<Fs>(acc, omega_inv);
   }
   h.c_n = (uint32_t)(cst.size() / 8);
+  Fe<Fs> nmont;
   {
     Fe<Fs> nf = fe_zero<Fs>();
     const uint64_t nn = 1ull << s->log_n;
     nf.l[0] = (uint32_t)nn;
     nf.l[1] = (uint32_t)(nn >> 32);
-    push_fe<Fs>(cst, fe_to_mont<Fs>(nf));
+    nmont = fe_to_mont<Fs>(nf);
+    push_fe<Fs>(cst, nmont);
   }
+  // R = 2^261 copies (x 2^5 of the R = 2^256 integers, canonical)
+  auto r261 = [](Fe<Fs> a) {
+    for (int k = 0; k < 5; k++) a = fe_add<Fs>(a, a);
+    return a;
+  };
+  h.c_wpow29 = (uint32_t)(cst.size() / 8);
+  acc = fe_one<Fs>();
+  for (uint32_t i = 0; i < s->blinding_factors + 2; i++) {
+    push_fe<Fs>(cst, r261(acc));
+    acc = fe_mul<Fs>(acc, omega_inv);
+  }
+  h.c_n29 = (uint32_t)(cst.size() / 8);
+  push_fe<Fs>(cst, r261(nmont));
   // --- VK points: fixed commitments, sigma commitments, g1
   std::vector<uint64_t> vk;
   for (uint32_t i = 0; i < s->num_fixed_columns; i++) vk.insert(vk.end(), s->fixed_commitments + 8 * i, s->fixed_commitments + 8 * i + 8);

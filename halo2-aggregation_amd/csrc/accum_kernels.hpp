@@ -40,6 +40,9 @@ struct AccumHdr {
   uint32_t h_slot0, nh;
   // constant table (8 u32 per element, Montgomery)
   uint32_t c_user, c_delta, c_omega_eval, c_wpow, c_n;
+  // the same w^i (i < bf + 2) and n as canonical R = 2^261 integers, packed
+  // (k_acc_scalars' Lagrange chain runs in the radix-2^29 form)
+  uint32_t c_wpow29, c_n29;
   // powers-of-two tables (split path): Tp proof-point terms; p_psrc: their
   // point indices in slot order (Tp words); p_rank: T words, term t's rank
   // among the proof-point terms (VK terms read the per-VK tables instead)
@@ -180,42 +183,61 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   Fe<Fs> l_0 = zero, l_last = zero, omb = zero, inv_xn1 = zero;
 
   if (live && role == 0) {
+    // The long chain of the kernel, in the radix-2^29 lazy form (one-lane
+    // products 0.38-0.46 us against 0.70 us for Fe; round 5).  Values stay
+    // Norm, < 4p; LDS rows hold them packed (< 2^256).
+    using K29 = F29Consts<Fs>;
+    auto put29 = [&](uint32_t row, const F29<Fs>& v) {
+      Fe<Fs> w;
+      f29_pack<Fs>(v, w.l);
+      wk.put<Fs>(row, w);
+    };
+    auto get29 = [&](uint32_t row) { return f29_unpack<Fs>(wk.get<Fs>(row).l); };
+    auto ld29 = [&](uint32_t idx) { return f29_unpack<Fs>(ldfe<Fs>(consts, idx).l); };  // canonical R261
     // x^n (verifier.rs:513-516)
-    Fe<Fs> xn = x;
-    for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
-    const Fe<Fs> xn1 = fe_sub<Fs>(xn, one);
+    const F29<Fs> x29 = f29_from_r256<Fs>(x.l);  // < 2p
+    F29<Fs> xn = x29;
+    for (uint32_t i = 0; i < h.log_n; i++) xn = f29_sqr_c<Fs>(xn);
+    const F29<Fs> one29 = f29_const<Fs>(K29::ONE);
+    const F29<Fs> xn1 = f29_reduce3<Fs>(f29_norm<Fs>(f29_sub<Fs>(xn, one29, K29::K2)));  // < 3p
     // l_i = w^i (x^n - 1) / (n (x - w^i)), w = omega^-1, i < bf + 2, plus
     // 1 / (x^n - 1) for h_eval: one batched inversion (Montgomery's trick).
     // rows: den_i at wk[i], prefix products at wk[K + i]
     const uint32_t K = h.bf + 3;
-    const Fe<Fs> nfe = ldfe<Fs>(consts, h.c_n);
-    Fe<Fs> pre = zero;
+    const F29<Fs> nfe = ld29(h.c_n29);
+    F29<Fs> pre = xn1;
     for (uint32_t i = 0; i < K; i++) {
-      const Fe<Fs> den = i + 1 < K ? fe_mul<Fs>(nfe, fe_sub<Fs>(x, ldfe<Fs>(consts, h.c_wpow + i))) : xn1;
-      pre = i ? fe_mul<Fs>(pre, den) : den;
-      wk.put<Fs>(i, den);
-      wk.put<Fs>(K + i, pre);
+      const F29<Fs> den =
+          i + 1 < K ? f29_mul_c<Fs>(nfe, f29_norm<Fs>(f29_sub<Fs>(x29, ld29(h.c_wpow29 + i), K29::K2))) : xn1;
+      pre = i ? f29_mul_c<Fs>(pre, den) : den;  // < 2p (< 3p for i = 0 = K - 1)
+      put29(i, den);
+      put29(K + i, pre);
     }
     // a zero denominator (x^n = 1, or x = omega^-i for a Lagrange basis
     // point) is where the reference's main_gate.div fails (vanishing.rs:175,
     // verifier.rs:580): flag the proof; its outputs are then unspecified
-    if (status && fe_is_zero<Fs>(fe_from_mont<Fs>(pre))) status[b] |= kAccStatusDenomZero;
-    Fe<Fs> inv = fe_inv_fast<Fs>(pre);
+    if (status && f29_is_zero_mod<Fs>(pre)) status[b] |= kAccStatusDenomZero;
+    F29<Fs> inv = f29_inv<Fs>(pre);  // variable-time safegcd, < 2p
     for (uint32_t i = K - 1; i > 0; i--) {
-      const Fe<Fs> t = fe_mul<Fs>(inv, wk.get<Fs>(K + i - 1));
-      inv = fe_mul<Fs>(inv, wk.get<Fs>(i));
-      wk.put<Fs>(i, t);  // now 1 / den_i
+      const F29<Fs> t = f29_mul_c<Fs>(inv, get29(K + i - 1));
+      inv = f29_mul_c<Fs>(inv, get29(i));
+      put29(i, t);  // now 1 / den_i
     }
-    wk.put<Fs>(0, inv);
-    Fe<Fs> l_blind = zero;
+    put29(0, inv);
+    F29<Fs> l0 = f29_zero<Fs>(), llast = l0, lblind = l0;
     for (uint32_t i = 0; i + 1 < K; i++) {
-      const Fe<Fs> li = fe_mul<Fs>(fe_mul<Fs>(ldfe<Fs>(consts, h.c_wpow + i), xn1), wk.get<Fs>(i));
-      if (i == 0) l_0 = li;
-      else if (i == h.bf + 1) l_last = li;
-      else l_blind = fe_add<Fs>(l_blind, li);
+      const F29<Fs> li = f29_mul_c<Fs>(f29_mul_c<Fs>(ld29(h.c_wpow29 + i), xn1), get29(i));  // < 2p
+      if (i == 0) l0 = li;
+      else if (i == h.bf + 1) llast = li;
+      else lblind = f29_reduce3<Fs>(f29_norm<Fs>(f29_add<Fs>(lblind, li)));  // < 3p
     }
-    inv_xn1 = wk.get<Fs>(K - 1);
-    omb = fe_sub<Fs>(one, fe_add<Fs>(l_last, l_blind));  // 1 - (l_last + l_blind)
+    // back to the Fe form of the fold below: l_0, l_last, 1 - (l_last + l_blind), 1 / (x^n - 1)
+    const F29<Fs> s = f29_reduce3<Fs>(f29_norm<Fs>(f29_add<Fs>(llast, lblind)));  // < 3p
+    const F29<Fs> o = f29_norm<Fs>(f29_sub<Fs>(one29, s, K29::K6));                   // < 7p
+    f29_to_r256<Fs>(l0, l_0.l);
+    f29_to_r256<Fs>(llast, l_last.l);
+    f29_to_r256<Fs>(f29_reduce3<Fs>(o), omb.l);
+    f29_to_r256<Fs>(get29(K - 1), inv_xn1.l);
   } else if (live && role == 1) {
     // gates (verifier.rs:593-605), then the identity values in fold order
     xr.put<Fs>(kAccXHvg, acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, stk, zero, y));
