@@ -954,7 +954,7 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None, light=
                                         "as instances)",
                       "parallelism": f"proof-batch x{world} + RCCL all-gather of B x 4 points"},
            "kernels_ms": kernels,
-           "roofline": accum_latency_roofline(B, T, nslots, ms, kernels),
+           "roofline": accum_latency_roofline(B, T, nslots, ms, kernels, shape=shape, psize=batch.psize),
            "status_nonzero": int((batch.status != 0).sum().item()),
            "from_decoded": {"ms_per_batch": round(ms_dec, 4), "value": round(world * B / (ms_dec * 1e-3), 1),
                             "entry": "pm_accum_batch_transcript_device (decoded points / scalars in HBM)",
@@ -1117,33 +1117,60 @@ def accum_two_in_flight(args, ctx, shape, batch, B):
             "quads_match_single_runs": ok, "errors": errs}
 
 
-def accum_latency_roofline(B, T, nslots, ms_batch, kernels, from_bytes=True):
-    """Latency roofline of the accumulator batch (round 4): every kernel on the
-    main stream's critical path is a chain of dependent steps run by lone
-    waves, so its floor is (steps on its longest chain) x (that step's
-    single-wave latency measured in isolation by tools/microbench_chain.hip,
-    profiles/r04/chain_latency.jsonl); the batch floor is the sum over
-    decode -> ladder -> term additions -> sums (the transcript replay and the
-    scalar block run beside the ladder on the side stream and are shorter).
-    Step counts follow the engine's lane rules (accum_engine.hpp):
-      decode   1 square root + 6 products per point lane
-      ladder   127 quad-cooperative Jacobian doublings (k_acc_powers)
-      termadd  ceil(85.3 / S) full XYZZ additions (the mean NAF weight of the
-               two 127-bit GLV halves, dealt over S lanes) + log2(S) butterfly
-      sum      ceil(nslots / (NL/4)) + log2(NL/4) quad-cooperative additions,
-               one quad-cooperative inversion, 5 products
-    frac = floor / measured; per-kernel fractions against the kernels_ms
-    breakdown (HIP events)."""
-    p = os.path.join(ROOT, "profiles", "r04", "chain_latency.jsonl")
-    if not os.path.exists(p):
-        return None
+def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0, from_bytes=True):
+    """Latency roofline of the accumulator batch: every kernel on the critical
+    path is a chain of dependent steps run by lone waves.  Two floors:
+
+    * `self_floor_ms` (round 4): steps on each kernel's longest chain x that
+      step's single-wave latency measured in isolation (tools/microbench_chain
+      .hip, profiles/r05/chain_latency.jsonl over r04; the row-sliced product
+      from profiles/r05/microbench_slice.jsonl) -- relative to this code's own
+      steps;
+    * `hw_floor_ms` (round 5): the same step counts x each step's
+      instruction count by class times the lone-wave issue cost of that class
+      (profiles/r05/hw_floor.json: tools/hw_floor.py over the gfx950 listings,
+      costs from tools/microbench_issue.hip) -- what the hardware allows for
+      this instruction stream; the variable-time safegcd inversion has no
+      static count and enters both floors with its measured time.
+
+    Chains: main stream decode -> ladder, side stream decode -> transcript ->
+    scalar block, then term additions -> sums (critical = the longer of the
+    two, plus the last two).  Step counts follow the engine's lane rules
+    (accum_engine.hpp): decode 305 row-sliced products per BN254 point (the
+    4-bit window of (p+1)/4) while B x points <= 4096, else one lane square
+    root; ladder 127 doublings (row-sliced: 3 dependent product levels each,
+    up to 800 chains; else quad-cooperative); transcript ceil(bytes / 128) + 7
+    Blake2b compressions per proof; scalar block log n + 4K - 3 radix-2^29
+    products (K = bf + 3), the inversion, then 2 per identity value + 2 + T/4
+    Fe products; term additions ceil(85.3 / S) + log2 S XYZZ additions (14
+    products each); sums ceil(nslots / (NL/4)) + log2(NL/4) quad additions
+    (4 product levels), the quad inversion and 5 products."""
     lat = {}
-    for line in open(p):
-        line = line.strip()
-        if line.startswith("{"):
-            d = json.loads(line)
-            if "step" in d:
-                lat[d["step"]] = d["us_per_step"]
+    for rel in (("r04", "chain_latency.jsonl"), ("r05", "chain_latency.jsonl")):
+        p = os.path.join(ROOT, "profiles", *rel)
+        if os.path.exists(p):
+            for line in open(p):
+                if line.strip().startswith("{"):
+                    d = json.loads(line)
+                    if "step" in d:
+                        lat[d["step"]] = d["us_per_step"]
+    p = os.path.join(ROOT, "profiles", "r05", "microbench_slice.jsonl")
+    if os.path.exists(p):
+        for line in open(p):
+            if line.strip().startswith("{"):
+                d = json.loads(line)
+                if d.get("field") == "bn254_fq":
+                    lat.setdefault("s29_mul", d.get("sliced_us_per_mul"))
+                    if "inv_safegcd_lane_us" in d:
+                        lat["inv_lane"] = d["inv_safegcd_lane_us"]
+                    if "inv_quad_safegcd_us" in d:
+                        lat["inv_q"] = d["inv_quad_safegcd_us"]
+    hw = {}
+    p = os.path.join(ROOT, "profiles", "r05", "hw_floor.json")
+    if os.path.exists(p):
+        hw = {k: v["issue_floor_us"] for k, v in json.load(open(p))["steps"].items()}
+    if not {"f29_mul", "xyzz_add", "xyzz_add_q", "ladder_dbl", "inv_q", "sqrt_bn254"} <= lat.keys():
+        return None
     budget = 1024 * 2 * 64
     nterm = B * T
     lg = 0
@@ -1158,23 +1185,61 @@ def accum_latency_roofline(B, T, nslots, ms_batch, kernels, from_bytes=True):
         lgL += 1
     NL = 1 << lgL
     nq = max(1, NL // 4)
-    floor = {
-        "proof_decode": lat["sqrt_bn254"] + 6 * lat["f29_mul"],
-        "acc_ladder": 127 * lat["ladder_dbl"],
-        "acc_termmul": (-(-85.3 // S) + lg) * lat["xyzz_add"],
-        "acc_sum": (-(-nslots // nq) + (nq.bit_length() - 1)) * lat["xyzz_add_q"] + lat["inv_q"] + 5 * lat["f29_mul"],
-    }
-    if not from_bytes:
-        floor.pop("proof_decode")
-    floor = {k: round(v / 1e3, 4) for k, v in floor.items()}
-    total = round(sum(floor.values()), 4)
-    return {"bound": "latency", "achieved": round(ms_batch, 4), "peak": total, "unit": "ms per batch (critical path)",
-            "frac": round(total / ms_batch, 4), "traffic": None,
-            "floor_ms": floor,
-            "kernel_frac": {k: round(floor[k] / kernels[k], 4) for k in floor if kernels.get(k)},
-            "lanes": {"term_additions_S": S, "sum_lanes_NL": NL},
-            "source": "profiles/r04/chain_latency.jsonl (tools/microbench_chain.hip, one wave per CU); "
-                      "PMC of the same kernels: profiles/r04/pmc_acc/"}
+    c = shape.c if shape is not None else None
+    npts = shape.layout()[0] if shape is not None else T
+    nsc = shape.layout()[1] if shape is not None else 0
+    npp = npts - (c.num_instance_columns if c is not None else 1)
+    sliced_dec = B * npp <= 4096
+    sliced_lad = B * npp <= 800
+    log_n = c.log_n if c is not None else 17
+    K = (c.blinding_factors if c is not None else 5) + 3
+    nsets_p = -(-c.n_perm_columns // c.perm_chunk_len) if c is not None and c.n_perm_columns else 0
+    nvals = (2 * nsets_p + 1 if nsets_p else 0) + 5 * (c.num_lookups if c is not None else 0)
+    comps = -(-(npts * 65 + nsc * 33 + 33) // 128) + 7
+    n29 = log_n + 4 * K - 3
+    nfe = 2 * nvals + 2 + -(-T // 4)
+    inv_lane = lat.get("inv_lane", lat["inv_q"])
+
+    def floors(st, hwm):
+        """per-kernel floors (us) from step costs st (measured) or hwm (hardware)"""
+        f = {}
+        f["proof_decode"] = (305 * st["s29_mul"] if sliced_dec else st["sqrt_bn254"]) + 6 * st["f29_mul"]
+        f["transcript"] = comps * st["b2_compress_q"]
+        f["acc_scalars"] = n29 * st["f29_mul"] + inv_lane + nfe * st["fe_mul"]
+        f["acc_ladder"] = 127 * (3 * st["s29_mul"] if sliced_lad else st["ladder_dbl"])
+        f["acc_termmul"] = (-(-85.3 // S) + lg) * st["xyzz_add"]
+        f["acc_sum"] = ((-(-nslots // nq) + (nq.bit_length() - 1)) * st["xyzz_add_q"] + lat["inv_q"]
+                        + 5 * st["f29_mul"])
+        if not from_bytes:
+            f.pop("proof_decode")
+        return f
+
+    def crit(f):
+        d = f.get("proof_decode", 0.0)
+        return max(d + f["acc_ladder"], d + f["transcript"] + f["acc_scalars"]) + f["acc_termmul"] + f["acc_sum"]
+
+    out = {"bound": "latency", "achieved": round(ms_batch, 4), "unit": "ms per batch (critical path)",
+           "traffic": None, "lanes": {"term_additions_S": S, "sum_lanes_NL": NL, "sliced_decode": sliced_dec,
+                                      "sliced_ladder": sliced_lad}}
+    st = dict(lat)
+    st.setdefault("b2_compress_q", 1.62)
+    fs = floors(st, None)
+    out["self_floor_ms"] = {k: round(v / 1e3, 4) for k, v in fs.items()}
+    out["peak"] = round(crit(fs) / 1e3, 4)
+    out["frac"] = round(out["peak"] / ms_batch, 4)
+    out["kernel_frac"] = {k: round(fs[k] / 1e3 / kernels[k], 4) for k in fs if kernels.get(k)}
+    if {"f29_mul", "fe_mul", "s29_mul", "b2_compress_q", "ladder_dbl"} <= hw.keys():
+        h = dict(hw)
+        h["xyzz_add"] = 14 * hw["f29_mul"]
+        h["xyzz_add_q"] = 4 * hw["f29_mul"]
+        h["sqrt_bn254"] = 305 * hw["f29_mul"]
+        fh = floors(h, None)
+        out["hw_floor_ms"] = {k: round(v / 1e3, 4) for k, v in fh.items()}
+        out["hw_peak"] = round(crit(fh) / 1e3, 4)
+        out["hw_frac"] = round(out["hw_peak"] / ms_batch, 4)
+    out["source"] = ("self: profiles/r05/chain_latency.jsonl (r04 where absent), profiles/r05/microbench_slice.jsonl; "
+                     "hw: profiles/r05/hw_floor.json (tools/hw_floor.py, issue costs tools/microbench_issue.hip)")
+    return out
 
 
 def accum_cpu_baseline(curve, shape, host, B, budget_s):

@@ -29,8 +29,32 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLK_NS = 1 / 2.4
-COST_NS = {"mad64": 65536 / 17.180e12 * 1e9, "valu": 65536 / 29.702e12 * 1e9, "lds": 65536 / 29.702e12 * 1e9,
-           "salu": CLK_NS}
+
+
+def issue_costs():
+    """ns per instruction of one lone wave, by class: the round-5 measurement
+    in the chains' own configuration (tools/microbench_issue.hip, one wave per
+    CU) when present, else round 1's one-wave-per-SIMD figures"""
+    c = {"mad64": 65536 / 17.180e12 * 1e9, "valu": 65536 / 29.702e12 * 1e9, "dpp": 65536 / 29.702e12 * 1e9,
+         "lds": 65536 / 29.702e12 * 1e9, "salu": CLK_NS}
+    src = "profiles/r01_s3/microbench_isa.jsonl (waves_per_simd 1)"
+    p = os.path.join(ROOT, "profiles", "r05", "issue_costs.jsonl")
+    if os.path.exists(p):
+        m = {}
+        for line in open(p):
+            if line.startswith("{"):
+                d = json.loads(line)
+                if "form" in d:
+                    m[d["form"]] = d["ns_per_instruction"]
+        c["mad64"] = m.get("v_mad_u64_u32 independent", c["mad64"])
+        c["valu"] = m.get("v_and_b32 independent", c["valu"])
+        c["dpp"] = m.get("v_mov_b32_dpp row_newbcast independent", c["valu"])
+        c["lds"] = c["valu"]  # issue only; the exchange latency is in the measured step
+        src = "profiles/r05/issue_costs.jsonl (tools/microbench_issue.hip, one wave per CU)"
+    return c, src
+
+
+COST_NS, COST_SRC = issue_costs()
 
 # (step, listing, kernel-name regex, what one loop iteration is)
 STEPS = [
@@ -87,6 +111,8 @@ def classify(ops):
         op = t.split()[0]
         if op.startswith(("v_mad_u64_u32", "v_mad_i64_i32")):
             k = "mad64"
+        elif op.startswith("v_") and ("_dpp" in op or "row_" in t or "quad_perm" in t):
+            k = "dpp"
         elif op.startswith("v_"):
             k = "valu"
         elif op.startswith("ds_"):
@@ -124,11 +150,40 @@ def measured():
     return m
 
 
+def sqrt_products():
+    """row-sliced products of one BN254 decompression (proof_kernels.hpp
+    sqrt_pow_s over make_schedule's 4-bit sliding window of (p + 1) / 4):
+    a^2, 7 odd powers, then the schedule's squarings and multiplications"""
+    p = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+    e = (p + 1) // 4
+    bits = [(e >> i) & 1 for i in range(256)]
+    i = 255
+    while i >= 0 and not bits[i]:
+        i -= 1
+    sq = mul = 0
+    first = True
+    while i >= 0:
+        if not bits[i]:
+            sq += 1
+            i -= 1
+            continue
+        j = max(i - 3, 0)
+        while not bits[j]:
+            j += 1
+        if not first:
+            sq += i - j + 1
+            mul += 1
+        first = False
+        i = j - 1
+    return {"squarings": sq, "multiplications": mul, "table": 8, "total": sq + mul + 8}
+
+
 def main():
     srcs = {"chain": listing(os.path.join(ROOT, "tools", "microbench_chain.hip")),
             "slice": listing(os.path.join(ROOT, "tools", "microbench_slice.hip"))}
     meas = measured()
-    out = {"what": __doc__.split("\n\n")[0].replace("\n", " "), "cost_ns": COST_NS, "clock_GHz": 2.4, "steps": {}}
+    out = {"what": __doc__.split("\n\n")[0].replace("\n", " "), "cost_ns": COST_NS, "cost_source": COST_SRC,
+           "clock_GHz": 2.4, "steps": {}, "bn254_sqrt_products": sqrt_products()}
     for step, src, pat, what in STEPS:
         ops, inner = loop_body(srcs[src], pat)
         c, ns = classify(ops)
