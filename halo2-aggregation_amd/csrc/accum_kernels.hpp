@@ -529,9 +529,9 @@ __global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* 
 //   L1  row 1 B = Y Y, row 2 Y Z, row 3 E = (3X) X            (row 0 idles)
 //   L2  row 0 4C = (4B) B, row 1 D = (4X) B, row 2 F = E E, row 3 ZZ3 = Z3 Z3
 //   L3  row 0 beta X3, rows 1, 2 E (D - X3), row 3 ZZZ3 = ZZ3 Z3
-// with the results other rows need gathered by ds_bpermute, and the same
-// values (the same integers: every step is the same Montgomery product,
-// reduction and normalisation) as k_acc_powers stores.  Each row's lanes 0-8
+// with the results other rows need gathered by ds_bpermute.  The stored
+// points equal k_acc_powers' as group elements; their X and Y are left
+// unreduced (below 9.4p, limbs <= 2^29: see the loop).  Each row's lanes 0-8
 // store one limb each: coordinate c of position j is 9 consecutive words.
 // Blocks of four waves (four chains: one wave per SIMD of a CU), each with an
 // LDS fence that keeps a second ladder block and every side-stream block
@@ -599,20 +599,26 @@ __global__ void __launch_bounds__(256) k_acc_powers_s(AccumHdr h, const uint32_t
     const uint32_t b2 = bsel(m0 | m1, B, bsel(m2, E, Z3));
     const uint32_t r2 = s29_mul<F>(S29<F>{a2}, S29<F>{b2}, k).v;
     const uint32_t C4 = s_row<0>(r2), D = s_row<1>(r2), FF = s_row<2>(r2);
-    const S29<F> X3 = s29_reduce3<F>(s29_norm<F>(S29<F>{FF + k.k8x3 - (D + D)}), k.p);
-    const uint32_t w = D + k.k6 - X3.v;  // < 9p, limbs < 2^31
+    // X3, Y3 stay unreduced (round 5): lazily normalised (limbs <= 2^29), with
+    // X < 9.1p, Y < 9.4p at every position (bounds: products of inputs below
+    // 10p stay below 2.94p (E), 1.69p (B), 1.48p (D), 1.09p (FF, C4), 1.31p
+    // (E w); X3 = FF + 8p - 2D in (5.0p, 9.1p), w = D + 12p - X3 in (2.9p,
+    // 13.5p), Y3 = E w + 8p - 2 C4 in (5.8p, 9.4p)); k_acc_termadd reduces
+    // what it stores or negates.  Two f29_reduce3 / exact normalisations less
+    // per doubling on the chain.
+    const S29<F> X3 = s29_norm<F>(S29<F>{FF + k.k8x3 - (D + D)});
+    const uint32_t w = D + k.k12 - X3.v;  // limbs < 2^31
     // L3: (beta, X3) / (E, w) / (E, w) / (ZZ3, Z3)
     const uint32_t a3 = bsel(m0, beta.v, bsel(m3, r2, E));
     const uint32_t b3 = bsel(m0, X3.v, bsel(m3, Z3, w));
     const uint32_t r3 = s29_mul<F>(S29<F>{a3}, S29<F>{b3}, k).v;
-    const S29<F> Y3r = s29_reduce3<F>(s29_norm<F>(S29<F>{r3 + k.k8x3 - (C4 + C4)}), k.p);  // rows 1, 2
+    const S29<F> Y3r = s29_norm<F>(S29<F>{r3 + k.k8x3 - (C4 + C4)});  // rows 1, 2
     const uint32_t Y3 = s_row<1>(Y3r.v);
     // stores: X3 (row 0), Y3 (row 1), ZZ3 (row 3) | beta X3 (row 0), ZZZ3 (row 3)
-    const uint32_t v1 = s29_norm_exact<F>(S29<F>{bsel(m0, X3.v, bsel(m1, Y3, r2))}).v;
-    const uint32_t v2 = s29_norm_exact<F>(S29<F>{r3}).v;
+    const uint32_t v1 = bsel(m0, X3.v, bsel(m1, Y3, r2));
     if (limb) {
       o32[j * kPosW + site1] = v1;
-      o32[j * kPosW + site2] = v2;
+      o32[j * kPosW + site2] = r3;
     }
     X = X3;
     Y = S29<F>{Y3};
@@ -653,7 +659,6 @@ __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t*
                                                      uint32_t lgS, Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
-  using K = F29Consts<F>;
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t S = 1u << lgS, g = gl >> lgS, j = gl & (S - 1);
   if (g >= h.B * h.T) return;  // whole groups only
@@ -704,11 +709,14 @@ __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t*
     Q.ZZZ = pow_ld<F>(o + 3 * kPowWords);
     return true;
   };
+  // table points: X, Y below 3p (k_acc_powers) or 9.4p (k_acc_powers_s,
+  // unreduced), limbs <= 2^29; they only enter products, the negation
+  // (12p - Y) and, reduced, the store
   Xyzz29<F> acc = xyzz29_inf<F>(), Q;
   uint32_t negm = 0;
   bool have = next(Q, negm);
   while (have) {
-    const F29<F> yn = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), Q.Y, K::K6)));  // Y < 3p
+    const F29<F> yn = f29_reduce3<F>(f29_norm<F>(f29_sub<F>(f29_zero<F>(), Q.Y, F29K12<F>::L)));  // < 3p
     Xyzz29<F> R = Q;
 #pragma unroll
     for (int i = 0; i < 9; i++) R.Y.l[i] = bsel(negm, yn.l[i], Q.Y.l[i]);
@@ -716,7 +724,11 @@ __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t*
     acc = xyzz29_add<F>(acc, R);
   }
   for (uint32_t m = 1; m < S; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
-  if (j == 0) store_xyzz29<F>(&part[g], acc);
+  if (j == 0) {  // a sum of one table point is that point, possibly unreduced
+    acc.X = f29_reduce3<F>(f29_norm<F>(acc.X));
+    acc.Y = f29_reduce3<F>(f29_norm<F>(acc.Y));
+    store_xyzz29<F>(&part[g], acc);
+  }
 }
 
 // k_acc_sum: 2^lgL lanes per (proof, output) (lgL <= 5): lane l sums terms

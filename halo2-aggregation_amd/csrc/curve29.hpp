@@ -266,7 +266,10 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_add(const Xyzz29<F>& p, const Xyzz29
   const F29<F> P = f29_norm<F>(f29_sub<F>(U2, U1, K::K6));
   const F29<F> R = f29_norm<F>(f29_sub<F>(S2, S1, K::K6));
   if (f29_is_zero_mod<F>(P)) {
-    if (f29_is_zero_mod<F>(R)) return xyzz29_dbl<F>(p);
+    // p == q: the doubling takes X, Y < 4p (an input may be a k_acc_powers_s
+    // table point, X, Y < 9.4p: reduce first; never taken in practice)
+    if (f29_is_zero_mod<F>(R))
+      return xyzz29_dbl<F>(Xyzz29<F>{f29_reduce3<F>(p.X), f29_reduce3<F>(p.Y), p.ZZ, p.ZZZ});
     return xyzz29_inf<F>();
   }
   const F29<F> PP = f29_sqr_c<F>(P);

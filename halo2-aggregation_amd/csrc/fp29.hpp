@@ -95,6 +95,27 @@ template <> struct F29Consts<Bn254Fr> {
 
 constexpr uint32_t kM29 = (1u << 29) - 1u;
 
+// 12p with every limb below the top in [2^30 - 2, 2^30 + 2^29): it dominates
+// any limb <= 2^29, so a + K12 - b is non-negative limb-wise for b lazily
+// normalised (limbs <= 2^29) and below 12p (the row-sliced ladder's unreduced
+// X3 / Y3, k_acc_powers_s, and their negation in k_acc_termadd)
+template <class P>
+constexpr uint32_t f29_k12_limb(int i) {
+  uint64_t c = 0, n = 0;
+  for (int k = 0; k <= i; k++) {
+    const uint64_t v = 12ull * F29Consts<P>::P[k] + c;
+    n = k < 8 ? (v & kM29) : v;
+    c = v >> 29;
+  }
+  return (uint32_t)(n + (i < 8 ? (1ull << 30) : 0ull) - (i > 0 ? 2ull : 0ull));
+}
+template <class P>
+struct F29K12 {
+  static constexpr uint32_t L[9] = {f29_k12_limb<P>(0), f29_k12_limb<P>(1), f29_k12_limb<P>(2),
+                                    f29_k12_limb<P>(3), f29_k12_limb<P>(4), f29_k12_limb<P>(5),
+                                    f29_k12_limb<P>(6), f29_k12_limb<P>(7), f29_k12_limb<P>(8)};
+};
+
 template <class P>
 __device__ __forceinline__ F29<P> f29_const(const uint32_t (&c)[9]) {
   F29<P> r;

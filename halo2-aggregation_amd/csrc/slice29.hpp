@@ -78,7 +78,7 @@ __device__ __forceinline__ uint32_t s_limbs(const uint32_t (&c)[9]) {
 template <class F>
 struct SConst {
   uint32_t pnz;  // p_l for 1 <= l <= 8, 0 in lane 0 and lanes 9..15
-  uint32_t p, k6, k8x3, k2, one;
+  uint32_t p, k6, k8x3, k2, one, k12;
   __device__ static SConst make() {
     using K = F29Consts<F>;
     SConst c;
@@ -88,6 +88,7 @@ struct SConst {
     c.k8x3 = s_limbs(K::K8x3);
     c.k2 = s_limbs(K::K2);
     c.one = s_limbs(K::ONE);
+    c.k12 = s_limbs(F29K12<F>::L);
     return c;
   }
 };
