@@ -282,6 +282,10 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // profiles/r02/pow/timing_pow1.jsonl)
   if (ctx->acc_split < 0 && lgS == 3)
     while (lgS < 5 && (nterm << (lgS + 1)) <= kAccLaneBudget / 2) lgS++;
+  // few terms (B <= ~34 for the simple shape): 16 quads per term with
+  // quad-cooperative additions (k_acc_termadd<Cv, true>)
+  const bool quad_terms = ctx->acc_split < 0 && lgS == 5 && nterm * 64 <= kAccLaneBudget / 2;
+  const uint32_t lgT = quad_terms ? 4u : lgS;  // log2 of lanes (or quads) per term
   const uint32_t S = 1u << lgS;
   // Streams: with the split ladder (points only, the critical chain) it goes
   // first on the main stream, and the transcript replay + k_acc_scalars run
@@ -353,9 +357,14 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   if (lgS > 0) {
     HIP_TRY(hipEventRecord(sc_done, side));
     HIP_TRY(hipStreamWaitEvent(st, sc_done, 0));
-    PM_LAUNCH(ctx, "acc_termmul",
-              (k_acc_termadd<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
-                  h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p, lgS, dpart)));
+    if (quad_terms)
+      PM_LAUNCH(ctx, "acc_termmul",
+                (k_acc_termadd<Cv, true><<<(unsigned)((nterm * 64 + 255) / 256), 256, 0, st>>>(
+                    h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p, lgT, dpart)));
+    else
+      PM_LAUNCH(ctx, "acc_termmul",
+                (k_acc_termadd<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
+                    h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p, lgS, dpart)));
   } else {
     PM_LAUNCH(ctx, "acc_termmul",
               (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(

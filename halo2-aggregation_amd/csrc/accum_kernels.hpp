@@ -652,14 +652,18 @@ __device__ __forceinline__ void naf128(const uint32_t* k, uint32_t* nz, uint32_t
 // round-robin, so lane j adds ranks j, j + S, ... (at most ceil(cnt / S)
 // additions, cnt ~ 85) with full XYZZ additions; the next point's loads are
 // issued before each addition.  Then log2(S) butterfly steps; lane 0 stores.
-template <class Cv>
+// QUAD (round 5, few terms): S quads per term instead of S lanes (S <= 16, a
+// term within one wave), each addition quad-cooperative (coop29.hpp, ~half
+// the latency of a one-lane addition): for B = 16 a term takes 6 + 4 quad
+// additions instead of 3 + 5 lane additions at ~2x the latency each.
+template <class Cv, bool QUAD = false>
 __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t* __restrict__ prog,
                                                      const uint32_t* __restrict__ coef,
                                                      const uint4* __restrict__ pw, const uint4* __restrict__ pwv,
                                                      uint32_t lgS, Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
-  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gl = (blockIdx.x * blockDim.x + threadIdx.x) >> (QUAD ? 2 : 0);  // lane or quad
   const uint32_t S = 1u << lgS, g = gl >> lgS, j = gl & (S - 1);
   if (g >= h.B * h.T) return;  // whole groups only
   uint32_t k1[6], k2[6];
@@ -721,10 +725,13 @@ __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t*
 #pragma unroll
     for (int i = 0; i < 9; i++) R.Y.l[i] = bsel(negm, yn.l[i], Q.Y.l[i]);
     have = next(Q, negm);
-    acc = xyzz29_add<F>(acc, R);
+    acc = QUAD ? xyzz29_add_q<F>(acc, R) : xyzz29_add<F>(acc, R);
   }
-  for (uint32_t m = 1; m < S; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
-  if (j == 0) {  // a sum of one table point is that point, possibly unreduced
+  for (uint32_t m = 1; m < S; m <<= 1) {
+    const Xyzz29<F> o = xyzz29_shfl_xor<F>(acc, (int)(QUAD ? 4 * m : m));
+    acc = QUAD ? xyzz29_add_q<F>(acc, o) : xyzz29_add<F>(acc, o);
+  }
+  if (j == 0 && (!QUAD || (threadIdx.x & 3u) == 0)) {  // a sum of one table point is that point, possibly unreduced
     acc.X = f29_reduce3<F>(f29_norm<F>(acc.X));
     acc.Y = f29_reduce3<F>(f29_norm<F>(acc.Y));
     store_xyzz29<F>(&part[g], acc);

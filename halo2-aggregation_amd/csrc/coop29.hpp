@@ -201,7 +201,9 @@ __device__ __forceinline__ Xyzz29<F> xyzz29_add_q(const Xyzz29<F>& p, const Xyzz
   const F29<F> P = f29_norm<F>(f29_sub<F>(U2, U1, K::K6));
   const F29<F> R = f29_norm<F>(f29_sub<F>(S2, S1, K::K6));
   if (f29_is_zero_mod<F>(P)) {
-    if (f29_is_zero_mod<F>(R)) return xyzz29_dbl_q<F>(p);
+    // p == o: reduce first (p may be a k_acc_powers_s table point, X, Y < 9.4p)
+    if (f29_is_zero_mod<F>(R))
+      return xyzz29_dbl_q<F>(Xyzz29<F>{f29_reduce3<F>(p.X), f29_reduce3<F>(p.Y), p.ZZ, p.ZZZ});
     return xyzz29_inf<F>();
   }
   // L2: PP = P^2, RR = R^2, ZZ12 = ZZ1 ZZ2, ZZZ12 = ZZZ1 ZZZ2
