@@ -280,9 +280,9 @@ __global__ void __launch_bounds__(256) k_tr_canon(uint32_t B, uint32_t npts, uin
   }
 }
 
-// points / scalars: canonical (k_tr_canon).  The next record's words are
-// loaded one record ahead (the record index comes from the uniform program,
-// so the address is known early) to hide the global-load latency.  64 lanes
+// points / scalars: canonical (k_tr_canon).  Records' words are loaded three
+// records ahead (the record index comes from the uniform program, so the
+// address is known early) to hide the global-load latency.  64 lanes
 // = 16 proofs x 4 lanes; a quad always runs (and exits) together, as the
 // DPP exchanges in the compression require.
 template <class Cv>
@@ -324,12 +324,16 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
 #pragma unroll
     for (int i = 0; i < 16; i++) w[i] = (uint32_t)i < nw ? src[i] : 0u;
   };
-  uint32_t cur[16], nxt[16];
+  // records are fetched three ahead: one record's bookkeeping (~150
+  // instructions, ~0.3 us for a lone wave) does not cover a global load
+  uint32_t cur[16], n1[16], n2[16], n3[16];
   fetch(0, cur);
+  fetch(1, n1);
+  fetch(2, n2);
   for (uint32_t k = 0; k < hd.nprog; k++) {
     const uint32_t op = prog[k];
     const uint32_t kind = op >> 24, idx = op & 0xffffffu;
-    fetch(k + 1, nxt);
+    fetch(k + 3, n3);
     if (kind == kTrPoint) {
       uint32_t z = 0;
 #pragma unroll
@@ -370,7 +374,11 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
                           q == 0 ? c.l[1] : q == 1 ? c.l[3] : q == 2 ? c.l[5] : c.l[7]);
     }
 #pragma unroll
-    for (int i = 0; i < 16; i++) cur[i] = nxt[i];
+    for (int i = 0; i < 16; i++) {
+      cur[i] = n1[i];
+      n1[i] = n2[i];
+      n2[i] = n3[i];
+    }
   }
   // dflags: the proof decode's flags of this batch (proof-bytes entry), taken
   // into the status word and cleared for the next batch
