@@ -346,10 +346,13 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // k_acc_scalars: 4 waves per block of np proofs, (nsc + T + exchange +
   // work) rows of 32 B per proof in LDS (proof stride np + 1), np <= 64
   // within a 128 KiB budget
-  const size_t row_bytes = (size_t)(L.nsc + T + kAccXVals + acc_num_vals(h) + 2 * (h.bf + 3) + kAccStack) * 32;
-  const uint32_t np = (uint32_t)std::min<size_t>(64, kAccScalarsLds / row_bytes - 1);
-  if (np == 0) return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
-  const size_t lds = std::max(row_bytes * (np + 1), lgS > 0 ? kAccScalarsLds : 0);
+  const size_t row_bytes =
+      (size_t)(L.nsc + T + kAccXVals + acc_num_vals(h) + 2 * (h.bf + 3) + kAccStack + h.nslots) * 32;
+  const size_t tail_bytes = (size_t)acc_scalars_tail_words(h) * 4;  // constants + program
+  if (tail_bytes + 2 * row_bytes > kAccScalarsLds)
+    return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
+  const uint32_t np = (uint32_t)std::min<size_t>(64, (kAccScalarsLds - tail_bytes) / row_bytes - 1);
+  const size_t lds = std::max(row_bytes * (np + 1) + tail_bytes, lgS > 0 ? kAccScalarsLds : 0);
   PM_LAUNCH_ST(ctx, side, "acc_scalars",
                (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, side>>>(
                    h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,

@@ -141,7 +141,9 @@ __device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const LdsRow
 // and of wave 1 (kAccStack: the expression stack).  Nothing is indexed at
 // run time in private arrays: those live in scratch memory, whose latency
 // sat on every chain (4 KiB of scratch per lane, ~0.23 ms per call).
-constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXVals = 3;  // exchange row offsets
+// exchange row offsets: gate value; per calc_witness wave (2, 3) the e-term
+// sum, the H-query coefficient sum and H's coefficient; then the identity values
+constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXCoefH = 3, kAccXW3 = 3, kAccXVals = 7;
 constexpr int kAccSelL0 = 0, kAccSelLast = 1, kAccSelOmb = 2;
 
 // identity values of the permutation / lookup arguments in h-fold order
@@ -150,9 +152,16 @@ __host__ __device__ inline uint32_t acc_num_vals(const AccumHdr& h) {
   return (h.n_perm_sets ? 2 * h.n_perm_sets + 1 : 0) + 5 * h.num_lookups;
 }
 
+// LDS words k_acc_scalars keeps after its per-proof rows: the constant table
+// and the program (read by every lane's chains; from LDS instead of global
+// loads, whose ~1 us latency sat on the lone-wave chains, round 5)
+__host__ __device__ inline uint32_t acc_scalars_tail_words(const AccumHdr& h) {
+  return 8 * (h.c_n29 + 1) + (h.p_rank + h.T);
+}
+
 template <class Fs>
-__global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t* __restrict__ prog,
-                                                     const uint32_t* __restrict__ consts,
+__global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t* __restrict__ prog_g,
+                                                     const uint32_t* __restrict__ consts_g,
                                                      const uint32_t* __restrict__ scalars,
                                                      const uint32_t* __restrict__ challenges,
                                                      uint32_t* __restrict__ coef, uint32_t* __restrict__ h_out,
@@ -161,22 +170,35 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const uint32_t role = threadIdx.x >> 6, pl = threadIdx.x & 63;
   const uint32_t b0 = blockIdx.x * np, b = b0 + pl;
   const uint32_t nv = min(np, h.B - b0);  // proofs in this block
-  {  // coalesced staging of the block's evaluations (rows [0, nsc))
+#ifdef PM_ACC_PROFILE
+  const uint64_t pc0 = wall_clock64();
+#endif
+  const uint32_t r_wk = h.nsc + h.T + kAccXVals + acc_num_vals(h);
+  // rows after the stack: wave 3's slot coefficients (cf3, nslots rows)
+  const uint32_t r_cf3 = r_wk + 2 * (h.bf + 3) + kAccStack;
+  uint32_t* const consts = acc_lds + (size_t)8 * (r_cf3 + h.nslots) * (np + 1);
+  uint32_t* const prog = consts + 8 * (h.c_n29 + 1);
+  {  // coalesced staging of the block's evaluations (rows [0, nsc)), the constants and the program
     const uint32_t per = 8 * h.nsc;
     const uint32_t* src = scalars + (size_t)per * b0;
     for (uint32_t f = threadIdx.x; f < per * nv; f += blockDim.x) {
       const uint32_t q = f / per, k = f - q * per;
       acc_lds[k * (np + 1) + q] = src[f];
     }
+    for (uint32_t f = threadIdx.x; f < 8 * (h.c_n29 + 1); f += blockDim.x) consts[f] = consts_g[f];
+    for (uint32_t f = threadIdx.x; f < h.p_rank + h.T; f += blockDim.x) prog[f] = prog_g[f];
   }
   __syncthreads();
+#ifdef PM_ACC_PROFILE
+  const uint64_t pc1 = wall_clock64();
+#endif
   const bool live = pl < nv;
   const LdsRows sc{acc_lds, pl, np + 1};
   const LdsRows cf{acc_lds + (size_t)8 * h.nsc * (np + 1), pl, np + 1};
   const LdsRows xr{acc_lds + (size_t)8 * (h.nsc + h.T) * (np + 1), pl, np + 1};
-  const uint32_t r_wk = h.nsc + h.T + kAccXVals + acc_num_vals(h);
   const LdsRows wk{acc_lds + (size_t)8 * r_wk * (np + 1), pl, np + 1};                      // wave 0
   const LdsRows stk{acc_lds + (size_t)8 * (r_wk + 2 * (h.bf + 3)) * (np + 1), pl, np + 1};  // wave 1
+  const LdsRows cf3{acc_lds + (size_t)8 * r_cf3 * (np + 1), pl, np + 1};                     // wave 3
   const uint32_t* ch = challenges + 8ull * 7 * (live ? b : b0);
   const Fe<Fs> one = fe_one<Fs>(), zero = fe_zero<Fs>();
   const Fe<Fs> y = ldfe<Fs>(ch, 3), x = ldfe<Fs>(ch, 4);
@@ -283,20 +305,30 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
         xr.put<Fs>(vi++, fe_mul<Fs>(as, fe_sub<Fs>(a, ap)));                      // omb
       }
     }
-  } else if (live && role == 2) {
-    // calc_witness coefficients (closed form of the Horner walks); the e term
-    // is -(sum_{non-H} c e + h_eval sum_{H queries} c), finished by wave 0
+  } else if (live && role >= 2) {
+    // calc_witness coefficients (closed form of the Horner walks), the
+    // query sets split between waves 2 (sets [J, S)) and 3 (sets [0, J)) at
+    // about half the queries (round 5: one wave took ~117 us at B = 16,
+    // profiles/r05/acc_scalars_roles.txt); each keeps its own slot sums
+    // (cf / cf3, added in the conversion) and e-term / H sums (exchange rows).
+    // The e term is -(sum_{non-H} c e + h_eval sum_{H queries} c), finished by
+    // wave 0; H's coefficients are expanded by wave 2 after the barrier.
+    const bool w3 = role == 3;
+    const LdsRows& cfs = w3 ? cf3 : cf;
     const Fe<Fs> v = ldfe<Fs>(ch, 5), u = ldfe<Fs>(ch, 6);
-    Fe<Fs> xn = x;
-    for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
-    for (uint32_t t = 0; t < h.nslots; t++) cf.put<Fs>(t, zero);
-    Fe<Fs> coefH = zero, ev = zero, ceh = zero;
+    for (uint32_t t = 0; t < h.nslots; t++) cfs.put<Fs>(t, zero);
+    uint32_t qtot = 0, J = 0;
+    for (uint32_t j = 0; j < h.nsets; j++) qtot += prog[h.p_setlen + j];
+    for (uint32_t acc = 0; J < h.nsets && 2 * (acc + prog[h.p_setlen + J]) <= qtot; J++) acc += prog[h.p_setlen + J];
+    const uint32_t jlo = w3 ? 0u : J, jhi = w3 ? J : h.nsets;
     uint32_t qi = 0;
-    for (uint32_t j = 0; j < h.nsets; j++) qi += prog[h.p_setlen + j];
+    for (uint32_t j = 0; j < jhi; j++) qi += prog[h.p_setlen + j];
     // sets from the last, so u^{S-1-j} is a running product (every
     // coefficient is a sum, so the order of the additions does not matter)
     Fe<Fs> upj = one;
-    for (int j = (int)h.nsets - 1; j >= 0; j--) {
+    for (uint32_t j = jhi; j < h.nsets; j++) upj = fe_mul<Fs>(upj, u);
+    Fe<Fs> coefH = zero, ev = zero, ceh = zero;
+    for (int j = (int)jhi - 1; j >= (int)jlo; j--) {
       const uint32_t m = prog[h.p_setlen + j];
       qi -= m;
       // c_i = u^{S-1-j} v^{m-1-i}, walked from the last query of the set
@@ -306,22 +338,36 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
         if (eidx == kEvalH) ceh = fe_add<Fs>(ceh, c);
         else ev = fe_add<Fs>(ev, fe_mul<Fs>(c, sc.get<Fs>(eidx)));
         if (slot == kSlotH) coefH = fe_add<Fs>(coefH, c);
-        else cf.put<Fs>(slot, fe_add<Fs>(cf.get<Fs>(slot), c));
+        else cfs.put<Fs>(slot, fe_add<Fs>(cfs.get<Fs>(slot), c));
         c = fe_mul<Fs>(c, v);
       }
       cf.put<Fs>(h.nslots + j, upj);
       cf.put<Fs>(h.nslots + h.nsets + j, fe_mul<Fs>(fe_mul<Fs>(upj, ldfe<Fs>(consts, h.c_omega_eval + j)), x));
       upj = fe_mul<Fs>(upj, u);
     }
+    const uint32_t xo = w3 ? kAccXW3 : 0u;
+    xr.put<Fs>(kAccXEvs + xo, ev);
+    xr.put<Fs>(kAccXCeh + xo, ceh);
+    xr.put<Fs>(kAccXCoefH + xo, coefH);
+  }
+#ifdef PM_ACC_PROFILE
+  const uint64_t pc2 = wall_clock64();
+#endif
+  __syncthreads();
+#ifdef PM_ACC_PROFILE
+  const uint64_t pc3 = wall_clock64();
+#endif
+  if (live && role == 2) {
+    // H = sum_i x^{n i} h_i (vanishing.rs:178-188): h_i's coefficient += coefH x^{n i}
+    const Fe<Fs> coefH = fe_add<Fs>(xr.get<Fs>(kAccXCoefH), xr.get<Fs>(kAccXCoefH + kAccXW3));
+    Fe<Fs> xn = x;
+    for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
     Fe<Fs> xp = one;
     for (uint32_t i = 0; i < h.nh; i++) {
       cf.put<Fs>(h.h_slot0 + i, fe_add<Fs>(cf.get<Fs>(h.h_slot0 + i), fe_mul<Fs>(coefH, xp)));
       xp = fe_mul<Fs>(xp, xn);
     }
-    xr.put<Fs>(kAccXEvs, ev);
-    xr.put<Fs>(kAccXCeh, ceh);
   }
-  __syncthreads();
   if (live && role == 0) {
     // expressions in order gates, permutation, lookups: h = h y + expr
     Fe<Fs> hv = xr.get<Fs>(kAccXHvg);
@@ -344,14 +390,29 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     }
     const Fe<Fs> h_eval = fe_mul<Fs>(hv, inv_xn1);
     if (h_out) stfe<Fs>(h_out, b, h_eval);
-    const Fe<Fs> ev = fe_add<Fs>(xr.get<Fs>(kAccXEvs), fe_mul<Fs>(xr.get<Fs>(kAccXCeh), h_eval));
+    const Fe<Fs> evs = fe_add<Fs>(xr.get<Fs>(kAccXEvs), xr.get<Fs>(kAccXEvs + kAccXW3));
+    const Fe<Fs> ceh = fe_add<Fs>(xr.get<Fs>(kAccXCeh), xr.get<Fs>(kAccXCeh + kAccXW3));
+    const Fe<Fs> ev = fe_add<Fs>(evs, fe_mul<Fs>(ceh, h_eval));
     cf.put<Fs>(h.T - 1, fe_neg<Fs>(ev));
   }
+#ifdef PM_ACC_PROFILE
+  const uint64_t pc4 = wall_clock64();
+#endif
   __syncthreads();
   if (live) {
     uint32_t* cfg = coef + 8ull * h.T * b;
-    for (uint32_t t = role; t < h.T; t += 4) stfe<Fs>(cfg, t, fe_from_mont<Fs>(cf.get<Fs>(t)));
+    for (uint32_t t = role; t < h.T; t += 4) {
+      const Fe<Fs> c = t < h.nslots ? fe_add<Fs>(cf.get<Fs>(t), cf3.get<Fs>(t)) : cf.get<Fs>(t);
+      stfe<Fs>(cfg, t, fe_from_mont<Fs>(c));
+    }
   }
+#ifdef PM_ACC_PROFILE  // A/B builds only: per-wave phase times of block 0 (10 ns ticks)
+  const uint64_t pc5 = wall_clock64();
+  if (blockIdx.x == 0 && pl == 0)
+    printf("acc_scalars role %u: stage %llu phase1 %llu sync1 %llu phase2 %llu conv %llu\n", role,
+           (unsigned long long)(pc1 - pc0), (unsigned long long)(pc2 - pc1), (unsigned long long)(pc3 - pc2),
+           (unsigned long long)(pc4 - pc3), (unsigned long long)(pc5 - pc4));
+#endif
 }
 
 // [k]P by GLV + Shamir on the radix-2^29 arithmetic: one 130-step joint
