@@ -61,7 +61,10 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
 // saves).
 constexpr size_t kAccLaneBudget = 1024 * 2 * 64;
 constexpr size_t kAccSumLanes = 16384;
-constexpr size_t kAccScalarsLds = 128 * 1024;
+// 152 KiB (round 5, was 128): k_acc_scalars' per-proof rows grew with wave
+// 3's slot sums and the fold rows, and 32 proofs (config 5's rank slice)
+// should still fit one block
+constexpr size_t kAccScalarsLds = 152 * 1024;
 // LDS fence: the transcript and k_acc_scalars blocks request kAccScalarsLds
 // and every ladder block kAccLadderFence (unused), so the two can never share
 // a CU (160 KiB per CU).  Both sides are single-wave latency chains; sharing
@@ -72,7 +75,8 @@ constexpr size_t kAccLadderFence = 40 * 1024;
 // four per block and one block per CU (kAccSlicedFence), leaving CUs for the
 // side stream's transcript / k_acc_scalars blocks (which a ladder block on
 // every CU kept waiting until the ladder ended: B = 16 transcript 0.10 ->
-// 0.27 ms with 64-thread ladder blocks, profiles/r05/ladder_ab/)
+// 0.27 ms with 64-thread ladder blocks, profiles/r05/ladder_ab/r05_lad_scaling.jsonl
+// against r05_lad_b_auto.jsonl)
 constexpr size_t kAccSlicedChains = 800;
 constexpr size_t kAccSlicedFence = 84 * 1024;
 static_assert(2 * kAccSlicedFence > 160 * 1024 && kAccSlicedFence + kAccScalarsLds > 160 * 1024,

@@ -141,9 +141,13 @@ __device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const LdsRow
 // and of wave 1 (kAccStack: the expression stack).  Nothing is indexed at
 // run time in private arrays: those live in scratch memory, whose latency
 // sat on every chain (4 KiB of scratch per lane, ~0.23 ms per call).
-// exchange row offsets: gate value; per calc_witness wave (2, 3) the e-term
-// sum, the H-query coefficient sum and H's coefficient; then the identity values
-constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXCoefH = 3, kAccXW3 = 3, kAccXVals = 7;
+// exchange row offsets: gate value (times y^N after wave 1's fold); per
+// calc_witness wave (2, 3) the e-term sum, the H-query coefficient sum and
+// H's coefficient; wave 1's fold of the
+// identity values by selector (l_0, l_last, 1 - l_last - l_blind); then the
+// identity values themselves
+constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXCoefH = 3, kAccXW3 = 3, kAccXFold = 7,
+                   kAccXVals = 10;
 constexpr int kAccSelL0 = 0, kAccSelLast = 1, kAccSelOmb = 2;
 
 // identity values of the permutation / lookup arguments in h-fold order
@@ -305,6 +309,39 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
         xr.put<Fs>(vi++, fe_mul<Fs>(as, fe_sub<Fs>(a, ap)));                      // omb
       }
     }
+    // Fold the values into h = h y + sel v (gates first, then these in order)
+    // per selector, so wave 0 needs only h = G y^N + l_0 A + l_last B + omb C
+    // once its l_i are known (round 5: the 2 N products of the fold moved off
+    // wave 0's chain, which is the kernel's longest)
+    Fe<Fs> G = xr.get<Fs>(kAccXHvg), A = zero, Bs = zero, C = zero;
+    uint32_t fi = kAccXVals;
+    auto fold = [&](int sel) {
+      const Fe<Fs> val = xr.get<Fs>(fi++);
+      G = fe_mul<Fs>(G, y);
+      A = fe_mul<Fs>(A, y);
+      Bs = fe_mul<Fs>(Bs, y);
+      C = fe_mul<Fs>(C, y);
+      if (sel == kAccSelL0) A = fe_add<Fs>(A, val);
+      else if (sel == kAccSelLast) Bs = fe_add<Fs>(Bs, val);
+      else C = fe_add<Fs>(C, val);
+    };
+    if (h.n_perm_sets) {
+      fold(kAccSelL0);
+      fold(kAccSelLast);
+      for (uint32_t i = 1; i < h.n_perm_sets; i++) fold(kAccSelL0);
+      for (uint32_t ci = 0; ci < h.n_perm_sets; ci++) fold(kAccSelOmb);
+    }
+    for (uint32_t i = 0; i < h.num_lookups; i++) {
+      fold(kAccSelL0);
+      fold(kAccSelLast);
+      fold(kAccSelOmb);
+      fold(kAccSelL0);
+      fold(kAccSelOmb);
+    }
+    xr.put<Fs>(kAccXHvg, G);
+    xr.put<Fs>(kAccXFold, A);
+    xr.put<Fs>(kAccXFold + 1, Bs);
+    xr.put<Fs>(kAccXFold + 2, C);
   } else if (live && role >= 2) {
     // calc_witness coefficients (closed form of the Horner walks), the
     // query sets split between waves 2 (sets [J, S)) and 3 (sets [0, J)) at
@@ -369,25 +406,11 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     }
   }
   if (live && role == 0) {
-    // expressions in order gates, permutation, lookups: h = h y + expr
-    Fe<Fs> hv = xr.get<Fs>(kAccXHvg);
-    uint32_t vi = kAccXVals;
-    auto fold = [&](const Fe<Fs>& sel) {
-      hv = fe_add<Fs>(fe_mul<Fs>(hv, y), fe_mul<Fs>(sel, xr.get<Fs>(vi++)));
-    };
-    if (h.n_perm_sets) {
-      fold(l_0);
-      fold(l_last);
-      for (uint32_t i = 1; i < h.n_perm_sets; i++) fold(l_0);
-      for (uint32_t ci = 0; ci < h.n_perm_sets; ci++) fold(omb);
-    }
-    for (uint32_t i = 0; i < h.num_lookups; i++) {
-      fold(l_0);
-      fold(l_last);
-      fold(omb);
-      fold(l_0);
-      fold(omb);
-    }
+    // expressions in order gates, permutation, lookups: h = h y + sel expr,
+    // folded per selector by wave 1
+    const Fe<Fs> hv = fe_add<Fs>(
+        fe_add<Fs>(xr.get<Fs>(kAccXHvg), fe_mul<Fs>(l_0, xr.get<Fs>(kAccXFold))),
+        fe_add<Fs>(fe_mul<Fs>(l_last, xr.get<Fs>(kAccXFold + 1)), fe_mul<Fs>(omb, xr.get<Fs>(kAccXFold + 2))));
     const Fe<Fs> h_eval = fe_mul<Fs>(hv, inv_xn1);
     if (h_out) stfe<Fs>(h_out, b, h_eval);
     const Fe<Fs> evs = fe_add<Fs>(xr.get<Fs>(kAccXEvs), xr.get<Fs>(kAccXEvs + kAccXW3));
