@@ -208,51 +208,67 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const Fe<Fs> y = ldfe<Fs>(ch, 3), x = ldfe<Fs>(ch, 4);
   Fe<Fs> l_0 = zero, l_last = zero, omb = zero, inv_xn1 = zero;
 
+  // Wave 0: the long chain of the kernel, in the radix-2^29 lazy form
+  // (one-lane products 0.38-0.46 us against 0.70 us for Fe; round 5).
+  // Values stay Norm, < 4p; LDS rows hold them packed (< 2^256).
+  using K29 = F29Consts<Fs>;
+  const uint32_t K = h.bf + 3;
+  auto put29 = [&](const LdsRows& r, uint32_t row, const F29<Fs>& v) {
+    Fe<Fs> w;
+    f29_pack<Fs>(v, w.l);
+    r.put<Fs>(row, w);
+  };
+  auto get29 = [&](const LdsRows& r, uint32_t row) { return f29_unpack<Fs>(r.get<Fs>(row).l); };
+  auto ld29 = [&](uint32_t idx) { return f29_unpack<Fs>(ldfe<Fs>(consts, idx).l); };  // canonical R261
+  const F29<Fs> one29 = f29_const<Fs>(K29::ONE);
   if (live && role == 0) {
-    // The long chain of the kernel, in the radix-2^29 lazy form (one-lane
-    // products 0.38-0.46 us against 0.70 us for Fe; round 5).  Values stay
-    // Norm, < 4p; LDS rows hold them packed (< 2^256).
-    using K29 = F29Consts<Fs>;
-    auto put29 = [&](uint32_t row, const F29<Fs>& v) {
-      Fe<Fs> w;
-      f29_pack<Fs>(v, w.l);
-      wk.put<Fs>(row, w);
-    };
-    auto get29 = [&](uint32_t row) { return f29_unpack<Fs>(wk.get<Fs>(row).l); };
-    auto ld29 = [&](uint32_t idx) { return f29_unpack<Fs>(ldfe<Fs>(consts, idx).l); };  // canonical R261
     // x^n (verifier.rs:513-516)
     const F29<Fs> x29 = f29_from_r256<Fs>(x.l);  // < 2p
     F29<Fs> xn = x29;
     for (uint32_t i = 0; i < h.log_n; i++) xn = f29_sqr_c<Fs>(xn);
-    const F29<Fs> one29 = f29_const<Fs>(K29::ONE);
     const F29<Fs> xn1 = f29_reduce3<Fs>(f29_norm<Fs>(f29_sub<Fs>(xn, one29, K29::K2)));  // < 3p
     // l_i = w^i (x^n - 1) / (n (x - w^i)), w = omega^-1, i < bf + 2, plus
     // 1 / (x^n - 1) for h_eval: one batched inversion (Montgomery's trick).
     // rows: den_i at wk[i], prefix products at wk[K + i]
-    const uint32_t K = h.bf + 3;
     const F29<Fs> nfe = ld29(h.c_n29);
     F29<Fs> pre = xn1;
     for (uint32_t i = 0; i < K; i++) {
       const F29<Fs> den =
           i + 1 < K ? f29_mul_c<Fs>(nfe, f29_norm<Fs>(f29_sub<Fs>(x29, ld29(h.c_wpow29 + i), K29::K2))) : xn1;
       pre = i ? f29_mul_c<Fs>(pre, den) : den;  // < 2p (< 3p for i = 0 = K - 1)
-      put29(i, den);
-      put29(K + i, pre);
+      put29(wk, i, den);
+      put29(wk, K + i, pre);
     }
     // a zero denominator (x^n = 1, or x = omega^-i for a Lagrange basis
     // point) is where the reference's main_gate.div fails (vanishing.rs:175,
     // verifier.rs:580): flag the proof; its outputs are then unspecified
     if (status && f29_is_zero_mod<Fs>(pre)) status[b] |= kAccStatusDenomZero;
-    F29<Fs> inv = f29_inv<Fs>(pre);  // variable-time safegcd, < 2p
-    for (uint32_t i = K - 1; i > 0; i--) {
-      const F29<Fs> t = f29_mul_c<Fs>(inv, get29(K + i - 1));
-      inv = f29_mul_c<Fs>(inv, get29(i));
-      put29(i, t);  // now 1 / den_i
+  }
+  if (role == 0) {
+    // the inverse of the product (variable-time safegcd, < 2p) into row 2K - 1:
+    // up to 16 proofs per block the whole wave works, a quad per proof
+    // (sg_inverse_q: 27 us against 34 us for one lane)
+    if (np <= 16) {
+      const LdsRows wq{wk.base, pl >> 2, wk.stride};
+      const bool own = (pl >> 2) < nv;
+      const F29<Fs> r = f29_inv_q<Fs>(own ? get29(wq, 2 * K - 1) : f29_zero<Fs>());
+      if (own && (pl & 3u) == 0) put29(wq, 2 * K - 1, r);
+    } else if (live) {
+      put29(wk, 2 * K - 1, f29_inv<Fs>(get29(wk, 2 * K - 1)));
     }
-    put29(0, inv);
+  }
+  if (live && role == 0) {
+    const F29<Fs> xn1 = get29(wk, K - 1);  // den_{K-1}, before the walk below replaces it
+    F29<Fs> inv = get29(wk, 2 * K - 1);
+    for (uint32_t i = K - 1; i > 0; i--) {
+      const F29<Fs> t = f29_mul_c<Fs>(inv, get29(wk, K + i - 1));
+      inv = f29_mul_c<Fs>(inv, get29(wk, i));
+      put29(wk, i, t);  // now 1 / den_i
+    }
+    put29(wk, 0, inv);
     F29<Fs> l0 = f29_zero<Fs>(), llast = l0, lblind = l0;
     for (uint32_t i = 0; i + 1 < K; i++) {
-      const F29<Fs> li = f29_mul_c<Fs>(f29_mul_c<Fs>(ld29(h.c_wpow29 + i), xn1), get29(i));  // < 2p
+      const F29<Fs> li = f29_mul_c<Fs>(f29_mul_c<Fs>(ld29(h.c_wpow29 + i), xn1), get29(wk, i));  // < 2p
       if (i == 0) l0 = li;
       else if (i == h.bf + 1) llast = li;
       else lblind = f29_reduce3<Fs>(f29_norm<Fs>(f29_add<Fs>(lblind, li)));  // < 3p
@@ -263,7 +279,7 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     f29_to_r256<Fs>(l0, l_0.l);
     f29_to_r256<Fs>(llast, l_last.l);
     f29_to_r256<Fs>(f29_reduce3<Fs>(o), omb.l);
-    f29_to_r256<Fs>(get29(K - 1), inv_xn1.l);
+    f29_to_r256<Fs>(get29(wk, K - 1), inv_xn1.l);
   } else if (live && role == 1) {
     // gates (verifier.rs:593-605), then the identity values in fold order
     xr.put<Fs>(kAccXHvg, acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, stk, zero, y));
@@ -313,32 +329,27 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     // per selector, so wave 0 needs only h = G y^N + l_0 A + l_last B + omb C
     // once its l_i are known (round 5: the 2 N products of the fold moved off
     // wave 0's chain, which is the kernel's longest)
-    Fe<Fs> G = xr.get<Fs>(kAccXHvg), A = zero, Bs = zero, C = zero;
-    uint32_t fi = kAccXVals;
-    auto fold = [&](int sel) {
-      const Fe<Fs> val = xr.get<Fs>(fi++);
-      G = fe_mul<Fs>(G, y);
-      A = fe_mul<Fs>(A, y);
-      Bs = fe_mul<Fs>(Bs, y);
-      C = fe_mul<Fs>(C, y);
-      if (sel == kAccSelL0) A = fe_add<Fs>(A, val);
-      else if (sel == kAccSelLast) Bs = fe_add<Fs>(Bs, val);
-      else C = fe_add<Fs>(C, val);
+    // value k of N is weighted y^{N-1-k}: walked from the last value with a
+    // running power of y (2 products per value instead of 4 Horner steps)
+    auto sel_of = [&](uint32_t k) {  // the selector of value k in fold order
+      if (h.n_perm_sets) {
+        if (k < 2 * h.n_perm_sets + 1) return k == 0 ? kAccSelL0 : k == 1 ? kAccSelLast : k <= h.n_perm_sets ? kAccSelL0 : kAccSelOmb;
+        k -= 2 * h.n_perm_sets + 1;
+      }
+      const uint32_t r = k % 5;  // lookups: l_0, l_last, omb, l_0, omb
+      return r == 0 || r == 3 ? kAccSelL0 : r == 1 ? kAccSelLast : kAccSelOmb;
     };
-    if (h.n_perm_sets) {
-      fold(kAccSelL0);
-      fold(kAccSelLast);
-      for (uint32_t i = 1; i < h.n_perm_sets; i++) fold(kAccSelL0);
-      for (uint32_t ci = 0; ci < h.n_perm_sets; ci++) fold(kAccSelOmb);
+    Fe<Fs> A = zero, Bs = zero, C = zero, yp = one;
+#pragma unroll 1
+    for (uint32_t k = vi - kAccXVals; k-- > 0;) {
+      const Fe<Fs> t = fe_mul<Fs>(xr.get<Fs>(kAccXVals + k), yp);
+      const int sel = sel_of(k);
+      if (sel == kAccSelL0) A = fe_add<Fs>(A, t);
+      else if (sel == kAccSelLast) Bs = fe_add<Fs>(Bs, t);
+      else C = fe_add<Fs>(C, t);
+      yp = fe_mul<Fs>(yp, y);
     }
-    for (uint32_t i = 0; i < h.num_lookups; i++) {
-      fold(kAccSelL0);
-      fold(kAccSelLast);
-      fold(kAccSelOmb);
-      fold(kAccSelL0);
-      fold(kAccSelOmb);
-    }
-    xr.put<Fs>(kAccXHvg, G);
+    xr.put<Fs>(kAccXHvg, fe_mul<Fs>(xr.get<Fs>(kAccXHvg), yp));  // G y^N
     xr.put<Fs>(kAccXFold, A);
     xr.put<Fs>(kAccXFold + 1, Bs);
     xr.put<Fs>(kAccXFold + 2, C);
