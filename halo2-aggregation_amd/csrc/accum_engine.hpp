@@ -408,6 +408,79 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
 // Batched Blake2b transcript replay (transcript_kernels.hpp): absorb program
 // in verifier read order, four lanes per proof, challenges written in the
 // (B, 7, 4) layout pm_accum_batch reads.
+// The byte stream every proof of the shape absorbs, laid out for
+// k_transcript_s (transcript_kernels.hpp): per 32-bit stream word the
+// constant bytes (record tags, the VK record, squeeze bytes) and up to two
+// runs of the proof's canonical data bytes (points region: 64 bytes per point
+// x || y; scalars region: 32 bytes each), then the point records' indices.
+// false: the shape's stream does not fit the kernel's LDS (or its encoding):
+// the per-record kernel runs instead.  PM_TRANSCRIPT_RECORDS=1 forces that
+// (A/B runs).
+inline bool tr_stream_plan(const std::vector<uint32_t>& prog, const TranscriptHdr& hd, TrStreamHdr& sh,
+                           std::vector<uint32_t>& wtab) {
+  static const bool force_records = [] {
+    const char* e = getenv("PM_TRANSCRIPT_RECORDS");
+    return e && *e == '1';
+  }();
+  if (force_records) return false;
+  struct Byte {
+    uint32_t kind, v;  // kind 0: constant v; 1 / 2: data byte v of the points / scalars region
+  };
+  std::vector<Byte> by;
+  std::vector<uint32_t> pts;
+  uint32_t nsq = 0;
+  for (uint32_t op : prog) {
+    const uint32_t kind = op >> 24, idx = op & (kTrLookupZFlag - 1u);
+    if (kind == kTrVk) {
+      by.push_back({0, 2});
+      for (int i = 0; i < 32; i++) by.push_back({0, (hd.vk[i / 4] >> (8 * (i % 4))) & 0xffu});
+    } else if (kind == kTrPoint) {
+      by.push_back({0, 1});
+      for (uint32_t i = 0; i < 64; i++) by.push_back({1, 64 * idx + i});
+      pts.push_back(idx);
+    } else if (kind == kTrScalar) {
+      by.push_back({0, 2});
+      for (uint32_t i = 0; i < 32; i++) by.push_back({2, 32 * idx + i});
+    } else {
+      by.push_back({0, 0});
+      if (idx != nsq || nsq >= kTrChallenges) return false;  // squeezes in challenge order
+      sh.L[nsq++] = (uint32_t)by.size();
+    }
+  }
+  if (nsq != kTrChallenges) return false;
+  sh.nw32 = (uint32_t)((by.size() + 3) / 4);
+  sh.nblk = (uint32_t)((by.size() + 127) / 128);
+  sh.npr = (uint32_t)pts.size();
+  wtab.assign(3 * (size_t)sh.nw32, 0u);
+  for (uint32_t w = 0; w < sh.nw32; w++) {
+    uint32_t nparts = 0;
+    for (uint32_t p = 0; p < 4; p++) {
+      const size_t i = 4 * (size_t)w + p;
+      if (i >= by.size()) break;
+      const Byte c = by[i];
+      if (c.kind == 0) {
+        wtab[3 * w] |= c.v << (8 * p);
+        continue;
+      }
+      const bool cont = p > 0 && by[i - 1].kind == c.kind && by[i - 1].v + 1 == c.v;
+      if (cont) {
+        uint32_t& part = wtab[3 * w + nparts];
+        const uint32_t n = ((part >> 23) & 7u) + 1, s8 = (part >> 28) & 3u;
+        part = (part & ~(7u << 23) & ~(1u << 22)) | (n << 23) | ((s8 + n > 4) ? 1u << 22 : 0u);
+        continue;
+      }
+      if (++nparts > 2) return false;
+      const uint32_t widx = c.v >> 2;
+      if (widx + 1 > kTrPartIdxMask) return false;
+      wtab[3 * w + nparts] = (1u << 31) | ((c.kind == 2 ? 1u : 0u) << 30) | ((c.v & 3u) << 28) | (p << 26) |
+                             (1u << 23) | widx;
+    }
+  }
+  wtab.insert(wtab.end(), pts.begin(), pts.end());
+  const TrStreamLds lay(sh.nw32, sh.nblk, sh.npr, hd.npts, hd.nsc);
+  return 4ull * lay.total <= kAccScalarsLds;
+}
+
 template <class Cv>
 int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_t vk_repr[4], const void* d_points,
                       const void* d_scalars, void* d_ch, void* d_status, hipStream_t st, bool canon_ready,
@@ -453,6 +526,10 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
 
   int rc;
   if ((rc = ctx->tr_prog.put(prog, st))) return rc;
+  TrStreamHdr sh{};
+  std::vector<uint32_t> wtab;
+  const bool streamed = tr_stream_plan(prog, hd, sh, wtab);
+  if (streamed && (rc = ctx->tr_wtab.put(wtab, st))) return rc;
   const size_t ncoord = B * 2 * (size_t)L.npts, nall = ncoord + B * (size_t)L.nsc;
   if ((rc = ctx->tr_canon.ensure(nall * 32))) return rc;
   uint32_t* cpts = (uint32_t*)ctx->tr_canon.p;
@@ -465,8 +542,16 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
     if (!canon_ready)
       k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
           (uint32_t)B, L.npts, L.nsc, (const uint32_t*)d_points, (const uint32_t*)d_scalars, cpts, cscs);
-    k_transcript<Cv><<<(unsigned)tblocks, 64, fence ? kAccScalarsLds : 0, st>>>(
-        hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status, dflags);
+    if (streamed) {
+      const size_t lds = std::max<size_t>(4ull * TrStreamLds(sh.nw32, sh.nblk, sh.npr, L.npts, L.nsc).total,
+                                          fence ? kAccScalarsLds : 0);
+      k_transcript_s<Cv><<<(unsigned)tblocks, 256, lds, st>>>(
+          hd, sh, (const uint32_t*)ctx->tr_prog.buf.p, (const uint32_t*)ctx->tr_wtab.buf.p, cpts, cscs,
+          (uint32_t*)d_ch, (uint32_t*)d_status, dflags);
+    } else {
+      k_transcript<Cv><<<(unsigned)tblocks, 64, fence ? kAccScalarsLds : 0, st>>>(
+          hd, (const uint32_t*)ctx->tr_prog.buf.p, cpts, cscs, (uint32_t*)d_ch, (uint32_t*)d_status, dflags);
+    }
   });
   return PM_OK;
 }

@@ -433,12 +433,14 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const uint64_t pc4 = wall_clock64();
 #endif
   __syncthreads();
-  if (live) {
-    uint32_t* cfg = coef + 8ull * h.T * b;
-    for (uint32_t t = role; t < h.T; t += 4) {
-      const Fe<Fs> c = t < h.nslots ? fe_add<Fs>(cf.get<Fs>(t), cf3.get<Fs>(t)) : cf.get<Fs>(t);
-      stfe<Fs>(cfg, t, fe_from_mont<Fs>(c));
-    }
+  // the T coefficients of the nv proofs over all 256 threads (item = (t,
+  // proof), consecutive threads on consecutive proofs): at np = 16 the
+  // lane-per-proof form left 3/4 of every wave idle and took ~20 us
+  for (uint32_t i = threadIdx.x; i < nv * h.T; i += blockDim.x) {
+    const uint32_t t = i / nv, q = i - t * nv;
+    const LdsRows cq{cf.base, q, cf.stride}, c3q{cf3.base, q, cf3.stride};
+    const Fe<Fs> c = t < h.nslots ? fe_add<Fs>(cq.get<Fs>(t), c3q.get<Fs>(t)) : cq.get<Fs>(t);
+    stfe<Fs>(coef + 8ull * h.T * (b0 + q), t, fe_from_mont<Fs>(c));
   }
 #ifdef PM_ACC_PROFILE  // A/B builds only: per-wave phase times of block 0 (10 ns ticks)
   const uint64_t pc5 = wall_clock64();

@@ -168,17 +168,27 @@ constexpr int kB2Sigma[10][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13,
     b = PM_B2_ROT(b ^ c, 63);         \
   } while (0)
 
-// F(h, m, t, f) of RFC 7693 §3.2 by the quad: m = the 16 words of the block
-// starting at 64-bit word w0 of the slot's buffer; lane q updates h[q] and
-// h[4 + q].
-template <int R>
-__device__ __forceinline__ void tr_round_q(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, const TrBuf& buf,
-                                           uint32_t slot, uint32_t w0, uint32_t q4) {
+// message readers of the compression: word i (< 16) of the block
+struct TrRingMsg {  // the per-record path's 256-byte ring (TrBuf)
+  const TrBuf& buf;
+  uint32_t slot, w0;
+  __device__ __forceinline__ uint64_t operator()(uint32_t i) const { return buf[(w0 + i) & 31][slot]; }
+};
+struct TrStreamMsg {  // the streamed path's LDS stream ([w64][kTrSlots], this slot's column)
+  const uint64_t* col;
+  uint32_t w0;
+  __device__ __forceinline__ uint64_t operator()(uint32_t i) const { return col[(w0 + i) * kTrSlots]; }
+};
+
+// F(h, m, t, f) of RFC 7693 §3.2 by the quad: lane q updates h[q] and h[4 + q].
+template <int R, class Msg>
+__device__ __forceinline__ void tr_round_q(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, const Msg& msg,
+                                           uint32_t q4) {
   constexpr TrSigma S = tr_sigma_pack(kB2Sigma[R % 10]);
-  const uint64_t x0 = buf[(w0 + ((S.colx >> q4) & 15)) & 31][slot];
-  const uint64_t y0 = buf[(w0 + ((S.coly >> q4) & 15)) & 31][slot];
-  const uint64_t x1 = buf[(w0 + ((S.diagx >> q4) & 15)) & 31][slot];
-  const uint64_t y1 = buf[(w0 + ((S.diagy >> q4) & 15)) & 31][slot];
+  const uint64_t x0 = msg((S.colx >> q4) & 15);
+  const uint64_t y0 = msg((S.coly >> q4) & 15);
+  const uint64_t x1 = msg((S.diagx >> q4) & 15);
+  const uint64_t y1 = msg((S.diagy >> q4) & 15);
   PM_B2_GQ(a, b, c, d, x0, y0);
   b = tr_qperm<kQRot1>(b);
   c = tr_qperm<kQRot2>(c);
@@ -190,30 +200,46 @@ __device__ __forceinline__ void tr_round_q(uint64_t& a, uint64_t& b, uint64_t& c
 }
 #undef PM_B2_GQ
 
-__device__ __forceinline__ void tr_compress_q(TrLane& s, const TrBuf& buf, uint32_t slot, uint32_t q, uint32_t w0,
-                                              uint64_t tcount, bool last) {
+template <class Msg>
+__device__ __forceinline__ void tr_compress_q(uint64_t& h0, uint64_t& h1, const Msg& msg, uint32_t q, uint64_t tcount,
+                                              bool last) {
   const uint64_t iv_c = q == 0 ? Blake2bIV::v[0] : q == 1 ? Blake2bIV::v[1] : q == 2 ? Blake2bIV::v[2]
                                                                                       : Blake2bIV::v[3];
   const uint64_t iv_d = q == 0 ? Blake2bIV::v[4] : q == 1 ? Blake2bIV::v[5] : q == 2 ? Blake2bIV::v[6]
                                                                                       : Blake2bIV::v[7];
-  uint64_t a = s.h0, b = s.h1, c = iv_c, d = iv_d;
+  uint64_t a = h0, b = h1, c = iv_c, d = iv_d;
   if (q == 0) d ^= tcount;    // v12 ^= t
   if (q == 2 && last) d = ~d;  // v14 = ~v14
   const uint32_t q4 = 4 * q;
-  tr_round_q<0>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<1>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<2>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<3>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<4>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<5>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<6>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<7>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<8>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<9>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<10>(a, b, c, d, buf, slot, w0, q4);
-  tr_round_q<11>(a, b, c, d, buf, slot, w0, q4);
-  s.h0 ^= a ^ c;
-  s.h1 ^= b ^ d;
+  tr_round_q<0>(a, b, c, d, msg, q4);
+  tr_round_q<1>(a, b, c, d, msg, q4);
+  tr_round_q<2>(a, b, c, d, msg, q4);
+  tr_round_q<3>(a, b, c, d, msg, q4);
+  tr_round_q<4>(a, b, c, d, msg, q4);
+  tr_round_q<5>(a, b, c, d, msg, q4);
+  tr_round_q<6>(a, b, c, d, msg, q4);
+  tr_round_q<7>(a, b, c, d, msg, q4);
+  tr_round_q<8>(a, b, c, d, msg, q4);
+  tr_round_q<9>(a, b, c, d, msg, q4);
+  tr_round_q<10>(a, b, c, d, msg, q4);
+  tr_round_q<11>(a, b, c, d, msg, q4);
+  h0 ^= a ^ c;
+  h1 ^= b ^ d;
+}
+
+// the 64-byte digest of the quad's state: word 2i, 2i + 1 = h[i], h[K] is
+// lane K's h0, h[4 + K] its h1 (all 4 lanes receive all 16 words)
+__device__ __forceinline__ void tr_digest_q(uint64_t h0, uint64_t h1, uint32_t d[16]) {
+#define PM_TR_BC(K)                                                                                            \
+  d[2 * K] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)h0, K * 0x55, 0xF, 0xF, false);                 \
+  d[2 * K + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(h0 >> 32), K * 0x55, 0xF, 0xF, false);     \
+  d[2 * K + 8] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)h1, K * 0x55, 0xF, 0xF, false);             \
+  d[2 * K + 9] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(h1 >> 32), K * 0x55, 0xF, 0xF, false);
+  PM_TR_BC(0)
+  PM_TR_BC(1)
+  PM_TR_BC(2)
+  PM_TR_BC(3)
+#undef PM_TR_BC
 }
 
 // Compress every full block that more data has arrived after; with `squeeze`
@@ -235,19 +261,9 @@ __device__ __forceinline__ void tr_settle(TrLane& s, TrBuf& buf, uint32_t slot, 
         if (j >= z0) tr_store(buf, slot, wd0 + j, 0u);
     }
     TrLane n = s;
-    tr_compress_q(n, buf, slot, q, wd0 >> 1, fin ? s.t + s.pos : s.t + 128, fin);
+    tr_compress_q(n.h0, n.h1, TrRingMsg{buf, slot, wd0 >> 1}, q, fin ? s.t + s.pos : s.t + 128, fin);
     if (fin) {
-// digest word 2i, 2i + 1 = h[i]: h[K] is lane K's h0, h[4 + K] its h1
-#define PM_TR_BC(K)                                                                                            \
-  d[2 * K] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)n.h0, K * 0x55, 0xF, 0xF, false);               \
-  d[2 * K + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(n.h0 >> 32), K * 0x55, 0xF, 0xF, false);   \
-  d[2 * K + 8] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)n.h1, K * 0x55, 0xF, 0xF, false);           \
-  d[2 * K + 9] = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(n.h1 >> 32), K * 0x55, 0xF, 0xF, false);
-      PM_TR_BC(0)
-      PM_TR_BC(1)
-      PM_TR_BC(2)
-      PM_TR_BC(3)
-#undef PM_TR_BC
+      tr_digest_q(n.h0, n.h1, d);
       return;
     }
     s.h0 = n.h0;
@@ -280,22 +296,16 @@ __global__ void __launch_bounds__(256) k_tr_canon(uint32_t B, uint32_t npts, uin
   }
 }
 
-// points / scalars: canonical (k_tr_canon).  Records' words are loaded three
-// records ahead (the record index comes from the uniform program, so the
-// address is known early) to hide the global-load latency.  64 lanes
-// = 16 proofs x 4 lanes; a quad always runs (and exits) together, as the
-// DPP exchanges in the compression require.
+// The per-record replay of one proof by its quad (points / scalars canonical,
+// k_tr_canon).  Records' words are loaded three records ahead (the record
+// index comes from the uniform program, so the address is known early) to
+// hide the global-load latency.  A quad always runs (and exits) together, as
+// the DPP exchanges in the compression require.  Returns the status bits.
 template <class Cv>
-__global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint32_t* __restrict__ prog,
-                                                   const uint32_t* __restrict__ points,
-                                                   const uint32_t* __restrict__ scalars,
-                                                   uint32_t* __restrict__ challenges, uint32_t* __restrict__ status,
-                                                   uint32_t* __restrict__ dflags) {
+__device__ uint32_t tr_replay(const TranscriptHdr& hd, const uint32_t* __restrict__ prog,
+                              const uint32_t* __restrict__ points, const uint32_t* __restrict__ scalars,
+                              uint32_t* __restrict__ challenges, TrBuf& buf, uint32_t slot, uint32_t q, uint32_t b) {
   using Fs = typename Cv::Scalar;
-  __shared__ TrBuf buf;
-  const uint32_t slot = threadIdx.x >> 2, q = threadIdx.x & 3;
-  const uint32_t b = blockIdx.x * kTrSlots + slot;
-  if (b >= hd.B) return;
   TrLane s;
   s.h0 = q == 0 ? hd.h0[0] : q == 1 ? hd.h0[1] : q == 2 ? hd.h0[2] : hd.h0[3];
   s.h1 = q == 0 ? hd.h0[4] : q == 1 ? hd.h0[5] : q == 2 ? hd.h0[6] : hd.h0[7];
@@ -369,9 +379,11 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
         p1.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pr.l[i], 0x55, 0xF, 0xF, false);
       }
       const Fe<Fs> c = fe_add<Fs>(p0, p1);  // = fe_from_bytes_wide(d)
-      uint2* out = reinterpret_cast<uint2*>(challenges + 8ull * (kTrChallenges * b + idx));
-      out[q] = make_uint2(q == 0 ? c.l[0] : q == 1 ? c.l[2] : q == 2 ? c.l[4] : c.l[6],
-                          q == 0 ? c.l[1] : q == 1 ? c.l[3] : q == 2 ? c.l[5] : c.l[7]);
+      if (b < hd.B) {
+        uint2* out = reinterpret_cast<uint2*>(challenges + 8ull * (kTrChallenges * b + idx));
+        out[q] = make_uint2(q == 0 ? c.l[0] : q == 1 ? c.l[2] : q == 2 ? c.l[4] : c.l[6],
+                            q == 0 ? c.l[1] : q == 1 ? c.l[3] : q == 2 ? c.l[5] : c.l[7]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) {
@@ -380,15 +392,193 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
       n2[i] = n3[i];
     }
   }
-  // dflags: the proof decode's flags of this batch (proof-bytes entry), taken
-  // into the status word and cleared for the next batch
-  if (q == 0) {
-    if (dflags) {
-      st |= dflags[b];
-      dflags[b] = 0;
-    }
-    if (status) status[b] = st;
+  return st;
+}
+
+// dflags: the proof decode's flags of this batch (proof-bytes entry), taken
+// into the status word and cleared for the next batch
+__device__ __forceinline__ void tr_finish_status(uint32_t st, uint32_t b, uint32_t* __restrict__ status,
+                                                 uint32_t* __restrict__ dflags) {
+  if (dflags) {
+    st |= dflags[b];
+    dflags[b] = 0;
   }
+  if (status) status[b] = st;
+}
+
+// The per-record kernel (shapes whose stream does not fit the streamed
+// kernel's LDS): 64 lanes = 16 proofs x 4 lanes.
+template <class Cv>
+__global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint32_t* __restrict__ prog,
+                                                   const uint32_t* __restrict__ points,
+                                                   const uint32_t* __restrict__ scalars,
+                                                   uint32_t* __restrict__ challenges, uint32_t* __restrict__ status,
+                                                   uint32_t* __restrict__ dflags) {
+  __shared__ TrBuf buf;
+  const uint32_t slot = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const uint32_t b = blockIdx.x * kTrSlots + slot;
+  if (b >= hd.B) return;
+  const uint32_t st = tr_replay<Cv>(hd, prog, points, scalars, challenges, buf, slot, q, b);
+  if (q == 0) tr_finish_status(st, b, status, dflags);
+}
+
+// ------------------------------------------------------ streamed replay
+// (round 5).  Every proof of a shape absorbs the same byte layout (record
+// tags, the VK record and the squeeze bytes are constants; point and scalar
+// bytes sit at fixed offsets), so the host lays the stream out once
+// (tr_stream_plan): per 32-bit stream word a constant and up to two byte runs
+// of the proof's canonical data.  One block of 4 waves per 16 proofs:
+//   A  all waves stage the proofs' canonical data and the word table in LDS,
+//      then assemble every proof's whole stream in LDS;
+//   B  wave 0 runs the compression chain (quad per proof, as above): the
+//      128-byte blocks in order, and at each squeeze the final compression of
+//      the zero-padded partial block (from the state after the blocks before
+//      it) -- no per-record bookkeeping on the chain (it was about half of
+//      k_transcript's ~0.10 ms);
+//   C  all waves turn the 7 x 16 digests into challenges.
+// A block with an identity point among its proofs (that record is skipped,
+// shifting the stream) runs the per-record replay instead.
+struct TrStreamHdr {
+  uint32_t nw32;     // stream words with content (ceil(bytes / 4))
+  uint32_t nblk;     // 128-byte blocks spanned by the stream
+  uint32_t npr;      // point records in prog (identity check)
+  uint32_t L[kTrChallenges];  // stream length at each squeeze (after its 0x00 byte)
+};
+// wtab: 3 words per stream word (the constant bytes, two parts), then the
+// point index of each point record (identity check).  Part: bit 31 present, 30 region (0 points, 1 scalars), 28-29
+// byte shift in the source word, 26-27 byte position in the stream word,
+// 23-25 byte count, 22 a second source word needed, 0-21 source word index
+constexpr uint32_t kTrPartIdxMask = (1u << 22) - 1u;
+constexpr uint32_t kTrDataStride = kTrSlots + 1;  // LDS data rows [word][slot], padded
+
+// LDS words (u32) of the streamed kernel, and its layout
+struct TrStreamLds {
+  uint32_t oT, oD, oS, oF, oG, oFlag, total;
+  __host__ __device__ TrStreamLds(uint32_t nw32, uint32_t nblk, uint32_t npr, uint32_t npts, uint32_t nsc) {
+    oT = 0;                                               // word table (3 per stream word), point records
+    oD = (3 * nw32 + npr + 1) & ~1u;                      // canonical data [word][17]
+    oS = (oD + kTrDataStride * (16 * npts + 8 * nsc) + 1) & ~1u;  // stream [w64][16] (u64)
+    oF = oS + 2 * kTrSlots * 16 * nblk;                   // final block [16][16] (u64)
+    oG = oF + 2 * kTrSlots * 16;                          // digests [7][16 slots][16]
+    oFlag = oG + kTrChallenges * kTrSlots * 16;
+    total = oFlag + 1;
+  }
+};
+
+template <class Cv>
+__global__ void __launch_bounds__(256) k_transcript_s(TranscriptHdr hd, TrStreamHdr sh,
+                                                     const uint32_t* __restrict__ prog,
+                                                     const uint32_t* __restrict__ wtab,
+                                                     const uint32_t* __restrict__ points,
+                                                     const uint32_t* __restrict__ scalars,
+                                                     uint32_t* __restrict__ challenges,
+                                                     uint32_t* __restrict__ status, uint32_t* __restrict__ dflags) {
+  using Fs = typename Cv::Scalar;
+  extern __shared__ __align__(16) uint32_t tr_lds[];
+  const TrStreamLds lay(sh.nw32, sh.nblk, sh.npr, hd.npts, hd.nsc);
+  uint32_t* const T = tr_lds + lay.oT;
+  uint32_t* const D = tr_lds + lay.oD;
+  uint64_t* const S = reinterpret_cast<uint64_t*>(tr_lds + lay.oS);
+  uint32_t* const G = tr_lds + lay.oG;
+  uint32_t* const flag = tr_lds + lay.oFlag;
+  const uint32_t tid = threadIdx.x, b0 = blockIdx.x * kTrSlots;
+  const uint32_t ndp = 16 * hd.npts, nd = ndp + 8 * hd.nsc;  // data words per proof
+  // --- A1: the word table and the 16 proofs' canonical data into LDS
+  if (tid == 0) *flag = 0;
+  for (uint32_t f = tid; f < 3 * sh.nw32 + sh.npr; f += blockDim.x) T[f] = wtab[f];
+  for (uint32_t f = tid; f < kTrSlots * (nd / 4); f += blockDim.x) {
+    const uint32_t sl = f / (nd / 4), w = 4 * (f - sl * (nd / 4)), b = b0 + sl;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (b < hd.B)
+      v = w < ndp ? *reinterpret_cast<const uint4*>(points + (size_t)ndp * b + w)
+                  : *reinterpret_cast<const uint4*>(scalars + (size_t)(nd - ndp) * b + (w - ndp));
+    D[(w + 0) * kTrDataStride + sl] = v.x;
+    D[(w + 1) * kTrDataStride + sl] = v.y;
+    D[(w + 2) * kTrDataStride + sl] = v.z;
+    D[(w + 3) * kTrDataStride + sl] = v.w;
+  }
+  __syncthreads();
+  // --- A2: the streams (item = (word, slot), slot fastest), and the identity check
+  uint32_t* const S32 = reinterpret_cast<uint32_t*>(S);
+  for (uint32_t f = tid; f < kTrSlots * 32 * sh.nblk; f += blockDim.x) {
+    const uint32_t w = f / kTrSlots, sl = f - w * kTrSlots;
+    uint32_t v = 0;
+    if (w < sh.nw32) {
+      v = T[3 * w];
+#pragma unroll
+      for (int k = 1; k <= 2; k++) {
+        const uint32_t pt = T[3 * w + k];
+        if (pt >> 31) {
+          const uint32_t idx = (pt & kTrPartIdxMask) + (((pt >> 30) & 1u) ? ndp : 0u);
+          const uint32_t lo = D[idx * kTrDataStride + sl];
+          const uint32_t hi = ((pt >> 22) & 1u) ? D[(idx + 1) * kTrDataStride + sl] : 0u;
+          const uint32_t sh8 = 8 * ((pt >> 28) & 3u), p8 = 8 * ((pt >> 26) & 3u), n = (pt >> 23) & 7u;
+          const uint32_t dv = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh8);
+          const uint32_t mask = n >= 4 ? ~0u : (1u << (8 * n)) - 1u;
+          v |= (dv & mask) << p8;
+        }
+      }
+    }
+    S32[2 * ((w >> 1) * kTrSlots + sl) + (w & 1)] = v;
+  }
+  for (uint32_t f = tid; f < kTrSlots * sh.npr; f += blockDim.x) {
+    const uint32_t r = f / kTrSlots, sl = f - r * kTrSlots;
+    const uint32_t idx = 16 * T[3 * sh.nw32 + r];
+    uint32_t z = 0;
+    for (int i = 0; i < 16; i++) z |= D[(idx + i) * kTrDataStride + sl];
+    if (z == 0 && b0 + sl < hd.B) atomicOr(flag, 1u);
+  }
+  __syncthreads();
+  const bool slow = *flag != 0;
+  // --- B: wave 0, a quad per proof
+  if (tid < 64) {
+    const uint32_t slot = tid >> 2, q = tid & 3, b = b0 + slot;
+    uint32_t st = 0;
+    if (slow) {
+      st = tr_replay<Cv>(hd, prog, points, scalars, challenges, *reinterpret_cast<TrBuf*>(tr_lds), slot, q, b);
+    } else {
+      uint64_t h0 = q == 0 ? hd.h0[0] : q == 1 ? hd.h0[1] : q == 2 ? hd.h0[2] : hd.h0[3];
+      uint64_t h1 = q == 0 ? hd.h0[4] : q == 1 ? hd.h0[5] : q == 2 ? hd.h0[6] : hd.h0[7];
+      const uint64_t* col = S + slot;
+      uint64_t* fin = S + 16 * kTrSlots * sh.nblk + slot;  // the final-block rows
+      uint32_t done = 0;
+      for (uint32_t k = 0; k < kTrChallenges; k++) {
+        const uint32_t L = sh.L[k], m = (L + 127) / 128 - 1;  // blocks compressed before the final one
+        for (; done < m; done++) tr_compress_q(h0, h1, TrStreamMsg{col, 16 * done}, q, 128ull * (done + 1), false);
+        // block m zero-padded after byte L (every lane of the quad writes the
+        // same 16 words, so each lane reads back only its own stores)
+        const uint32_t lim = L - 128 * m;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++) {
+          const uint64_t v = col[(16 * m + i) * kTrSlots];
+          const uint32_t lo = 8 * i;
+          fin[i * kTrSlots] = lo + 8 <= lim ? v : lo >= lim ? 0ull : v & ((1ull << (8 * (lim - lo))) - 1ull);
+        }
+        uint64_t f0 = h0, f1 = h1;
+        tr_compress_q(f0, f1, TrStreamMsg{fin, 0}, q, (uint64_t)L, true);
+        uint32_t d[16];
+        tr_digest_q(f0, f1, d);
+        uint32_t* g = G + 16 * (k * kTrSlots + slot);
+#pragma unroll
+        for (int i = 0; i < 4; i++) g[4 * q + i] = d[4 * q + i];
+      }
+    }
+    if (q == 0 && b < hd.B) tr_finish_status(st, b, status, dflags);
+  }
+  __syncthreads();
+  // --- C: challenges = from_bytes_wide(digest), 7 x 16 items over the block
+  if (!slow)
+    for (uint32_t f = tid; f < kTrChallenges * kTrSlots; f += blockDim.x) {
+      const uint32_t k = f / kTrSlots, sl = f - k * kTrSlots, b = b0 + sl;
+      if (b >= hd.B) continue;
+      uint32_t d[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) d[i] = G[16 * (k * kTrSlots + sl) + i];
+      const Fe<Fs> c = fe_from_bytes_wide<Fs>(d);
+      uint4* out = reinterpret_cast<uint4*>(challenges + 8ull * (kTrChallenges * b + k));
+      out[0] = make_uint4(c.l[0], c.l[1], c.l[2], c.l[3]);
+      out[1] = make_uint4(c.l[4], c.l[5], c.l[6], c.l[7]);
+    }
 }
 
 }  // namespace pm

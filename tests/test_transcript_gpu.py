@@ -54,6 +54,25 @@ def test_random_transcripts_vs_oracle(gpu_ctx, cid, shape):
         assert np.array_equal(ch[b], np.array([A.to_limbs_mont(C.r, c) for c in want], dtype=np.uint64)), b
 
 
+def test_streamed_and_record_blocks_mixed(gpu_ctx):
+    """k_transcript_s: a block of 16 proofs with an identity commitment (its
+    record is skipped, so the stream shifts) runs the per-record replay while
+    the other blocks run the streamed chain; every proof against the oracle."""
+    C, sh, proofs = U.make_case(2, "simple", 10, 40, 0x7C9)
+    k, _ = sh.point_offsets()["adv"]
+    proofs[20].points[k] = None                    # block 1
+    ps = U.to_product_shape(2, sh)
+    vkr = T.vk_repr(C.r, b"vk-mixed")
+    vk = np.array(A.to_limbs_mont(C.r, vkr), dtype=np.uint64)
+    pts, scs, _ = A.pack_proofs(C, sh, proofs)
+    ch, st = gpu_ctx.transcript_batch(ps, pts, scs, vk)
+    assert st.tolist() == [1 if b == 20 else 0 for b in range(40)]
+    for b in range(40):
+        want, skipped = T.replay_challenges(C, sh, proofs[b], vkr)
+        assert skipped == (b == 20)
+        assert np.array_equal(ch[b], np.array([A.to_limbs_mont(C.r, c) for c in want], dtype=np.uint64)), b
+
+
 def test_accum_with_replayed_challenges(gpu_ctx):
     """Transcript + accumulator in one call == oracle accumulate on the
     transcript's challenges; also == pm_accum_batch fed those challenges."""

@@ -76,7 +76,9 @@ __global__ void __launch_bounds__(64) k_chain(uint32_t* out, int iters, const Sq
                                   s_kidx);
       x = ok ? r : f29_sqr_c<F>(x);
     }
-    if (V == 9) tr_compress_q(ln, buf, threadIdx.x >> 2, threadIdx.x & 3, (uint32_t)k & 15, 128 * (k + 1), false);
+    if (V == 9)
+      tr_compress_q(ln.h0, ln.h1, TrRingMsg{buf, threadIdx.x >> 2, (uint32_t)k & 15}, threadIdx.x & 3, 128 * (k + 1),
+                    false);
   }
   uint32_t s = acc ^ (uint32_t)ln.h0 ^ fa.l[0];
   for (int i = 0; i < 9; i++) s ^= j.X.l[i] ^ a.X.l[i] ^ x.l[i];
