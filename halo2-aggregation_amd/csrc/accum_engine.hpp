@@ -6,6 +6,7 @@
 // + MultiopenChip::calc_witness (/root/reference/src/verifier.rs:512-733,
 // src/multiopen.rs:271-509).
 #pragma once
+#include <functional>
 #include <vector>
 #include <hip/hip_ext.h>
 
@@ -71,6 +72,9 @@ constexpr size_t kAccScalarsLds = 152 * 1024;
 // a SIMD with a ladder wave doubled k_acc_scalars (0.14 -> 0.27 ms at
 // B = 256).
 constexpr size_t kAccLadderFence = 40 * 1024;
+// (the quad ladder takes kAccSlicedFence, one block per CU, while its grid fits
+// the CUs: beside the twisted ladder's decode on the other stream its blocks
+// were otherwise packed two or three per CU, B = 256 ladder 0.27 -> 0.68 ms)
 // row-sliced ladder (k_acc_powers_s) up to this many chains: one wave each,
 // four per block and one block per CU (kAccSlicedFence), leaving CUs for the
 // side stream's transcript / k_acc_scalars blocks (which a ladder block on
@@ -91,13 +95,43 @@ inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
   return lg;
 }
 
+// static LDS of a decode instantiation (the fence is the block's total)
+template <class Cv, bool SLICED>
+size_t decode_static_lds() {
+  static const size_t v = [] {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_proof_decode<Cv, SLICED>)) == hipSuccess
+               ? (size_t)a.sharedSizeBytes
+               : kDecodeStaticLds;  // the non-sliced arrays: an upper bound
+  }();
+  return v;
+}
+
+// The proof-bytes entry's square-root decode (proof_kernels.hpp), launched
+// by accum_device_impl on the stream (and with the LDS fence) it picks:
+// beside the twisted ladder on the reduction stream when the powers tables
+// are built (the ladder needs only the proofs' x bytes, acc_chain_start),
+// else first on the main stream.  off_of: the byte offset within a proof of
+// every point index read from the bytes (kAccNoByte: instance commitments).
+struct AccDecode {
+  std::function<int(hipStream_t, size_t)> launch;  // (stream, LDS fence bytes)
+  const void* proofs;
+  size_t stride;
+  const void* inst;
+  std::vector<uint32_t> off_of;
+};
+// a decode block beside a ladder block would share its SIMDs (both are
+// issue-bound lone-wave chains): its LDS request keeps it off any CU holding
+// a ladder block (sliced 84 KiB, quad 40 KiB) or a side-stream block
+constexpr size_t kDecodeFence = 124 * 1024;
+
 // vk_repr != nullptr: the challenges are first replayed into d_ch on the
 // device (transcript_device_impl); the split ladder then runs concurrently
 // with the replay and k_acc_scalars on the reduction stream.
 template <class Cv>
 int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d_points, const void* d_scalars,
                       void* d_ch, void* d_out, void* d_hout, const uint64_t* vk_repr, void* d_status,
-                      bool canon_ready = false, uint32_t* dflags = nullptr, hipEvent_t inputs_ready = nullptr) {
+                      bool canon_ready = false, uint32_t* dflags = nullptr, const AccDecode* dec = nullptr) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   std::vector<AccQuery> q;
@@ -204,6 +238,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   prog.insert(prog.end(), psrc.begin(), psrc.end());
   h.p_rank = (uint32_t)prog.size();
   prog.insert(prog.end(), rank.begin(), rank.end());
+  h.p_pbyte = (uint32_t)prog.size();
+  if (dec) {
+    for (uint32_t idx : psrc) prog.push_back(idx < dec->off_of.size() ? dec->off_of[idx] : kAccNoByte);
+    h.pstride = (uint32_t)dec->stride;
+    h.ninst = s->num_instance_columns;
+  }
 
   // --- constants (Montgomery)
   std::vector<uint32_t> cst;
@@ -260,10 +300,6 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   if ((rc = ctx->acc_prog.put(prog, st))) return rc;
   if ((rc = ctx->acc_const.put(cst, st, 32))) return rc;
   if ((rc = ctx->acc_vk.put(vk, st))) return rc;
-  // a shape / VK / constants change re-sends these behind the caller's
-  // inputs_ready point on st: the side stream must then wait for the copies
-  // too, not only for the decode (k_acc_scalars reads dprog and acc_const)
-  if (ctx->acc_prog.sent || ctx->acc_const.sent || ctx->acc_vk.sent) inputs_ready = nullptr;
   if ((rc = ctx->acc_coef.ensure((size_t)B * T * 32))) return rc;
   if ((rc = ctx->acc_part.ensure((size_t)B * T * sizeof(Xyzz<F>)))) return rc;
   const uint32_t* dprog = (const uint32_t*)ctx->acc_prog.buf.p;
@@ -299,6 +335,16 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // cross-stream wake-up on the critical path (profiles/r01_s4/ktrace_*).
   hipStream_t side = st;
   hipEvent_t up = nullptr, sc_done = nullptr;
+  // proof bytes with the powers tables: the ladder runs on the twist from the
+  // x bytes on the reduction stream, beside the decode -> replay -> scalar
+  // block chain on the main stream, which is then the critical one and has no
+  // cross-stream hop (AccDecode; PM_ACC_TWIST=0: the ladder after the decode)
+  static const bool twist_on = [] {
+    const char* e = getenv("PM_ACC_TWIST");
+    return !(e && *e == '0');
+  }();
+  h.twist = dec && lgS > 0 && twist_on ? 1u : 0u;
+  if (h.twist && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4)))) return rc;
   std::vector<uint64_t> built_key;  // VK tables built by this call (committed after its final sync)
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
     const size_t tab = (size_t)kPowPos * kPowPoint * sizeof(uint4), nvk = vk.size() / 8;
@@ -311,25 +357,30 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     key.push_back((uint64_t)F::MOD[1] << 32 | F::MOD[2]);  // the curve (its base field)
     const bool vk_current = ctx->acc_vkpow_gen == ctx->acc_vkpow.gen && ctx->acc_vkpow_key == key;
     const uint32_t nvk_build = vk_current ? 0u : (uint32_t)nvk;
-    // inputs_ready: the proof decode's own completion event (proof-bytes
-    // entry), so no marker sits between the decode and the ladder
-    up = inputs_ready ? inputs_ready : ctx->next_event();
+    // up: the inputs and uploads (programs, constants, the decoder's map)
+    // are complete; the other stream starts from it
+    up = ctx->next_event();
     sc_done = ctx->next_event();
     if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
-    if (!inputs_ready) HIP_TRY(hipEventRecord(up, st));
+    HIP_TRY(hipEventRecord(up, st));
+    const hipStream_t lst = h.twist ? ctx->red_stream : st;  // the ladder's stream
+    if (h.twist) HIP_TRY(hipStreamWaitEvent(lst, up, 0));
+    const uint32_t* lproofs = h.twist ? (const uint32_t*)dec->proofs : nullptr;
+    const uint32_t* linst = h.twist ? (const uint32_t*)dec->inst : nullptr;
     // few chains: one row-sliced wave per chain (slice29.hpp, ~2x shorter
     // steps while the waves fit one per SIMD); more: a quad per chain
     const size_t chains = nprf + nvk_build;
     const bool sliced = ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1 : chains <= kAccSlicedChains;
     if (chains > 0 && sliced)
-      PM_LAUNCH(ctx, "acc_ladder",
-                (k_acc_powers_s<Cv><<<(unsigned)((chains + 3) / 4), 256, kAccSlicedFence, st>>>(
-                    h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
+      PM_LAUNCH_ST(ctx, lst, "acc_ladder",
+                (k_acc_powers_s<Cv><<<(unsigned)((chains + 3) / 4), 256, kAccSlicedFence, lst>>>(
+                    h, dprog, (const uint32_t*)d_points, lproofs, linst, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
                     (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
     else if (chains > 0)
-      PM_LAUNCH(ctx, "acc_ladder",
-                (k_acc_powers<Cv><<<(unsigned)((4 * chains + 255) / 256), 256, kAccLadderFence, st>>>(
-                    h, dprog, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
+      PM_LAUNCH_ST(ctx, lst, "acc_ladder",
+                (k_acc_powers<Cv><<<(unsigned)((4 * chains + 255) / 256), 256,
+                                    4 * chains <= 256 * 256 ? kAccSlicedFence : kAccLadderFence, lst>>>(
+                    h, dprog, (const uint32_t*)d_points, lproofs, linst, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
                     (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
     if (!vk_current) {
       // the tables count as built only once this call's work has completed
@@ -338,9 +389,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
       ctx->acc_vkpow_key.clear();
       built_key.swap(key);
     }
-    side = ctx->red_stream;
-    HIP_TRY(hipStreamWaitEvent(side, up, 0));
+    if (!h.twist) {
+      side = ctx->red_stream;
+      HIP_TRY(hipStreamWaitEvent(side, up, 0));
+    }
   }
+  if (dec && (rc = dec->launch(side, h.twist ? kDecodeFence : 0))) return rc;
   if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side,
                                              canon_ready, dflags)))
     return rc;
@@ -362,16 +416,20 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
                    h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
                    dcoef, (uint32_t*)d_hout, np, (uint32_t*)d_status)));
   if (lgS > 0) {
-    HIP_TRY(hipEventRecord(sc_done, side));
+    // the term additions wait for the other stream: the scalar block (side),
+    // or with the twist the ladder
+    HIP_TRY(hipEventRecord(sc_done, h.twist ? ctx->red_stream : side));
     HIP_TRY(hipStreamWaitEvent(st, sc_done, 0));
     if (quad_terms)
       PM_LAUNCH(ctx, "acc_termmul",
                 (k_acc_termadd<Cv, true><<<(unsigned)((nterm * 64 + 255) / 256), 256, 0, st>>>(
-                    h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p, lgT, dpart)));
+                    h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p,
+                    (const uint4*)ctx->acc_corr.p, lgT, dpart)));
     else
       PM_LAUNCH(ctx, "acc_termmul",
                 (k_acc_termadd<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
-                    h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p, lgS, dpart)));
+                    h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p,
+                    (const uint4*)ctx->acc_corr.p, lgS, dpart)));
   } else {
     PM_LAUNCH(ctx, "acc_termmul",
               (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
@@ -641,39 +699,36 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   h.nblk_pts = (uint32_t)((B * npp + per_blk - 1) / per_blk);
   const size_t nblk_sc = (B * ((size_t)L.nsc + ninst) + kDecodeThreads - 1) / kDecodeThreads;
   if (stride > 0xffffffffull) return set_error(PM_ERR_UNSUPPORTED, "proof stride above 4 GiB");
-  // untimed calls launch the decode with its completion event attached to the
-  // dispatch (hipExtLaunchKernel): the side stream waits on it, and the ladder
-  // follows the decode directly instead of behind an event-record marker
-  hipEvent_t dec_done = nullptr;
-  if (vk_repr && !ctx->timing) {
-    dec_done = ctx->next_event();
-    if (!dec_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+  AccDecode dec;
+  dec.proofs = d_proofs;
+  dec.stride = stride;
+  dec.inst = d_inst;
+  dec.off_of.assign(L.npts, kAccNoByte);
+  for (size_t i = 0; i + 1 < map.size(); i += 2) dec.off_of[map[i + 1]] = map[i];
+  const SqrtTab* tabp = (const SqrtTab*)ctx->sqrt_tab[slot].p;
+  const uint32_t* dmap = (const uint32_t*)ctx->pf_map.buf.p;
+  dec.launch = [=](hipStream_t dst, size_t fence) -> int {
+    // the fence is the whole block's LDS (the kernel's static arrays count);
+    // a fenced decode runs beside the twisted ladder and writes its factors
+    // (acc_corr, sized by accum_device_impl before it launches this)
     auto kern = sliced ? k_proof_decode<Cv, true> : k_proof_decode<Cv, false>;
-    hipExtLaunchKernelGGL(kern, dim3((unsigned)(h.nblk_pts + nblk_sc)), dim3(kDecodeThreads), 0, st,
-                          nullptr, dec_done, 0, h, (const SqrtTab*)ctx->sqrt_tab[slot].p,
-                          (const uint32_t*)ctx->pf_map.buf.p, (const uint32_t*)d_proofs, (const uint32_t*)d_inst,
-                          (uint32_t*)d_points, (uint32_t*)d_scalars, cpts, cscs, dflags);
-    HIP_TRY(hipGetLastError());
-  } else if (sliced) {
-    PM_LAUNCH(ctx, "proof_decode",
-              (k_proof_decode<Cv, true><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
-                  h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
-                  (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
-                  cscs, dflags)));
-  } else {
-    PM_LAUNCH(ctx, "proof_decode",
-              (k_proof_decode<Cv, false><<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, 0, st>>>(
-                  h, (const SqrtTab*)ctx->sqrt_tab[slot].p, (const uint32_t*)ctx->pf_map.buf.p,
-                  (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points, (uint32_t*)d_scalars, cpts,
-                  cscs, dflags)));
-  }
+    const size_t stat = sliced ? decode_static_lds<Cv, true>() : decode_static_lds<Cv, false>();
+    const size_t dyn = fence > stat ? fence - stat : 0;
+    uint4* cp = fence ? (uint4*)ctx->acc_corr.p : nullptr;
+    PM_LAUNCH_ST(ctx, dst, "proof_decode",
+                 (kern<<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, dyn, dst>>>(
+                     h, tabp, dmap, (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points,
+                     (uint32_t*)d_scalars, cpts, cscs, dflags, cp)));
+    return PM_OK;
+  };
   if (!vk_repr) {
+    if ((rc = dec.launch(st, 0))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     ctx->end_call();
     return PM_OK;
   }
   rc = accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, dflags,
-                             dec_done);
+                             &dec);
   if (rc == PM_OK) ctx->pf_flags_dirty = false;  // k_transcript has cleared every word
   return rc;
 }

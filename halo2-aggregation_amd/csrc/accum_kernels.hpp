@@ -47,7 +47,16 @@ struct AccumHdr {
   // point indices in slot order (Tp words); p_rank: T words, term t's rank
   // among the proof-point terms (VK terms read the per-VK tables instead)
   uint32_t Tp, p_psrc, p_rank;
+  // proof-bytes entry (round 5): twist = 1 makes the ladders read each proof
+  // point's x from the proof bytes (p_pbyte: Tp words, the byte offset of
+  // term tp's point in a proof, kAccNoByte for an instance commitment, read
+  // affine from inst) and run on the twist E_A (acc_chain_start), so they need
+  // no decoded points; k_acc_termadd maps its sums back to the curve with the
+  // decoder's factors (A, y A) per point
+  uint32_t twist, p_pbyte, pstride, ninst;
 };
+constexpr uint32_t kAccNoByte = 0xffffffffu;
+constexpr uint32_t kAccCorrWords = 6;  // uint4 per point in the correction table: A, y A (pow_st layout)
 
 template <class Fs>
 __device__ __forceinline__ Fe<Fs> ldfe(const uint32_t* base, uint32_t idx) {
@@ -574,12 +583,59 @@ __device__ __forceinline__ void pow_store(uint4* o, const PowSites& ps, const Ja
   pow_st<F>(o + ps.ext, ext);
 }
 
+// Start point of chain g < nprf + nvk as canonical R = 2^261 coordinates.
+// Affine input (points / inst / vk, Rust R = 2^256 Montgomery): (x, y), inf
+// for (0, 0).  From the proof bytes (h.twist): with A = x^3 + b, the point
+// P_A = (A x, A^2) of E_A: y^2 = x^3 + A^3 b.  psi(X, Y) = (X / A, y0 Y / A^2)
+// (y0 = sqrt(A), the decoded y) maps E_A onto the curve as a group
+// isomorphism that commutes with phi (beta x, y), and doublings and additions
+// never use b, so the ladder's table of E_A multiples is the curve's under
+// psi; in XYZZ psi only scales ZZ by A and ZZZ by y0 A (y0^2 = A), which
+// k_acc_termadd applies to each term's sum.  The chain thus needs only x: it
+// runs beside the square-root decode instead of after it.  (An invalid x
+// gives a meaningless chain; the decoder flags that proof.)
+template <class Cv>
+__device__ __forceinline__ void acc_chain_start(const AccumHdr& h, const uint32_t* __restrict__ prog,
+                                                const uint32_t* __restrict__ points,
+                                                const uint32_t* __restrict__ proofs,
+                                                const uint32_t* __restrict__ inst, const uint32_t* __restrict__ vk,
+                                                uint32_t g, F29<typename Cv::Base>& x, F29<typename Cv::Base>& y,
+                                                bool& inf) {
+  using F = typename Cv::Base;
+  const uint32_t nprf = h.B * h.Tp;
+  const uint32_t* pp;
+  if (g < nprf) {
+    const uint32_t b = g / h.Tp, tp = g - b * h.Tp, idx = prog[h.p_psrc + tp];
+    const uint32_t off = h.twist ? prog[h.p_pbyte + tp] : kAccNoByte;
+    if (off != kAccNoByte) {
+      const uint4* src = reinterpret_cast<const uint4*>(proofs + ((size_t)b * h.pstride + off) / 4);
+      const uint4 lo = src[0], hi = src[1];
+      const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w & 0x7fffffffu};
+      const F29<F> X = f29_mul_c<F>(f29_unpack<F>(w), f29_const<F>(F29Consts<F>::R522));  // < 2p
+      const F29<F> A = f29_norm<F>(f29_add<F>(f29_mul_c<F>(f29_sqr_c<F>(X), X), f29_const<F>(Glv<Cv>::B29)));
+      x = f29_canon<F>(f29_reduce3<F>(f29_mul_c<F>(A, X)));
+      y = f29_canon<F>(f29_reduce3<F>(f29_sqr_c<F>(A)));
+      inf = false;
+      return;
+    }
+    pp = h.twist ? inst + 16ull * ((size_t)h.ninst * b + idx) : points + 16ull * ((size_t)h.npts * b + idx);
+  } else {
+    pp = vk + 16ull * (g - nprf);
+  }
+  const Aff<F> P = load_aff<F>(pp);
+  inf = aff_is_inf<F>(P);
+  x = f29_canon<F>(f29_from_r256<F>(P.x.l));
+  y = f29_canon<F>(f29_from_r256<F>(P.y.l));
+}
+
 // Quad g < B Tp: proof b's proof-point term of rank tp (g = b Tp + tp) -> pw;
 // quad B Tp + v (v < nvk): VK point v -> pwv, the per-VK tables shared by
 // every proof of this and later batches (nvk = 0 when they are current).
 template <class Cv>
 __global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* __restrict__ prog,
                                                     const uint32_t* __restrict__ points,
+                                                    const uint32_t* __restrict__ proofs,
+                                                    const uint32_t* __restrict__ inst,
                                                     const uint32_t* __restrict__ vk, uint32_t nvk,
                                                     uint4* __restrict__ pw, uint4* __restrict__ pwv) {
   using F = typename Cv::Base;
@@ -588,26 +644,18 @@ __global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* 
   const uint32_t g = gl >> 2, q = gl & 3u;
   const uint32_t nprf = h.B * h.Tp;
   if (g >= nprf + nvk) return;  // whole quads
-  const uint32_t* pp;
-  uint4* out;
-  if (g < nprf) {
-    const uint32_t b = g / h.Tp, tp = g - b * h.Tp;
-    pp = points + 16ull * ((size_t)h.npts * b + prog[h.p_psrc + tp]);
-    out = pw + (size_t)g * kPowPos * kPowPoint;
-  } else {
-    pp = vk + 16ull * (g - nprf);
-    out = pwv + (size_t)(g - nprf) * kPowPos * kPowPoint;
-  }
-  const Aff<F> P = load_aff<F>(pp);
+  uint4* out = g < nprf ? pw + (size_t)g * kPowPos * kPowPoint : pwv + (size_t)(g - nprf) * kPowPos * kPowPoint;
+  F29<F> px, py;
+  bool inf;
+  acc_chain_start<Cv>(h, prog, points, proofs, inst, vk, g, px, py, inf);
   const PowSites ps(q);
   const F29<F> one = f29_const<F>(K::ONE);
-  if (aff_is_inf<F>(P)) {  // the identity (ZZ = 0) at every power
+  if (inf) {  // the identity (ZZ = 0) at every power
     const F29<F> zero = f29_zero<F>();
     for (uint32_t j = 0; j < kPowPos; j++) pow_store<F>(out + j * kPowPoint, ps, Jac29<F>{one, one, one}, zero, one);
     return;
   }
   const F29<F> beta = f29_const<F>(Glv<Cv>::BETA29);
-  const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
   Jac29<F> cur{px, py, one};
   pow_store<F>(out, ps, cur, one, q == 0u ? f29_mul_c<F>(beta, px) : one);
   for (uint32_t j = 1; j < kPowPos; j++) {
@@ -637,22 +685,15 @@ __global__ void __launch_bounds__(256) k_acc_powers(AccumHdr h, const uint32_t* 
 template <class Cv>
 __global__ void __launch_bounds__(256) k_acc_powers_s(AccumHdr h, const uint32_t* __restrict__ prog,
                                                     const uint32_t* __restrict__ points,
+                                                    const uint32_t* __restrict__ proofs,
+                                                    const uint32_t* __restrict__ inst,
                                                     const uint32_t* __restrict__ vk, uint32_t nvk,
                                                     uint4* __restrict__ pw, uint4* __restrict__ pwv) {
   using F = typename Cv::Base;
   const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
   const uint32_t nprf = h.B * h.Tp;
   if (g >= nprf + nvk) return;
-  const uint32_t* pp;
-  uint4* out;
-  if (g < nprf) {
-    const uint32_t b = g / h.Tp, tp = g - b * h.Tp;
-    pp = points + 16ull * ((size_t)h.npts * b + prog[h.p_psrc + tp]);
-    out = pw + (size_t)g * kPowPos * kPowPoint;
-  } else {
-    pp = vk + 16ull * (g - nprf);
-    out = pwv + (size_t)(g - nprf) * kPowPos * kPowPoint;
-  }
+  uint4* out = g < nprf ? pw + (size_t)g * kPowPos * kPowPoint : pwv + (size_t)(g - nprf) * kPowPos * kPowPoint;
   const uint32_t row = s_rowid(), l = s_lane();
   const bool limb = l < 9u;
   uint32_t* o32 = reinterpret_cast<uint32_t*>(out) + l;  // + position * kPowPoint * 4 + coordinate * 12
@@ -661,8 +702,10 @@ __global__ void __launch_bounds__(256) k_acc_powers_s(AccumHdr h, const uint32_t
   const uint32_t site1 = (row == 0 ? 0u : row == 1 ? 1u : row == 3 ? 2u : 5u) * kCoordW;
   const uint32_t site2 = (row == 0 ? 4u : row == 3 ? 3u : 5u) * kCoordW;
   const SConst<F> k = SConst<F>::make();
-  const Aff<F> P = load_aff<F>(pp);
-  if (aff_is_inf<F>(P)) {  // the identity (ZZ = 0) at every power, as k_acc_powers stores it
+  F29<F> px, py;
+  bool inf;
+  acc_chain_start<Cv>(h, prog, points, proofs, inst, vk, g, px, py, inf);
+  if (inf) {  // the identity (ZZ = 0) at every power, as k_acc_powers stores it
     const uint32_t v1 = row == 3 ? 0u : k.one;
     for (uint32_t j = 0; j < kPowPos; j++)
       if (limb) {
@@ -674,8 +717,8 @@ __global__ void __launch_bounds__(256) k_acc_powers_s(AccumHdr h, const uint32_t
   const uint32_t m0 = row == 0 ? ~0u : 0u, m1 = row == 1 ? ~0u : 0u, m2 = row == 2 ? ~0u : 0u,
                  m3 = row == 3 ? ~0u : 0u;
   const S29<F> beta{s_limbs(Glv<Cv>::BETA29)};
-  S29<F> X = s29_from<F>(f29_canon<F>(f29_from_r256<F>(P.x.l)));
-  S29<F> Y = s29_from<F>(f29_canon<F>(f29_from_r256<F>(P.y.l)));
+  S29<F> X = s29_from<F>(px);
+  S29<F> Y = s29_from<F>(py);
   S29<F> Z{k.one};
   {  // position 0: (x, y, 1, 1, beta x)
     const S29<F> bx = s29_norm_exact<F>(s29_mul<F>(beta, X, k));
@@ -757,7 +800,8 @@ template <class Cv, bool QUAD = false>
 __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t* __restrict__ prog,
                                                      const uint32_t* __restrict__ coef,
                                                      const uint4* __restrict__ pw, const uint4* __restrict__ pwv,
-                                                     uint32_t lgS, Xyzz<typename Cv::Base>* __restrict__ part) {
+                                                     const uint4* __restrict__ corr, uint32_t lgS,
+                                                     Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
   const uint32_t gl = (blockIdx.x * blockDim.x + threadIdx.x) >> (QUAD ? 2 : 0);  // lane or quad
@@ -829,6 +873,11 @@ __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t*
     acc = QUAD ? xyzz29_add_q<F>(acc, o) : xyzz29_add<F>(acc, o);
   }
   if (j == 0 && (!QUAD || (threadIdx.x & 3u) == 0)) {  // a sum of one table point is that point, possibly unreduced
+    if (h.twist && (src >> 28) == 0) {  // psi: E_A -> the curve (acc_chain_start)
+      const uint4* c = corr + ((size_t)b * h.npts + (src & 0x0FFFFFFFu)) * kAccCorrWords;
+      acc.ZZ = f29_mul_c<F>(acc.ZZ, pow_ld<F>(c));
+      acc.ZZZ = f29_mul_c<F>(acc.ZZZ, pow_ld<F>(c + kPowWords));
+    }
     acc.X = f29_reduce3<F>(f29_norm<F>(acc.X));
     acc.Y = f29_reduce3<F>(f29_norm<F>(acc.Y));
     store_xyzz29<F>(&part[g], acc);

@@ -44,6 +44,7 @@ template <> struct F29Consts<PallasFp> {
   static constexpr uint32_t INV = 0x1fffffffu;  // -p^-1 mod 2^29
   static constexpr uint32_t ONE[9] = {0x1fffff81u, 0x14a5d367u, 0x141ad3c0u, 0x1435eec5u, 0x1ffeefefu, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // 2^261 mod p
   static constexpr uint32_t TO261[9] = {0x1ffff001u, 0x10f30767u, 0x0ecfe231u, 0x0db0ce73u, 0x1fddbb8bu, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // 2^266 mod p: R256 -> R261
+  static constexpr uint32_t R522[9] = {0x00003b6au, 0x19c10910u, 0x1a6a0188u, 0x12a4fd88u, 0x0634b36du, 0x178792bau, 0x07797a99u, 0x1dce5b8au, 0x003506bdu};  // 2^522 mod p: canonical -> R261
   static constexpr uint32_t TO256[9] = {0x1ffffffdu, 0x03c369c7u, 0x06452b4du, 0x186a17c8u, 0x1ffff992u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // 2^256 mod p: R261 -> R256
   static constexpr uint32_t K2[9] = {0x20000002u, 0x32d30ecfu, 0x267c8dcbu, 0x3a63f024u, 0x20000447u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x007fffffu};  // 2p, limbs >= 2^29 - 1
   static constexpr uint32_t K6[9] = {0x20000006u, 0x38792c6fu, 0x3375a964u, 0x2f2bd06eu, 0x20000cd9u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x017fffffu};  // 6p, limbs >= 2^29 - 1
@@ -57,6 +58,7 @@ template <> struct F29Consts<VestaFp> {
   static constexpr uint32_t INV = 0x1fffffffu;  // -p^-1 mod 2^29
   static constexpr uint32_t ONE[9] = {0x1fffff81u, 0x068ad507u, 0x100e85dau, 0x1435ee7eu, 0x1ffeefefu, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // 2^261 mod p
   static constexpr uint32_t TO261[9] = {0x1ffff001u, 0x0ca6d907u, 0x01b40647u, 0x0db0c57eu, 0x1fddbb8bu, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // 2^266 mod p: R256 -> R261
+  static constexpr uint32_t R522[9] = {0x00003b6au, 0x02b1b550u, 0x1027888au, 0x1ea4ed96u, 0x0418ad7au, 0x000999ebu, 0x17fae231u, 0x1e67ed54u, 0x003506bdu};  // 2^522 mod p: canonical -> R261
   static constexpr uint32_t TO256[9] = {0x1ffffffdu, 0x1959f4e7u, 0x108159d6u, 0x186a17c6u, 0x1ffff992u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // 2^256 mod p: R261 -> R256
   static constexpr uint32_t K2[9] = {0x20000002u, 0x246eb20fu, 0x2a546ec5u, 0x3a63f025u, 0x20000447u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x007fffffu};  // 2p, limbs >= 2^29 - 1
   static constexpr uint32_t K6[9] = {0x20000006u, 0x2d4c162fu, 0x3efd4c51u, 0x2f2bd071u, 0x20000cd9u, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x017fffffu};  // 6p, limbs >= 2^29 - 1
@@ -70,6 +72,7 @@ template <> struct F29Consts<Bn254Fq> {
   static constexpr uint32_t INV = 0x04866389u;  // -p^-1 mod 2^29
   static constexpr uint32_t ONE[9] = {0x157ccc21u, 0x141c2758u, 0x185230d3u, 0x014c0419u, 0x0aa36fb9u, 0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};  // 2^261 mod p
   static constexpr uint32_t TO261[9] = {0x13349ca1u, 0x1a5d84a8u, 0x0a3e5cacu, 0x100249e0u, 0x12b951e8u, 0x0e92d304u, 0x14cb95b3u, 0x041b9d3du, 0x00058003u};  // 2^266 mod p: R256 -> R261
+  static constexpr uint32_t R522[9] = {0x059bac10u, 0x0d1503a3u, 0x018016b8u, 0x10ab0ca8u, 0x02632639u, 0x02c0169fu, 0x169bfd53u, 0x11869d4cu, 0x002a11a6u};  // 2^522 mod p: canonical -> R261
   static constexpr uint32_t TO256[9] = {0x058f0d9du, 0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462c0a7u, 0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};  // 2^256 mod p: R261 -> R256
   static constexpr uint32_t K2[9] = {0x30f9fa8eu, 0x2208c16cu, 0x38e5469du, 0x25aa45a0u, 0x2b0bb2efu, 0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu};  // 2p, limbs >= 2^29 - 1
   static constexpr uint32_t K6[9] = {0x32edefaau, 0x261a4447u, 0x2aafd3d9u, 0x30fed0e4u, 0x212318cfu, 0x31238483u, 0x23e94785u, 0x3628e537u, 0x012259d5u};  // 6p, limbs >= 2^29 - 1

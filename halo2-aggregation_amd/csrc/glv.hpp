@@ -18,6 +18,7 @@ struct Glv;
 // PallasCurve: phi(x, y) = (beta x, y) = [lambda](x, y), lambda = 0x397e65a7d7c1ad71aee24b27e308f0a61259527ec1d4752e619d1840af55f1b1
 template <> struct Glv<PallasCurve> {
   static constexpr uint32_t BETA29[9] = {0x0cbd58ebu, 0x1a2f8f16u, 0x0d140efau, 0x007bdfb9u, 0x1333ecadu, 0x0a33785bu, 0x04eacc49u, 0x09617a1eu, 0x0004ff6cu};  // beta * 2^261 mod p, radix 2^29
+  static constexpr uint32_t B29[9] = {0x1ffffd81u, 0x01970367u, 0x178d072au, 0x1045c991u, 0x1ffaa71cu, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // curve b * 2^261 mod p, radix 2^29
   static constexpr uint32_t BETA[8] = {0x9e65eac8u, 0xfbdfd7aau, 0xe50025fbu, 0x0cd4d654u, 0x3785b99au, 0xd59892a3u, 0x585e8789u, 0x2a27fb62u};  // Montgomery
   static constexpr uint32_t A1[4] = {0x00000000u, 0x8cb12793u, 0x40a89953u, 0x49e69d16u};
   static constexpr uint32_t NB1[4] = {0x00000001u, 0x7fcae1c7u, 0x40f04915u, 0x49e69d16u};  // -b1 > 0
@@ -29,6 +30,7 @@ template <> struct Glv<PallasCurve> {
 // VestaCurve: phi(x, y) = (beta x, y) = [lambda](x, y), lambda = 0x12ccca834acdba712caad5dc57aab1b01d1f8bd237ad31491dad5ebdfdfe4ab9
 template <> struct Glv<VestaCurve> {
   static constexpr uint32_t BETA29[9] = {0x02222437u, 0x00286338u, 0x1ad2e167u, 0x0c255d0eu, 0x16526d7eu, 0x1fb135b2u, 0x0801613au, 0x0220916cu, 0x0003a53fu};  // beta * 2^261 mod p, radix 2^29
+  static constexpr uint32_t B29[9] = {0x1ffffd81u, 0x17d8c507u, 0x1b9fbfb6u, 0x1045c82bu, 0x1ffaa71cu, 0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x003fffffu};  // curve b * 2^261 mod p, radix 2^29
   static constexpr uint32_t BETA[8] = {0x80111122u, 0x7c541a84u, 0x56ed29dau, 0x40630b9cu, 0x135b2b29u, 0x02c275fbu, 0x88245b10u, 0x121d29f8u};  // Montgomery
   static constexpr uint32_t A1[4] = {0x00000000u, 0x7fcae1c7u, 0x40f04915u, 0x49e69d16u};
   static constexpr uint32_t NB1[4] = {0x00000001u, 0x8cb12793u, 0x40a89953u, 0x49e69d16u};  // -b1 > 0
@@ -40,6 +42,7 @@ template <> struct Glv<VestaCurve> {
 // Bn254Curve: phi(x, y) = (beta x, y) = [lambda](x, y), lambda = 0x30644e72e131a029048b6e193fd84104cc37a73fec2bc5e9b8ca0b2d36636f23
 template <> struct Glv<Bn254Curve> {
   static constexpr uint32_t BETA29[9] = {0x18ccb791u, 0x175b1c3au, 0x0b83d6e2u, 0x0e8ed071u, 0x1282bee2u, 0x04220e84u, 0x1fe4017fu, 0x15084d4au, 0x00169119u};  // beta * 2^261 mod p, radix 2^29
+  static constexpr uint32_t B29[9] = {0x00766463u, 0x1c54760au, 0x08f6927au, 0x03e40c4du, 0x1fea4f2bu, 0x17c6c26au, 0x157fe417u, 0x0f8056f9u, 0x002958a2u};  // curve b * 2^261 mod p, radix 2^29
   static constexpr uint32_t BETA[8] = {0x13e80b9cu, 0x3350c88eu, 0xdb5e56b9u, 0x7dce557cu, 0xb615564au, 0x6001b4b8u, 0x020217e0u, 0x2682e617u};  // Montgomery
   static constexpr uint32_t A1[4] = {0x7d4f1128u, 0x8211bbebu, 0xeeb859fcu, 0x6f4d8248u};
   static constexpr uint32_t NB1[4] = {0x94d213e3u, 0x89d32568u, 0x00000000u, 0x00000000u};  // -b1 > 0

@@ -45,6 +45,7 @@
 #include "msm_kernels.hpp"
 #include "slice29.hpp"
 #include "runtime.hpp"
+#include "accum_kernels.hpp"  // acc_chain_start's correction table layout
 
 namespace pm {
 
@@ -358,20 +359,23 @@ struct ProofDecodeHdr {
 // Blocks [0, nblk_pts): one lane per proof point (pt_map[j] = (byte offset /
 // 4) << 8 | destination point index ... as two words: offset, index).
 // Blocks after: one lane per scalar, then per instance commitment.
-constexpr int kDecodeThreads = 64;
+// 256 (round 5, was 64): with the twisted ladder the decode runs beside it
+// and takes whole CUs (kDecodeFence), so a block fills one CU's four SIMDs
+constexpr int kDecodeThreads = 256;
 
 // SLICED (p = 3 mod 4 curves, few points): one point per 16-lane row, the
 // square root's exponentiation row-sliced (sqrt_pow_s); every lane of a row
 // runs the rest of the point's code redundantly and lane 0 stores.
+constexpr size_t kDecodeStaticLds = 4ull * (kSqrtWin * 9 * kDecodeThreads + 3 * 256);
 template <class Cv, bool SLICED = false>
 __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
     ProofDecodeHdr h, const SqrtTab* __restrict__ tabp, const uint32_t* __restrict__ pt_map,
     const uint32_t* __restrict__ proofs, const uint32_t* __restrict__ inst, uint32_t* __restrict__ points,
     uint32_t* __restrict__ scalars, uint32_t* __restrict__ cpts, uint32_t* __restrict__ cscs,
-    uint32_t* __restrict__ status) {
+    uint32_t* __restrict__ status, uint4* __restrict__ corr) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
-  __shared__ uint32_t s_odd[kSqrtWin * 9 * kDecodeThreads];
+  __shared__ uint32_t s_odd[kSqrtWin * 9 * kDecodeThreads];  // (kDecodeStaticLds)
   __shared__ uint32_t s_klo[256], s_khi[256], s_kidx[256];
   const SqrtTab& T = *tabp;
   const uint32_t lane = threadIdx.x;
@@ -402,6 +406,9 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
     bool ok = words_lt_mod<F>(w) && (any != 0 || ysign != 0);
     uint32_t xo[8] = {0, 0, 0, 0, 0, 0, 0, 0}, yo[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t xc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, yc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // the twisted ladder's factors (A, y A) for this point (accum_kernels.hpp
+    // acc_chain_start): A = x^3 + b as the ladder computes it, y signed
+    F29<F> cA = f29_const<F>(F29Consts<F>::ONE), cYA = cA;
     if (ok) {
       const F29<F> X = f29_mul_c<F>(f29_unpack<F>(w), f29_ld<F>(T.r2));  // R261
       const F29<F> rhs = f29_norm<F>(f29_add<F>(f29_mul_c<F>(f29_sqr_c<F>(X), X), f29_ld<F>(T.b)));
@@ -418,6 +425,8 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
         }
         f29_to_r256<F>(X, xo);
         f29_to_r256<F>(Y, yo);
+        cA = rhs;
+        cYA = f29_mul_c<F>(Y, rhs);
 #pragma unroll
         for (int i = 0; i < 8; i++) xc[i] = w[i];
         f29_pack<F>(y, yc);
@@ -436,6 +445,10 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
     co[1] = make_uint4(xc[4], xc[5], xc[6], xc[7]);
     co[2] = make_uint4(yc[0], yc[1], yc[2], yc[3]);
     co[3] = make_uint4(yc[4], yc[5], yc[6], yc[7]);
+    if (corr) {
+      pow_st<F>(corr + pi * kAccCorrWords, cA);
+      pow_st<F>(corr + pi * kAccCorrWords + kPowWords, cYA);
+    }
     return;
   }
   const size_t e = (size_t)(blockIdx.x - h.nblk_pts) * kDecodeThreads + lane;
@@ -467,6 +480,11 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
   uint4* co = reinterpret_cast<uint4*>(cpts + 16 * pi);
   store_fe4<F>(co, fe_from_mont<F>(x));
   store_fe4<F>(co + 2, fe_from_mont<F>(y));
+  if (corr) {  // an affine input: the ladder ran on the curve itself
+    const F29<F> one = f29_const<F>(F29Consts<F>::ONE);
+    pow_st<F>(corr + pi * kAccCorrWords, one);
+    pow_st<F>(corr + pi * kAccCorrWords + kPowWords, one);
+  }
 }
 
 }  // namespace pm

@@ -431,10 +431,11 @@ __global__ void __launch_bounds__(64) k_transcript(TranscriptHdr hd, const uint3
 //   A  all waves stage the proofs' canonical data and the word table in LDS,
 //      then assemble every proof's whole stream in LDS;
 //   B  wave 0 runs the compression chain (quad per proof, as above): the
-//      128-byte blocks in order, and at each squeeze the final compression of
-//      the zero-padded partial block (from the state after the blocks before
-//      it) -- no per-record bookkeeping on the chain (it was about half of
-//      k_transcript's ~0.10 ms);
+//      128-byte blocks in order -- no per-record bookkeeping on the chain (it
+//      was about half of k_transcript's ~0.10 ms); at each squeeze it leaves
+//      its state in LDS and raises that squeeze's flag, and waves 1-3 (squeeze
+//      k on wave 1 + k % 3) run the final compression of the zero-padded
+//      partial block from it, off the chain;
 //   C  all waves turn the 7 x 16 digests into challenges.
 // A block with an identity point among its proofs (that record is skipped,
 // shifting the stream) runs the per-record replay instead.
@@ -453,15 +454,16 @@ constexpr uint32_t kTrDataStride = kTrSlots + 1;  // LDS data rows [word][slot],
 
 // LDS words (u32) of the streamed kernel, and its layout
 struct TrStreamLds {
-  uint32_t oT, oD, oS, oF, oG, oFlag, total;
+  uint32_t oT, oD, oS, oF, oH, oG, oFlag, total;
   __host__ __device__ TrStreamLds(uint32_t nw32, uint32_t nblk, uint32_t npr, uint32_t npts, uint32_t nsc) {
     oT = 0;                                               // word table (3 per stream word), point records
     oD = (3 * nw32 + npr + 1) & ~1u;                      // canonical data [word][17]
     oS = (oD + kTrDataStride * (16 * npts + 8 * nsc) + 1) & ~1u;  // stream [w64][16] (u64)
-    oF = oS + 2 * kTrSlots * 16 * nblk;                   // final block [16][16] (u64)
-    oG = oF + 2 * kTrSlots * 16;                          // digests [7][16 slots][16]
-    oFlag = oG + kTrChallenges * kTrSlots * 16;
-    total = oFlag + 1;
+    oF = oS + 2 * kTrSlots * 16 * nblk;                   // final blocks of waves 1-3, [16][16] (u64) each
+    oH = oF + 3 * 2 * kTrSlots * 16;                      // chain states at the squeezes [7][16 slots][8] (u64)
+    oG = oH + 2 * kTrChallenges * kTrSlots * 8;           // digests [7][16 slots][16]
+    oFlag = oG + kTrChallenges * kTrSlots * 16;           // identity flag, then one flag per squeeze
+    total = oFlag + 1 + kTrChallenges;
   }
 };
 
@@ -484,7 +486,7 @@ __global__ void __launch_bounds__(256) k_transcript_s(TranscriptHdr hd, TrStream
   const uint32_t tid = threadIdx.x, b0 = blockIdx.x * kTrSlots;
   const uint32_t ndp = 16 * hd.npts, nd = ndp + 8 * hd.nsc;  // data words per proof
   // --- A1: the word table and the 16 proofs' canonical data into LDS
-  if (tid == 0) *flag = 0;
+  if (tid <= kTrChallenges) flag[tid] = 0;
   for (uint32_t f = tid; f < 3 * sh.nw32 + sh.npr; f += blockDim.x) T[f] = wtab[f];
   for (uint32_t f = tid; f < kTrSlots * (nd / 4); f += blockDim.x) {
     const uint32_t sl = f / (nd / 4), w = 4 * (f - sl * (nd / 4)), b = b0 + sl;
@@ -536,15 +538,30 @@ __global__ void __launch_bounds__(256) k_transcript_s(TranscriptHdr hd, TrStream
     uint32_t st = 0;
     if (slow) {
       st = tr_replay<Cv>(hd, prog, points, scalars, challenges, *reinterpret_cast<TrBuf*>(tr_lds), slot, q, b);
-    } else {
+    }
+    if (q == 0 && b < hd.B) tr_finish_status(st, b, status, dflags);
+  }
+  if (!slow) {
+    const uint32_t w = tid >> 6, slot = (tid & 63) >> 2, q = tid & 3;
+    uint64_t* const H = reinterpret_cast<uint64_t*>(tr_lds + lay.oH);
+    const uint64_t* col = S + slot;
+    if (w == 0) {  // the chain
       uint64_t h0 = q == 0 ? hd.h0[0] : q == 1 ? hd.h0[1] : q == 2 ? hd.h0[2] : hd.h0[3];
       uint64_t h1 = q == 0 ? hd.h0[4] : q == 1 ? hd.h0[5] : q == 2 ? hd.h0[6] : hd.h0[7];
-      const uint64_t* col = S + slot;
-      uint64_t* fin = S + 16 * kTrSlots * sh.nblk + slot;  // the final-block rows
       uint32_t done = 0;
       for (uint32_t k = 0; k < kTrChallenges; k++) {
-        const uint32_t L = sh.L[k], m = (L + 127) / 128 - 1;  // blocks compressed before the final one
+        const uint32_t m = (sh.L[k] + 127) / 128 - 1;  // blocks compressed before the final one
         for (; done < m; done++) tr_compress_q(h0, h1, TrStreamMsg{col, 16 * done}, q, 128ull * (done + 1), false);
+        H[8 * (k * kTrSlots + slot) + q] = h0;
+        H[8 * (k * kTrSlots + slot) + 4 + q] = h1;
+        if (tid == 0) __hip_atomic_store(&flag[1 + k], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else {  // the finals of squeezes w - 1, w + 2, ...
+      uint64_t* fin = reinterpret_cast<uint64_t*>(tr_lds + lay.oF) + (w - 1) * 16 * kTrSlots + slot;
+      for (uint32_t k = w - 1; k < kTrChallenges; k += 3) {
+        while (__hip_atomic_load(&flag[1 + k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+          __builtin_amdgcn_s_sleep(1);
+        const uint32_t L = sh.L[k], m = (L + 127) / 128 - 1;
         // block m zero-padded after byte L (every lane of the quad writes the
         // same 16 words, so each lane reads back only its own stores)
         const uint32_t lim = L - 128 * m;
@@ -554,7 +571,7 @@ __global__ void __launch_bounds__(256) k_transcript_s(TranscriptHdr hd, TrStream
           const uint32_t lo = 8 * i;
           fin[i * kTrSlots] = lo + 8 <= lim ? v : lo >= lim ? 0ull : v & ((1ull << (8 * (lim - lo))) - 1ull);
         }
-        uint64_t f0 = h0, f1 = h1;
+        uint64_t f0 = H[8 * (k * kTrSlots + slot) + q], f1 = H[8 * (k * kTrSlots + slot) + 4 + q];
         tr_compress_q(f0, f1, TrStreamMsg{fin, 0}, q, (uint64_t)L, true);
         uint32_t d[16];
         tr_digest_q(f0, f1, d);
@@ -563,7 +580,6 @@ __global__ void __launch_bounds__(256) k_transcript_s(TranscriptHdr hd, TrStream
         for (int i = 0; i < 4; i++) g[4 * q + i] = d[4 * q + i];
       }
     }
-    if (q == 0 && b < hd.B) tr_finish_status(st, b, status, dflags);
   }
   __syncthreads();
   // --- C: challenges = from_bytes_wide(digest), 7 x 16 items over the block

@@ -30,3 +30,22 @@ def test_field_constants():
         assert one == P.R_MONT % p, name
         assert r2 == P.R_MONT * P.R_MONT % p, name
         assert nbits == p.bit_length(), name
+
+
+def _limbs29(src, key):
+    m = re.search(r"%s\[9\] = \{(.*?)\};" % key, src, re.S)
+    return sum(int(x.strip().rstrip("u"), 16) << (29 * i) for i, x in enumerate(m.group(1).split(",")))
+
+
+def test_twist_ladder_constants():
+    """R522 (canonical -> R = 2^261 Montgomery) and the curves' b in that form:
+    the ladder's start point on the twist y^2 = x^3 + A^3 b (accum_kernels.hpp)
+    is built from the proof's x bytes with them."""
+    fp29 = open(os.path.join(ROOT, "halo2-aggregation_amd", "csrc", "fp29.hpp")).read()
+    glv = open(os.path.join(ROOT, "halo2-aggregation_amd", "csrc", "glv.hpp")).read()
+    for field, curve, p, b in [("PallasFp", "PallasCurve", P.PALLAS_P, 5), ("VestaFp", "VestaCurve", P.VESTA_P, 5),
+                               ("Bn254Fq", "Bn254Curve", P.BN254_P, 3)]:
+        body = fp29[fp29.index("struct F29Consts<%s>" % field):]
+        assert _limbs29(body, "R522") == pow(2, 522, p), field
+        gb = glv[glv.index("struct Glv<%s>" % curve):]
+        assert _limbs29(gb, "B29") == b * pow(2, 261, p) % p, curve

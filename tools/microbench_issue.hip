@@ -17,7 +17,7 @@
 constexpr int kUnroll = 8;
 
 template <int V>
-__global__ void __launch_bounds__(64) k_issue(uint32_t* out, uint64_t* clk, int iters) {
+__global__ void __launch_bounds__(256) k_issue(uint32_t* out, uint64_t* clk, int iters) {
   uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
   uint32_t x = threadIdx.x * 0x9E3779B9u, y = x ^ 0x85EBCA6Bu, z = x + 7u;
   uint32_t w0 = x, w1 = y, w2 = z, w3 = x ^ z, w4 = x + 1, w5 = y + 1, w6 = z + 1, w7 = x + 2;
@@ -59,30 +59,34 @@ __global__ void __launch_bounds__(64) k_issue(uint32_t* out, uint64_t* clk, int 
     }
   }
   const uint64_t t1 = wall_clock64();
-  out[blockIdx.x * 64 + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7) ^ w0 ^ w1 ^ w2 ^ w3 ^ w4 ^ w5 ^
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7) ^ w0 ^ w1 ^ w2 ^ w3 ^ w4 ^ w5 ^
                                        w6 ^ w7;
   if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
 }
 
+// wpc: waves per CU (one block of wpc waves on each of 256 CUs; wave 0 timed)
 template <int V>
-void run(const char* name, uint32_t* buf, uint64_t* clk, int iters) {
+void run(const char* name, uint32_t* buf, uint64_t* clk, int iters, int wpc = 1) {
   const int blocks = 256;
-  k_issue<V><<<blocks, 64>>>(buf, clk, 2);
-  k_issue<V><<<blocks, 64>>>(buf, clk, iters);
+  k_issue<V><<<blocks, 64 * wpc>>>(buf, clk, 2);
+  k_issue<V><<<blocks, 64 * wpc>>>(buf, clk, iters);
   (void)hipDeviceSynchronize();
   uint64_t h[256];
   (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
   double s = 0;
   for (int b = 0; b < blocks; b++) s += (double)h[b];
   const double ns = s / blocks * 10.0 / ((double)iters * kUnroll * 64);  // wall_clock64 at 100 MHz
-  printf("{\"form\": \"%s\", \"ns_per_instruction\": %.4f}\n", name, ns);
+  if (wpc == 1)
+    printf("{\"form\": \"%s\", \"ns_per_instruction\": %.4f}\n", name, ns);
+  else
+    printf("{\"form\": \"%s\", \"waves_per_cu\": %d, \"ns_per_instruction\": %.4f}\n", name, wpc, ns);
   fflush(stdout);
 }
 
 int main() {
   uint32_t* buf;
   uint64_t* clk;
-  (void)hipMalloc(&buf, 256 * 64 * 4);
+  (void)hipMalloc(&buf, 256 * 256 * 4);
   (void)hipMalloc(&clk, 256 * 8);
   run<0>("v_mad_u64_u32 independent", buf, clk, 2000);
   run<1>("v_mad_u64_u32 dependent", buf, clk, 2000);
@@ -91,5 +95,9 @@ int main() {
   run<4>("v_lshrrev_b64 independent", buf, clk, 2000);
   run<5>("v_mov_b32_dpp row_newbcast independent", buf, clk, 2000);
   run<6>("ds_bpermute_b32 dependent (with s_waitcnt)", buf, clk, 500);
+  // four waves per CU (one per SIMD): does the per-wave issue rate hold?
+  run<0>("v_mad_u64_u32 independent", buf, clk, 2000, 4);
+  run<2>("v_and_b32 independent", buf, clk, 2000, 4);
+  run<5>("v_mov_b32_dpp row_newbcast independent", buf, clk, 2000, 4);
   return 0;
 }

@@ -23,10 +23,11 @@ __device__ void seed(uint32_t t, F29<F>& x, F29<F>& y) {
   y.l[8] &= 0xfffff;
 }
 
-// chain id = blockIdx.x * 4 + row
+// chain id = (blockIdx.x * waves per block + wave) * 4 + row; one or more
+// waves per block (a block of W waves puts W chains' waves on one CU)
 template <class F>
-__global__ void __launch_bounds__(64) k_slice(uint32_t* out, uint64_t* clk, int iters) {
-  const uint32_t row = threadIdx.x >> 4, id = blockIdx.x * 4 + row;
+__global__ void __launch_bounds__(256) k_slice(uint32_t* out, uint64_t* clk, int iters) {
+  const uint32_t row = (threadIdx.x >> 4) & 3u, id = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 4 + row;
   F29<F> x0, y0;
   seed<F>(id, x0, y0);
   const SConst<F> k = SConst<F>::make();
@@ -37,7 +38,7 @@ __global__ void __launch_bounds__(64) k_slice(uint32_t* out, uint64_t* clk, int 
   const uint64_t t1 = wall_clock64() + (r.l[0] & 0u);
   if (s_lane() == 0)
     for (int i = 0; i < 9; i++) out[id * 9 + i] = r.l[i];
-  if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
+  if ((threadIdx.x & 63) == 0) clk[blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)] = t1 - t0;
 }
 
 template <class F>
@@ -210,6 +211,21 @@ void run(const char* name) {
   // wall_clock64 runs at 100 MHz
   printf("{\"field\": \"%s\", \"sliced_us_per_mul\": %.4f, \"lane_us_per_mul\": %.4f, \"mismatches\": %d}\n", name,
          s / blocks * 0.01 / iters, l / blocks * 0.01 / iters, bad);
+  // the same 256 sliced chains as 2 and 4 waves per block (per CU)
+  for (int wpb = 2; wpb <= 4; wpb *= 2) {
+    k_slice<F><<<blocks / wpb, 64 * wpb>>>(d_s, c_s, iters);
+    k_slice<F><<<blocks / wpb, 64 * wpb>>>(d_s, c_s, iters);
+    hipDeviceSynchronize();
+    std::vector<uint32_t> h2(blocks * 4 * 9);
+    hipMemcpy(h2.data(), d_s, h2.size() * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(cs.data(), c_s, blocks * 8, hipMemcpyDeviceToHost);
+    int bad2 = 0;
+    for (size_t i = 0; i < h2.size(); i++) bad2 += h2[i] != hs[i];
+    double s2 = 0;
+    for (int b = 0; b < blocks; b++) s2 += cs[b];
+    printf("{\"field\": \"%s\", \"waves_per_cu\": %d, \"sliced_us_per_mul\": %.4f, \"mismatches\": %d}\n", name,
+           wpb, s2 / blocks * 0.01 / iters, bad2);
+  }
   hipFree(d_s);
   hipFree(d_l);
   hipFree(c_s);
