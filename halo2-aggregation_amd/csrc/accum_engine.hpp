@@ -405,7 +405,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // work) rows of 32 B per proof in LDS (proof stride np + 1), np <= 64
   // within a 128 KiB budget
   const size_t row_bytes =
-      (size_t)(L.nsc + T + kAccXVals + acc_num_vals(h) + 2 * (h.bf + 3) + kAccStack + h.nslots) * 32;
+      (size_t)(L.nsc + T + kAccXVals + acc_num_vals(h) + 2 * (h.bf + 3) + kAccStack + h.nslots + h.nh) * 32;
   const size_t tail_bytes = (size_t)acc_scalars_tail_words(h) * 4;  // constants + program
   if (tail_bytes + 2 * row_bytes > kAccScalarsLds)
     return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");

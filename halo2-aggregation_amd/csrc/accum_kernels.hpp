@@ -155,7 +155,7 @@ __device__ Fe<Fs> acc_eval_code(const uint32_t* code, uint32_t len, const LdsRow
 // H's coefficient; wave 1's fold of the
 // identity values by selector (l_0, l_last, 1 - l_last - l_blind); then the
 // identity values themselves
-constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXCoefH = 3, kAccXW3 = 3, kAccXFold = 7,
+constexpr uint32_t kAccXHvg = 0, kAccXEvs = 1, kAccXCeh = 2, kAccXW3 = 3, kAccXFold = 7,
                    kAccXVals = 10;
 constexpr int kAccSelL0 = 0, kAccSelLast = 1, kAccSelOmb = 2;
 
@@ -187,9 +187,12 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const uint64_t pc0 = wall_clock64();
 #endif
   const uint32_t r_wk = h.nsc + h.T + kAccXVals + acc_num_vals(h);
-  // rows after the stack: wave 3's slot coefficients (cf3, nslots rows)
-  const uint32_t r_cf3 = r_wk + 2 * (h.bf + 3) + kAccStack;
-  uint32_t* const consts = acc_lds + (size_t)8 * (r_cf3 + h.nslots) * (np + 1);
+  // rows after the stack: wave 3's slot coefficients (cf3, nslots rows), then
+  // the powers x^{n i} of the H expansion (nh rows)
+  const uint32_t r_cf3 = r_wk + 2 * (h.bf + 3) + kAccStack, r_xp = r_cf3 + h.nslots;
+  uint32_t* const consts = acc_lds + (size_t)8 * (r_xp + h.nh) * (np + 1);
+  __shared__ uint32_t xp_ready;  // wave 3 has written the x^{n i} rows
+  if (threadIdx.x == 0) xp_ready = 0;
   uint32_t* const prog = consts + 8 * (h.c_n29 + 1);
   {  // coalesced staging of the block's evaluations (rows [0, nsc)), the constants and the program
     const uint32_t per = 8 * h.nsc;
@@ -212,6 +215,7 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const LdsRows wk{acc_lds + (size_t)8 * r_wk * (np + 1), pl, np + 1};                      // wave 0
   const LdsRows stk{acc_lds + (size_t)8 * (r_wk + 2 * (h.bf + 3)) * (np + 1), pl, np + 1};  // wave 1
   const LdsRows cf3{acc_lds + (size_t)8 * r_cf3 * (np + 1), pl, np + 1};                     // wave 3
+  const LdsRows xpr{acc_lds + (size_t)8 * r_xp * (np + 1), pl, np + 1};                      // wave 3 -> 2
   const uint32_t* ch = challenges + 8ull * 7 * (live ? b : b0);
   const Fe<Fs> one = fe_one<Fs>(), zero = fe_zero<Fs>();
   const Fe<Fs> y = ldfe<Fs>(ch, 3), x = ldfe<Fs>(ch, 4);
@@ -369,7 +373,7 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     // profiles/r05/acc_scalars_roles.txt); each keeps its own slot sums
     // (cf / cf3, added in the conversion) and e-term / H sums (exchange rows).
     // The e term is -(sum_{non-H} c e + h_eval sum_{H queries} c), finished by
-    // wave 0; H's coefficients are expanded by wave 2 after the barrier.
+    // wave 0; H's coefficients are expanded below (x^{n i} from wave 3).
     const bool w3 = role == 3;
     const LdsRows& cfs = w3 ? cf3 : cf;
     const Fe<Fs> v = ldfe<Fs>(ch, 5), u = ldfe<Fs>(ch, 6);
@@ -405,7 +409,29 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     const uint32_t xo = w3 ? kAccXW3 : 0u;
     xr.put<Fs>(kAccXEvs + xo, ev);
     xr.put<Fs>(kAccXCeh + xo, ceh);
-    xr.put<Fs>(kAccXCoefH + xo, coefH);
+    // H = sum_i x^{n i} h_i (vanishing.rs:178-188): h_i's coefficient gains
+    // coefH x^{n i}, each wave adding its own share of coefH to its own slot
+    // rows.  Wave 3 (far ahead of wave 2) makes the powers and raises
+    // xp_ready; wave 2 then needs nh products.  (Round 5: wave 2 did it all
+    // after the barrier, ~20 us on the kernel's critical path.)
+    if (h.nh) {
+      if (w3) {
+        Fe<Fs> xn = x;
+        for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
+        Fe<Fs> xp = one;
+        for (uint32_t i = 0; i < h.nh; i++) {
+          xpr.put<Fs>(i, xp);
+          cf3.put<Fs>(h.h_slot0 + i, fe_add<Fs>(cf3.get<Fs>(h.h_slot0 + i), fe_mul<Fs>(coefH, xp)));
+          xp = fe_mul<Fs>(xp, xn);
+        }
+        if (pl == 0) __hip_atomic_store(&xp_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        while (__hip_atomic_load(&xp_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+          __builtin_amdgcn_s_sleep(1);
+        for (uint32_t i = 0; i < h.nh; i++)
+          cf.put<Fs>(h.h_slot0 + i, fe_add<Fs>(cf.get<Fs>(h.h_slot0 + i), fe_mul<Fs>(coefH, xpr.get<Fs>(i))));
+      }
+    }
   }
 #ifdef PM_ACC_PROFILE
   const uint64_t pc2 = wall_clock64();
@@ -414,17 +440,6 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
 #ifdef PM_ACC_PROFILE
   const uint64_t pc3 = wall_clock64();
 #endif
-  if (live && role == 2) {
-    // H = sum_i x^{n i} h_i (vanishing.rs:178-188): h_i's coefficient += coefH x^{n i}
-    const Fe<Fs> coefH = fe_add<Fs>(xr.get<Fs>(kAccXCoefH), xr.get<Fs>(kAccXCoefH + kAccXW3));
-    Fe<Fs> xn = x;
-    for (uint32_t i = 0; i < h.log_n; i++) xn = fe_sqr<Fs>(xn);
-    Fe<Fs> xp = one;
-    for (uint32_t i = 0; i < h.nh; i++) {
-      cf.put<Fs>(h.h_slot0 + i, fe_add<Fs>(cf.get<Fs>(h.h_slot0 + i), fe_mul<Fs>(coefH, xp)));
-      xp = fe_mul<Fs>(xp, xn);
-    }
-  }
   if (live && role == 0) {
     // expressions in order gates, permutation, lookups: h = h y + sel expr,
     // folded per selector by wave 1
