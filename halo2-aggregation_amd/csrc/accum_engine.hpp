@@ -114,11 +114,13 @@ size_t decode_static_lds() {
 // else first on the main stream.  off_of: the byte offset within a proof of
 // every point index read from the bytes (kAccNoByte: instance commitments).
 struct AccDecode {
-  std::function<int(hipStream_t, size_t)> launch;  // (stream, LDS fence bytes)
+  std::function<int(hipStream_t, size_t, uint4*)> launch;  // (stream, LDS fence bytes, twist factors or null)
   const void* proofs;
   size_t stride;
   const void* inst;
   std::vector<uint32_t> off_of;
+  bool sliced;         // row-sliced square roots (few points)
+  uint32_t pt_blocks;  // the point part's blocks (one CU each when fenced)
 };
 // a decode block beside a ladder block would share its SIMDs (both are
 // issue-bound lone-wave chains): its LDS request keeps it off any CU holding
@@ -343,9 +345,18 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     const char* e = getenv("PM_ACC_TWIST");
     return !(e && *e == '0');
   }();
-  h.twist = dec && lgS > 0 && twist_on ? 1u : 0u;
+  // (only with the row-sliced decode, profiles/r05/twist_ab/: the one-lane
+  // decode beside the quad ladder ran 0.12-0.33 ms against 0.13 alone)
+  // and while the decode's point blocks and the ladder's blocks fit the CUs
+  // side by side: beyond, they queue for each other (B = 256: 256 + 100)
+  {
+    const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
+    h.twist = dec && dec->sliced && lgS > 0 && twist_on && dec->pt_blocks + lad_blocks <= 256 ? 1u : 0u;
+  }
   if (h.twist && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4)))) return rc;
   std::vector<uint64_t> built_key;  // VK tables built by this call (committed after its final sync)
+  // without the twist the decode comes first: everything after reads its points
+  if (dec && !h.twist && (rc = dec->launch(st, kDecodeFence, nullptr))) return rc;
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
     const size_t tab = (size_t)kPowPos * kPowPoint * sizeof(uint4), nvk = vk.size() / 8;
     if ((rc = ctx->acc_lad.ensure(std::max<size_t>(nprf, 1) * tab))) return rc;
@@ -394,7 +405,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
       HIP_TRY(hipStreamWaitEvent(side, up, 0));
     }
   }
-  if (dec && (rc = dec->launch(side, h.twist ? kDecodeFence : 0))) return rc;
+  if (dec && h.twist && (rc = dec->launch(side, kDecodeFence, (uint4*)ctx->acc_corr.p))) return rc;
   if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side,
                                              canon_ready, dflags)))
     return rc;
@@ -703,18 +714,22 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   dec.proofs = d_proofs;
   dec.stride = stride;
   dec.inst = d_inst;
+  dec.sliced = sliced;
+  dec.pt_blocks = h.nblk_pts;
   dec.off_of.assign(L.npts, kAccNoByte);
   for (size_t i = 0; i + 1 < map.size(); i += 2) dec.off_of[map[i + 1]] = map[i];
   const SqrtTab* tabp = (const SqrtTab*)ctx->sqrt_tab[slot].p;
   const uint32_t* dmap = (const uint32_t*)ctx->pf_map.buf.p;
-  dec.launch = [=](hipStream_t dst, size_t fence) -> int {
-    // the fence is the whole block's LDS (the kernel's static arrays count);
-    // a fenced decode runs beside the twisted ladder and writes its factors
-    // (acc_corr, sized by accum_device_impl before it launches this)
+  dec.launch = [=](hipStream_t dst, size_t fence, uint4* cp) -> int {
+    // the fence is the whole block's LDS (the kernel's static arrays count):
+    // one block per CU, beside nothing (latency-bound chains; unfenced, the
+    // dispatcher packed several blocks per CU, B = 16 decode 0.11 -> 0.16 ms);
+    // cp: the twisted ladder's factors (acc_corr, sized by accum_device_impl)
     auto kern = sliced ? k_proof_decode<Cv, true> : k_proof_decode<Cv, false>;
     const size_t stat = sliced ? decode_static_lds<Cv, true>() : decode_static_lds<Cv, false>();
+    // a grid beyond one block per CU is throughput work: packing is fine there
+    if (h.nblk_pts > 256) fence = 0;
     const size_t dyn = fence > stat ? fence - stat : 0;
-    uint4* cp = fence ? (uint4*)ctx->acc_corr.p : nullptr;
     PM_LAUNCH_ST(ctx, dst, "proof_decode",
                  (kern<<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, dyn, dst>>>(
                      h, tabp, dmap, (const uint32_t*)d_proofs, (const uint32_t*)d_inst, (uint32_t*)d_points,
@@ -722,7 +737,7 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     return PM_OK;
   };
   if (!vk_repr) {
-    if ((rc = dec.launch(st, 0))) return rc;
+    if ((rc = dec.launch(st, kDecodeFence, nullptr))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     ctx->end_call();
     return PM_OK;

@@ -356,9 +356,9 @@ struct ProofDecodeHdr {
   uint32_t nblk_pts;   // blocks of the point part (the scalar part follows)
 };
 
-// Blocks [0, nblk_pts): one lane per proof point (pt_map[j] = (byte offset /
-// 4) << 8 | destination point index ... as two words: offset, index).
-// Blocks after: one lane per scalar, then per instance commitment.
+// Point blocks (the last nblk_pts): one lane (SLICED: one 16-lane row) per
+// proof point (pt_map: byte offset, destination point index per point).
+// The blocks before: one lane per scalar, then per instance commitment.
 // 256 (round 5, was 64): with the twisted ladder the decode runs beside it
 // and takes whole CUs (kDecodeFence), so a block fills one CU's four SIMDs
 constexpr int kDecodeThreads = 256;
@@ -379,7 +379,11 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
   __shared__ uint32_t s_klo[256], s_khi[256], s_kidx[256];
   const SqrtTab& T = *tabp;
   const uint32_t lane = threadIdx.x;
-  if (blockIdx.x < h.nblk_pts) {
+  // blocks [0, nblk_sc): scalars and instance commitments (quick, first, so
+  // that fenced point blocks never wait behind them); then the points
+  const uint32_t nblk_sc = gridDim.x - h.nblk_pts;
+  if (blockIdx.x >= nblk_sc) {
+    const uint32_t pb = blockIdx.x - nblk_sc;
     if (!SLICED && T.ts) {
       for (uint32_t i = lane; i < 256; i += kDecodeThreads) {
         s_klo[i] = T.key_lo[i];
@@ -388,8 +392,7 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
       }
       __syncthreads();
     }
-    const size_t e = SLICED ? (size_t)blockIdx.x * (kDecodeThreads / 16) + (lane >> 4)
-                            : (size_t)blockIdx.x * kDecodeThreads + lane;
+    const size_t e = SLICED ? (size_t)pb * (kDecodeThreads / 16) + (lane >> 4) : (size_t)pb * kDecodeThreads + lane;
     if (e >= (size_t)h.B * h.npp) return;  // whole rows when SLICED
     const bool writer = !SLICED || (lane & 15u) == 0u;
     const uint32_t b = (uint32_t)(e / h.npp), j = (uint32_t)(e % h.npp);
@@ -451,7 +454,7 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
     }
     return;
   }
-  const size_t e = (size_t)(blockIdx.x - h.nblk_pts) * kDecodeThreads + lane;
+  const size_t e = (size_t)blockIdx.x * kDecodeThreads + lane;
   const size_t nsc_all = (size_t)h.B * h.nsc;
   if (e < nsc_all) {  // a scalar: canonical check, Montgomery form
     const uint32_t b = (uint32_t)(e / h.nsc), k = (uint32_t)(e % h.nsc);
