@@ -374,6 +374,9 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     sc_done = ctx->next_event();
     if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(up, st));
+    // with the twist the decode heads the critical chain on st: launched
+    // before the ladder's wait and launch (~8 us of host API time)
+    if (h.twist && (rc = dec->launch(st, kDecodeFence, (uint4*)ctx->acc_corr.p))) return rc;
     const hipStream_t lst = h.twist ? ctx->red_stream : st;  // the ladder's stream
     if (h.twist) HIP_TRY(hipStreamWaitEvent(lst, up, 0));
     const uint32_t* lproofs = h.twist ? (const uint32_t*)dec->proofs : nullptr;
@@ -405,7 +408,6 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
       HIP_TRY(hipStreamWaitEvent(side, up, 0));
     }
   }
-  if (dec && h.twist && (rc = dec->launch(side, kDecodeFence, (uint4*)ctx->acc_corr.p))) return rc;
   if (vk_repr && (rc = transcript_launch<Cv>(ctx, s, B, vk_repr, d_points, d_scalars, d_ch, d_status, side,
                                              canon_ready, dflags)))
     return rc;

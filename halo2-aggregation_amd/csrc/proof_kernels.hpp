@@ -266,11 +266,16 @@ __device__ S29<F> sqrt_pow_s(const SqrtTab& T, S29<F> a, const SConst<F>& k) {
     for (int i = 1; i < kSqrtWin; i++) v = idx == (uint32_t)i ? odd[i].v : v;
     return S29<F>{v};
   };
+  // the schedule word is loaded one step ahead: its scalar load (and the wait
+  // on it) no longer heads every step
+  const uint32_t ns = T.nsched;
   S29<F> acc = pick(T.sched[0] & 0xffu);
-  for (uint32_t j = 1; j < T.nsched; j++) {
-    const uint32_t s = T.sched[j];
+  uint32_t s = ns > 1 ? T.sched[1] : 0u;
+  for (uint32_t j = 1; j < ns; j++) {
+    const uint32_t sn = T.sched[j + 1 < ns ? j + 1 : j];
     for (uint32_t q = s >> 8; q; q--) acc = s29_mul<F>(acc, acc, k);
     if ((s & 0xffu) != 0xffu) acc = s29_mul<F>(acc, pick(s & 0xffu), k);
+    s = sn;
   }
   return acc;
 }
@@ -384,6 +389,11 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
   const uint32_t nblk_sc = gridDim.x - h.nblk_pts;
   if (blockIdx.x >= nblk_sc) {
     const uint32_t pb = blockIdx.x - nblk_sc;
+#ifdef PM_DECODE_PROFILE  // A/B builds only: phase times of the first point block's row 0 (10 ns ticks)
+    const uint64_t pd0 = wall_clock64();
+    uint64_t pd1 = 0, pd2 = 0;
+    const bool prof = pb == 0 && lane == 0;
+#endif
     if (!SLICED && T.ts) {
       for (uint32_t i = lane; i < 256; i += kDecodeThreads) {
         s_klo[i] = T.key_lo[i];
@@ -401,6 +411,7 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
     uint32_t w[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) w[i] = src[i];
+
     const uint32_t ysign = w[7] >> 31;
     w[7] &= 0x7fffffffu;
     uint32_t any = 0;
@@ -413,10 +424,16 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
     // acc_chain_start): A = x^3 + b as the ladder computes it, y signed
     F29<F> cA = f29_const<F>(F29Consts<F>::ONE), cYA = cA;
     if (ok) {
+#ifdef PM_DECODE_PROFILE
+      pd1 = wall_clock64() + (w[0] & 0u);
+#endif
       const F29<F> X = f29_mul_c<F>(f29_unpack<F>(w), f29_ld<F>(T.r2));  // R261
       const F29<F> rhs = f29_norm<F>(f29_add<F>(f29_mul_c<F>(f29_sqr_c<F>(X), X), f29_ld<F>(T.b)));
       F29<F> Y;
       ok = f29_sqrt<F, SLICED>(T, rhs, Y, s_odd + lane, kDecodeThreads, s_klo, s_khi, s_kidx);
+#ifdef PM_DECODE_PROFILE
+      pd2 = wall_clock64() + (Y.l[0] & 0u);
+#endif
       if (ok) {
         F29<F> one = f29_zero<F>();
         one.l[0] = 1;
@@ -435,6 +452,12 @@ __global__ void __launch_bounds__(kDecodeThreads) k_proof_decode(
         f29_pack<F>(y, yc);
       }
     }
+#ifdef PM_DECODE_PROFILE
+    if (prof)
+      printf("decode: start->loaded %llu loaded->sqrt_done %llu sqrt_done->end %llu (start %llu)\n",
+             (unsigned long long)(pd1 - pd0), (unsigned long long)(pd2 - pd1),
+             (unsigned long long)(wall_clock64() + (yc[0] & 0u) - pd2), (unsigned long long)pd0);
+#endif
     if (!writer) return;
     if (!ok) atomicOr(&status[b], kProofBadPoint);
     const size_t pi = (size_t)b * h.npts + dst;
