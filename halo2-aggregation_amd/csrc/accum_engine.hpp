@@ -121,6 +121,8 @@ struct AccDecode {
   std::vector<uint32_t> off_of;
   bool sliced;         // row-sliced square roots (few points)
   uint32_t pt_blocks;  // the point part's blocks (one CU each when fenced)
+  hipEvent_t in_ready = nullptr;  // on st: the inputs are on the device (recorded before the decode)
+  bool launched = false;          // the decode is already queued on st (it writes the twist factors)
 };
 // a decode block beside a ladder block would share its SIMDs (both are
 // issue-bound lone-wave chains): its LDS request keeps it off any CU holding
@@ -353,10 +355,11 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
     h.twist = dec && dec->sliced && lgS > 0 && twist_on && dec->pt_blocks + lad_blocks <= 256 ? 1u : 0u;
   }
-  if (h.twist && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4)))) return rc;
+  if (h.twist && !dec->launched && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4))))
+    return rc;
   std::vector<uint64_t> built_key;  // VK tables built by this call (committed after its final sync)
   // without the twist the decode comes first: everything after reads its points
-  if (dec && !h.twist && (rc = dec->launch(st, kDecodeFence, nullptr))) return rc;
+  if (dec && !dec->launched && !h.twist && (rc = dec->launch(st, kDecodeFence, nullptr))) return rc;
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
     const size_t tab = (size_t)kPowPos * kPowPoint * sizeof(uint4), nvk = vk.size() / 8;
     if ((rc = ctx->acc_lad.ensure(std::max<size_t>(nprf, 1) * tab))) return rc;
@@ -373,10 +376,17 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     up = ctx->next_event();
     sc_done = ctx->next_event();
     if (!up || !sc_done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
-    HIP_TRY(hipEventRecord(up, st));
-    // with the twist the decode heads the critical chain on st: launched
-    // before the ladder's wait and launch (~8 us of host API time)
-    if (h.twist && (rc = dec->launch(st, kDecodeFence, (uint4*)ctx->acc_corr.p))) return rc;
+    // with the twist the decode heads the critical chain on st, queued by
+    // proofs_device_impl before this plan was built; the ladder waits only for
+    // the inputs (or, when this call re-sent programs or VK points, for those
+    // copies, which sit behind the decode)
+    const bool resent = ctx->acc_prog.sent || ctx->acc_const.sent || ctx->acc_vk.sent;
+    if (h.twist && dec->launched && !resent && dec->in_ready) {
+      up = dec->in_ready;
+    } else {
+      HIP_TRY(hipEventRecord(up, st));
+    }
+    if (h.twist && !dec->launched && (rc = dec->launch(st, kDecodeFence, (uint4*)ctx->acc_corr.p))) return rc;
     const hipStream_t lst = h.twist ? ctx->red_stream : st;  // the ladder's stream
     if (h.twist) HIP_TRY(hipStreamWaitEvent(lst, up, 0));
     const uint32_t* lproofs = h.twist ? (const uint32_t*)dec->proofs : nullptr;
@@ -744,6 +754,15 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     ctx->end_call();
     return PM_OK;
   }
+  // the decode first, before the accumulator's plan is even built (host time
+  // off the critical chain), writing the twisted ladder's factors in case the
+  // plan picks the twist; in_ready lets the twisted ladder start beside it
+  dec.in_ready = ctx->next_event();
+  if (!dec.in_ready) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+  HIP_TRY(hipEventRecord(dec.in_ready, st));
+  if ((rc = ctx->acc_corr.ensure(B * (size_t)L.npts * kAccCorrWords * sizeof(uint4)))) return rc;
+  if ((rc = dec.launch(st, kDecodeFence, (uint4*)ctx->acc_corr.p))) return rc;
+  dec.launched = true;
   rc = accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, dflags,
                              &dec);
   if (rc == PM_OK) ctx->pf_flags_dirty = false;  // k_transcript has cleared every word
