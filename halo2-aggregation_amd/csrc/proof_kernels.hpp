@@ -255,15 +255,34 @@ __device__ F29<F> sqrt_pow(const SqrtTab& T, const F29<F>& a, uint32_t* odd, uin
 // VGPRs, the schedule is the same for every row (one exponent per curve).
 template <class F>
 __device__ S29<F> sqrt_pow_s(const SqrtTab& T, S29<F> a, const SConst<F>& k) {
+  static_assert(kSqrtWin == 8, "eight odd powers");
+  // eight named registers, not an array: the compiler promoted the array to
+  // LDS and each pick then waited on an LDS read
   const S29<F> a2 = s29_mul<F>(a, a, k);
-  S29<F> odd[kSqrtWin];
-  odd[0] = a;
-#pragma unroll
-  for (int i = 1; i < kSqrtWin; i++) odd[i] = s29_mul<F>(odd[i - 1], a2, k);
-  auto pick = [&](uint32_t idx) {
-    uint32_t v = odd[0].v;
-#pragma unroll
-    for (int i = 1; i < kSqrtWin; i++) v = idx == (uint32_t)i ? odd[i].v : v;
+  const uint32_t o0 = a.v;
+  const uint32_t o1 = s29_mul<F>(S29<F>{o0}, a2, k).v;
+  const uint32_t o2 = s29_mul<F>(S29<F>{o1}, a2, k).v;
+  const uint32_t o3 = s29_mul<F>(S29<F>{o2}, a2, k).v;
+  const uint32_t o4 = s29_mul<F>(S29<F>{o3}, a2, k).v;
+  const uint32_t o5 = s29_mul<F>(S29<F>{o4}, a2, k).v;
+  const uint32_t o6 = s29_mul<F>(S29<F>{o5}, a2, k).v;
+  const uint32_t o7 = s29_mul<F>(S29<F>{o6}, a2, k).v;
+  // idx is wave-uniform; the empty asm keeps each select a register select
+  // (the compiler otherwise turned the chain into a table of pointers in LDS
+  // and an indirect scratch load per pick)
+  auto pick = [=](uint32_t idx) {
+    uint32_t v = o0;
+#define PM_PICK(I, O)                 \
+  v = idx == (I) ? (O) : v;           \
+  asm volatile("" : "+v"(v));
+    PM_PICK(1u, o1)
+    PM_PICK(2u, o2)
+    PM_PICK(3u, o3)
+    PM_PICK(4u, o4)
+    PM_PICK(5u, o5)
+    PM_PICK(6u, o6)
+    PM_PICK(7u, o7)
+#undef PM_PICK
     return S29<F>{v};
   };
   // the schedule word is loaded one step ahead: its scalar load (and the wait
