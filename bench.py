@@ -1133,14 +1133,17 @@ def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0,
       this instruction stream; the variable-time safegcd inversion has no
       static count and enters both floors with its measured time.
 
-    Chains: main stream decode -> ladder, side stream decode -> transcript ->
-    scalar block, then term additions -> sums (critical = the longer of the
-    two, plus the last two).  Step counts follow the engine's lane rules
+    Chains: decode -> transcript -> scalar block and the ladder, then term
+    additions -> sums.  The ladder follows the decode, or (round 5, twisted
+    ladder: row-sliced decode and decode + ladder blocks within the 256 CUs)
+    runs beside it from the proof bytes; critical = the longer chain plus the
+    last two.  Step counts follow the engine's lane rules
     (accum_engine.hpp): decode 305 row-sliced products per BN254 point (the
     4-bit window of (p+1)/4) while B x points <= 4096, else one lane square
     root; ladder 127 doublings (row-sliced: 3 dependent product levels each,
     up to 800 chains; else quad-cooperative); transcript ceil(bytes / 128) + 7
-    Blake2b compressions per proof; scalar block log n + 4K - 3 radix-2^29
+    Blake2b compressions per proof (round 5 streamed replay: ceil(bytes /
+    128) on the chain, the squeeze finals beside it); scalar block log n + 4K - 3 radix-2^29
     products (K = bf + 3), the inversion, then 2 per identity value + 2 + T/4
     Fe products; term additions ceil(85.3 / S) + log2 S XYZZ additions (14
     products each); sums ceil(nslots / (NL/4)) + log2(NL/4) quad additions
@@ -1195,7 +1198,10 @@ def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0,
     K = (c.blinding_factors if c is not None else 5) + 3
     nsets_p = -(-c.n_perm_columns // c.perm_chunk_len) if c is not None and c.n_perm_columns else 0
     nvals = (2 * nsets_p + 1 if nsets_p else 0) + 5 * (c.num_lookups if c is not None else 0)
-    comps = -(-(npts * 65 + nsc * 33 + 33) // 128) + 7
+    comps = -(-(npts * 65 + nsc * 33 + 33) // 128)  # streamed: the finals run beside the block chain
+    nprf = B * npts  # proof-point chains (about one per proof point)
+    twist = (from_bytes and sliced_dec and
+             -(-B * npp // 16) + (-(-nprf // 4) if nprf <= 800 else -(-4 * nprf // 256)) <= 256)
     n29 = log_n + 4 * K - 3
     nfe = 2 * nvals + 2 + -(-T // 4)
     inv_lane = lat.get("inv_lane", lat["inv_q"])
@@ -1216,11 +1222,12 @@ def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0,
 
     def crit(f):
         d = f.get("proof_decode", 0.0)
-        return max(d + f["acc_ladder"], d + f["transcript"] + f["acc_scalars"]) + f["acc_termmul"] + f["acc_sum"]
+        lad = f["acc_ladder"] if twist else d + f["acc_ladder"]
+        return max(lad, d + f["transcript"] + f["acc_scalars"]) + f["acc_termmul"] + f["acc_sum"]
 
     out = {"bound": "latency", "achieved": round(ms_batch, 4), "unit": "ms per batch (critical path)",
            "traffic": None, "lanes": {"term_additions_S": S, "sum_lanes_NL": NL, "sliced_decode": sliced_dec,
-                                      "sliced_ladder": sliced_lad}}
+                                      "sliced_ladder": sliced_lad, "twisted_ladder": twist}}
     st = dict(lat)
     st.setdefault("b2_compress_q", 1.62)
     fs = floors(st, None)
