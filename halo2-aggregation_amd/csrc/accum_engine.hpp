@@ -432,7 +432,10 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   const size_t tail_bytes = (size_t)acc_scalars_tail_words(h) * 4;  // constants + program
   if (tail_bytes + 2 * row_bytes > kAccScalarsLds)
     return set_error(PM_ERR_UNSUPPORTED, "accum: too many evaluations / terms per proof");
-  const uint32_t np = (uint32_t)std::min<size_t>(64, (kAccScalarsLds - tail_bytes) / row_bytes - 1);
+  // 16 proofs per block (round 5): wave 0 then runs the Lagrange chain with a
+  // quad per proof (acc_lagrange_q, ~half the one-lane chain); more blocks
+  // only spread the batch over more CUs
+  const uint32_t np = (uint32_t)std::min<size_t>(16, (kAccScalarsLds - tail_bytes) / row_bytes - 1);
   const size_t lds = std::max(row_bytes * (np + 1) + tail_bytes, lgS > 0 ? kAccScalarsLds : 0);
   PM_LAUNCH_ST(ctx, side, "acc_scalars",
                (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, side>>>(

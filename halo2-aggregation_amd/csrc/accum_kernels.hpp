@@ -172,6 +172,124 @@ __host__ __device__ inline uint32_t acc_scalars_tail_words(const AccumHdr& h) {
   return 8 * (h.c_n29 + 1) + (h.p_rank + h.T);
 }
 
+// Wave 0's Lagrange chain with a quad per proof (blocks of up to 16 proofs,
+// round 5): the lone-lane chain (x^n, 2K products into the batched inverse,
+// 2K back out, 2K for the l_i: ~72 us) split over the quad's four lanes.
+//   A  lane 0 squares x log n times; meanwhile lane j = 1..3 forms its dens
+//      den_i = n (x - w^i), i = j - 1 (mod 3), with its own prefix products
+//      and w^i * prefix (rows i and K + i)
+//   B  A = P1 P2, Bv = P3 (x^n - 1), then D = A Bv and the cofactors of each
+//      lane's product (S1 = P2 Bv, S2 = P1 Bv, S3 = A (x^n - 1), S4 = A P3)
+//   C  1 / D (quad safegcd)
+//   D  one step: lane 0 1 / (x^n - 1), lane j 1 / P_j
+//   E  lane j walks its dens back: t_i = w^i / den_i = R (w^i prefix_i),
+//      R *= den_i; sums t_i over the blinding rows, keeps t_0, t_{bf+1}
+//   F  l_0, l_last, l_blind = (x^n - 1) t (one step over three lanes)
+// Results (Fe, R = 2^256) go to the proof's wk rows 0..3: l_0, l_last,
+// l_blind, 1 / (x^n - 1); wave 0's lane for the proof reads them after the
+// barrier.  Same values as the one-lane chain.
+template <class Fs>
+__device__ __forceinline__ void acc_lagrange_q(const AccumHdr& h, const LdsRows& wk, const uint32_t* consts,
+                                               const uint32_t* __restrict__ challenges, uint32_t b0, uint32_t nv,
+                                               uint32_t* __restrict__ status) {
+  using K29 = F29Consts<Fs>;
+  const uint32_t pl = threadIdx.x & 63u, p = pl >> 2, q = pl & 3u;
+  const bool own = p < nv;
+  const LdsRows wq{wk.base, p, wk.stride};
+  const uint32_t K = h.bf + 3, nd = K - 1;  // dens of x - w^i, i < nd (the K-th is x^n - 1)
+  auto put29 = [&](uint32_t row, const F29<Fs>& v) {
+    Fe<Fs> w;
+    f29_pack<Fs>(v, w.l);
+    wq.put<Fs>(row, w);
+  };
+  auto get29 = [&](uint32_t row) { return f29_unpack<Fs>(wq.get<Fs>(row).l); };
+  auto ld29 = [&](uint32_t idx) { return f29_unpack<Fs>(ldfe<Fs>(consts, idx).l); };  // canonical R261
+  const uint32_t mq0 = q == 0 ? ~0u : 0u;
+  auto sel = [&](uint32_t m, const F29<Fs>& a, const F29<Fs>& b) {  // m ? a : b, limb-wise
+    F29<Fs> r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = bsel(m, a.l[i], b.l[i]);
+    return r;
+  };
+  const Fe<Fs> xfe = ldfe<Fs>(challenges + 8ull * 7 * (b0 + (own ? p : 0u)), 4);
+  const F29<Fs> x29 = f29_from_r256<Fs>(xfe.l);  // < 2p
+  const F29<Fs> one29 = f29_const<Fs>(K29::ONE), nfe = ld29(h.c_n29);
+  // --- A
+  const uint32_t nk = q == 0 ? 0u : (nd + 3u - q) / 3u;  // dens of this lane (i = q - 1 + 3 k)
+  const uint32_t nkmax = (nd + 2u) / 3u;
+  const uint32_t steps = max(h.log_n, 3u * nkmax);
+  F29<Fs> xn = x29, pre = one29, den = one29;
+  for (uint32_t s = 0; s < steps; s++) {
+    const uint32_t kind = s % 3u, k = s / 3u;
+    const uint32_t i = q - 1u + 3u * k, ic = i < nd ? i : 0u;
+    const bool valid = q != 0 && k < nk;
+    const F29<Fs> w = ld29(h.c_wpow29 + ic);
+    F29<Fs> a, b;
+    if (kind == 0) {  // den_i = n (x - w^i)
+      a = nfe;
+      b = f29_norm<Fs>(f29_sub<Fs>(x29, w, K29::K2));
+    } else if (kind == 1) {  // w^i * prefix before i
+      a = w;
+      b = pre;
+    } else {  // prefix *= den_i
+      a = pre;
+      b = den;
+    }
+    const F29<Fs> r = f29_mul_c<Fs>(sel(mq0, xn, a), sel(mq0, xn, b));
+    if (q == 0) {
+      if (s < h.log_n) xn = r;
+    } else if (valid) {
+      if (kind == 0) {
+        den = r;
+        put29(ic, r);
+      } else if (kind == 1) {
+        put29(K + ic, r);
+      } else {
+        pre = r;
+      }
+    }
+  }
+  // --- B
+  const F29<Fs> xn1 = f29_reduce3<Fs>(f29_norm<Fs>(f29_sub<Fs>(qbc<0>(xn), one29, K29::K2)));  // < 3p
+  const F29<Fs> P1 = qbc<1>(pre), P2 = qbc<2>(pre), P3 = qbc<3>(pre);
+  const F29<Fs> r1 = qmul<Fs>(q, P1, P2, P3, xn1, one29, one29, one29, one29);
+  const F29<Fs> A = qbc<0>(r1), Bv = qbc<1>(r1);
+  const F29<Fs> r2 = qmul<Fs>(q, A, Bv, P2, Bv, P1, Bv, A, xn1);  // D, S1, S2, S3
+  const F29<Fs> S4 = f29_mul_c<Fs>(A, P3);
+  const F29<Fs> D = qbc<0>(r2);
+  // a zero denominator (x^n = 1, or x = omega^-i for a Lagrange basis point)
+  // is where the reference's main_gate.div fails (vanishing.rs:175,
+  // verifier.rs:580): flag the proof; its outputs are then unspecified
+  if (q == 0 && own && status && f29_is_zero_mod<Fs>(D)) status[b0 + p] |= kAccStatusDenomZero;
+  // --- C, D
+  const F29<Fs> inv = f29_inv_q<Fs>(D);
+  F29<Fs> R = f29_mul_c<Fs>(inv, sel(mq0, S4, r2));  // lane 0: 1 / (x^n - 1); lane j: 1 / P_j
+  const F29<Fs> inv_xn1 = qbc<0>(R);
+  // --- E
+  F29<Fs> t0 = f29_zero<Fs>(), tl = t0, tb = t0;
+  for (uint32_t kk = 0; kk < nkmax; kk++) {
+    const bool valid = kk < nk;
+    const uint32_t k = valid ? nk - 1u - kk : 0u, i = q - 1u + 3u * k, ic = q != 0 && i < nd ? i : 0u;
+    const F29<Fs> t = f29_mul_c<Fs>(R, get29(K + ic));  // w^i / den_i
+    R = f29_mul_c<Fs>(R, get29(ic));
+    if (valid) {
+      if (i == 0) t0 = t;
+      else if (i == h.bf + 1) tl = t;
+      else tb = f29_reduce3<Fs>(f29_norm<Fs>(f29_add<Fs>(tb, t)));  // < 3p
+    }
+  }
+  auto qsum = [&](const F29<Fs>& v) {  // sum over lanes 1..3, < 9p
+    return f29_norm<Fs>(f29_add<Fs>(f29_add<Fs>(qbc<1>(v), qbc<2>(v)), qbc<3>(v)));
+  };
+  const F29<Fs> t0s = f29_reduce3<Fs>(qsum(t0)), tls = f29_reduce3<Fs>(qsum(tl)), tbs = f29_reduce3<Fs>(qsum(tb));
+  // --- F: lane 0 l_0, 1 l_last, 2 l_blind, 3 carries 1 / (x^n - 1)
+  // (lane 3's product by one (R) is 1 / (x^n - 1) itself, < 2p like the others)
+  const F29<Fs> lv = qmul<Fs>(q, xn1, t0s, xn1, tls, xn1, tbs, inv_xn1, one29);
+  Fe<Fs> o;
+  f29_to_r256<Fs>(lv, o.l);
+  if (own) wq.put<Fs>(q, o);
+}
+
 template <class Fs>
 __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t* __restrict__ prog_g,
                                                      const uint32_t* __restrict__ consts_g,
@@ -234,7 +352,10 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   auto get29 = [&](const LdsRows& r, uint32_t row) { return f29_unpack<Fs>(r.get<Fs>(row).l); };
   auto ld29 = [&](uint32_t idx) { return f29_unpack<Fs>(ldfe<Fs>(consts, idx).l); };  // canonical R261
   const F29<Fs> one29 = f29_const<Fs>(K29::ONE);
-  if (live && role == 0) {
+  if (role == 0 && np <= 16) {
+    // a quad per proof (acc_lagrange_q); the results are read after the barrier
+    acc_lagrange_q<Fs>(h, wk, consts, challenges, b0, nv, status);
+  } else if (live && role == 0) {
     // x^n (verifier.rs:513-516)
     const F29<Fs> x29 = f29_from_r256<Fs>(x.l);  // < 2p
     F29<Fs> xn = x29;
@@ -256,23 +377,9 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     // point) is where the reference's main_gate.div fails (vanishing.rs:175,
     // verifier.rs:580): flag the proof; its outputs are then unspecified
     if (status && f29_is_zero_mod<Fs>(pre)) status[b] |= kAccStatusDenomZero;
-  }
-  if (role == 0) {
-    // the inverse of the product (variable-time safegcd, < 2p) into row 2K - 1:
-    // up to 16 proofs per block the whole wave works, a quad per proof
-    // (sg_inverse_q: 27 us against 34 us for one lane)
-    if (np <= 16) {
-      const LdsRows wq{wk.base, pl >> 2, wk.stride};
-      const bool own = (pl >> 2) < nv;
-      const F29<Fs> r = f29_inv_q<Fs>(own ? get29(wq, 2 * K - 1) : f29_zero<Fs>());
-      if (own && (pl & 3u) == 0) put29(wq, 2 * K - 1, r);
-    } else if (live) {
-      put29(wk, 2 * K - 1, f29_inv<Fs>(get29(wk, 2 * K - 1)));
-    }
-  }
-  if (live && role == 0) {
-    const F29<Fs> xn1 = get29(wk, K - 1);  // den_{K-1}, before the walk below replaces it
-    F29<Fs> inv = get29(wk, 2 * K - 1);
+    // the inverse of the product (variable-time safegcd, < 2p)
+    F29<Fs> inv = f29_inv<Fs>(pre);
+    const F29<Fs> xn1d = get29(wk, K - 1);  // den_{K-1}, before the walk below replaces it
     for (uint32_t i = K - 1; i > 0; i--) {
       const F29<Fs> t = f29_mul_c<Fs>(inv, get29(wk, K + i - 1));
       inv = f29_mul_c<Fs>(inv, get29(wk, i));
@@ -281,7 +388,7 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
     put29(wk, 0, inv);
     F29<Fs> l0 = f29_zero<Fs>(), llast = l0, lblind = l0;
     for (uint32_t i = 0; i + 1 < K; i++) {
-      const F29<Fs> li = f29_mul_c<Fs>(f29_mul_c<Fs>(ld29(h.c_wpow29 + i), xn1), get29(wk, i));  // < 2p
+      const F29<Fs> li = f29_mul_c<Fs>(f29_mul_c<Fs>(ld29(h.c_wpow29 + i), xn1d), get29(wk, i));  // < 2p
       if (i == 0) l0 = li;
       else if (i == h.bf + 1) llast = li;
       else lblind = f29_reduce3<Fs>(f29_norm<Fs>(f29_add<Fs>(lblind, li)));  // < 3p
@@ -441,6 +548,12 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const uint64_t pc3 = wall_clock64();
 #endif
   if (live && role == 0) {
+    if (np <= 16) {  // acc_lagrange_q's results
+      l_0 = wk.get<Fs>(0);
+      l_last = wk.get<Fs>(1);
+      omb = fe_sub<Fs>(one, fe_add<Fs>(l_last, wk.get<Fs>(2)));
+      inv_xn1 = wk.get<Fs>(3);
+    }
     // expressions in order gates, permutation, lookups: h = h y + sel expr,
     // folded per selector by wave 1
     const Fe<Fs> hv = fe_add<Fs>(
