@@ -120,7 +120,7 @@ struct AccDecode {
   const void* inst;
   std::vector<uint32_t> off_of;
   bool sliced;         // row-sliced square roots (few points)
-  uint32_t pt_blocks;  // the point part's blocks (one CU each when fenced)
+  uint32_t pt_cus;     // CUs the fenced point blocks take (~0u: unfenced, no room for a ladder beside)
   hipEvent_t in_ready = nullptr;  // on st: the inputs are on the device (recorded before the decode)
   bool launched = false;          // the decode is already queued on st (it writes the twist factors)
 };
@@ -353,7 +353,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // side by side: beyond, they queue for each other (B = 256: 256 + 100)
   {
     const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
-    h.twist = dec && dec->sliced && lgS > 0 && twist_on && dec->pt_blocks + lad_blocks <= 256 ? 1u : 0u;
+    h.twist = dec && dec->sliced && lgS > 0 && twist_on && (size_t)dec->pt_cus + lad_blocks <= 256 ? 1u : 0u;
   }
   if (h.twist && !dec->launched && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4))))
     return rc;
@@ -730,7 +730,12 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   dec.stride = stride;
   dec.inst = d_inst;
   dec.sliced = sliced;
-  dec.pt_blocks = h.nblk_pts;
+  // the decode's fence: one block per CU up to 256 point blocks (beyond, the
+  // grid is throughput work and packing is fine).  (Two per CU beside the
+  // twisted ladder at B = 256 measured no gain: the ladder then ran 0.26 ->
+  // 0.36 ms, the whole chip busy; round 5.)
+  const size_t dec_fence = h.nblk_pts <= 256 ? kDecodeFence : 0;
+  dec.pt_cus = h.nblk_pts <= 256 ? h.nblk_pts : ~0u;
   dec.off_of.assign(L.npts, kAccNoByte);
   for (size_t i = 0; i + 1 < map.size(); i += 2) dec.off_of[map[i + 1]] = map[i];
   const SqrtTab* tabp = (const SqrtTab*)ctx->sqrt_tab[slot].p;
@@ -742,8 +747,6 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     // cp: the twisted ladder's factors (acc_corr, sized by accum_device_impl)
     auto kern = sliced ? k_proof_decode<Cv, true> : k_proof_decode<Cv, false>;
     const size_t stat = sliced ? decode_static_lds<Cv, true>() : decode_static_lds<Cv, false>();
-    // a grid beyond one block per CU is throughput work: packing is fine there
-    if (h.nblk_pts > 256) fence = 0;
     const size_t dyn = fence > stat ? fence - stat : 0;
     PM_LAUNCH_ST(ctx, dst, "proof_decode",
                  (kern<<<(unsigned)(h.nblk_pts + nblk_sc), kDecodeThreads, dyn, dst>>>(
@@ -752,7 +755,7 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     return PM_OK;
   };
   if (!vk_repr) {
-    if ((rc = dec.launch(st, kDecodeFence, nullptr))) return rc;
+    if ((rc = dec.launch(st, dec_fence, nullptr))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     ctx->end_call();
     return PM_OK;
@@ -764,7 +767,7 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   if (!dec.in_ready) return set_error(PM_ERR_HIP, "hipEventCreate failed");
   HIP_TRY(hipEventRecord(dec.in_ready, st));
   if ((rc = ctx->acc_corr.ensure(B * (size_t)L.npts * kAccCorrWords * sizeof(uint4)))) return rc;
-  if ((rc = dec.launch(st, kDecodeFence, (uint4*)ctx->acc_corr.p))) return rc;
+  if ((rc = dec.launch(st, dec_fence, (uint4*)ctx->acc_corr.p))) return rc;
   dec.launched = true;
   rc = accum_device_impl<Cv>(ctx, s, B, d_points, d_scalars, d_ch, d_quads, d_h, vk_repr, d_status, true, dflags,
                              &dec);
