@@ -1024,6 +1024,9 @@ __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename 
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t NL = 1u << lgL, g = gl >> lgL, lane = gl & (NL - 1);
   if (g >= h.B * 4) return;  // whole groups only (a group never straddles a wave)
+#ifdef PM_ACC_PROFILE
+  const uint64_t pc0 = wall_clock64();
+#endif
   const uint32_t b = g >> 2, o = g & 3;
   const uint32_t lo = o == 0 ? h.nslots : o == 1 ? h.nslots + h.nsets : o == 2 ? 0 : h.T - 1;
   const uint32_t hi = o == 0 ? h.nslots + h.nsets : o == 1 ? h.nslots + 2 * h.nsets : o == 2 ? h.nslots : h.T;
@@ -1043,13 +1046,26 @@ __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename 
   // each lane then stores one 16-B quarter), or by lane 0 alone
   const bool quad = NL >= 4;
   if (lane >= (quad ? 4u : 1u)) return;
+#ifdef PM_ACC_PROFILE
+  const uint64_t pc1 = wall_clock64();
+  uint64_t pc2 = pc1;
+#endif
   uint32_t wx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!xyzz29_is_inf<F>(acc)) {  // uniform over the quad (equal acc)
     const F29<F> zz = f29_mul_c<F>(acc.ZZ, acc.ZZZ);
     const F29<F> inv = quad ? f29_inv_q<F>(zz) : f29_inv<F>(zz);  // 1 / (ZZ ZZZ)
+#ifdef PM_ACC_PROFILE
+    pc2 = wall_clock64();
+#endif
     f29_to_r256<F>(f29_canon<F>(f29_mul_c<F>(acc.X, f29_mul_c<F>(inv, acc.ZZZ))), wx);
     f29_to_r256<F>(f29_canon<F>(f29_mul_c<F>(acc.Y, f29_mul_c<F>(inv, acc.ZZ))), wy);
   }
+#ifdef PM_ACC_PROFILE  // A/B builds only: fold / inversion / affine times of group 0..3 (10 ns ticks)
+  const uint64_t pc3 = wall_clock64();
+  if (g < 4 && lane == 0)
+    printf("acc_sum g %u NL %u: fold %llu inv %llu affine %llu\n", g, NL, (unsigned long long)(pc1 - pc0),
+           (unsigned long long)(pc2 - pc1), (unsigned long long)(pc3 - pc2));
+#endif
   uint4* q = reinterpret_cast<uint4*>(out + 16ull * g);
   if (!quad || lane == 0) q[0] = make_uint4(wx[0], wx[1], wx[2], wx[3]);
   if (!quad || lane == 1) q[1] = make_uint4(wx[4], wx[5], wx[6], wx[7]);
