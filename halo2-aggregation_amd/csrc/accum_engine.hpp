@@ -358,6 +358,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   if (h.twist && !dec->launched && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4))))
     return rc;
   std::vector<uint64_t> built_key;  // VK tables built by this call (committed after its final sync)
+  bool lad_sliced = false;          // the ladder's chain form (below)
   // without the twist the decode comes first: everything after reads its points
   if (dec && !dec->launched && !h.twist && (rc = dec->launch(st, kDecodeFence, nullptr))) return rc;
   if (lgS > 0) {  // inputs and uploads are ready at this point of the stream
@@ -395,6 +396,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     // steps while the waves fit one per SIMD); more: a quad per chain
     const size_t chains = nprf + nvk_build;
     const bool sliced = ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1 : chains <= kAccSlicedChains;
+    lad_sliced = sliced;
     if (chains > 0 && sliced)
       PM_LAUNCH_ST(ctx, lst, "acc_ladder",
                 (k_acc_powers_s<Cv><<<(unsigned)((chains + 3) / 4), 256, kAccSlicedFence, lst>>>(
@@ -441,19 +443,31 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
                (k_acc_scalars<Fs><<<(unsigned)((B + np - 1) / np), 256, lds, side>>>(
                    h, dprog, (const uint32_t*)ctx->acc_const.buf.p, (const uint32_t*)d_scalars, (const uint32_t*)d_ch,
                    dcoef, (uint32_t*)d_hout, np, (uint32_t*)d_status)));
+  // the stream of the term additions and sums (tst): the one whose chain
+  // ends last, so the cross-stream wait finds its event already signalled.
+  // With the twist and the quad ladder (0.26 ms against decode -> transcript
+  // -> scalars ~0.25) that is the ladder's stream; with the sliced ladder
+  // (0.15 ms) the main one.  Waiting for the later stream cost ~5-10 us more
+  // (profiles/r05/tail_ab/, interleaved runs: B = 64 0.433 -> 0.427 ms, B =
+  // 128 0.454 -> 0.446; B = 16 0.341 -> 0.347 had it followed the ladder too)
+  static const bool tail_red = [] {
+    const char* e = getenv("PM_ACC_TAIL_RED");
+    return !(e && *e == '0');
+  }();
+  const hipStream_t tst = lgS > 0 && h.twist && !lad_sliced && tail_red ? ctx->red_stream : st;
   if (lgS > 0) {
     // the term additions wait for the other stream: the scalar block (side),
-    // or with the twist the ladder
-    HIP_TRY(hipEventRecord(sc_done, h.twist ? ctx->red_stream : side));
-    HIP_TRY(hipStreamWaitEvent(st, sc_done, 0));
+    // or with the twist the ladder (or, on the ladder's stream, the scalar block)
+    HIP_TRY(hipEventRecord(sc_done, h.twist ? (tst == st ? ctx->red_stream : st) : side));
+    HIP_TRY(hipStreamWaitEvent(tst, sc_done, 0));
     if (quad_terms)
-      PM_LAUNCH(ctx, "acc_termmul",
-                (k_acc_termadd<Cv, true><<<(unsigned)((nterm * 64 + 255) / 256), 256, 0, st>>>(
+      PM_LAUNCH_ST(ctx, tst, "acc_termmul",
+                (k_acc_termadd<Cv, true><<<(unsigned)((nterm * 64 + 255) / 256), 256, 0, tst>>>(
                     h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p,
                     (const uint4*)ctx->acc_corr.p, lgT, dpart)));
     else
-      PM_LAUNCH(ctx, "acc_termmul",
-                (k_acc_termadd<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, st>>>(
+      PM_LAUNCH_ST(ctx, tst, "acc_termmul",
+                (k_acc_termadd<Cv><<<(unsigned)((nterm * S + 255) / 256), 256, 0, tst>>>(
                     h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p,
                     (const uint4*)ctx->acc_corr.p, lgS, dpart)));
   } else {
@@ -472,10 +486,10 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     if (!done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     const unsigned nblk = (unsigned)((B * 4 * (1u << lgL) + 63) / 64);
     if (ctx->timing) {
-      PM_LAUNCH(ctx, "acc_sum", (k_acc_sum<Cv><<<nblk, 64, 0, st>>>(h, dpart, lgL, (uint32_t*)d_out)));
-      HIP_TRY(hipEventRecord(done, st));
+      PM_LAUNCH_ST(ctx, tst, "acc_sum", (k_acc_sum<Cv><<<nblk, 64, 0, tst>>>(h, dpart, lgL, (uint32_t*)d_out)));
+      HIP_TRY(hipEventRecord(done, tst));
     } else {  // the completion event rides on the dispatch (no marker packet behind it)
-      hipExtLaunchKernelGGL(k_acc_sum<Cv>, dim3(nblk), dim3(64), 0, st, nullptr, done, 0, h, dpart, lgL,
+      hipExtLaunchKernelGGL(k_acc_sum<Cv>, dim3(nblk), dim3(64), 0, tst, nullptr, done, 0, h, dpart, lgL,
                             (uint32_t*)d_out);
       HIP_TRY(hipGetLastError());
     }
