@@ -471,9 +471,20 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
                     h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p,
                     (const uint4*)ctx->acc_corr.p, lgS, dpart)));
   } else {
-    PM_LAUNCH(ctx, "acc_termmul",
-              (k_acc_termmul<Cv><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
-                  h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, dpart)));
+    // GLV products by signed 3-bit windows (PM_ACC_GLVW=0: the joint
+    // double-and-add of round 2)
+    static const bool w3 = [] {
+      const char* e = getenv("PM_ACC_GLVW");
+      return !(e && *e == '0');
+    }();
+    if (w3)
+      PM_LAUNCH(ctx, "acc_termmul",
+                (k_acc_termmul<Cv, true><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
+                    h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, dpart)));
+    else
+      PM_LAUNCH(ctx, "acc_termmul",
+                (k_acc_termmul<Cv, false><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
+                    h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, dpart)));
   }
   // lanes per output: at most ~16 K in total.  The affine conversion runs on
   // lane 0 of each group, and it slowed from ~0.08 to ~0.14 ms when 32

@@ -77,10 +77,11 @@ def test_device_code_has_every_launched_kernel():
 
     assert count("11k_sort_hist") == 3 * 16 * 2  # 3 scalar fields x 16 window counts x {2-B, 4-B digits}
     for stem in ("12k_accumulate", "14k_bucket_seg_q", "13k_bucket_bits", "15k_bases_to_r261",
-                 "16k_selftest_field", "13k_acc_termmul", "9k_acc_sum", "13k_acc_scalars", "12k_acc_powers",
+                 "16k_selftest_field", "9k_acc_sum", "13k_acc_scalars", "12k_acc_powers",
                  "15k_synth_scalars", "13k_synth_bases", "14k_transcript_s", "12k_transcriptI", "14k_acc_powers_s"):
         assert count(stem) == 3, stem
     assert count("13k_acc_termadd") == 3 * 2  # lane groups / quad-cooperative form
+    assert count("13k_acc_termmul") == 3 * 2  # signed 3-bit windows / the joint double-and-add
     # the retired A/B kernels are gone (GLV mode, separate fixups, bit-sum fold pass)
     for stem in ("15k_sort_hist_glv", "11k_bases_glv", "7k_fixupI", "12k_fixup_long", "13k_fixup_short",
                  "12k_bucket_segI", "14k_bits_combine"):
