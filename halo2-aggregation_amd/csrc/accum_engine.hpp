@@ -249,6 +249,21 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     h.ninst = s->num_instance_columns;
   }
 
+  // pairs of terms of one output for the one-lane form's two-term lanes
+  // (k_acc_termmul NT = 2), per output range as k_acc_sum folds them
+  const uint32_t p_pairs = (uint32_t)prog.size();
+  uint32_t npair = 0;
+  {
+    const uint32_t T0 = (uint32_t)termsrc.size(), ns = nslots, nst = L.nsets;
+    const uint32_t lo[4] = {0, ns, ns + nst, T0 - 1}, hi[4] = {ns, ns + nst, ns + 2 * nst, T0};
+    for (int o = 0; o < 4; o++)
+      for (uint32_t t = lo[o]; t < hi[o]; t += 2) {
+        prog.push_back(t);
+        prog.push_back(t + 1 < hi[o] ? t + 1 : kAccNoByte);
+        npair++;
+      }
+  }
+
   // --- constants (Montgomery)
   std::vector<uint32_t> cst;
   h.c_user = 0;
@@ -477,14 +492,27 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
       const char* e = getenv("PM_ACC_GLVW");
       return !(e && *e == '0');
     }();
-    if (w3)
+    // two terms of one output per lane (shared doublings) once one term per
+    // lane would put more than one wave on a SIMD, while the pairs still fit
+    // one wave per SIMD (their 144 KiB of LDS tables per block keep one block
+    // per CU); PM_ACC_TPL = 1 / 2 forces
+    const char* tpl_env = getenv("PM_ACC_TPL");
+    const bool pairs_fit = (size_t)B * npair <= kAccLaneBudget / 2;
+    const int tpl = tpl_env && *tpl_env ? (atoi(tpl_env) == 2 ? 2 : 1)
+                                        : (nterm > kAccLaneBudget / 2 && pairs_fit ? 2 : 1);
+    const uint32_t* dvk = (const uint32_t*)ctx->acc_vk.buf.p;
+    if (w3 && tpl == 2)
       PM_LAUNCH(ctx, "acc_termmul",
-                (k_acc_termmul<Cv, true><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
-                    h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, dpart)));
+                (k_acc_termmul<Cv, true, 2><<<(unsigned)(((size_t)B * npair + 255) / 256), 256, 0, st>>>(
+                    h, dprog, dcoef, (const uint32_t*)d_points, dvk, p_pairs, npair, dpart)));
+    else if (w3)
+      PM_LAUNCH(ctx, "acc_termmul",
+                (k_acc_termmul<Cv, true, 1><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
+                    h, dprog, dcoef, (const uint32_t*)d_points, dvk, 0u, 0u, dpart)));
     else
       PM_LAUNCH(ctx, "acc_termmul",
-                (k_acc_termmul<Cv, false><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
-                    h, dprog, dcoef, (const uint32_t*)d_points, (const uint32_t*)ctx->acc_vk.buf.p, dpart)));
+                (k_acc_termmul<Cv, false, 1><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
+                    h, dprog, dcoef, (const uint32_t*)d_points, dvk, 0u, 0u, dpart)));
   }
   // lanes per output: at most ~16 K in total.  The affine conversion runs on
   // lane 0 of each group, and it slowed from ~0.08 to ~0.14 ms when 32

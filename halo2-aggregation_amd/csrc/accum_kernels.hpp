@@ -637,6 +637,15 @@ __device__ Xyzz29<typename Cv::Base> glv_mul(const Fe<typename Cv::Scalar>& k, c
 // 256, two blocks per CU), picked by address instead of register selects (in
 // registers the kernel spilled).
 constexpr uint32_t kW3Words = 4 * 18;
+// [k]P with signed base-8 windows (round 5): both rounded GLV halves (|k_i| <
+// 2^127) recoded into 43 digits in [-4, 4] each; a table [m]P, m = 1..4
+// (affine, one batched inversion) serves both halves (phi: beta x per use).
+// Per window 3 doublings and 2 mixed additions: 129 + 86 steps against
+// glv_mul's 128 + 128 (a wave adds whenever any of its lanes has a set bit,
+// so the joint form's zero pairs save nothing).
+// The table lives in LDS, [word][lane] (72 words per lane: 72 KiB per block of
+// 256, two blocks per CU), picked by address instead of register selects (in
+// registers the kernel spilled).
 template <class Cv>
 __device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P,
                                                 uint32_t (*tab)[256]) {
@@ -726,24 +735,163 @@ __device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3(const Fe<typenam
   return acc;
 }
 
-template <class Cv, bool W3 = true>
+// One term's half of the work: the rounded GLV split recoded into the digit
+// codes (magnitude | sign << 3, 8 per word, window 0 lowest; the half's sign
+// folded in) and its table [m]P, m = 1..4, at LDS rows r0 + 18 (m - 1) + limb
+// (x), + 9 (y).
+template <class Cv>
+__device__ __forceinline__ void w3_prepare(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P,
+                                           uint32_t (*tab)[256], uint32_t r0, uint32_t c1[6], uint32_t c2[6]) {
+  using F = typename Cv::Base;
+  using K = F29Consts<F>;
+  constexpr int kWin = 43;  // 3-bit windows over bits 0..128
+  uint32_t k1[6], k2[6];
+  bool n1, n2;
+  glv_split<Cv, true>(k, k1, k2, n1, n2);
+  const uint32_t s1 = n1 ? 8u : 0u, s2 = n2 ? 8u : 0u;
+  {
+    uint32_t cy1 = 0, cy2 = 0;
+#pragma unroll
+    for (int i = 0; i < kWin; i++) {
+      const int b = 3 * i, wd = b >> 5, sh = b & 31;
+      const uint64_t w1 = (uint64_t)k1[wd] | (wd + 1 < 6 ? (uint64_t)k1[wd + 1] << 32 : 0ull);
+      const uint64_t w2 = (uint64_t)k2[wd] | (wd + 1 < 6 ? (uint64_t)k2[wd + 1] << 32 : 0ull);
+      const uint32_t v1 = (uint32_t)(w1 >> sh) & 7u, v2 = (uint32_t)(w2 >> sh) & 7u;
+      const uint32_t u1 = v1 + cy1, u2 = v2 + cy2;
+      cy1 = u1 > 4u ? 1u : 0u;
+      cy2 = u2 > 4u ? 1u : 0u;
+      // u = 8: digit 0, carry 1; a nonzero digit's sign is flipped by the half's
+      const uint32_t e1 = cy1 ? (u1 < 8u ? (8u - u1) | (8u ^ s1) : 0u) : (u1 ? u1 | s1 : 0u);
+      const uint32_t e2 = cy2 ? (u2 < 8u ? (8u - u2) | (8u ^ s2) : 0u) : (u2 ? u2 | s2 : 0u);
+      c1[i >> 3] |= e1 << (4 * (i & 7));
+      c2[i >> 3] |= e2 << (4 * (i & 7));
+    }
+  }
+  const uint32_t ln = threadIdx.x;
+  auto put = [&](uint32_t row, const F29<F>& v) {
+#pragma unroll
+    for (int t = 0; t < 9; t++) tab[r0 + row + t][ln] = v.l[t];
+  };
+  const F29<F> one = f29_const<F>(K::ONE);
+  const F29<F> x1 = f29_canon<F>(f29_from_r256<F>(P.x.l)), y1 = f29_canon<F>(f29_from_r256<F>(P.y.l));
+  put(0, x1);
+  put(9, y1);
+  const Xyzz29<F> Q2 = xyzz29_dbl_impl<F, true>(x1, y1, one, one);
+  bool qi = false;
+  const Xyzz29<F> Q3 = xyzz29_madd<F>(Q2, x1, y1, qi);  // 2P + P: 2P != +-P (odd order)
+  const Xyzz29<F> Q4 = xyzz29_dbl<F>(Q2);
+  const F29<F> d2 = f29_mul_c<F>(Q2.ZZ, Q2.ZZZ), d3 = f29_mul_c<F>(Q3.ZZ, Q3.ZZZ), d4 = f29_mul_c<F>(Q4.ZZ, Q4.ZZZ);
+  const F29<F> d23 = f29_mul_c<F>(d2, d3);
+  const F29<F> inv = f29_inv<F>(f29_mul_c<F>(d23, d4));  // 1 / (d2 d3 d4)
+  const F29<F> i4 = f29_mul_c<F>(inv, d23), i23 = f29_mul_c<F>(inv, d4);
+  const F29<F> i2 = f29_mul_c<F>(i23, d3), i3 = f29_mul_c<F>(i23, d2);
+  // 1 / ZZ = ZZZ / d, 1 / ZZZ = ZZ / d
+  put(18, f29_canon<F>(f29_mul_c<F>(Q2.X, f29_mul_c<F>(i2, Q2.ZZZ))));
+  put(27, f29_canon<F>(f29_mul_c<F>(Q2.Y, f29_mul_c<F>(i2, Q2.ZZ))));
+  put(36, f29_canon<F>(f29_mul_c<F>(Q3.X, f29_mul_c<F>(i3, Q3.ZZZ))));
+  put(45, f29_canon<F>(f29_mul_c<F>(Q3.Y, f29_mul_c<F>(i3, Q3.ZZ))));
+  put(54, f29_canon<F>(f29_mul_c<F>(Q4.X, f29_mul_c<F>(i4, Q4.ZZZ))));
+  put(63, f29_canon<F>(f29_mul_c<F>(Q4.Y, f29_mul_c<F>(i4, Q4.ZZ))));
+}
+
+// sum_j [k_j] P_j over NT terms (NT = 1, 2) with signed base-8 windows
+// (round 5): both rounded GLV halves of each k_j (|k_i| < 2^127) in 43 digits
+// in [-4, 4], a table [m]P_j, m = 1..4 (affine, one batched inversion per
+// term) serving both halves (phi: beta x per use).  Per window 3 doublings,
+// shared by the NT terms (Straus), and 2 NT mixed additions: 129 + 86 steps per
+// term against glv_mul's 128 + 128 (a wave adds whenever any of its lanes has
+// a set bit, so the joint form's zero pairs save nothing), 65 + 86 at NT = 2.
+// The tables live in LDS, [word][lane] (72 words per lane and term), picked by
+// address instead of register selects (in registers the kernel spilled).
+// live: bit j set when term j is present and its point is not the identity.
+template <class Cv, int NT>
+__device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3n(const Fe<typename Cv::Scalar>& k0,
+                                                                const Aff<typename Cv::Base>& P0,
+                                                                const Fe<typename Cv::Scalar>& k1,
+                                                                const Aff<typename Cv::Base>& P1, uint32_t live,
+                                                                uint32_t (*tab)[256]) {
+  using F = typename Cv::Base;
+  constexpr int kWin = 43;
+  uint32_t c[NT][2][6];
+#pragma unroll
+  for (int j = 0; j < NT; j++)
+#pragma unroll
+    for (int w = 0; w < 6; w++) c[j][0][w] = c[j][1][w] = 0u;
+  if (live & 1u) w3_prepare<Cv>(k0, P0, tab, 0, c[0][0], c[0][1]);
+  if (NT > 1 && (live & 2u)) w3_prepare<Cv>(k1, P1, tab, kW3Words, c[NT - 1][0], c[NT - 1][1]);
+  const uint32_t ln = threadIdx.x;
+  const F29<F> beta = f29_const<F>(Glv<Cv>::BETA29);
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  bool acc_inf = true;
+  for (int i = kWin - 1; i >= 0; i--) {
+    acc = xyzz29_dbl<F>(xyzz29_dbl<F>(xyzz29_dbl<F>(acc)));
+    const uint32_t sh = 4u * (uint32_t)(i & 7);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        // this window's code (register words picked by selects, not scratch)
+        uint32_t wv = 0;
+#pragma unroll
+        for (int w = 0; w < 6; w++) wv = w == (i >> 3) ? c[j][half][w] : wv;
+        const uint32_t e = (wv >> sh) & 15u, m = e & 7u;
+        if (m == 0) continue;
+        F29<F> qx, qy;
+        const uint32_t r0 = kW3Words * j + 18u * (m - 1u);
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+          qx.l[t] = tab[r0 + t][ln];
+          qy.l[t] = tab[r0 + 9 + t][ln];
+        }
+        if (half) qx = f29_canon<F>(f29_mul_c<F>(beta, qx));
+        if (e & 8u) qy = f29_canon<F>(f29_neg_canon<F>(qy));
+        acc = xyzz29_madd<F>(acc, qx, qy, acc_inf);
+      }
+    }
+  }
+  return acc;
+}
+
+// k_acc_termmul: a lane per term (NT = 1, or W3 = false: glv_mul), or with
+// NT = 2 a lane per pair of terms of one output (prog[p_pairs]: npair (t0, t1)
+// per proof, t1 = kAccNoByte for a single); the lane stores the pair's sum at
+// t0 and the identity at t1, so k_acc_sum folds the same rows.
+template <class Cv, bool W3 = true, int NT = 1>
 __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t* __restrict__ prog,
                                                      const uint32_t* __restrict__ coef,
                                                      const uint32_t* __restrict__ points,
-                                                     const uint32_t* __restrict__ vk,
-                                                     Xyzz<typename Cv::Base>* __restrict__ part) {
+                                                     const uint32_t* __restrict__ vk, uint32_t p_pairs,
+                                                     uint32_t npair, Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;  // part[] holds packed R261 (curve29.hpp) points
-  __shared__ uint32_t w3tab[W3 ? kW3Words : 1][256];
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= h.B * h.T) return;
-  const uint32_t b = g / h.T, t = g - b * h.T;
-  const uint32_t src = prog[h.p_termsrc + t];
-  const uint32_t idx = src & 0x0FFFFFFFu;
-  const uint32_t* pp = (src >> 28) == 0 ? points + 16ull * ((size_t)h.npts * b + idx) : vk + 16ull * idx;
-  const Aff<F> P = load_aff<F>(pp);
-  const Fe<Fs> c = ldfe<Fs>(coef, g);
-  store_xyzz29<F>(&part[g], aff_is_inf<F>(P) ? xyzz29_inf<F>() : W3 ? glv_mul_w3<Cv>(c, P, w3tab) : glv_mul<Cv>(c, P));
+  __shared__ uint32_t w3tab[W3 ? NT * kW3Words : 1][256];
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t per = NT == 1 ? h.T : npair;
+  if (gl >= h.B * per) return;
+  const uint32_t b = gl / per, r = gl - b * per;
+  const uint32_t t0 = NT == 1 ? r : prog[p_pairs + 2 * r];
+  const uint32_t t1 = NT == 1 ? kAccNoByte : prog[p_pairs + 2 * r + 1];
+  auto term_point = [&](uint32_t t) {
+    const uint32_t src = prog[h.p_termsrc + t];
+    const uint32_t idx = src & 0x0FFFFFFFu;
+    return load_aff<F>((src >> 28) == 0 ? points + 16ull * ((size_t)h.npts * b + idx) : vk + 16ull * idx);
+  };
+  const Aff<F> P0 = term_point(t0);
+  const Fe<Fs> k0 = ldfe<Fs>(coef, b * h.T + t0);
+  uint32_t live = aff_is_inf<F>(P0) ? 0u : 1u;
+  Aff<F> P1 = P0;
+  Fe<Fs> k1 = k0;
+  if (NT > 1 && t1 != kAccNoByte) {
+    P1 = term_point(t1);
+    k1 = ldfe<Fs>(coef, b * h.T + t1);
+    if (!aff_is_inf<F>(P1)) live |= 2u;
+  }
+  Xyzz29<F> acc;
+  if (W3 && NT > 1) acc = live ? glv_mul_w3n<Cv, NT>(k0, P0, k1, P1, live, w3tab) : xyzz29_inf<F>();
+  else if (W3) acc = live ? glv_mul_w3<Cv>(k0, P0, w3tab) : xyzz29_inf<F>();
+  else acc = live ? glv_mul<Cv>(k0, P0) : xyzz29_inf<F>();
+  store_xyzz29<F>(&part[b * h.T + t0], acc);
+  if (NT > 1 && t1 != kAccNoByte) store_xyzz29<F>(&part[b * h.T + t1], xyzz29_inf<F>());
 }
 
 

@@ -53,6 +53,32 @@ def test_split_ladder_widths(gpu_ctx, lg):
         gpu_ctx.set_accum_split(-1)
 
 
+@pytest.mark.parametrize("tpl", ["1", "2"])
+def test_one_lane_windows_terms_per_lane(gpu_ctx, tpl):
+    """The one-lane form's GLV products by signed 3-bit windows with one term
+    per lane and with two terms of one output per lane (shared doublings, the
+    pair's sum at its first row and the identity at its second; chosen
+    automatically for large batches, forced here with PM_ACC_TPL) reproduce
+    the golden vectors and random rich-shape proofs on Pallas and BN254."""
+    import os
+
+    gpu_ctx.set_accum_split(0)
+    os.environ["PM_ACC_TPL"] = tpl
+    try:
+        test_golden_accumulator(gpu_ctx)
+        for cid in (0, 2):
+            C, sh, proofs = U.make_case(cid, "rich", 12, 5, 0x7B1 + cid)
+            ps = U.to_product_shape(cid, sh)
+            pts, scs, chs = A.pack_proofs(C, sh, proofs)
+            quads, h = gpu_ctx.accum_batch(ps, pts, scs, chs)
+            for b, pf in enumerate(proofs):
+                q, hh = A.pack_result(C, A.accumulate_msm(C, sh, pf))
+                assert np.array_equal(h[b], hh) and np.array_equal(quads[b], q), (cid, b)
+    finally:
+        del os.environ["PM_ACC_TPL"]
+        gpu_ctx.set_accum_split(-1)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_ladder_modes(gpu_ctx, mode):
     """Both forms of the powers-of-two table chains (0: a quad of lanes per
