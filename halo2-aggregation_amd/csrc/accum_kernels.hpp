@@ -812,13 +812,11 @@ __device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3n(const Fe<typena
                                                                 uint32_t (*tab)[256]) {
   using F = typename Cv::Base;
   constexpr int kWin = 43;
-  uint32_t c[NT][2][6];
-#pragma unroll
-  for (int j = 0; j < NT; j++)
-#pragma unroll
-    for (int w = 0; w < 6; w++) c[j][0][w] = c[j][1][w] = 0u;
-  if (live & 1u) w3_prepare<Cv>(k0, P0, tab, 0, c[0][0], c[0][1]);
-  if (NT > 1 && (live & 2u)) w3_prepare<Cv>(k1, P1, tab, kW3Words, c[NT - 1][0], c[NT - 1][1]);
+  // four named code arrays (a [2][2][6] array went to scratch)
+  uint32_t ca1[6] = {0, 0, 0, 0, 0, 0}, ca2[6] = {0, 0, 0, 0, 0, 0};
+  uint32_t cb1[6] = {0, 0, 0, 0, 0, 0}, cb2[6] = {0, 0, 0, 0, 0, 0};
+  if (live & 1u) w3_prepare<Cv>(k0, P0, tab, 0, ca1, ca2);
+  if (NT > 1 && (live & 2u)) w3_prepare<Cv>(k1, P1, tab, kW3Words, cb1, cb2);
   const uint32_t ln = threadIdx.x;
   const F29<F> beta = f29_const<F>(Glv<Cv>::BETA29);
   Xyzz29<F> acc = xyzz29_inf<F>();
@@ -831,9 +829,10 @@ __device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3n(const Fe<typena
 #pragma unroll
       for (int half = 0; half < 2; half++) {
         // this window's code (register words picked by selects, not scratch)
+        const uint32_t* cw = j == 0 ? (half ? ca2 : ca1) : (half ? cb2 : cb1);
         uint32_t wv = 0;
 #pragma unroll
-        for (int w = 0; w < 6; w++) wv = w == (i >> 3) ? c[j][half][w] : wv;
+        for (int w = 0; w < 6; w++) wv = w == (i >> 3) ? cw[w] : wv;
         const uint32_t e = (wv >> sh) & 15u, m = e & 7u;
         if (m == 0) continue;
         F29<F> qx, qy;
