@@ -46,7 +46,7 @@ BYTES_PER_PAIR = 96            # 32 B scalar + 64 B affine base
 SEED_SCALARS, SEED_BASES = 0x5EED, 0xA11CE
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -79,7 +79,130 @@ def parse():
                     help="also time BASELINE config 3: 16 simple-example proofs at k = 14 per GPU (1) or skip (0)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous check only: no GPU work (gloo), prints the JSON skeleton")
-    return ap.parse_args()
+    ap.add_argument("--detail", default=DETAIL_DEFAULT,
+                    help="file for the full per-leg record (kernel breakdowns, small_n curve, configs); "
+                         "the stdout line carries only compact leg summaries ('' = do not write it)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# output: ONE compact stdout line (the driver parses it; round 5's 22 KB line
+# was not parsed) + the full record in a JSON file beside it
+# ---------------------------------------------------------------------------
+DETAIL_DEFAULT = os.path.join("profiles", "bench_detail_last.json")
+LINE_LIMIT = 12000                 # bytes; tests/test_bench_line.py holds the line to it
+CONTRACT_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                 "scaling", "vs_baseline", "dtype", "data")
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "avg_launch_ms",
+             "alg_bytes_per_launch")
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "matches_gpu")
+
+
+def _r(v, nd=4):
+    return round(v, nd) if isinstance(v, float) else v
+
+
+def leg_summary(leg):
+    """value / unit / ms / frac / matches of one sub-leg (the verbose fields
+    stay in the detail file)."""
+    s = {"value": _r(leg.get("value")), "unit": leg.get("unit")}
+    for k in ("ms_per_step", "ms_per_batch", "ms_per_ntt", "warm_ms_per_msm"):
+        if k in leg:
+            s["ms"] = _r(leg[k])
+            break
+    roof = leg.get("roofline")
+    if isinstance(roof, dict):
+        s["frac"] = _r(roof.get("frac"), 5)
+        s["bound"] = roof.get("bound")
+    matches = [v for k, v in leg.items() if (k.startswith("matches") or k.startswith("quads_match"))
+               and isinstance(v, bool)]
+    for sub in ("from_decoded", "per_proof_loop"):
+        if isinstance(leg.get(sub), dict):
+            matches += [v for k, v in leg[sub].items() if k.startswith(("matches", "quads_match"))
+                        and isinstance(v, bool)]
+    if isinstance(leg.get("cpu_baseline"), dict):
+        cb = leg["cpu_baseline"]
+        s["cpu"] = {"value": _r(cb.get("value")), "cores": cb.get("cores"), "kind": cb.get("kind")}
+        for k in ("matches_gpu", "matches"):
+            if isinstance(cb.get(k), bool):
+                matches.append(cb[k])
+    if "status_nonzero" in leg:
+        matches.append(leg["status_nonzero"] == 0)
+    if matches:
+        s["matches"] = all(matches)
+    return {k: v for k, v in s.items() if v is not None}
+
+
+def compact_line(out, detail_path=None):
+    """The stdout JSON line: the contract keys, `config` (workload names only),
+    `roofline` and `cpu_baseline` of the headline, and one compact summary per
+    sub-leg.  Guaranteed under LINE_LIMIT bytes: if the summaries ever grow past
+    it, the least important fields go first and the legs last."""
+    line = {k: out.get(k) for k in CONTRACT_KEYS}
+    cfg = out.get("config") or {}
+    line["config"] = {k: cfg[k] for k in ("workload", "curve", "n_per_gpu", "n_total", "parallelism")
+                      if k in cfg}
+    roof = out.get("roofline")
+    if isinstance(roof, dict):
+        r = {k: roof.get(k) for k in ROOF_KEYS if k in roof}
+        v = roof.get("valu_int")
+        if isinstance(v, dict):
+            r["valu_int"] = {k: v.get(k) for k in ("achieved", "peak", "unit", "frac", "issue_frac")}
+        line["roofline"] = r
+    cpu = out.get("cpu_baseline")
+    if isinstance(cpu, dict):
+        line["cpu_baseline"] = {k: cpu.get(k) for k in CPU_KEYS if k in cpu}
+    legs = {}
+    for k, v in out.items():
+        if k in CONTRACT_KEYS or k in ("config", "roofline", "cpu_baseline", "kernels_ms"):
+            continue
+        if isinstance(v, dict) and "value" in v:
+            legs[k] = leg_summary(v)
+        elif k == "small_n" and isinstance(v, dict):
+            rows = {r["n"]: r for r in v.get("curve", [])}
+            legs[k] = {"gpu_us": {n: rows[n].get("gpu_us") for n in (1, 32, 4096) if n in rows},
+                       "gpu_us_fresh_bases": {n: rows[n].get("gpu_us_fresh_bases") for n in (1, 32, 4096)
+                                              if n in rows},
+                       "matches": all(r.get("match", True) for r in rows.values())}
+        elif k == "dropin_pm_msm" and isinstance(v, dict):
+            legs[k] = {"value": v.get("warm_Mscalar_s"), "unit": "Mscalar/s", "ms": v.get("warm_ms_per_msm"),
+                       "first_ms": v.get("first_ms"), "matches": v.get("matches")}
+        elif k == "host_scalars" and isinstance(v, dict) and isinstance(v.get("pageable"), dict):
+            p = v["pageable"]
+            legs[k] = {"value": p.get("Mscalar_s"), "unit": "Mscalar/s", "ms": p.get("ms_per_msm"),
+                       "matches": p.get("matches")}
+    if legs:
+        line["legs"] = legs
+    if detail_path:
+        line["detail"] = detail_path
+    s = json.dumps(line, separators=(",", ":"))
+    for drop in (("bound",), ("cpu",), ("frac", "ms")):
+        if len(s) < LINE_LIMIT:
+            break
+        for leg in legs.values():
+            for k in drop:
+                leg.pop(k, None)
+        s = json.dumps(line, separators=(",", ":"))
+    if len(s) >= LINE_LIMIT:
+        line.pop("legs", None)
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
+def emit(out, detail_path):
+    """Write the full record to `detail_path` (when set), then print the
+    compact line as the LAST line of stdout."""
+    if detail_path:
+        try:
+            d = os.path.dirname(detail_path)
+            if d:
+                os.makedirs(d, exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(out, f, indent=1)
+        except OSError as e:  # a read-only tree must not cost the headline
+            print(f"bench.py: detail file not written: {e}", file=sys.stderr)
+            detail_path = None
+    print(compact_line(out, detail_path), flush=True)
 
 
 def cpu_threads():
@@ -366,7 +489,7 @@ def main():
         if accum_large is not None:
             accum_large.pop("_state", None)
             out[f"accumulator_b{args.accum_large}"] = accum_large
-        print(json.dumps(out), flush=True)
+        emit(out, args.detail)
     if dist:
         dist.destroy_process_group()
 
@@ -726,10 +849,11 @@ def dry_run(args, rank, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mscalar/s", "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 4), "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "dry run (no GPU work)",
-                          "config": {"workload": f"pallas_msm_2^{args.logn}_per_gpu"}}), flush=True)
+        print(compact_line({"metric": METRIC, "value": None, "unit": "Mscalar/s", "n_gpus": world,
+                            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 4),
+                            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                            "data": "dry run (no GPU work)",
+                            "config": {"workload": f"pallas_msm_2^{args.logn}_per_gpu"}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
