@@ -357,18 +357,15 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // proof bytes with the powers tables: the ladder runs on the twist from the
   // x bytes on the reduction stream, beside the decode -> replay -> scalar
   // block chain on the main stream, which is then the critical one and has no
-  // cross-stream hop (AccDecode; PM_ACC_TWIST=0: the ladder after the decode)
-  static const bool twist_on = [] {
-    const char* e = getenv("PM_ACC_TWIST");
-    return !(e && *e == '0');
-  }();
+  // cross-stream hop (AccDecode; PM_ACC_OPT_TWIST = 0: the ladder after the decode)
+  const bool twist_on = ctx->acc_twist != 0;
   // (only with the row-sliced decode, profiles/r05/twist_ab/: the one-lane
   // decode beside the quad ladder ran 0.12-0.33 ms against 0.13 alone)
   // and while the decode's point blocks and the ladder's blocks fit the CUs
   // side by side: beyond, they queue for each other (B = 256: 256 + 100)
   {
     const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
-    h.twist = dec && dec->sliced && lgS > 0 && twist_on && (size_t)dec->pt_cus + lad_blocks <= 256 ? 1u : 0u;
+    h.twist = dec && dec->sliced && lgS > 0 && twist_on && (size_t)dec->pt_cus + lad_blocks <= (size_t)ctx->num_cus ? 1u : 0u;
   }
   if (h.twist && !dec->launched && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4))))
     return rc;
@@ -420,7 +417,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     else if (chains > 0)
       PM_LAUNCH_ST(ctx, lst, "acc_ladder",
                 (k_acc_powers<Cv><<<(unsigned)((4 * chains + 255) / 256), 256,
-                                    4 * chains <= 256 * 256 ? kAccSlicedFence : kAccLadderFence, lst>>>(
+                                    4 * chains <= 256 * (size_t)ctx->num_cus ? kAccSlicedFence : kAccLadderFence, lst>>>(
                     h, dprog, (const uint32_t*)d_points, lproofs, linst, (const uint32_t*)ctx->acc_vk.buf.p, nvk_build,
                     (uint4*)ctx->acc_lad.p, (uint4*)ctx->acc_vkpow.p)));
     if (!vk_current) {
@@ -465,10 +462,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // (0.15 ms) the main one.  Waiting for the later stream cost ~5-10 us more
   // (profiles/r05/tail_ab/, interleaved runs: B = 64 0.433 -> 0.427 ms, B =
   // 128 0.454 -> 0.446; B = 16 0.341 -> 0.347 had it followed the ladder too)
-  static const bool tail_red = [] {
-    const char* e = getenv("PM_ACC_TAIL_RED");
-    return !(e && *e == '0');
-  }();
+  const bool tail_red = ctx->acc_tail != 0;  // PM_ACC_OPT_TAIL_STREAM = 0: always the main stream
   const hipStream_t tst = lgS > 0 && h.twist && !lad_sliced && tail_red ? ctx->red_stream : st;
   if (lgS > 0) {
     // the term additions wait for the other stream: the scalar block (side),
@@ -486,32 +480,21 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
                     h, dprog, dcoef, (const uint4*)ctx->acc_lad.p, (const uint4*)ctx->acc_vkpow.p,
                     (const uint4*)ctx->acc_corr.p, lgS, dpart)));
   } else {
-    // GLV products by signed 3-bit windows (PM_ACC_GLVW=0: the joint
-    // double-and-add of round 2)
-    static const bool w3 = [] {
-      const char* e = getenv("PM_ACC_GLVW");
-      return !(e && *e == '0');
-    }();
-    // two terms of one output per lane (shared doublings) once one term per
-    // lane would put more than one wave on a SIMD, while the pairs still fit
-    // one wave per SIMD (their 144 KiB of LDS tables per block keep one block
-    // per CU); PM_ACC_TPL = 1 / 2 forces
-    const char* tpl_env = getenv("PM_ACC_TPL");
+    // GLV products by signed 3-bit windows; two terms of one output per lane
+    // (shared doublings) once one term per lane would put more than one wave
+    // on a SIMD, while the pairs still fit one wave per SIMD (their 144 KiB of
+    // LDS tables per block keep one block per CU); PM_ACC_OPT_TERMS_PER_LANE
+    // forces 1 or 2
     const bool pairs_fit = (size_t)B * npair <= kAccLaneBudget / 2;
-    const int tpl = tpl_env && *tpl_env ? (atoi(tpl_env) == 2 ? 2 : 1)
-                                        : (nterm > kAccLaneBudget / 2 && pairs_fit ? 2 : 1);
+    const int tpl = ctx->acc_tpl > 0 ? ctx->acc_tpl : (nterm > kAccLaneBudget / 2 && pairs_fit ? 2 : 1);
     const uint32_t* dvk = (const uint32_t*)ctx->acc_vk.buf.p;
-    if (w3 && tpl == 2)
+    if (tpl == 2)
       PM_LAUNCH(ctx, "acc_termmul",
-                (k_acc_termmul<Cv, true, 2><<<(unsigned)(((size_t)B * npair + 255) / 256), 256, 0, st>>>(
+                (k_acc_termmul<Cv, 2><<<(unsigned)(((size_t)B * npair + 255) / 256), 256, 0, st>>>(
                     h, dprog, dcoef, (const uint32_t*)d_points, dvk, p_pairs, npair, dpart)));
-    else if (w3)
-      PM_LAUNCH(ctx, "acc_termmul",
-                (k_acc_termmul<Cv, true, 1><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
-                    h, dprog, dcoef, (const uint32_t*)d_points, dvk, 0u, 0u, dpart)));
     else
       PM_LAUNCH(ctx, "acc_termmul",
-                (k_acc_termmul<Cv, false, 1><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
+                (k_acc_termmul<Cv, 1><<<(unsigned)((nterm + 255) / 256), 256, 0, st>>>(
                     h, dprog, dcoef, (const uint32_t*)d_points, dvk, 0u, 0u, dpart)));
   }
   // lanes per output: at most ~16 K in total.  The affine conversion runs on
@@ -551,15 +534,10 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
 // runs of the proof's canonical data bytes (points region: 64 bytes per point
 // x || y; scalars region: 32 bytes each), then the point records' indices.
 // false: the shape's stream does not fit the kernel's LDS (or its encoding):
-// the per-record kernel runs instead.  PM_TRANSCRIPT_RECORDS=1 forces that
-// (A/B runs).
+// the per-record kernel runs instead (as it does under PM_ACC_OPT_TRANSCRIPT = 0,
+// the caller's check).
 inline bool tr_stream_plan(const std::vector<uint32_t>& prog, const TranscriptHdr& hd, TrStreamHdr& sh,
                            std::vector<uint32_t>& wtab) {
-  static const bool force_records = [] {
-    const char* e = getenv("PM_TRANSCRIPT_RECORDS");
-    return e && *e == '1';
-  }();
-  if (force_records) return false;
   struct Byte {
     uint32_t kind, v;  // kind 0: constant v; 1 / 2: data byte v of the points / scalars region
   };
@@ -665,7 +643,7 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
   if ((rc = ctx->tr_prog.put(prog, st))) return rc;
   TrStreamHdr sh{};
   std::vector<uint32_t> wtab;
-  const bool streamed = tr_stream_plan(prog, hd, sh, wtab);
+  const bool streamed = ctx->acc_tr_stream != 0 && tr_stream_plan(prog, hd, sh, wtab);
   if (streamed && (rc = ctx->tr_wtab.put(wtab, st))) return rc;
   const size_t ncoord = B * 2 * (size_t)L.npts, nall = ncoord + B * (size_t)L.nsc;
   if ((rc = ctx->tr_canon.ensure(nall * 32))) return rc;
@@ -674,7 +652,7 @@ int transcript_launch(Ctx* ctx, const pm_proof_shape* s, size_t B, const uint64_
   // LDS fence against the accumulator's ladder (kAccLadderFence) while the
   // blocks fit one per CU; larger batches run without the ladder anyway
   const size_t tblocks = (B + kTrSlots - 1) / kTrSlots;
-  const bool fence = tblocks <= 256;
+  const bool fence = tblocks <= (size_t)ctx->num_cus;
   PM_LAUNCH_ST(ctx, st, "transcript", {
     if (!canon_ready)
       k_tr_canon<Cv><<<(unsigned)((nall + 255) / 256), 256, 0, st>>>(
@@ -783,12 +761,13 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   dec.stride = stride;
   dec.inst = d_inst;
   dec.sliced = sliced;
-  // the decode's fence: one block per CU up to 256 point blocks (beyond, the
+  // the decode's fence: one block per CU up to num_cus (256) point blocks (beyond, the
   // grid is throughput work and packing is fine).  (Two per CU beside the
   // twisted ladder at B = 256 measured no gain: the ladder then ran 0.26 ->
   // 0.36 ms, the whole chip busy; round 5.)
-  const size_t dec_fence = h.nblk_pts <= 256 ? kDecodeFence : 0;
-  dec.pt_cus = h.nblk_pts <= 256 ? h.nblk_pts : ~0u;
+  const bool dec_fits = h.nblk_pts <= (uint32_t)ctx->num_cus;
+  const size_t dec_fence = dec_fits ? kDecodeFence : 0;
+  dec.pt_cus = dec_fits ? h.nblk_pts : ~0u;
   dec.off_of.assign(L.npts, kAccNoByte);
   for (size_t i = 0; i + 1 < map.size(); i += 2) dec.off_of[map[i + 1]] = map[i];
   const SqrtTab* tabp = (const SqrtTab*)ctx->sqrt_tab[slot].p;

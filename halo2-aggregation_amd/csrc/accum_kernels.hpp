@@ -337,69 +337,12 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const uint32_t* ch = challenges + 8ull * 7 * (live ? b : b0);
   const Fe<Fs> one = fe_one<Fs>(), zero = fe_zero<Fs>();
   const Fe<Fs> y = ldfe<Fs>(ch, 3), x = ldfe<Fs>(ch, 4);
-  Fe<Fs> l_0 = zero, l_last = zero, omb = zero, inv_xn1 = zero;
 
-  // Wave 0: the long chain of the kernel, in the radix-2^29 lazy form
-  // (one-lane products 0.38-0.46 us against 0.70 us for Fe; round 5).
-  // Values stay Norm, < 4p; LDS rows hold them packed (< 2^256).
-  using K29 = F29Consts<Fs>;
-  const uint32_t K = h.bf + 3;
-  auto put29 = [&](const LdsRows& r, uint32_t row, const F29<Fs>& v) {
-    Fe<Fs> w;
-    f29_pack<Fs>(v, w.l);
-    r.put<Fs>(row, w);
-  };
-  auto get29 = [&](const LdsRows& r, uint32_t row) { return f29_unpack<Fs>(r.get<Fs>(row).l); };
-  auto ld29 = [&](uint32_t idx) { return f29_unpack<Fs>(ldfe<Fs>(consts, idx).l); };  // canonical R261
-  const F29<Fs> one29 = f29_const<Fs>(K29::ONE);
-  if (role == 0 && np <= 16) {
-    // a quad per proof (acc_lagrange_q); the results are read after the barrier
+  if (role == 0) {
+    // Wave 0: the long chain of the kernel, the Lagrange values and 1 / (x^n
+    // - 1) in the radix-2^29 lazy form with a quad per proof (acc_lagrange_q;
+    // np <= 16: the host caps it); the results are read after the barrier
     acc_lagrange_q<Fs>(h, wk, consts, challenges, b0, nv, status);
-  } else if (live && role == 0) {
-    // x^n (verifier.rs:513-516)
-    const F29<Fs> x29 = f29_from_r256<Fs>(x.l);  // < 2p
-    F29<Fs> xn = x29;
-    for (uint32_t i = 0; i < h.log_n; i++) xn = f29_sqr_c<Fs>(xn);
-    const F29<Fs> xn1 = f29_reduce3<Fs>(f29_norm<Fs>(f29_sub<Fs>(xn, one29, K29::K2)));  // < 3p
-    // l_i = w^i (x^n - 1) / (n (x - w^i)), w = omega^-1, i < bf + 2, plus
-    // 1 / (x^n - 1) for h_eval: one batched inversion (Montgomery's trick).
-    // rows: den_i at wk[i], prefix products at wk[K + i]
-    const F29<Fs> nfe = ld29(h.c_n29);
-    F29<Fs> pre = xn1;
-    for (uint32_t i = 0; i < K; i++) {
-      const F29<Fs> den =
-          i + 1 < K ? f29_mul_c<Fs>(nfe, f29_norm<Fs>(f29_sub<Fs>(x29, ld29(h.c_wpow29 + i), K29::K2))) : xn1;
-      pre = i ? f29_mul_c<Fs>(pre, den) : den;  // < 2p (< 3p for i = 0 = K - 1)
-      put29(wk, i, den);
-      put29(wk, K + i, pre);
-    }
-    // a zero denominator (x^n = 1, or x = omega^-i for a Lagrange basis
-    // point) is where the reference's main_gate.div fails (vanishing.rs:175,
-    // verifier.rs:580): flag the proof; its outputs are then unspecified
-    if (status && f29_is_zero_mod<Fs>(pre)) status[b] |= kAccStatusDenomZero;
-    // the inverse of the product (variable-time safegcd, < 2p)
-    F29<Fs> inv = f29_inv<Fs>(pre);
-    const F29<Fs> xn1d = get29(wk, K - 1);  // den_{K-1}, before the walk below replaces it
-    for (uint32_t i = K - 1; i > 0; i--) {
-      const F29<Fs> t = f29_mul_c<Fs>(inv, get29(wk, K + i - 1));
-      inv = f29_mul_c<Fs>(inv, get29(wk, i));
-      put29(wk, i, t);  // now 1 / den_i
-    }
-    put29(wk, 0, inv);
-    F29<Fs> l0 = f29_zero<Fs>(), llast = l0, lblind = l0;
-    for (uint32_t i = 0; i + 1 < K; i++) {
-      const F29<Fs> li = f29_mul_c<Fs>(f29_mul_c<Fs>(ld29(h.c_wpow29 + i), xn1d), get29(wk, i));  // < 2p
-      if (i == 0) l0 = li;
-      else if (i == h.bf + 1) llast = li;
-      else lblind = f29_reduce3<Fs>(f29_norm<Fs>(f29_add<Fs>(lblind, li)));  // < 3p
-    }
-    // back to the Fe form of the fold below: l_0, l_last, 1 - (l_last + l_blind), 1 / (x^n - 1)
-    const F29<Fs> s = f29_reduce3<Fs>(f29_norm<Fs>(f29_add<Fs>(llast, lblind)));  // < 3p
-    const F29<Fs> o = f29_norm<Fs>(f29_sub<Fs>(one29, s, K29::K6));                   // < 7p
-    f29_to_r256<Fs>(l0, l_0.l);
-    f29_to_r256<Fs>(llast, l_last.l);
-    f29_to_r256<Fs>(f29_reduce3<Fs>(o), omb.l);
-    f29_to_r256<Fs>(get29(wk, K - 1), inv_xn1.l);
   } else if (live && role == 1) {
     // gates (verifier.rs:593-605), then the identity values in fold order
     xr.put<Fs>(kAccXHvg, acc_eval_code<Fs>(prog + h.p_gate, h.n_gate, sc, h, consts, stk, zero, y));
@@ -548,12 +491,10 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
   const uint64_t pc3 = wall_clock64();
 #endif
   if (live && role == 0) {
-    if (np <= 16) {  // acc_lagrange_q's results
-      l_0 = wk.get<Fs>(0);
-      l_last = wk.get<Fs>(1);
-      omb = fe_sub<Fs>(one, fe_add<Fs>(l_last, wk.get<Fs>(2)));
-      inv_xn1 = wk.get<Fs>(3);
-    }
+    // acc_lagrange_q's results
+    const Fe<Fs> l_0 = wk.get<Fs>(0), l_last = wk.get<Fs>(1);
+    const Fe<Fs> omb = fe_sub<Fs>(one, fe_add<Fs>(l_last, wk.get<Fs>(2)));
+    const Fe<Fs> inv_xn1 = wk.get<Fs>(3);
     // expressions in order gates, permutation, lookups: h = h y + sel expr,
     // folded per selector by wave 1
     const Fe<Fs> hv = fe_add<Fs>(
@@ -588,152 +529,10 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
 #endif
 }
 
-// [k]P by GLV + Shamir on the radix-2^29 arithmetic: one 130-step joint
-// double-and-add over (k1, k2) with the canonical affine table {P1, P2,
-// P1 + P2} (P1 = +-P, P2 = +-phi(P)); P1 + P2 costs one inversion.  Every
-// step does one dbl and (unless both bits are 0) one mixed add of a selected
-// table point, so lanes of a wave stay convergent.  Result in packed R261.
-template <class Cv>
-__device__ Xyzz29<typename Cv::Base> glv_mul(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P) {
-  using F = typename Cv::Base;
-  uint32_t k1[6], k2[6];
-  bool n1, n2;
-  glv_split<Cv>(k, k1, k2, n1, n2);
-  const F29<F> px = f29_canon<F>(f29_from_r256<F>(P.x.l)), py = f29_canon<F>(f29_from_r256<F>(P.y.l));
-  const F29<F> bx = f29_canon<F>(f29_mul_c<F>(f29_const<F>(Glv<Cv>::BETA29), px));  // phi(P).x
-  const F29<F> y1 = n1 ? f29_canon<F>(f29_neg_canon<F>(py)) : py;
-  const F29<F> y2 = n2 ? f29_canon<F>(f29_neg_canon<F>(py)) : py;
-  // P12 = P1 + P2 (x1 != x2 for a non-identity P: beta != 1)
-  bool inf12 = true;
-  Xyzz29<F> s12 = xyzz29_madd<F>(xyzz29_inf<F>(), px, y1, inf12);
-  s12 = xyzz29_madd<F>(s12, bx, y2, inf12);
-  F29<F> x12 = f29_zero<F>(), y12 = f29_zero<F>();
-  if (!inf12) xyzz29_to_aff<F>(s12, x12, y12);
-  Xyzz29<F> acc = xyzz29_inf<F>();
-  bool acc_inf = true;
-  for (int i = kGlvBits - 1; i >= 0; i--) {
-    acc = xyzz29_dbl<F>(acc);
-    const uint32_t b1 = (k1[i >> 5] >> (i & 31)) & 1u, b2 = (k2[i >> 5] >> (i & 31)) & 1u;
-    const uint32_t sel = b1 | (b2 << 1);
-    if (sel == 0 || (sel == 3 && inf12)) continue;
-    F29<F> qx, qy;
-#pragma unroll
-    for (int t = 0; t < 9; t++) {
-      qx.l[t] = sel == 1 ? px.l[t] : sel == 2 ? bx.l[t] : x12.l[t];
-      qy.l[t] = sel == 1 ? y1.l[t] : sel == 2 ? y2.l[t] : y12.l[t];
-    }
-    acc = xyzz29_madd<F>(acc, qx, qy, acc_inf);
-  }
-  return acc;
-}
-
-// [k]P with signed base-8 windows (round 5): both rounded GLV halves (|k_i| <
-// 2^127) recoded into 43 digits in [-4, 4] each; a table [m]P, m = 1..4
-// (affine, one batched inversion) serves both halves (phi: beta x per use).
-// Per window 3 doublings and 2 mixed additions: 129 + 86 steps against
-// glv_mul's 128 + 128 (a wave adds whenever any of its lanes has a set bit,
-// so the joint form's zero pairs save nothing).
-// The table lives in LDS, [word][lane] (72 words per lane: 72 KiB per block of
-// 256, two blocks per CU), picked by address instead of register selects (in
-// registers the kernel spilled).
+// The term tables of glv_mul_w3n live in LDS, [word][lane] (72 words per lane
+// and term), picked by address instead of register selects (in registers the
+// kernel spilled).
 constexpr uint32_t kW3Words = 4 * 18;
-// [k]P with signed base-8 windows (round 5): both rounded GLV halves (|k_i| <
-// 2^127) recoded into 43 digits in [-4, 4] each; a table [m]P, m = 1..4
-// (affine, one batched inversion) serves both halves (phi: beta x per use).
-// Per window 3 doublings and 2 mixed additions: 129 + 86 steps against
-// glv_mul's 128 + 128 (a wave adds whenever any of its lanes has a set bit,
-// so the joint form's zero pairs save nothing).
-// The table lives in LDS, [word][lane] (72 words per lane: 72 KiB per block of
-// 256, two blocks per CU), picked by address instead of register selects (in
-// registers the kernel spilled).
-template <class Cv>
-__device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P,
-                                                uint32_t (*tab)[256]) {
-  using F = typename Cv::Base;
-  using K = F29Consts<F>;
-  constexpr int kWin = 43;  // 3-bit windows over bits 0..128
-  uint32_t k1[6], k2[6];
-  bool n1, n2;
-  glv_split<Cv, true>(k, k1, k2, n1, n2);
-  // digit codes (magnitude | sign << 3), 8 per word, window 0 lowest
-  uint32_t c1[6] = {0, 0, 0, 0, 0, 0}, c2[6] = {0, 0, 0, 0, 0, 0};
-  {
-    uint32_t cy1 = 0, cy2 = 0;
-#pragma unroll
-    for (int i = 0; i < kWin; i++) {
-      const int b = 3 * i, wd = b >> 5, sh = b & 31;
-      const uint64_t w1 = (uint64_t)k1[wd] | (wd + 1 < 6 ? (uint64_t)k1[wd + 1] << 32 : 0ull);
-      const uint64_t w2 = (uint64_t)k2[wd] | (wd + 1 < 6 ? (uint64_t)k2[wd + 1] << 32 : 0ull);
-      const uint32_t v1 = (uint32_t)(w1 >> sh) & 7u, v2 = (uint32_t)(w2 >> sh) & 7u;
-      const uint32_t u1 = v1 + cy1, u2 = v2 + cy2;
-      cy1 = u1 > 4u ? 1u : 0u;
-      cy2 = u2 > 4u ? 1u : 0u;
-      const uint32_t e1 = cy1 ? ((8u - u1) | (u1 < 8u ? 8u : 0u)) : u1;  // u = 8: digit 0, carry 1
-      const uint32_t e2 = cy2 ? ((8u - u2) | (u2 < 8u ? 8u : 0u)) : u2;
-      c1[i >> 3] |= e1 << (4 * (i & 7));
-      c2[i >> 3] |= e2 << (4 * (i & 7));
-    }
-  }
-  // table [m] P, m = 1..4, affine canonical: rows 18 (m - 1) + limb (x), + 9 (y)
-  const uint32_t ln = threadIdx.x;
-  auto put = [&](uint32_t row, const F29<F>& v) {
-#pragma unroll
-    for (int t = 0; t < 9; t++) tab[row + t][ln] = v.l[t];
-  };
-  const F29<F> one = f29_const<F>(K::ONE);
-  {
-    const F29<F> x1 = f29_canon<F>(f29_from_r256<F>(P.x.l)), y1 = f29_canon<F>(f29_from_r256<F>(P.y.l));
-    put(0, x1);
-    put(9, y1);
-    const Xyzz29<F> Q2 = xyzz29_dbl_impl<F, true>(x1, y1, one, one);
-    bool qi = false;
-    const Xyzz29<F> Q3 = xyzz29_madd<F>(Q2, x1, y1, qi);  // 2P + P: 2P != +-P (odd order)
-    const Xyzz29<F> Q4 = xyzz29_dbl<F>(Q2);
-    const F29<F> d2 = f29_mul_c<F>(Q2.ZZ, Q2.ZZZ), d3 = f29_mul_c<F>(Q3.ZZ, Q3.ZZZ), d4 = f29_mul_c<F>(Q4.ZZ, Q4.ZZZ);
-    const F29<F> d23 = f29_mul_c<F>(d2, d3);
-    const F29<F> inv = f29_inv<F>(f29_mul_c<F>(d23, d4));  // 1 / (d2 d3 d4)
-    const F29<F> i4 = f29_mul_c<F>(inv, d23), i23 = f29_mul_c<F>(inv, d4);
-    const F29<F> i2 = f29_mul_c<F>(i23, d3), i3 = f29_mul_c<F>(i23, d2);
-    // 1 / ZZ = ZZZ / d, 1 / ZZZ = ZZ / d
-    put(18, f29_canon<F>(f29_mul_c<F>(Q2.X, f29_mul_c<F>(i2, Q2.ZZZ))));
-    put(27, f29_canon<F>(f29_mul_c<F>(Q2.Y, f29_mul_c<F>(i2, Q2.ZZ))));
-    put(36, f29_canon<F>(f29_mul_c<F>(Q3.X, f29_mul_c<F>(i3, Q3.ZZZ))));
-    put(45, f29_canon<F>(f29_mul_c<F>(Q3.Y, f29_mul_c<F>(i3, Q3.ZZ))));
-    put(54, f29_canon<F>(f29_mul_c<F>(Q4.X, f29_mul_c<F>(i4, Q4.ZZZ))));
-    put(63, f29_canon<F>(f29_mul_c<F>(Q4.Y, f29_mul_c<F>(i4, Q4.ZZ))));
-  }
-  const F29<F> beta = f29_const<F>(Glv<Cv>::BETA29);
-  const uint32_t s1 = n1 ? 8u : 0u, s2 = n2 ? 8u : 0u;  // the half's sign flips every digit
-  Xyzz29<F> acc = xyzz29_inf<F>();
-  bool acc_inf = true;
-  for (int i = kWin - 1; i >= 0; i--) {
-    acc = xyzz29_dbl<F>(xyzz29_dbl<F>(xyzz29_dbl<F>(acc)));
-    // this window's codes (register words picked by selects, not scratch)
-    uint32_t w1 = 0, w2 = 0;
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-      w1 = j == (i >> 3) ? c1[j] : w1;
-      w2 = j == (i >> 3) ? c2[j] : w2;
-    }
-    const uint32_t sh = 4u * (uint32_t)(i & 7);
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-      const uint32_t e = ((half ? w2 : w1) >> sh) & 15u, m = e & 7u;
-      if (m == 0) continue;
-      F29<F> qx, qy;
-      const uint32_t r0 = 18u * (m - 1u);
-#pragma unroll
-      for (int t = 0; t < 9; t++) {
-        qx.l[t] = tab[r0 + t][ln];
-        qy.l[t] = tab[r0 + 9 + t][ln];
-      }
-      if (half) qx = f29_canon<F>(f29_mul_c<F>(beta, qx));
-      if (((e ^ (half ? s2 : s1)) & 8u) != 0u) qy = f29_canon<F>(f29_neg_canon<F>(qy));
-      acc = xyzz29_madd<F>(acc, qx, qy, acc_inf);
-    }
-  }
-  return acc;
-}
 
 // One term's half of the work: the rounded GLV split recoded into the digit
 // codes (magnitude | sign << 3, 8 per word, window 0 lowest; the half's sign
@@ -799,10 +598,9 @@ __device__ __forceinline__ void w3_prepare(const Fe<typename Cv::Scalar>& k, con
 // in [-4, 4], a table [m]P_j, m = 1..4 (affine, one batched inversion per
 // term) serving both halves (phi: beta x per use).  Per window 3 doublings,
 // shared by the NT terms (Straus), and 2 NT mixed additions: 129 + 86 steps per
-// term against glv_mul's 128 + 128 (a wave adds whenever any of its lanes has
-// a set bit, so the joint form's zero pairs save nothing), 65 + 86 at NT = 2.
-// The tables live in LDS, [word][lane] (72 words per lane and term), picked by
-// address instead of register selects (in registers the kernel spilled).
+// term against the 128 + 128 of a joint binary double-and-add (a wave adds
+// whenever any of its lanes has a set bit, so a joint form's zero pairs save
+// nothing; that form was retired in round 6), 65 + 86 at NT = 2.
 // live: bit j set when term j is present and its point is not the identity.
 template <class Cv, int NT>
 __device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3n(const Fe<typename Cv::Scalar>& k0,
@@ -851,11 +649,11 @@ __device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3n(const Fe<typena
   return acc;
 }
 
-// k_acc_termmul: a lane per term (NT = 1, or W3 = false: glv_mul), or with
-// NT = 2 a lane per pair of terms of one output (prog[p_pairs]: npair (t0, t1)
-// per proof, t1 = kAccNoByte for a single); the lane stores the pair's sum at
-// t0 and the identity at t1, so k_acc_sum folds the same rows.
-template <class Cv, bool W3 = true, int NT = 1>
+// k_acc_termmul: a lane per term (NT = 1), or with NT = 2 a lane per pair of
+// terms of one output (prog[p_pairs]: npair (t0, t1) per proof, t1 =
+// kAccNoByte for a single); the lane stores the pair's sum at t0 and the
+// identity at t1, so k_acc_sum folds the same rows.
+template <class Cv, int NT = 1>
 __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t* __restrict__ prog,
                                                      const uint32_t* __restrict__ coef,
                                                      const uint32_t* __restrict__ points,
@@ -863,7 +661,7 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
                                                      uint32_t npair, Xyzz<typename Cv::Base>* __restrict__ part) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;  // part[] holds packed R261 (curve29.hpp) points
-  __shared__ uint32_t w3tab[W3 ? NT * kW3Words : 1][256];
+  __shared__ uint32_t w3tab[NT * kW3Words][256];
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t per = NT == 1 ? h.T : npair;
   if (gl >= h.B * per) return;
@@ -885,10 +683,7 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
     k1 = ldfe<Fs>(coef, b * h.T + t1);
     if (!aff_is_inf<F>(P1)) live |= 2u;
   }
-  Xyzz29<F> acc;
-  if (W3 && NT > 1) acc = live ? glv_mul_w3n<Cv, NT>(k0, P0, k1, P1, live, w3tab) : xyzz29_inf<F>();
-  else if (W3) acc = live ? glv_mul_w3<Cv>(k0, P0, w3tab) : xyzz29_inf<F>();
-  else acc = live ? glv_mul<Cv>(k0, P0) : xyzz29_inf<F>();
+  const Xyzz29<F> acc = live ? glv_mul_w3n<Cv, NT>(k0, P0, k1, P1, live, w3tab) : xyzz29_inf<F>();
   store_xyzz29<F>(&part[b * h.T + t0], acc);
   if (NT > 1 && t1 != kAccNoByte) store_xyzz29<F>(&part[b * h.T + t1], xyzz29_inf<F>());
 }

@@ -358,6 +358,15 @@ int pm_ctx_create(int device, pm_ctx** out) {
   std::unique_ptr<Ctx> c(new Ctx());
   c->device = device;
   HIP_TRY(hipSetDevice(device));
+  {  // gfx950 only: the kernels' LDS layouts and fences assume 160 KiB per CU
+    int cus = 0, lds = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    HIP_TRY(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device));
+    if (lds < (int)kMaxLds)
+      return set_error(PM_ERR_UNSUPPORTED, "device has " + std::to_string(lds) +
+                                               " B of LDS per CU; this build needs gfx950's 160 KiB");
+    c->num_cus = std::max(1, cus);
+  }
   // the context's own stream is a BLOCKING stream: it is ordered after work
   // the caller queued on the legacy null stream (torch's default stream), so
   // a *_device entry sees inputs the caller has just written there.  The
@@ -421,6 +430,27 @@ int pm_ctx_set_accum_split(pm_ctx* ctx, int lg_lanes) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->acc_split = lg_lanes;
   return PM_OK;
+}
+
+int pm_ctx_set_accum_option(pm_ctx* ctx, int option, int value) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  switch (option) {
+    case PM_ACC_OPT_TWIST:
+    case PM_ACC_OPT_TAIL_STREAM:
+    case PM_ACC_OPT_TRANSCRIPT:
+      if (value < -1 || value > 0) return set_error(PM_ERR_ARG, "accum option value out of range (-1 auto, 0 off)");
+      (option == PM_ACC_OPT_TWIST ? ctx->acc_twist : option == PM_ACC_OPT_TAIL_STREAM ? ctx->acc_tail
+                                                                                      : ctx->acc_tr_stream) = value;
+      return PM_OK;
+    case PM_ACC_OPT_TERMS_PER_LANE:
+      if (value < -1 || value == 0 || value > 2)
+        return set_error(PM_ERR_ARG, "terms per lane out of range (-1 auto, 1, 2)");
+      ctx->acc_tpl = value;
+      return PM_OK;
+    default:
+      return set_error(PM_ERR_ARG, "unknown accum option");
+  }
 }
 
 int pm_ctx_set_window(pm_ctx* ctx, int c) {
@@ -805,8 +835,15 @@ static void dropin_release_all(pm_ctx* ctx) {
   ctx->dropin_small.clear();
 }
 
-static size_t dropin_total(const pm_ctx* ctx) {
+static size_t dropin_small_total(const pm_ctx* ctx) {
   size_t s = 0;
+  for (auto& e : ctx->dropin_small) s += e.bytes;
+  return s;
+}
+
+// every byte the drop-in cache holds: the large sets and the small sets' tables
+static size_t dropin_total(const pm_ctx* ctx) {
+  size_t s = dropin_small_total(ctx);
   for (auto& e : ctx->dropin) s += e.bytes;
   return s;
 }
@@ -843,16 +880,16 @@ static void dropin_make_room(pm_ctx* ctx, size_t bytes) {
 // pm_msm_resident_many (no doublings, no host Horner); first sightings and
 // sets that do not fit run the small-MSM path on the host inputs.  The keyed
 // digest of a small set is cheap (at most 1 MiB of bases).
-// up to this many points (measured, profiles/r05/small_n_cache.json: a kept
-// set against the small-MSM path 38 vs 66 us at n = 1, 63 vs 73 at 32, 82 vs
-// 93 at 512, 107 vs 106 at 1024, 174 vs 139 at 4096)
-constexpr size_t kDropinSmallMaxN = 512;
+// up to pm::kDropinSmallMaxN = 64 points (measured,
+// profiles/r05/small_n_cache.json: a kept set against the small-MSM path 38 vs
+// 66 us at n = 1, 63 vs 73 at 32, 82 vs 93 at 512 -- the last not worth its
+// 256 MiB table, ADVICE r5 -- 107 vs 106 at 1024, 174 vs 139 at 4096)
 static int dropin_small_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64_t* bases, size_t n,
                             uint32_t flags, uint64_t out[8]) {
   const CurveOps* ops = curve_ops(curve);
   auto small = [&]() { return ops->msm_small(ctx, scalars, true, bases, true, false, n, flags, out); };
   const size_t tbytes = n * pm::many_bytes_per_base(pm::many_pick_c(n));
-  if (n > kDropinSmallMaxN || tbytes > pm::kDropinSmallBytes / 2) return small();
+  if (n > pm::kDropinSmallMaxN || tbytes > pm::kDropinSmallBytes / 2) return small();
   pm::u128 part[2];
   pm::digest_chunk(ctx->dropin_key, bases, 8 * n, part);
   uint64_t d[4];
@@ -873,13 +910,24 @@ static int dropin_small_msm(Ctx* ctx, int curve, const uint64_t* scalars, const 
       return small();
     }
     ctx->dropin_small_seen.erase(seen);
-    // LRU room against the entry count and the byte budget
+    // LRU room against the entry count, the small sets' byte cap and the
+    // drop-in cache's whole budget (large sets included: min(kDropinBytes,
+    // free device memory / kDropinFreeDiv)); a set that still does not fit
+    // is not admitted
+    const size_t need = tbytes + 64 * n;
+    size_t free_b = 0, total_b = 0;
+    const bool have_info = hipMemGetInfo(&free_b, &total_b) == hipSuccess;
     for (;;) {
-      size_t held = 0;
-      for (auto& e : ctx->dropin_small) held += e.bytes;
-      if ((int)ctx->dropin_small.size() < kDropinSmallEntries && held + tbytes + 64 * n <= pm::kDropinSmallBytes) break;
+      const size_t held = dropin_total(ctx), held_small = dropin_small_total(ctx);
+      size_t budget = kDropinBytes;
+      if (have_info) budget = std::min(budget, (free_b + held) / kDropinFreeDiv);
+      if ((int)ctx->dropin_small.size() < kDropinSmallEntries && held_small + need <= pm::kDropinSmallBytes &&
+          held + need <= budget)
+        break;
+      if (ctx->dropin_small.empty()) return small();
       auto lru = std::min_element(ctx->dropin_small.begin(), ctx->dropin_small.end(),
                                   [](const pm::DropinEntry& x, const pm::DropinEntry& y) { return x.last_use < y.last_use; });
+      if (have_info) free_b += lru->bytes;
       pm_bases_release(lru->b);
       ctx->dropin_small.erase(lru);
     }

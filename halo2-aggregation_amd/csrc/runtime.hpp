@@ -54,10 +54,14 @@ constexpr size_t kDropinFreeDiv = 2;
 // base sets seen once and not admitted: a set becomes resident on its second
 // sighting, so one-shot bases never pay the row-table build
 constexpr int kDropinSeen = 8;
-// small drop-in sets (multiples tables): at most this many, and this many
-// bytes of tables, per context
+// small drop-in sets (multiples tables, capi.hip dropin_small_msm): at most
+// this many, and this many bytes of tables, per context.  A table costs
+// 512 KiB per base at c = 8, so only sets of at most kDropinSmallMaxN points
+// are kept (512-point sets held 256 MiB each); their bytes count in
+// the drop-in cache's free-memory-aware budget with the large sets'.
 constexpr int kDropinSmallEntries = 8;
-constexpr size_t kDropinSmallBytes = size_t(4) << 30;
+constexpr size_t kDropinSmallMaxN = 64;
+constexpr size_t kDropinSmallBytes = size_t(256) << 20;
 // small-MSM path (msm_small.hpp): pm_msm* calls with n <= ctx->small_max (and
 // the automatic window) run the two-launch table + window-sum kernels instead
 // of the sorting pipeline; kSmallLimit bounds pm_ctx_set_small_msm
@@ -231,6 +235,15 @@ struct pm_ctx {
   int ntt_passes = 0;  // NTT passes over HBM, 0 = auto (test hook: PM_NTT_PASSES env)
   int acc_split = -1; // accumulator lanes per term = 2^acc_split, -1 = auto (pm_ctx_set_accum_split)
   int acc_ladder = -1; // powers-table chains: 0 quads, 1 row-sliced waves, -1 = auto (pm_ctx_set_accum_ladder)
+  // pm_ctx_set_accum_option (-1 = auto for each): the twisted ladder (0 off),
+  // the stream of the term additions / sums (0 main), the one-lane form's
+  // terms per lane (1, 2), the streamed transcript replay (0: per record)
+  int acc_twist = -1, acc_tail = -1, acc_tpl = -1, acc_tr_stream = -1;
+  // the device's CU count (hipDeviceAttributeMultiprocessorCount, 256 on an
+  // MI355X): the one-block-per-CU fences of the latency-bound accumulator
+  // kernels are sized against it (pm_ctx_create refuses a device with less
+  // than the 160 KiB of LDS per CU those fences and kernels assume)
+  int num_cus = 256;
   bool timing = false;
   std::string timing_filter;  // time only launches with this name ("" = all)
   bool timed(const char* name) const { return timing && (timing_filter.empty() || timing_filter == name); }

@@ -25,6 +25,7 @@ LIB_PATH = os.environ.get("PM_LIB") or os.path.join(_HERE, "lib", "libpasta_msm.
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "pasta_msm.h")
 
 PALLAS, VESTA, BN254 = 0, 1, 2
+ACC_OPT_TWIST, ACC_OPT_TAIL_STREAM, ACC_OPT_TERMS_PER_LANE, ACC_OPT_TRANSCRIPT = 1, 2, 3, 4  # pm_ctx_set_accum_option
 SCALARS_CANONICAL = 1
 LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
 # PM_MSM_GPU_MIN_N: below this many terms the Rust shim would keep halo2's CPU
@@ -225,6 +226,7 @@ def _load():
         "pm_ctx_set_pipeline": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_split": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_ladder": ([_vp, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_accum_option": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_glv": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing_filter": ([_vp, ctypes.c_char_p], ctypes.c_int),
@@ -569,6 +571,11 @@ class Context:
     def set_accum_ladder(self, mode=-1):
         """pm_ctx_set_accum_ladder: 0 quads, 1 row-sliced waves, -1 auto."""
         _check(lib().pm_ctx_set_accum_ladder(self.h, mode))
+
+    def set_accum_option(self, option, value=-1):
+        """pm_ctx_set_accum_option: ACC_OPT_TWIST / _TAIL_STREAM / _TRANSCRIPT
+        (0 off, -1 auto), ACC_OPT_TERMS_PER_LANE (1, 2, -1 auto)."""
+        _check(lib().pm_ctx_set_accum_option(self.h, option, value))
 
     def set_accum_split(self, lg_lanes=-1):
         """Accumulator: 2^lg_lanes lanes (bit segments) per MSM term, 0..5 (-1 = automatic)."""

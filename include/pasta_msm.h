@@ -108,6 +108,24 @@ int pm_ctx_set_accum_split(pm_ctx* ctx, int lg_lanes);
  * up to 800 chains, and the proof decoder's square roots row-sliced for up
  * to 4096 points on BN254).  Results do not depend on it. */
 int pm_ctx_set_accum_ladder(pm_ctx* ctx, int mode);
+/* Batch accumulator schedule options (round 6; they replace the PM_ACC_*
+ * environment switches of round 5, so a test can flip them per context).
+ * value -1 = automatic (the default) for every option.  Results never depend
+ * on them.
+ *   PM_ACC_OPT_TWIST           0: no twisted ladder (the powers-table ladder
+ *                                 waits for the decoded points)
+ *   PM_ACC_OPT_TAIL_STREAM     0: term additions and sums on the main stream
+ *   PM_ACC_OPT_TERMS_PER_LANE  1 or 2: the one-lane GLV form's terms per lane
+ *   PM_ACC_OPT_TRANSCRIPT      0: per-record transcript replay (no streamed
+ *                                 byte layout)
+ * PM_ERR_ARG for an unknown option or a value out of range. */
+enum {
+  PM_ACC_OPT_TWIST = 1,
+  PM_ACC_OPT_TAIL_STREAM = 2,
+  PM_ACC_OPT_TERMS_PER_LANE = 3,
+  PM_ACC_OPT_TRANSCRIPT = 4
+};
+int pm_ctx_set_accum_option(pm_ctx* ctx, int option, int value);
 /* Per-kernel HIP-event timing on the context stream (for bench/profiling).
  * Every event pair costs ~10 us of stream time on MI355X, so a timed region
  * should restrict events to the kernel it measures:

@@ -58,12 +58,11 @@ def test_one_lane_windows_terms_per_lane(gpu_ctx, tpl):
     """The one-lane form's GLV products by signed 3-bit windows with one term
     per lane and with two terms of one output per lane (shared doublings, the
     pair's sum at its first row and the identity at its second; chosen
-    automatically for large batches, forced here with PM_ACC_TPL) reproduce
-    the golden vectors and random rich-shape proofs on Pallas and BN254."""
-    import os
-
+    automatically for large batches, forced here with
+    PM_ACC_OPT_TERMS_PER_LANE) reproduce the golden vectors and random
+    rich-shape proofs on Pallas and BN254."""
     gpu_ctx.set_accum_split(0)
-    os.environ["PM_ACC_TPL"] = tpl
+    gpu_ctx.set_accum_option(H.ACC_OPT_TERMS_PER_LANE, int(tpl))
     try:
         test_golden_accumulator(gpu_ctx)
         for cid in (0, 2):
@@ -75,7 +74,7 @@ def test_one_lane_windows_terms_per_lane(gpu_ctx, tpl):
                 q, hh = A.pack_result(C, A.accumulate_msm(C, sh, pf))
                 assert np.array_equal(h[b], hh) and np.array_equal(quads[b], q), (cid, b)
     finally:
-        del os.environ["PM_ACC_TPL"]
+        gpu_ctx.set_accum_option(H.ACC_OPT_TERMS_PER_LANE, -1)
         gpu_ctx.set_accum_split(-1)
 
 

@@ -81,7 +81,7 @@ def test_device_code_has_every_launched_kernel():
                  "15k_synth_scalars", "13k_synth_bases", "14k_transcript_s", "12k_transcriptI", "14k_acc_powers_s"):
         assert count(stem) == 3, stem
     assert count("13k_acc_termadd") == 3 * 2  # lane groups / quad-cooperative form
-    assert count("13k_acc_termmul") == 3 * 3  # windows one / two terms per lane, the joint double-and-add
+    assert count("13k_acc_termmul") == 3 * 2  # windows: one / two terms per lane (joint form retired, round 6)
     # the retired A/B kernels are gone (GLV mode, separate fixups, bit-sum fold pass)
     for stem in ("15k_sort_hist_glv", "11k_bases_glv", "7k_fixupI", "12k_fixup_long", "13k_fixup_short",
                  "12k_bucket_segI", "14k_bits_combine"):

@@ -190,7 +190,7 @@ def test_small_set_dropin_cache(curve):
     try:
         S, B = _inputs(curve, 8192, 0x5A5 + curve)
         admitted = 0
-        for n in (1, 5, 32, 300, 512):
+        for n in (1, 5, 32, 48, 64):
             b = np.ascontiguousarray(B[:n])
             for k in range(4):
                 s = np.ascontiguousarray(S[k:k + n])
@@ -199,6 +199,9 @@ def test_small_set_dropin_cache(curve):
             admitted += 1
             st = ctx.dropin_small_stats()
             assert st["admitted"] == admitted and st["entries"] == min(admitted, 8), (n, st)
+            # a kept table costs 512 KiB per base (c = 8); only sets
+            # of at most 64 points are kept, within the 256 MiB small-set cap
+            assert st["device_bytes"] <= admitted * 64 * (2**19 + 64), st
         assert ctx.dropin_small_stats()["hits"] == 2 * 5
         # a base changed in place: a new key (first sighting, small path), still exact
         b = np.ascontiguousarray(B[:32]).copy()
@@ -208,10 +211,11 @@ def test_small_set_dropin_cache(curve):
         assert ctx.dropin_small_stats()["hits"] == 10
         assert ctx.dropin_stats()["entries"] == 0   # the large-set cache is untouched
         # above the small-set limit: the small-MSM path, never kept
-        b = np.ascontiguousarray(B[:1000])
-        for k in range(3):
-            s = np.ascontiguousarray(S[k:k + 1000])
-            assert np.array_equal(ctx.msm(curve, s, b), msm_ref.best_multiexp(curve, s, b, threads=4))
+        for nb in (65, 300, 1000):
+            b = np.ascontiguousarray(B[:nb])
+            for k in range(3):
+                s = np.ascontiguousarray(S[k:k + nb])
+                assert np.array_equal(ctx.msm(curve, s, b), msm_ref.best_multiexp(curve, s, b, threads=4)), nb
         assert ctx.dropin_small_stats()["admitted"] == 5
         ctx.dropin_clear()
         assert ctx.dropin_small_stats()["entries"] == 0

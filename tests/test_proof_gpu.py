@@ -309,3 +309,68 @@ def test_large_batch_vs_c_port():
                                   batch.inst.data_ptr(), c.data_ptr(), q.data_ptr(), h.data_ptr(), st.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(q, batch.quads[:sub]) and torch.equal(h, batch.h_eval[:sub])
+
+
+@pytest.mark.parametrize("B,logn", [(16, 14), (200, 17)])
+def test_schedule_options_vs_c_port(B, logn):
+    """Config 3 (16 simple-example proofs at k = 14) and a B = 200 batch at
+    k = 17 through the proof-bytes entry the bench times, against
+    oracle/accum_ref.c on the same bytes; then the same batch under every
+    accumulator schedule option (pm_ctx_set_accum_option: twisted ladder off,
+    term additions on the main stream, per-record transcript, one / two terms
+    per lane with the one-lane form, both ladder forms), each bit-identical
+    (no env-gated path left untested)."""
+    import torch
+
+    import accum_ref
+    import workloads as Wk
+
+    ctx = H.Context(0)
+    shape = Wk.simple_example_shape(ctx, H.BN254, logn)
+    batch = Wk.SyntheticBatch(ctx, shape, B, seed=0xC3 + B)
+    batch.to_proof_bytes(shape)
+    batch.run_bytes(ctx, shape)
+    torch.cuda.synchronize()
+    o = accum_ref.batch_proofs(H.BN254, shape.c, batch.proofs.cpu().numpy(), batch.inst.cpu().numpy().view(np.uint64),
+                               vk_repr=np.asarray(batch.vk_repr, dtype=np.uint64), threads=8)
+    want_q, want_h = batch.quads.clone(), batch.h_eval.clone()
+    assert not o["status"].any() and not batch.status.cpu().numpy().any()
+    assert np.array_equal(o["challenges"].reshape(B, 7, 4), batch.challenges.cpu().numpy().view(np.uint64))
+    assert np.array_equal(o["quads"].reshape(B, 4, 8), want_q.cpu().numpy().view(np.uint64))
+    assert np.array_equal(o["h_eval"].reshape(B, 4), want_h.cpu().numpy().view(np.uint64))
+    settings = [
+        [(H.ACC_OPT_TWIST, 0)],
+        [(H.ACC_OPT_TAIL_STREAM, 0)],
+        [(H.ACC_OPT_TWIST, 0), (H.ACC_OPT_TAIL_STREAM, 0)],
+        [(H.ACC_OPT_TRANSCRIPT, 0)],
+        [("ladder", 0)],
+        [("ladder", 1)],
+        [("split", 0), (H.ACC_OPT_TERMS_PER_LANE, 1)],
+        [("split", 0), (H.ACC_OPT_TERMS_PER_LANE, 2)],
+    ]
+    for opts in settings:
+        c2 = H.Context(0)
+        for k, v in opts:
+            if k == "ladder":
+                c2.set_accum_ladder(v)
+            elif k == "split":
+                c2.set_accum_split(v)
+            else:
+                c2.set_accum_option(k, v)
+        batch.quads.zero_()
+        batch.h_eval.zero_()
+        batch.run_bytes(c2, shape)
+        torch.cuda.synchronize()
+        assert not batch.status.cpu().numpy().any(), opts
+        assert torch.equal(batch.quads, want_q) and torch.equal(batch.h_eval, want_h), opts
+        c2.close()
+
+
+def test_accum_option_arguments(gpu_ctx):
+    """Unknown options and out-of-range values are refused (PM_ERR_ARG)."""
+    for opt, val in [(0, 0), (99, -1), (H.ACC_OPT_TWIST, 1), (H.ACC_OPT_TERMS_PER_LANE, 0),
+                     (H.ACC_OPT_TERMS_PER_LANE, 3), (H.ACC_OPT_TRANSCRIPT, -2)]:
+        with pytest.raises(H.PmError):
+            gpu_ctx.set_accum_option(opt, val)
+    for opt in (H.ACC_OPT_TWIST, H.ACC_OPT_TAIL_STREAM, H.ACC_OPT_TERMS_PER_LANE, H.ACC_OPT_TRANSCRIPT):
+        gpu_ctx.set_accum_option(opt, -1)
