@@ -351,7 +351,7 @@ def main():
     import torch
 
     import halo2_amd as H
-    from sharded import combine_partials, shard_range, split_range
+    from sharded import combine_partials, points_fold, shard_range, split_range
 
     share = world > 1 and os.environ.get("PM_BENCH_SHARE_GPU") == "1"
     if share:
@@ -378,9 +378,7 @@ def main():
     d_s, d_b, result = leg.pop("_d_s"), leg.pop("_d_b"), leg.pop("_result")
     gathered = torch.zeros(world * 8, dtype=torch.int64, device=dev)  # one all-gather target
 
-    def padd(a, b):
-        return H.point_add(curve, a, b)
-
+    padd = points_fold(curve)  # the partials' fold: one pm_points_sum call
     fixed = run_fixed_base(args, ctx, dist, dev, world, d_s, d_b, n, gathered, padd, result) if args.fixed else None
     cpu = cpu_baseline(d_s, d_b, n, result, args.cpu_seconds) if (rank == 0 and world == 1 and not args.no_cpu) \
         else None
@@ -558,7 +556,7 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     import torch
 
     import halo2_amd as H
-    from sharded import PartialPipe
+    from sharded import PartialPipe, points_fold
 
     d_s = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
     d_b = torch.empty((max(n, 1), 8), dtype=torch.int64, device=dev)
@@ -570,8 +568,7 @@ def run_msm_leg(args, ctx, dist, dev, world, curve, n, i0, roofline, breakdown, 
     upload_ms = (time.perf_counter() - t0) * 1e3
     gathered = torch.zeros(world * 8, dtype=torch.int64, device=dev)  # one all-gather target
 
-    def padd(a, b):
-        return H.point_add(curve, a, b)
+    padd = points_fold(curve)
 
     # the exchange of MSM k (all-gather of the partials + fold) runs behind
     # MSM k + 1's kernels; every partial is still gathered and folded inside
@@ -665,13 +662,14 @@ def run_variable_base(args, ctx, dist, dev, world, curve, d_s, d_b, n, want, nam
     import torch
 
     import halo2_amd as H
-    from sharded import combine_partials
+    from sharded import combine_partials, points_fold
 
     gathered = torch.zeros(world * 8, dtype=torch.int64, device=dev)  # one all-gather target
+    fold = points_fold(curve)
 
     def raw():
         part = ctx.msm_device(curve, d_s.data_ptr(), d_b.data_ptr(), n)
-        return combine_partials(part, dist, dev, lambda a, b: H.point_add(curve, a, b), world, gathered)
+        return combine_partials(part, dist, dev, fold, world, gathered)
 
     steps = max(5, args.steps // 2)
     for _ in range(args.warmup):

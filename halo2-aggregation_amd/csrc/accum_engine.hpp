@@ -845,7 +845,7 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
                          &fixed_table_impl<Cv>, &ntt_device_impl<Cv>, &msm_fixed_to_aff<Cv>,    \
                          &bases_to29_impl<Cv>, &msm_resident_batch_impl<Cv>, &proofs_device_impl<Cv>,    \
                          &msm_start_impl<Cv>, &msm_finish_impl<Cv>, &msm_small_impl<Cv>,         \
-                         &many_table_impl<Cv>, &msm_many_impl<Cv>};
+                         &many_table_impl<Cv>, &msm_many_impl<Cv>, &points_sum_impl<typename Cv::Base>};
 #endif
 #define PM_DEFINE_CURVE_OPS(Cv, name)                                                          \
   namespace pm {                                                                               \

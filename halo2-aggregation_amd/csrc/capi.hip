@@ -567,10 +567,7 @@ int pm_msm_multi(int curve, const uint64_t* scalars, const uint64_t* bases, size
   for (auto& t : th) t.join();
   for (int g = 0; g < ngpu; g++)
     if (rcs[g]) return set_error(rcs[g], "device " + std::to_string(g) + ": " + errs[g]);
-  uint64_t acc[8] = {0};
-  for (int g = 0; g < ngpu; g++) pm_point_add(curve, acc, &parts[8 * g], acc);
-  std::memcpy(out, acc, 64);
-  return PM_OK;
+  return pm_points_sum(curve, parts.data(), (size_t)ngpu, out);
 }
 
 // Resident SRS bases: stored in the pipeline's R = 2^261 canonical form
@@ -1307,6 +1304,17 @@ int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t o
   const CurveOps* ops = curve_ops(curve);
   if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
   return ops->point_add(a, b, out);
+}
+
+int pm_points_sum(int curve, const uint64_t* points, size_t n, uint64_t out[8]) {
+  if (!out || (n && !points)) return set_error(PM_ERR_ARG, "null argument");
+  const CurveOps* ops = curve_ops(curve);
+  if (!ops) return set_error(PM_ERR_ARG, "unknown curve id");
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    return PM_OK;
+  }
+  return ops->points_sum(points, n, out);
 }
 
 int pm_synth_scalars(pm_ctx* ctx, int curve, uint64_t seed, uint64_t i0, size_t n, uint32_t flags, void* d_out) {

@@ -856,6 +856,16 @@ int point_add_impl(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {
   return PM_OK;
 }
 
+// the fold of the per-rank partials of a sharded MSM (sharded.py): one call,
+// additions in index order in XYZZ, one conversion (inversion) at the end
+template <class F>
+int points_sum_impl(const uint64_t* points, size_t n, uint64_t out[8]) {
+  Xyzz<F> r = xyzz_from_aff<F>(aff_from_u64<F>(points));  // (0, 0) = identity
+  for (size_t i = 1; i < n; i++) r = xyzz_add_aff<F>(r, aff_from_u64<F>(points + 8 * i));
+  aff_to_u64<F>(xyzz_to_aff<F>(r), out);
+  return PM_OK;
+}
+
 template <class Cv>
 int synth_scalars_impl(Ctx* ctx, uint64_t seed, uint64_t i0, uint32_t n, uint32_t mont, void* d_out) {
   k_synth_scalars<typename Cv::Scalar><<<(n + 255) / 256, 256, 0, ctx->stream>>>(seed, i0, n, mont, (uint32_t*)d_out);

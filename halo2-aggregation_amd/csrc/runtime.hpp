@@ -355,6 +355,8 @@ struct CurveOps {
   int (*many_table)(Ctx* ctx, const void* d_bases29, size_t n, ManyTable* t);
   int (*msm_many)(Ctx* ctx, const ManyTable* t, size_t B, const size_t* n, const size_t* off, const void* scalars,
                   bool s_host, uint32_t flags, uint64_t* out);
+  // host: out = sum of n affine points (XYZZ accumulation, one inversion)
+  int (*points_sum)(const uint64_t* points, size_t n, uint64_t out[8]);
 };
 extern const CurveOps kPallasOps, kVestaOps, kBn254Ops;
 

@@ -263,6 +263,7 @@ def _load():
         "pm_bases_many_prepare": ([_vp, _vp, ctypes.c_size_t], ctypes.c_int),
         "pm_bases_many_info": ([_vp, _szp, ctypes.POINTER(ctypes.c_int), _szp], ctypes.c_int),
         "pm_point_add": ([ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
+        "pm_points_sum": ([ctypes.c_int, _u64p, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_selftest_field": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_selftest_host": ([ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, _u64p], ctypes.c_int),
         "pm_synth_scalars": ([_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
@@ -377,6 +378,15 @@ def point_add(curve, a, b):
     a, b = _as_u64(a, 8)[0].copy(), _as_u64(b, 8)[0].copy()
     out = np.zeros(8, dtype=np.uint64)
     _check(lib().pm_point_add(curve, _p(a), _p(b), _p(out)))
+    return out
+
+
+def points_sum(curve, points):
+    """pm_points_sum: the sum of n affine points ((n, 8) u64, (0,0) =
+    identity) in one call -- the fold of a sharded MSM's partials."""
+    pts = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1, 8)
+    out = np.zeros(8, dtype=np.uint64)
+    _check(lib().pm_points_sum(curve, _p(pts), pts.shape[0], _p(out)))
     return out
 
 

@@ -25,11 +25,13 @@ def split_range(rank: int, world: int, n_total: int):
     return lo, hi - lo
 
 
-def _fold(rows, point_add):
-    acc = np.zeros(8, dtype=np.uint64)
-    for r in rows:
-        acc = point_add(acc, r)
-    return acc
+def points_fold(curve: int):
+    """The fold every caller passes: the library's pm_points_sum over the
+    gathered (world, 8) partials -- one host call and one inversion (round 5
+    folded them with one pm_point_add ctypes call per rank)."""
+    import halo2_amd as H
+
+    return lambda rows: H.points_sum(curve, rows)
 
 
 def start_gather(part, dist, device, world: int, out=None):
@@ -46,22 +48,23 @@ def start_gather(part, dist, device, world: int, out=None):
     return work, out
 
 
-def finish_gather(pending, point_add):
-    """Wait for start_gather's collective and fold the partials in rank order."""
+def finish_gather(pending, fold):
+    """Wait for start_gather's collective and fold the partials in rank order
+    (`fold(rows) -> 8 x u64`, rows the (world, 8) partials: points_fold)."""
     work, out = pending
     work.wait()
     rows = out.cpu().numpy().view(np.uint64).reshape(-1, 8)
-    return _fold(rows, point_add)
+    return np.asarray(fold(rows), dtype=np.uint64).reshape(8)
 
 
-def combine_partials(part, dist, device, point_add, world: int, gathered=None):
-    """All-gather each rank's affine partial (8 x u64) and fold them in rank
-    order with `point_add(a, b) -> 8 x u64`.  Returns the full MSM result on
+def combine_partials(part, dist, device, fold, world: int, gathered=None):
+    """All-gather each rank's affine partial (8 x u64) and fold them with
+    `fold(rows) -> 8 x u64` (points_fold).  Returns the full MSM result on
     every rank.  (`gathered`: an optional reusable (world * 8) int64 tensor.)"""
     part = np.ascontiguousarray(part, dtype=np.uint64).reshape(8)
     if world == 1:
         return part
-    return finish_gather(start_gather(part, dist, device, world, gathered), point_add)
+    return finish_gather(start_gather(part, dist, device, world, gathered), fold)
 
 
 class PartialPipe:
@@ -70,10 +73,10 @@ class PartialPipe:
     folds the last one.  Every partial is gathered and folded; only the
     collective's latency moves behind the next MSM's kernels."""
 
-    def __init__(self, dist, device, point_add, world: int):
+    def __init__(self, dist, device, fold, world: int):
         import torch
 
-        self.dist, self.device, self.point_add, self.world = dist, device, point_add, world
+        self.dist, self.device, self.fold, self.world = dist, device, fold, world
         self.bufs = [torch.empty(world * 8, dtype=torch.int64, device=device) for _ in range(2)]
         self.k = 0
         self.pending = None
@@ -84,13 +87,13 @@ class PartialPipe:
         nxt = start_gather(part, self.dist, self.device, self.world, self.bufs[self.k & 1])
         self.k += 1
         prev, self.pending = self.pending, nxt
-        return finish_gather(prev, self.point_add) if prev is not None else None
+        return finish_gather(prev, self.fold) if prev is not None else None
 
     def drain(self):
         if self.pending is None:
             return None
         prev, self.pending = self.pending, None
-        return finish_gather(prev, self.point_add)
+        return finish_gather(prev, self.fold)
 
 
 def gather_batches(local, dist, world: int, gathered=None):

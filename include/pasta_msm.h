@@ -279,6 +279,10 @@ int pm_selftest_host(int curve, uint64_t seed, size_t n, uint64_t* mismatches);
 
 /* Affine helpers (host) for combining partial results: out = a + b. */
 int pm_point_add(int curve, const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
+/* out = points[0] + ... + points[n-1] (n affine points, 8 limbs each, (0,0) =
+ * identity; n == 0 yields the identity): the fold of a sharded MSM's per-rank
+ * partials in one call (round 6; one inversion instead of one per addition). */
+int pm_points_sum(int curve, const uint64_t* points, size_t n, uint64_t out[8]);
 
 /* Synthetic inputs generated on the device: scalar i is
  * uniform in [0, r) from a SplitMix64 stream keyed by (seed, i0 + i);

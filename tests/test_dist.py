@@ -1,8 +1,8 @@
 """CPU multi-process test of the N>1 path (gloo, world_size 2 and 3): each
 rank computes its slice's partial MSM (C oracle stands in for the GPU), the
 partials are all-gathered and folded by halo2-aggregation_amd/sharded.py with
-the library's host pm_point_add exactly as in bench.py, and every rank must
-hold the full MSM."""
+the library's host pm_points_sum (one call per fold, sharded.points_fold)
+exactly as in bench.py, and every rank must hold the full MSM."""
 import os
 import socket
 
@@ -32,7 +32,7 @@ def _worker(rank, world, port, n_per_rank, q, host_collectives=False):
     import halo2_amd as H
     import msm_ref
     import pasta as P
-    from sharded import PartialPipe, combine_partials, shard_range
+    from sharded import PartialPipe, combine_partials, points_fold, shard_range
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -48,8 +48,7 @@ def _worker(rank, world, port, n_per_rank, q, host_collectives=False):
     B = msm_ref.synth_bases(0, P.SEED_BASES, i0, n, threads=2)
     part = msm_ref.best_multiexp(0, S, B, threads=2)
 
-    def padd(a, b):  # the fold bench.py runs: the library's host pm_point_add
-        return H.point_add(0, a, b)
+    padd = points_fold(0)  # the fold bench.py runs: one pm_points_sum call
 
     full = combine_partials(part, dist, torch.device("cpu"), padd, world)
     # bench.py's pipelined form (sharded.PartialPipe): step k returns step
@@ -215,3 +214,32 @@ def test_accum_multi_shard_math_cpu():
                 got[i].append(out[i])
         for i in range(4):
             assert np.array_equal(np.concatenate(got[i]), whole[i]), (nctx, i)
+
+
+@pytest.mark.parametrize("curve", [0, 1, 2])
+def test_points_sum_one_call(curve):
+    """pm_points_sum (the partials' fold) equals the oracle's sum and the
+    pairwise pm_point_add fold, including the identity, a repeated point
+    (doubling), P + (-P) and n = 0 / 1."""
+    import sys
+
+    for p in (os.path.join(ROOT, "halo2-aggregation_amd"), os.path.join(ROOT, "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import halo2_amd as H
+    import pasta as P
+
+    C = (P.PALLAS, P.VESTA, P.BN254)[curve]
+    pts = [C.mul(7 + 3 * i, C.gen) for i in range(6)]
+    neg = C.neg(pts[2]) if hasattr(C, "neg") else C.mul(C.r - 9 - 6, C.gen)
+    cases = [[], [pts[0]], pts, pts + [None, pts[1]], [pts[3], pts[3]], [pts[2], neg], [None, None]]
+    for case in cases:
+        rows = np.array([P.point_to_limbs(C, q) for q in case], dtype=np.uint64).reshape(-1, 8)
+        got = H.points_sum(curve, rows)
+        acc = np.zeros(8, dtype=np.uint64)
+        want = None
+        for r, q in zip(rows, case):
+            acc = H.point_add(curve, acc, r)
+            want = q if want is None else (C.add(want, q) if q is not None else want)
+        assert np.array_equal(got, acc), case
+        assert P.limbs_to_point(C, [int(v) for v in got]) == want, case
