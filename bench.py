@@ -1239,63 +1239,89 @@ def accum_two_in_flight(args, ctx, shape, batch, B):
             "quads_match_single_runs": ok, "errors": errs}
 
 
-def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0, from_bytes=True):
-    """Latency roofline of the accumulator batch: every kernel on the critical
-    path is a chain of dependent steps run by lone waves.  Two floors:
-
-    * `self_floor_ms` (round 4): steps on each kernel's longest chain x that
-      step's single-wave latency measured in isolation (tools/microbench_chain
-      .hip, profiles/r05/chain_latency.jsonl over r04; the row-sliced product
-      from profiles/r05/microbench_slice.jsonl) -- relative to this code's own
-      steps;
-    * `hw_floor_ms` (round 5): the same step counts x each step's
-      instruction count by class times the lone-wave issue cost of that class
-      (profiles/r05/hw_floor.json: tools/hw_floor.py over the gfx950 listings,
-      costs from tools/microbench_issue.hip) -- what the hardware allows for
-      this instruction stream; the variable-time safegcd inversion has no
-      static count and enters both floors with its measured time.
-
-    Chains: decode -> transcript -> scalar block and the ladder, then term
-    additions -> sums.  The ladder follows the decode, or (round 5, twisted
-    ladder: row-sliced decode and decode + ladder blocks within the 256 CUs)
-    runs beside it from the proof bytes; critical = the longer chain plus the
-    last two.  Step counts follow the engine's lane rules
-    (accum_engine.hpp): decode 305 row-sliced products per BN254 point (the
-    4-bit window of (p+1)/4) while B x points <= 4096, else one lane square
-    root; ladder 127 doublings (row-sliced: 3 dependent product levels each,
-    up to 800 chains; else quad-cooperative); transcript ceil(bytes / 128) + 7
-    Blake2b compressions per proof (round 5 streamed replay: ceil(bytes /
-    128) on the chain, the squeeze finals beside it); scalar block log n + 4K - 3 radix-2^29
-    products (K = bf + 3), the inversion, then 2 per identity value + 2 + T/4
-    Fe products; term additions ceil(85.3 / S) + log2 S XYZZ additions (14
-    products each); sums ceil(nslots / (NL/4)) + log2(NL/4) quad additions
-    (4 product levels), the quad inversion and 5 products."""
-    lat = {}
-    for rel in (("r04", "chain_latency.jsonl"), ("r05", "chain_latency.jsonl")):
-        p = os.path.join(ROOT, "profiles", *rel)
-        if os.path.exists(p):
-            for line in open(p):
-                if line.strip().startswith("{"):
-                    d = json.loads(line)
-                    if "step" in d:
-                        lat[d["step"]] = d["us_per_step"]
-    p = os.path.join(ROOT, "profiles", "r05", "microbench_slice.jsonl")
-    if os.path.exists(p):
-        for line in open(p):
+def _jsonl(path):
+    if os.path.exists(path):
+        for line in open(path):
             if line.strip().startswith("{"):
-                d = json.loads(line)
-                if d.get("field") == "bn254_fq":
-                    lat.setdefault("s29_mul", d.get("sliced_us_per_mul"))
-                    if "inv_safegcd_lane_us" in d:
-                        lat["inv_lane"] = d["inv_safegcd_lane_us"]
-                    if "inv_quad_safegcd_us" in d:
-                        lat["inv_q"] = d["inv_quad_safegcd_us"]
-    hw = {}
-    p = os.path.join(ROOT, "profiles", "r05", "hw_floor.json")
-    if os.path.exists(p):
-        hw = {k: v["issue_floor_us"] for k, v in json.load(open(p))["steps"].items()}
-    if not {"f29_mul", "xyzz_add", "xyzz_add_q", "ladder_dbl", "inv_q", "sqrt_bn254"} <= lat.keys():
+                yield json.loads(line)
+
+
+def accum_step_costs():
+    """The step costs of the accumulator's algorithmic floor, all from
+    committed measurements: the best dependent field product (the row-sliced
+    BN254 product, profiles/r05/microbench_slice.jsonl, the minimum over its
+    occupancies), the best inversion (quad-cooperative safegcd, same file) and
+    one Blake2b compression (profiles/r05/chain_latency.jsonl)."""
+    P = INV = None
+    for d in _jsonl(os.path.join(ROOT, "profiles", "r05", "microbench_slice.jsonl")):
+        if d.get("field") != "bn254_fq":
+            continue
+        if "sliced_us_per_mul" in d:
+            P = d["sliced_us_per_mul"] if P is None else min(P, d["sliced_us_per_mul"])
+        if "inv_quad_safegcd_us" in d:
+            INV = d["inv_quad_safegcd_us"]
+    B2 = next((d["us_per_step"] for d in _jsonl(os.path.join(ROOT, "profiles", "r05", "chain_latency.jsonl"))
+               if d.get("step") == "b2_compress_q"), None)
+    if None in (P, INV, B2):
         return None
+    return {"product_us": P, "inverse_us": INV, "blake2b_compress_us": B2,
+            "source": "profiles/r05/microbench_slice.jsonl (min sliced BN254 product, quad safegcd inverse), "
+                      "profiles/r05/chain_latency.jsonl (b2_compress_q)"}
+
+
+def accum_valu_roofline(B, ms_batch):
+    """Throughput legs (the one-lane form, B >= 2048): integer-VALU roofline of
+    the whole batch from committed SQ counters of the same workload
+    (profiles/pmc_acc_valu.json, tools/acc_valu.py over tools/gpu_r06_acc.sh):
+    the issue time the batch's VALU instructions need at the measured peaks
+    (INT64 class at the v_mad_u64_u32 peak, the rest at the simple-op peak,
+    profiles/valu_peak.json) over the batch time."""
+    p = os.path.join(ROOT, "profiles", "pmc_acc_valu.json")
+    if not os.path.exists(p):
+        return None
+    d = json.load(open(p)).get("batches", {}).get(str(B))
+    if not d:
+        return None
+    issue_s = d["issue_seconds_per_batch"]
+    lane_ops = d["valu_lane_insts_per_batch"]
+    return {"bound": "valu", "achieved": round(lane_ops / (ms_batch * 1e-3) / 1e12, 3),
+            "peak": d["int64_peak_Tops"], "unit": "T lane-ops/s", "frac": round(issue_s / (ms_batch * 1e-3), 4),
+            "traffic": None, "kernel_frac": {k: round(v["issue_frac"], 4) for k, v in d["kernels"].items()},
+            "note": "frac = VALU issue time at the measured peaks (INT64 class 33.944 T/s, other 61.164 T/s) over "
+                    "the batch time; kernel_frac = the same per kernel over its own duration",
+            "source": d["source"]}
+
+
+def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0, from_bytes=True):
+    """Latency roofline of the accumulator batch: every
+    kernel on the critical path is a chain of dependent steps, and its floor
+    is ALGORITHMIC -- the dependent field products the computation needs (not
+    this code's instruction count) x the best product latency measured on
+    MI355X, plus the best measured inversion and Blake2b compression
+    (accum_step_costs):
+
+      decode      the BN254 square root a^((p+1)/4): 251 dependent squarings
+      transcript  ceil(stream bytes / 128) sequential Blake2b compressions
+      scalars     x^n (log n squarings), 1 product into the batched
+                  denominator, 1 inversion, 4 products (l_i, the fold, h_eval,
+                  the e coefficient)
+      ladder      127 doublings x 3 product levels
+      term adds   ceil(85.3 / S) + log2 S additions x 4 product levels (S lanes
+                  share a term's ~85.3 NAF digits)
+      sums        ceil(nslots / (NL/4)) + log2(NL/4) additions x 4 levels, 1
+                  inversion, 2 products (affine x, y)
+
+    critical = max(ladder (after the decode unless twisted), decode +
+    transcript + scalars) + term adds + sums.  Large batches (the one-lane
+    form) are throughput work: their roofline is accum_valu_roofline."""
+    if B >= 2048:
+        v = accum_valu_roofline(B, ms_batch)
+        if v:
+            return v
+    cost = accum_step_costs()
+    if cost is None:
+        return None
+    P, INV, B2 = cost["product_us"], cost["inverse_us"], cost["blake2b_compress_us"]
     budget = 1024 * 2 * 64
     nterm = B * T
     lg = 0
@@ -1308,66 +1334,30 @@ def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0,
     lgL = 0
     while lgL < 5 and ((B * 4) << (lgL + 1)) <= 16384:
         lgL += 1
-    NL = 1 << lgL
-    nq = max(1, NL // 4)
+    nq = max(1, (1 << lgL) // 4)
     c = shape.c if shape is not None else None
     npts = shape.layout()[0] if shape is not None else T
     nsc = shape.layout()[1] if shape is not None else 0
     npp = npts - (c.num_instance_columns if c is not None else 1)
-    sliced_dec = B * npp <= 4096
-    sliced_lad = B * npp <= 800
     log_n = c.log_n if c is not None else 17
-    K = (c.blinding_factors if c is not None else 5) + 3
-    nsets_p = -(-c.n_perm_columns // c.perm_chunk_len) if c is not None and c.n_perm_columns else 0
-    nvals = (2 * nsets_p + 1 if nsets_p else 0) + 5 * (c.num_lookups if c is not None else 0)
-    comps = -(-(npts * 65 + nsc * 33 + 33) // 128)  # streamed: the finals run beside the block chain
-    nprf = B * npts  # proof-point chains (about one per proof point)
-    twist = (from_bytes and sliced_dec and
+    comps = -(-(npts * 65 + nsc * 33 + 33) // 128)
+    nprf = B * npts
+    twist = (from_bytes and B * npp <= 4096 and
              -(-B * npp // 16) + (-(-nprf // 4) if nprf <= 800 else -(-4 * nprf // 256)) <= 256)
-    n29 = log_n + 4 * K - 3
-    nfe = 2 * nvals + 2 + -(-T // 4)
-    inv_lane = lat.get("inv_lane", lat["inv_q"])
-
-    def floors(st, hwm):
-        """per-kernel floors (us) from step costs st (measured) or hwm (hardware)"""
-        f = {}
-        f["proof_decode"] = (305 * st["s29_mul"] if sliced_dec else st["sqrt_bn254"]) + 6 * st["f29_mul"]
-        f["transcript"] = comps * st["b2_compress_q"]
-        f["acc_scalars"] = n29 * st["f29_mul"] + inv_lane + nfe * st["fe_mul"]
-        f["acc_ladder"] = 127 * (3 * st["s29_mul"] if sliced_lad else st["ladder_dbl"])
-        f["acc_termmul"] = (-(-85.3 // S) + lg) * st["xyzz_add"]
-        f["acc_sum"] = ((-(-nslots // nq) + (nq.bit_length() - 1)) * st["xyzz_add_q"] + lat["inv_q"]
-                        + 5 * st["f29_mul"])
-        if not from_bytes:
-            f.pop("proof_decode")
-        return f
-
-    def crit(f):
-        d = f.get("proof_decode", 0.0)
-        lad = f["acc_ladder"] if twist else d + f["acc_ladder"]
-        return max(lad, d + f["transcript"] + f["acc_scalars"]) + f["acc_termmul"] + f["acc_sum"]
-
+    f = {"proof_decode": 251 * P, "transcript": comps * B2, "acc_scalars": (log_n + 1 + 4) * P + INV,
+         "acc_ladder": 127 * 3 * P, "acc_termmul": (-(-85.3 // S) + lg) * 4 * P,
+         "acc_sum": ((-(-nslots // nq) + (nq.bit_length() - 1)) * 4 + 2) * P + INV}
+    if not from_bytes:
+        f.pop("proof_decode")
+    d = f.get("proof_decode", 0.0)
+    lad = f["acc_ladder"] if twist else d + f["acc_ladder"]
+    crit = max(lad, d + f["transcript"] + f["acc_scalars"]) + f["acc_termmul"] + f["acc_sum"]
     out = {"bound": "latency", "achieved": round(ms_batch, 4), "unit": "ms per batch (critical path)",
-           "traffic": None, "lanes": {"term_additions_S": S, "sum_lanes_NL": NL, "sliced_decode": sliced_dec,
-                                      "sliced_ladder": sliced_lad, "twisted_ladder": twist}}
-    st = dict(lat)
-    st.setdefault("b2_compress_q", 1.62)
-    fs = floors(st, None)
-    out["self_floor_ms"] = {k: round(v / 1e3, 4) for k, v in fs.items()}
-    out["peak"] = round(crit(fs) / 1e3, 4)
-    out["frac"] = round(out["peak"] / ms_batch, 4)
-    out["kernel_frac"] = {k: round(fs[k] / 1e3 / kernels[k], 4) for k in fs if kernels.get(k)}
-    if {"f29_mul", "fe_mul", "s29_mul", "b2_compress_q", "ladder_dbl"} <= hw.keys():
-        h = dict(hw)
-        h["xyzz_add"] = 14 * hw["f29_mul"]
-        h["xyzz_add_q"] = 4 * hw["f29_mul"]
-        h["sqrt_bn254"] = 305 * hw["f29_mul"]
-        fh = floors(h, None)
-        out["hw_floor_ms"] = {k: round(v / 1e3, 4) for k, v in fh.items()}
-        out["hw_peak"] = round(crit(fh) / 1e3, 4)
-        out["hw_frac"] = round(out["hw_peak"] / ms_batch, 4)
-    out["source"] = ("self: profiles/r05/chain_latency.jsonl (r04 where absent), profiles/r05/microbench_slice.jsonl; "
-                     "hw: profiles/r05/hw_floor.json (tools/hw_floor.py, issue costs tools/microbench_issue.hip)")
+           "peak": round(crit / 1e3, 4), "frac": round(crit / 1e3 / ms_batch, 4), "traffic": None,
+           "alg_floor_ms": {k: round(v / 1e3, 4) for k, v in f.items()},
+           "kernel_frac": {k: round(f[k] / 1e3 / kernels[k], 4) for k in f if kernels.get(k)},
+           "lanes": {"term_additions_S": S, "sum_lanes_NL": 1 << lgL, "twisted_ladder": twist},
+           "step_costs": cost}
     return out
 
 

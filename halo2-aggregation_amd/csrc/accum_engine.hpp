@@ -365,7 +365,13 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // side by side: beyond, they queue for each other (B = 256: 256 + 100)
   {
     const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
-    h.twist = dec && dec->sliced && lgS > 0 && twist_on && (size_t)dec->pt_cus + lad_blocks <= (size_t)ctx->num_cus ? 1u : 0u;
+    // (PM_ACC_OPT_TWIST = 1 forces it whenever the powers tables are built:
+    // the decode then runs unfenced beside the ladder, proofs_device_impl)
+    h.twist = dec && lgS > 0 &&
+                      (ctx->acc_twist == 1 ||
+                       (dec->sliced && twist_on && (size_t)dec->pt_cus + lad_blocks <= (size_t)ctx->num_cus))
+                  ? 1u
+                  : 0u;
   }
   if (h.twist && !dec->launched && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4))))
     return rc;
@@ -765,7 +771,7 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   // grid is throughput work and packing is fine).  (Two per CU beside the
   // twisted ladder at B = 256 measured no gain: the ladder then ran 0.26 ->
   // 0.36 ms, the whole chip busy; round 5.)
-  const bool dec_fits = h.nblk_pts <= (uint32_t)ctx->num_cus;
+  const bool dec_fits = h.nblk_pts <= (uint32_t)ctx->num_cus && ctx->acc_twist != 1;
   const size_t dec_fence = dec_fits ? kDecodeFence : 0;
   dec.pt_cus = dec_fits ? h.nblk_pts : ~0u;
   dec.off_of.assign(L.npts, kAccNoByte);

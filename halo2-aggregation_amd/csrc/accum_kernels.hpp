@@ -534,38 +534,49 @@ __global__ void __launch_bounds__(256) k_acc_scalars(AccumHdr h, const uint32_t*
 // kernel spilled).
 constexpr uint32_t kW3Words = 4 * 18;
 
-// One term's half of the work: the rounded GLV split recoded into the digit
-// codes (magnitude | sign << 3, 8 per word, window 0 lowest; the half's sign
-// folded in) and its table [m]P, m = 1..4, at LDS rows r0 + 18 (m - 1) + limb
-// (x), + 9 (y).
-template <class Cv>
-__device__ __forceinline__ void w3_prepare(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P,
-                                           uint32_t (*tab)[256], uint32_t r0, uint32_t c1[6], uint32_t c2[6]) {
-  using F = typename Cv::Base;
-  using K = F29Consts<F>;
+// The rounded GLV split of k (|k_i| < 2^127) recoded into 43 signed base-8
+// digits per half, as codes (magnitude | sign << 3, 8 per word, window 0
+// lowest).  FOLD: the half's sign (s1, s2 = 8 when the half is negated) is
+// folded into every nonzero digit; else it is returned for the use site
+// (glv_mul_w3: fewer live registers in its loop, two waves per SIMD).
+template <class Cv, bool FOLD>
+__device__ __forceinline__ void w3_codes(const Fe<typename Cv::Scalar>& k, uint32_t c1[6], uint32_t c2[6],
+                                         uint32_t& s1, uint32_t& s2) {
   constexpr int kWin = 43;  // 3-bit windows over bits 0..128
   uint32_t k1[6], k2[6];
   bool n1, n2;
   glv_split<Cv, true>(k, k1, k2, n1, n2);
-  const uint32_t s1 = n1 ? 8u : 0u, s2 = n2 ? 8u : 0u;
-  {
-    uint32_t cy1 = 0, cy2 = 0;
+  s1 = n1 ? 8u : 0u;
+  s2 = n2 ? 8u : 0u;
+  uint32_t cy1 = 0, cy2 = 0;
 #pragma unroll
-    for (int i = 0; i < kWin; i++) {
-      const int b = 3 * i, wd = b >> 5, sh = b & 31;
-      const uint64_t w1 = (uint64_t)k1[wd] | (wd + 1 < 6 ? (uint64_t)k1[wd + 1] << 32 : 0ull);
-      const uint64_t w2 = (uint64_t)k2[wd] | (wd + 1 < 6 ? (uint64_t)k2[wd + 1] << 32 : 0ull);
-      const uint32_t v1 = (uint32_t)(w1 >> sh) & 7u, v2 = (uint32_t)(w2 >> sh) & 7u;
-      const uint32_t u1 = v1 + cy1, u2 = v2 + cy2;
-      cy1 = u1 > 4u ? 1u : 0u;
-      cy2 = u2 > 4u ? 1u : 0u;
-      // u = 8: digit 0, carry 1; a nonzero digit's sign is flipped by the half's
-      const uint32_t e1 = cy1 ? (u1 < 8u ? (8u - u1) | (8u ^ s1) : 0u) : (u1 ? u1 | s1 : 0u);
-      const uint32_t e2 = cy2 ? (u2 < 8u ? (8u - u2) | (8u ^ s2) : 0u) : (u2 ? u2 | s2 : 0u);
-      c1[i >> 3] |= e1 << (4 * (i & 7));
-      c2[i >> 3] |= e2 << (4 * (i & 7));
+  for (int i = 0; i < kWin; i++) {
+    const int b = 3 * i, wd = b >> 5, sh = b & 31;
+    const uint64_t w1 = (uint64_t)k1[wd] | (wd + 1 < 6 ? (uint64_t)k1[wd + 1] << 32 : 0ull);
+    const uint64_t w2 = (uint64_t)k2[wd] | (wd + 1 < 6 ? (uint64_t)k2[wd + 1] << 32 : 0ull);
+    const uint32_t v1 = (uint32_t)(w1 >> sh) & 7u, v2 = (uint32_t)(w2 >> sh) & 7u;
+    const uint32_t u1 = v1 + cy1, u2 = v2 + cy2;
+    cy1 = u1 > 4u ? 1u : 0u;
+    cy2 = u2 > 4u ? 1u : 0u;
+    uint32_t e1, e2;
+    if (FOLD) {  // u = 8: digit 0, carry 1; a nonzero digit's sign is flipped by the half's
+      e1 = cy1 ? (u1 < 8u ? (8u - u1) | (8u ^ s1) : 0u) : (u1 ? u1 | s1 : 0u);
+      e2 = cy2 ? (u2 < 8u ? (8u - u2) | (8u ^ s2) : 0u) : (u2 ? u2 | s2 : 0u);
+    } else {     // u = 8: digit 0 (magnitude 0), carry 1
+      e1 = cy1 ? ((8u - u1) | (u1 < 8u ? 8u : 0u)) : u1;
+      e2 = cy2 ? ((8u - u2) | (u2 < 8u ? 8u : 0u)) : u2;
     }
+    c1[i >> 3] |= e1 << (4 * (i & 7));
+    c2[i >> 3] |= e2 << (4 * (i & 7));
   }
+}
+
+// The table [m]P, m = 1..4, affine canonical (one batched inversion) at LDS
+// rows r0 + 18 (m - 1) + limb (x), + 9 (y), column threadIdx.x.
+template <class Cv>
+__device__ __forceinline__ void w3_table(const Aff<typename Cv::Base>& P, uint32_t (*tab)[256], uint32_t r0) {
+  using F = typename Cv::Base;
+  using K = F29Consts<F>;
   const uint32_t ln = threadIdx.x;
   auto put = [&](uint32_t row, const F29<F>& v) {
 #pragma unroll
@@ -591,6 +602,61 @@ __device__ __forceinline__ void w3_prepare(const Fe<typename Cv::Scalar>& k, con
   put(45, f29_canon<F>(f29_mul_c<F>(Q3.Y, f29_mul_c<F>(i3, Q3.ZZ))));
   put(54, f29_canon<F>(f29_mul_c<F>(Q4.X, f29_mul_c<F>(i4, Q4.ZZZ))));
   put(63, f29_canon<F>(f29_mul_c<F>(Q4.Y, f29_mul_c<F>(i4, Q4.ZZ))));
+}
+
+// One term's half of the work in glv_mul_w3n: the codes with the halves'
+// signs folded in, and the table at rows r0..
+template <class Cv>
+__device__ __forceinline__ void w3_prepare(const Fe<typename Cv::Scalar>& k, const Aff<typename Cv::Base>& P,
+                                           uint32_t (*tab)[256], uint32_t r0, uint32_t c1[6], uint32_t c2[6]) {
+  uint32_t s1, s2;
+  w3_codes<Cv, true>(k, c1, c2, s1, s2);
+  w3_table<Cv>(P, tab, r0);
+}
+
+// [k]P, one term (k_acc_termmul NT = 1): per window 3 doublings and the two
+// halves' mixed additions, the half's sign applied at use.  (glv_mul_w3n<Cv,
+// 1> over w3_prepare needs 322 registers against this loop's 247: one wave per
+// SIMD instead of two.)
+template <class Cv>
+__device__ __forceinline__ Xyzz29<typename Cv::Base> glv_mul_w3(const Fe<typename Cv::Scalar>& k,
+                                                               const Aff<typename Cv::Base>& P, uint32_t (*tab)[256]) {
+  using F = typename Cv::Base;
+  constexpr int kWin = 43;
+  uint32_t c1[6] = {0, 0, 0, 0, 0, 0}, c2[6] = {0, 0, 0, 0, 0, 0}, s1, s2;
+  w3_codes<Cv, false>(k, c1, c2, s1, s2);
+  w3_table<Cv>(P, tab, 0);
+  const uint32_t ln = threadIdx.x;
+  const F29<F> beta = f29_const<F>(Glv<Cv>::BETA29);
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  bool acc_inf = true;
+  for (int i = kWin - 1; i >= 0; i--) {
+    acc = xyzz29_dbl<F>(xyzz29_dbl<F>(xyzz29_dbl<F>(acc)));
+    // this window's codes (register words picked by selects, not scratch)
+    uint32_t w1 = 0, w2 = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      w1 = j == (i >> 3) ? c1[j] : w1;
+      w2 = j == (i >> 3) ? c2[j] : w2;
+    }
+    const uint32_t sh = 4u * (uint32_t)(i & 7);
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      const uint32_t e = ((half ? w2 : w1) >> sh) & 15u, m = e & 7u;
+      if (m == 0) continue;
+      F29<F> qx, qy;
+      const uint32_t r0 = 18u * (m - 1u);
+#pragma unroll
+      for (int t = 0; t < 9; t++) {
+        qx.l[t] = tab[r0 + t][ln];
+        qy.l[t] = tab[r0 + 9 + t][ln];
+      }
+      if (half) qx = f29_canon<F>(f29_mul_c<F>(beta, qx));
+      if (((e ^ (half ? s2 : s1)) & 8u) != 0u) qy = f29_canon<F>(f29_neg_canon<F>(qy));
+      acc = xyzz29_madd<F>(acc, qx, qy, acc_inf);
+    }
+  }
+  return acc;
 }
 
 // sum_j [k_j] P_j over NT terms (NT = 1, 2) with signed base-8 windows
@@ -683,7 +749,9 @@ __global__ void __launch_bounds__(256) k_acc_termmul(AccumHdr h, const uint32_t*
     k1 = ldfe<Fs>(coef, b * h.T + t1);
     if (!aff_is_inf<F>(P1)) live |= 2u;
   }
-  const Xyzz29<F> acc = live ? glv_mul_w3n<Cv, NT>(k0, P0, k1, P1, live, w3tab) : xyzz29_inf<F>();
+  Xyzz29<F> acc = xyzz29_inf<F>();
+  if (NT == 1 && live) acc = glv_mul_w3<Cv>(k0, P0, w3tab);
+  else if (live) acc = glv_mul_w3n<Cv, NT>(k0, P0, k1, P1, live, w3tab);
   store_xyzz29<F>(&part[b * h.T + t0], acc);
   if (NT > 1 && t1 != kAccNoByte) store_xyzz29<F>(&part[b * h.T + t1], xyzz29_inf<F>());
 }

@@ -437,11 +437,13 @@ int pm_ctx_set_accum_option(pm_ctx* ctx, int option, int value) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   switch (option) {
     case PM_ACC_OPT_TWIST:
+      if (value < -1 || value > 1) return set_error(PM_ERR_ARG, "twist option out of range (-1 auto, 0 off, 1 force)");
+      ctx->acc_twist = value;
+      return PM_OK;
     case PM_ACC_OPT_TAIL_STREAM:
     case PM_ACC_OPT_TRANSCRIPT:
       if (value < -1 || value > 0) return set_error(PM_ERR_ARG, "accum option value out of range (-1 auto, 0 off)");
-      (option == PM_ACC_OPT_TWIST ? ctx->acc_twist : option == PM_ACC_OPT_TAIL_STREAM ? ctx->acc_tail
-                                                                                      : ctx->acc_tr_stream) = value;
+      (option == PM_ACC_OPT_TAIL_STREAM ? ctx->acc_tail : ctx->acc_tr_stream) = value;
       return PM_OK;
     case PM_ACC_OPT_TERMS_PER_LANE:
       if (value < -1 || value == 0 || value > 2)

@@ -316,7 +316,8 @@ def test_schedule_options_vs_c_port(B, logn):
     """Config 3 (16 simple-example proofs at k = 14) and a B = 200 batch at
     k = 17 through the proof-bytes entry the bench times, against
     oracle/accum_ref.c on the same bytes; then the same batch under every
-    accumulator schedule option (pm_ctx_set_accum_option: twisted ladder off,
+    accumulator schedule option (pm_ctx_set_accum_option: twisted ladder off
+    and forced,
     term additions on the main stream, per-record transcript, one / two terms
     per lane with the one-lane form, both ladder forms), each bit-identical
     (no env-gated path left untested)."""
@@ -340,6 +341,7 @@ def test_schedule_options_vs_c_port(B, logn):
     assert np.array_equal(o["h_eval"].reshape(B, 4), want_h.cpu().numpy().view(np.uint64))
     settings = [
         [(H.ACC_OPT_TWIST, 0)],
+        [(H.ACC_OPT_TWIST, 1)],
         [(H.ACC_OPT_TAIL_STREAM, 0)],
         [(H.ACC_OPT_TWIST, 0), (H.ACC_OPT_TAIL_STREAM, 0)],
         [(H.ACC_OPT_TRANSCRIPT, 0)],
@@ -368,7 +370,7 @@ def test_schedule_options_vs_c_port(B, logn):
 
 def test_accum_option_arguments(gpu_ctx):
     """Unknown options and out-of-range values are refused (PM_ERR_ARG)."""
-    for opt, val in [(0, 0), (99, -1), (H.ACC_OPT_TWIST, 1), (H.ACC_OPT_TERMS_PER_LANE, 0),
+    for opt, val in [(0, 0), (99, -1), (H.ACC_OPT_TWIST, 2), (H.ACC_OPT_TAIL_STREAM, 1), (H.ACC_OPT_TERMS_PER_LANE, 0),
                      (H.ACC_OPT_TERMS_PER_LANE, 3), (H.ACC_OPT_TRANSCRIPT, -2)]:
         with pytest.raises(H.PmError):
             gpu_ctx.set_accum_option(opt, val)

@@ -47,12 +47,15 @@ __global__ void __launch_bounds__(256) k_madd(uint32_t* out, int iters) {
     acc.X = y; acc.Y = x; acc.ZZ = x; acc.ZZZ = y;
     bool inf = false;
     for (int k = 0; k < iters; k++)
-      acc = V == 1 ? xyzz29_madd<F>(acc, x, y, inf) : xyzz29_madd_signed<F>(acc, x, y, (uint32_t)k & 1u ? ~0u : 0u);
+      acc = V == 1   ? xyzz29_madd<F>(acc, x, y, inf)
+            : V == 2 ? xyzz29_madd_signed<F>(acc, x, y, (uint32_t)k & 1u ? ~0u : 0u)
+                     : xyzz29_madd_lazy<F>(acc, x, y, (uint32_t)k & 1u ? ~0u : 0u);  // k_accumulate's step (r5)
     for (int i = 0; i < 8; i++) out[8 * t + i] = acc.X.l[i];
   }
 }
 
-// field inversion throughput (binary GCD, f29_inv): the cost a batch-affine
+// field inversion throughput (f29_inv: binary GCD in round 2, the safegcd
+// since round 5): the cost a batch-affine
 // bucket accumulation would amortise over the independent additions of a batch
 __global__ void __launch_bounds__(256) k_inv(uint32_t* out, int iters) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -161,12 +164,13 @@ int main() {
   run("xyzz_madd_32", k_madd<0>, buf, 128, 1);
   run("xyzz_madd_29", k_madd<1>, buf, 128, 1);
   run("xyzz_madd_signed_29", k_madd<2>, buf, 128, 1);
-  run("f29_inv_bgcd", k_inv, buf, 16, 1);
+  run("xyzz_madd_lazy_29", k_madd<3>, buf, 128, 1);
+  run("f29_inv_safegcd", k_inv, buf, 16, 1);
   // batch-affine: lanes = 1024 blocks x 256 (k_accumulate's grid at 2^20)
   {
     const uint32_t blocks = 1024, threads = 256, nl = blocks * threads;
     uint32_t* scratch;
-    hipMalloc(&scratch, (size_t)nl * 128 * 27 * 4);
+    hipMalloc(&scratch, (size_t)nl * 256 * 27 * 4);
     auto ba = [&](const char* name, auto kern, int K, int iters) {
       hipEvent_t e0, e1;
       hipEventCreate(&e0); hipEventCreate(&e1);
@@ -184,6 +188,7 @@ int main() {
     ba("batch_affine_mem", k_batch_affine<32, false>, 32, 2);
     ba("batch_affine_mem", k_batch_affine<64, false>, 64, 1);
     ba("batch_affine_mem", k_batch_affine<128, false>, 128, 1);
+    ba("batch_affine_mem", k_batch_affine<256, false>, 256, 1);
     hipFree(scratch);
   }
   return 0;
