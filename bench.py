@@ -1338,12 +1338,12 @@ def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0,
     c = shape.c if shape is not None else None
     npts = shape.layout()[0] if shape is not None else T
     nsc = shape.layout()[1] if shape is not None else 0
-    npp = npts - (c.num_instance_columns if c is not None else 1)
     log_n = c.log_n if c is not None else 17
     comps = -(-(npts * 65 + nsc * 33 + 33) // 128)
     nprf = B * npts
-    twist = (from_bytes and B * npp <= 4096 and
-             -(-B * npp // 16) + (-(-nprf // 4) if nprf <= 800 else -(-4 * nprf // 256)) <= 256)
+    # round 6: from bytes the ladder always runs beside the decode while the
+    # powers tables are built (accum_engine.hpp proofs_device_impl)
+    twist = from_bytes and 4 * (nprf << 2) <= 3 * budget
     f = {"proof_decode": 251 * P, "transcript": comps * B2, "acc_scalars": (log_n + 1 + 4) * P + INV,
          "acc_ladder": 127 * 3 * P, "acc_termmul": (-(-85.3 // S) + lg) * 4 * P,
          "acc_sum": ((-(-nslots // nq) + (nq.bit_length() - 1)) * 4 + 2) * P + INV}

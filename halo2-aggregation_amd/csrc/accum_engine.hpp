@@ -95,6 +95,70 @@ inline uint32_t acc_auto_lanes(size_t items, uint32_t maxlg) {
   return lg;
 }
 
+// The MSM term slots of one proof (accum_device_impl's plan): one slot per
+// distinct commitment of f in first-use order, then H's h_i, the W_j of w and
+// of zw, and g1 for e; qprog = (slot, eval) per query in set order.
+struct AccTerms {
+  std::vector<uint32_t> termsrc;  // (kind << 28) | idx ; VK index space: fixed, sigma, g1
+  std::vector<uint32_t> qprog;
+  uint32_t nslots = 0, h_slot0 = 0, T = 0, Tp = 0;  // Tp: proof-point terms (the powers-table chains)
+};
+inline void acc_terms(const pm_proof_shape* s, const AccLayout& L, const std::vector<std::vector<AccQuery>>& sets,
+                      AccTerms& t) {
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot_of;
+  auto vk_index = [&](uint32_t kind, uint32_t idx) -> uint32_t {
+    return kind == kRefFixed ? idx : s->num_fixed_columns + idx;
+  };
+  for (auto& st : sets)
+    for (auto& x : st) {
+      uint32_t slot = kSlotH;
+      if (x.ref_kind != kRefH) {
+        auto key = std::make_pair(x.ref_kind, x.ref_idx);
+        auto it = slot_of.find(key);
+        if (it == slot_of.end()) {
+          slot = (uint32_t)t.termsrc.size();
+          slot_of[key] = slot;
+          t.termsrc.push_back(x.ref_kind == kRefProof ? x.ref_idx : ((1u << 28) | vk_index(x.ref_kind, x.ref_idx)));
+        } else {
+          slot = it->second;
+        }
+      }
+      t.qprog.push_back(slot);
+      t.qprog.push_back(x.eval);
+    }
+  t.h_slot0 = (uint32_t)t.termsrc.size();
+  for (uint32_t i = 0; i < s->quotient_degree; i++) t.termsrc.push_back(L.p_h + i);
+  t.nslots = (uint32_t)t.termsrc.size();
+  for (uint32_t j = 0; j < L.nsets; j++) t.termsrc.push_back(L.p_W + j);  // w
+  for (uint32_t j = 0; j < L.nsets; j++) t.termsrc.push_back(L.p_W + j);  // zw
+  t.termsrc.push_back((1u << 28) | (s->num_fixed_columns + s->n_perm_columns));  // e: g1
+  t.T = (uint32_t)t.termsrc.size();
+  t.Tp = 0;
+  for (uint32_t v : t.termsrc) t.Tp += (v >> 28) == 0 ? 1u : 0u;
+}
+
+// log2 of the lanes per term of the split (powers-table) form, 0 = the
+// one-lane GLV form.  The powers tables pay only while their chains stay
+// within ~3/4 of the lane budget: beyond it the 127-doubling chains share
+// SIMDs and queue, while the one-lane GLV products still run in one pass at
+// a flat ~1.16 ms.  Simple shape, T = 30 of which 21 proof points, wall per
+// batch (profiles/r02/vkt/): split 1.13 ms at B = 1024, 1.67 at 1536 against
+// one-lane 1.54 / 1.57 (the old rule without VK tables, 4 B T <= budget:
+// profiles/r02/xover/).
+inline uint32_t acc_split_lanes(const Ctx* ctx, size_t B, const AccTerms& t) {
+  const size_t nterm = B * t.T, nprf = B * t.Tp;
+  uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split
+                 : 4 * (nprf << 2) > 3 * kAccLaneBudget ? 0u
+                                                        : acc_auto_lanes(nterm, 3);
+  // 16 / 32 lanes per term only while the term additions still fit one wave
+  // per SIMD (B = 16: k_acc_termadd 0.075 ms at 16 lanes, 0.061 at 32; B = 256
+  // stays at 8 lanes: 0.129 ms, 16 lanes 0.138, 32 lanes 0.197:
+  // profiles/r02/pow/timing_pow1.jsonl)
+  if (ctx->acc_split < 0 && lgS == 3)
+    while (lgS < 5 && (nterm << (lgS + 1)) <= kAccLaneBudget / 2) lgS++;
+  return lgS;
+}
+
 // static LDS of a decode instantiation (the fence is the block's total)
 template <class Cv, bool SLICED>
 size_t decode_static_lds() {
@@ -120,9 +184,9 @@ struct AccDecode {
   const void* inst;
   std::vector<uint32_t> off_of;
   bool sliced;         // row-sliced square roots (few points)
-  uint32_t pt_cus;     // CUs the fenced point blocks take (~0u: unfenced, no room for a ladder beside)
   hipEvent_t in_ready = nullptr;  // on st: the inputs are on the device (recorded before the decode)
   bool launched = false;          // the decode is already queued on st (it writes the twist factors)
+  bool twist = false;             // the plan runs the twisted ladder beside it (proofs_device_impl)
 };
 // a decode block beside a ladder block would share its SIMDs (both are
 // issue-bound lone-wave chains): its LDS request keeps it off any CU holding
@@ -152,38 +216,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   for (auto& st : sets)
     if (st.size() > kAccMaxPerSet) return set_error(PM_ERR_UNSUPPORTED, "accum: rotation set too large");
 
-  // --- term slots: distinct commitments of f in first-use order, then h_i
-  std::vector<uint32_t> termsrc;  // (kind << 28) | idx ; VK index space: fixed, sigma, g1
-  std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot_of;
-  auto vk_index = [&](uint32_t kind, uint32_t idx) -> uint32_t {
-    return kind == kRefFixed ? idx : s->num_fixed_columns + idx;
-  };
-  std::vector<uint32_t> qprog;
-  for (auto& st : sets)
-    for (auto& x : st) {
-      uint32_t slot = kSlotH;
-      if (x.ref_kind != kRefH) {
-        auto key = std::make_pair(x.ref_kind, x.ref_idx);
-        auto it = slot_of.find(key);
-        if (it == slot_of.end()) {
-          slot = (uint32_t)termsrc.size();
-          slot_of[key] = slot;
-          termsrc.push_back(x.ref_kind == kRefProof ? x.ref_idx : ((1u << 28) | vk_index(x.ref_kind, x.ref_idx)));
-        } else {
-          slot = it->second;
-        }
-      }
-      qprog.push_back(slot);
-      qprog.push_back(x.eval);
-    }
-  const uint32_t h_slot0 = (uint32_t)termsrc.size();
-  for (uint32_t i = 0; i < s->quotient_degree; i++) termsrc.push_back(L.p_h + i);
-  const uint32_t nslots = (uint32_t)termsrc.size();
-  for (uint32_t j = 0; j < L.nsets; j++) termsrc.push_back(L.p_W + j);  // w
-  for (uint32_t j = 0; j < L.nsets; j++) termsrc.push_back(L.p_W + j);  // zw
-  const uint32_t g1_index = s->num_fixed_columns + s->n_perm_columns;
-  termsrc.push_back((1u << 28) | g1_index);                            // e
-  const uint32_t T = (uint32_t)termsrc.size();
+  // --- term slots (acc_terms)
+  AccTerms tm;
+  acc_terms(s, L, sets, tm);
+  const std::vector<uint32_t>& termsrc = tm.termsrc;
+  const std::vector<uint32_t>& qprog = tm.qprog;
+  const uint32_t h_slot0 = tm.h_slot0, nslots = tm.nslots, T = tm.T;
 
   // --- program words
   AccumHdr h{};
@@ -325,22 +363,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   uint32_t* dcoef = (uint32_t*)ctx->acc_coef.p;
   Xyzz<F>* dpart = (Xyzz<F>*)ctx->acc_part.p;
   const size_t nterm = (size_t)B * T, nprf = (size_t)B * h.Tp;
-  // The powers tables (a quad per proof-point term) pay only while their
-  // chains stay within ~3/4 of the lane budget: beyond it the 127-doubling
-  // chains share SIMDs and queue, while the one-lane GLV products still run
-  // in one pass at a flat ~1.16 ms.  Simple shape, T = 30 of which 21 proof
-  // points, wall per batch (profiles/r02/vkt/): split 1.13 ms at B = 1024,
-  // 1.67 at 1536 against one-lane 1.54 / 1.57 (the old rule without VK
-  // tables, 4 B T <= budget: profiles/r02/xover/).
-  uint32_t lgS = ctx->acc_split >= 0 ? (uint32_t)ctx->acc_split
-                 : 4 * (nprf << 2) > 3 * kAccLaneBudget ? 0u
-                                                        : acc_auto_lanes(nterm, 3);
-  // 16 / 32 lanes per term only while the term additions still fit one wave
-  // per SIMD (B = 16: k_acc_termadd 0.075 ms at 16 lanes, 0.061 at 32; B = 256
-  // stays at 8 lanes: 0.129 ms, 16 lanes 0.138, 32 lanes 0.197:
-  // profiles/r02/pow/timing_pow1.jsonl)
-  if (ctx->acc_split < 0 && lgS == 3)
-    while (lgS < 5 && (nterm << (lgS + 1)) <= kAccLaneBudget / 2) lgS++;
+  const uint32_t lgS = acc_split_lanes(ctx, B, tm);
   // few terms (B <= ~34 for the simple shape): 16 quads per term with
   // quad-cooperative additions (k_acc_termadd<Cv, true>)
   const bool quad_terms = ctx->acc_split < 0 && lgS == 5 && nterm * 64 <= kAccLaneBudget / 2;
@@ -357,22 +380,8 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // proof bytes with the powers tables: the ladder runs on the twist from the
   // x bytes on the reduction stream, beside the decode -> replay -> scalar
   // block chain on the main stream, which is then the critical one and has no
-  // cross-stream hop (AccDecode; PM_ACC_OPT_TWIST = 0: the ladder after the decode)
-  const bool twist_on = ctx->acc_twist != 0;
-  // (only with the row-sliced decode, profiles/r05/twist_ab/: the one-lane
-  // decode beside the quad ladder ran 0.12-0.33 ms against 0.13 alone)
-  // and while the decode's point blocks and the ladder's blocks fit the CUs
-  // side by side: beyond, they queue for each other (B = 256: 256 + 100)
-  {
-    const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
-    // (PM_ACC_OPT_TWIST = 1 forces it whenever the powers tables are built:
-    // the decode then runs unfenced beside the ladder, proofs_device_impl)
-    h.twist = dec && lgS > 0 &&
-                      (ctx->acc_twist == 1 ||
-                       (dec->sliced && twist_on && (size_t)dec->pt_cus + lad_blocks <= (size_t)ctx->num_cus))
-                  ? 1u
-                  : 0u;
-  }
+  // cross-stream hop (decided with the decode's fence by proofs_device_impl)
+  h.twist = dec && dec->twist && lgS > 0 ? 1u : 0u;
   if (h.twist && !dec->launched && (rc = ctx->acc_corr.ensure((size_t)B * L.npts * kAccCorrWords * sizeof(uint4))))
     return rc;
   std::vector<uint64_t> built_key;  // VK tables built by this call (committed after its final sync)
@@ -767,13 +776,35 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   dec.stride = stride;
   dec.inst = d_inst;
   dec.sliced = sliced;
-  // the decode's fence: one block per CU up to num_cus (256) point blocks (beyond, the
-  // grid is throughput work and packing is fine).  (Two per CU beside the
-  // twisted ladder at B = 256 measured no gain: the ladder then ran 0.26 ->
-  // 0.36 ms, the whole chip busy; round 5.)
-  const bool dec_fits = h.nblk_pts <= (uint32_t)ctx->num_cus && ctx->acc_twist != 1;
-  const size_t dec_fence = dec_fits ? kDecodeFence : 0;
-  dec.pt_cus = dec_fits ? h.nblk_pts : ~0u;
+  // The twisted ladder (accum_device_impl) and the decode's fence, decided
+  // together before the plan is built.  With the powers tables (split form)
+  // the ladder always runs beside the decode (PM_ACC_OPT_TWIST = 0: after
+  // it).  While the row-sliced decode's point blocks and the ladder's blocks
+  // fit the CUs side by side, the decode keeps its fence (one block per CU,
+  // beside nothing: unfenced, the dispatcher packed several blocks per CU, B
+  // = 16 decode 0.11 -> 0.16 ms); beyond, it runs unfenced among the ladder's
+  // blocks (round 6, profiles/r06/twist_ab.jsonl: B = 256 0.595 -> 0.542 ms,
+  // 512 0.750 -> 0.718, 768 1.042 -> 0.931, 1024 1.148 -> 1.128; in round 5
+  // the FENCED decode beside the ladder lost at B = 256: 256 decode + 100
+  // ladder blocks queued for each other).  PM_ACC_OPT_TWIST = 1: always
+  // unfenced.  Without the split form (the one-lane GLV products) the decode
+  // is fenced up to num_cus point blocks (beyond, throughput work).
+  bool twist = false, fenced;
+  {
+    std::vector<int32_t> rots;
+    std::vector<std::vector<AccQuery>> sets;
+    acc_group_sets(q, rots, sets);
+    AccTerms tm;
+    acc_terms(s, L, sets, tm);
+    const bool split = vk_repr && acc_split_lanes(ctx, B, tm) > 0;
+    const size_t nprf = B * (size_t)tm.Tp;
+    const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
+    const bool fits = sliced && (size_t)h.nblk_pts + lad_blocks <= (size_t)ctx->num_cus;
+    twist = split && ctx->acc_twist != 0;
+    fenced = twist ? fits && ctx->acc_twist != 1 : h.nblk_pts <= (uint32_t)ctx->num_cus;
+  }
+  const size_t dec_fence = fenced ? kDecodeFence : 0;
+  dec.twist = twist;
   dec.off_of.assign(L.npts, kAccNoByte);
   for (size_t i = 0; i + 1 < map.size(); i += 2) dec.off_of[map[i + 1]] = map[i];
   const SqrtTab* tabp = (const SqrtTab*)ctx->sqrt_tab[slot].p;

@@ -644,6 +644,15 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   const uint32_t* ds = (const uint32_t*)scalars;
   const uint32_t* db = (const uint32_t*)bases;
   const auto tstage = std::chrono::steady_clock::now();
+  // host phases (pm_ctx_set_timing_filter(ctx, "small_host"): no kernel is
+  // event-timed, the call runs exactly as untimed and records small_stage,
+  // small_launch, small_wait, host_tail and small_finish)
+  auto phase = [&](const char* name, std::chrono::steady_clock::time_point t0) {
+    if (!ctx->timing) return;
+    auto& stt = ctx->stats[name];
+    stt.first += 1;
+    stt.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
   if (s_host || b_host) {
     const size_t sb = s_host ? n * 32 : 0, bb = b_host ? n * 64 : 0;
     if ((rc = ctx->ensure_small_pin(sb + bb))) return rc;
@@ -658,11 +667,8 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
       db = (const uint32_t*)((char*)dp + sb);
     }
   }
-  if (ctx->timing) {
-    auto& stt = ctx->stats["small_stage"];  // host copy into the pinned staging buffer
-    stt.first += 1;
-    stt.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tstage).count();
-  }
+  phase("small_stage", tstage);  // host copy into the pinned staging buffer
+  const auto tlaunch = std::chrono::steady_clock::now();
   if (!fused) {
     if ((rc = ctx->small_tab.ensure(n * kSmallMults * sizeof(Xyzz<F>)))) return rc;
     if ((rc = ctx->small_dig.ensure((size_t)kSmallWin * T))) return rc;
@@ -705,9 +711,12 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   }
   hipEvent_t ev = ctx->grp_ev[0];
   HIP_TRY(hipEventRecord(ev, st));
+  phase("small_launch", tlaunch);  // buffers, counters and the launches queued
+  const auto twait = std::chrono::steady_clock::now();
   // the flag instead of the event: 66.5 / 80.3 / 138.8 us against 71.9 /
   // 86.4 / 144.5 at n = 1 / 32 / 4096 (profiles/r04/small/flag_vs_event.txt)
-  if (ctx->timing) {  // the timed launches' events must complete (end_call)
+  const bool kev = ctx->timed("small_fused") || ctx->timed("small_table") || ctx->timed("small_sum");
+  if (kev) {  // the timed launches' events must complete (end_call)
     if ((rc = wait_event(ctx, ev))) return rc;
   } else {
     for (uint32_t it = 1;; it++) {
@@ -727,15 +736,14 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
       __builtin_ia32_pause();
     }
   }
+  phase("small_wait", twait);  // launches -> the completion flag
   const auto t0 = std::chrono::steady_clock::now();
   const host::Pt<F> r = host_has_bmi2() ? small_horner_bmi2<F>(hW) : small_horner<F, false>(hW);
-  if (ctx->timing) {
-    auto& stt = ctx->stats["host_tail"];
-    stt.first += 1;
-    stt.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
+  phase("host_tail", t0);
+  const auto tfin = std::chrono::steady_clock::now();
   ctx->end_call();
   aff_to_u64<F>(xyzz_to_aff<F>(host::to_dev<F>(r)), out);
+  phase("small_finish", tfin);  // end_call + the affine conversion
   return PM_OK;
 }
 
