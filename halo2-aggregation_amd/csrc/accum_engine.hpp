@@ -192,6 +192,11 @@ struct AccDecode {
 // issue-bound lone-wave chains): its LDS request keeps it off any CU holding
 // a ladder block (sliced 84 KiB, quad 40 KiB) or a side-stream block
 constexpr size_t kDecodeFence = 124 * 1024;
+// two decode blocks per CU, and none beside a ladder block fenced at
+// kAccSlicedFence (84 KiB)
+constexpr size_t kDecodePairFence = 80 * 1024;
+static_assert(2 * kDecodePairFence <= 160 * 1024 && kDecodePairFence + kAccSlicedFence > 160 * 1024,
+              "decode pair fence");
 
 // vk_repr != nullptr: the challenges are first replayed into d_ch on the
 // device (transcript_device_impl); the split ladder then runs concurrently
@@ -778,18 +783,24 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   dec.sliced = sliced;
   // The twisted ladder (accum_device_impl) and the decode's fence, decided
   // together before the plan is built.  With the powers tables (split form)
-  // the ladder always runs beside the decode (PM_ACC_OPT_TWIST = 0: after
-  // it).  While the row-sliced decode's point blocks and the ladder's blocks
-  // fit the CUs side by side, the decode keeps its fence (one block per CU,
-  // beside nothing: unfenced, the dispatcher packed several blocks per CU, B
-  // = 16 decode 0.11 -> 0.16 ms); beyond, it runs unfenced among the ladder's
-  // blocks (round 6, profiles/r06/twist_ab.jsonl: B = 256 0.595 -> 0.542 ms,
-  // 512 0.750 -> 0.718, 768 1.042 -> 0.931, 1024 1.148 -> 1.128; in round 5
-  // the FENCED decode beside the ladder lost at B = 256: 256 decode + 100
-  // ladder blocks queued for each other).  PM_ACC_OPT_TWIST = 1: always
-  // unfenced.  Without the split form (the one-lane GLV products) the decode
-  // is fenced up to num_cus point blocks (beyond, throughput work).
-  bool twist = false, fenced;
+  // the ladder runs beside the decode (PM_ACC_OPT_TWIST = 0: after it); the
+  // decode's fence then keeps its blocks off the ladder's CUs where the CUs
+  // allow (round 6, profiles/r06/twist_fence_ab.jsonl, B = 128 .. 1024):
+  //  * decode and ladder blocks fit the CUs side by side: kDecodeFence, one
+  //    decode block per CU beside nothing (B <= 128, 384, 512);
+  //  * else, while the decode's blocks alone leave CUs free: kDecodePairFence
+  //    (B = 192: 0.507 ms against 0.540 unfenced, 0.60 without the twist);
+  //  * else unfenced, among the ladder's blocks: the dispatcher spreads the
+  //    first blocks one per CU, so a pair-fenced decode filling every CU kept
+  //    the ladder waiting (B = 256: 0.547 unfenced, 0.600 paired or no twist).
+  // (In round 5 the twist beside a fenced decode lost at B = 256 for that
+  // reason and was kept to the first case.)  PM_ACC_OPT_TWIST = 1 / 2 force
+  // the unfenced / paired decode.  Without the split form (the one-lane GLV
+  // products) the decode is fenced up to num_cus point blocks (beyond,
+  // throughput work).
+  const size_t nblk_dec = h.nblk_pts + nblk_sc;
+  bool twist = false;
+  size_t dec_fence;
   {
     std::vector<int32_t> rots;
     std::vector<std::vector<AccQuery>> sets;
@@ -797,13 +808,14 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     AccTerms tm;
     acc_terms(s, L, sets, tm);
     const bool split = vk_repr && acc_split_lanes(ctx, B, tm) > 0;
-    const size_t nprf = B * (size_t)tm.Tp;
+    const size_t nprf = B * (size_t)tm.Tp, cus = (size_t)ctx->num_cus;
     const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
-    const bool fits = sliced && (size_t)h.nblk_pts + lad_blocks <= (size_t)ctx->num_cus;
     twist = split && ctx->acc_twist != 0;
-    fenced = twist ? fits && ctx->acc_twist != 1 : h.nblk_pts <= (uint32_t)ctx->num_cus;
+    if (!twist) dec_fence = h.nblk_pts <= cus ? kDecodeFence : 0;
+    else if (ctx->acc_twist == 1) dec_fence = 0;
+    else if (ctx->acc_twist == 2) dec_fence = kDecodePairFence;
+    else dec_fence = nblk_dec + lad_blocks <= cus ? kDecodeFence : nblk_dec < cus ? kDecodePairFence : 0;
   }
-  const size_t dec_fence = fenced ? kDecodeFence : 0;
   dec.twist = twist;
   dec.off_of.assign(L.npts, kAccNoByte);
   for (size_t i = 0; i + 1 < map.size(); i += 2) dec.off_of[map[i + 1]] = map[i];

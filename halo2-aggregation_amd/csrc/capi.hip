@@ -437,7 +437,8 @@ int pm_ctx_set_accum_option(pm_ctx* ctx, int option, int value) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   switch (option) {
     case PM_ACC_OPT_TWIST:
-      if (value < -1 || value > 1) return set_error(PM_ERR_ARG, "twist option out of range (-1 auto, 0 off, 1 force)");
+      if (value < -1 || value > 2)
+        return set_error(PM_ERR_ARG, "twist option out of range (-1 auto, 0 off, 1 unfenced decode, 2 paired decode)");
       ctx->acc_twist = value;
       return PM_OK;
     case PM_ACC_OPT_TAIL_STREAM:

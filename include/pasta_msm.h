@@ -113,9 +113,10 @@ int pm_ctx_set_accum_ladder(pm_ctx* ctx, int mode);
  * value -1 = automatic (the default) for every option.  Results never depend
  * on them.
  *   PM_ACC_OPT_TWIST           0: no twisted ladder (the powers-table ladder
- *                                 waits for the decoded points); 1: the
+ *                                 waits for the decoded points); 1 / 2: the
  *                                 twisted ladder whenever the powers tables
  *                                 are built, the decode unfenced beside it
+ *                                 (1) or two decode blocks per CU (2)
  *   PM_ACC_OPT_TAIL_STREAM     0: term additions and sums on the main stream
  *   PM_ACC_OPT_TERMS_PER_LANE  1 or 2: the one-lane GLV form's terms per lane
  *   PM_ACC_OPT_TRANSCRIPT      0: per-record transcript replay (no streamed

@@ -342,6 +342,7 @@ def test_schedule_options_vs_c_port(B, logn):
     settings = [
         [(H.ACC_OPT_TWIST, 0)],
         [(H.ACC_OPT_TWIST, 1)],
+        [(H.ACC_OPT_TWIST, 2)],
         [(H.ACC_OPT_TAIL_STREAM, 0)],
         [(H.ACC_OPT_TWIST, 0), (H.ACC_OPT_TAIL_STREAM, 0)],
         [(H.ACC_OPT_TRANSCRIPT, 0)],
@@ -370,7 +371,7 @@ def test_schedule_options_vs_c_port(B, logn):
 
 def test_accum_option_arguments(gpu_ctx):
     """Unknown options and out-of-range values are refused (PM_ERR_ARG)."""
-    for opt, val in [(0, 0), (99, -1), (H.ACC_OPT_TWIST, 2), (H.ACC_OPT_TAIL_STREAM, 1), (H.ACC_OPT_TERMS_PER_LANE, 0),
+    for opt, val in [(0, 0), (99, -1), (H.ACC_OPT_TWIST, 3), (H.ACC_OPT_TAIL_STREAM, 1), (H.ACC_OPT_TERMS_PER_LANE, 0),
                      (H.ACC_OPT_TERMS_PER_LANE, 3), (H.ACC_OPT_TRANSCRIPT, -2)]:
         with pytest.raises(H.PmError):
             gpu_ctx.set_accum_option(opt, val)
