@@ -1352,6 +1352,8 @@ def accum_latency_roofline(B, T, nslots, ms_batch, kernels, shape=None, psize=0,
     lgL = 0
     while lgL < 5 and ((B * 4) << (lgL + 1)) <= 16384:
         lgL += 1
+    while lgL < 3 and ((B * 4) << (lgL + 1)) <= budget // 2:  # quads at large B (accum_engine.hpp)
+        lgL += 1
     nq = max(1, (1 << lgL) // 4)
     c = shape.c if shape is not None else None
     npts = shape.layout()[0] if shape is not None else T

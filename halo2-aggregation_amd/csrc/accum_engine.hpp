@@ -523,6 +523,12 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // (profiles/r01_s4/accum_sum_lanes.jsonl).
   uint32_t lgL = 0;
   while (lgL < 5 && ((size_t)B * 4 << (lgL + 1)) <= kAccSumLanes) lgL++;
+  // large batches: still quads (quad-cooperative additions and inversion),
+  // up to two per output, within one wave per SIMD; one lane per output ran
+  // f's ~12 term sums and a lone-lane inversion while the w / zw / e lanes of
+  // its wave idled (round 6, profiles/r06/sum_lanes_ab.jsonl: B = 4096 0.133
+  // -> 0.114 ms, 3072 0.133 -> 0.080)
+  while (lgL < 3 && ((size_t)B * 4 << (lgL + 1)) <= kAccLaneBudget / 2) lgL++;
   {
     hipEvent_t done = ctx->next_event();
     if (!done) return set_error(PM_ERR_HIP, "hipEventCreate failed");

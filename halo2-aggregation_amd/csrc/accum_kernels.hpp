@@ -11,10 +11,12 @@
 //                  per query, H expanded as sum_i x^{n i} h_i
 //                  (vanishing.rs:178-188), z_j u^{S-1-j} for zw and
 //                  -eval_multi for e = [.] g1.
-//   k_acc_termmul  one lane per (proof, term): [coef] P by GLV + Shamir
-//                  (130 joint double-and-add steps in XYZZ).
-//   k_acc_sum      one lane per (proof, output): sums its terms, converts to
-//                  the unique affine point (w, zw, f, e order of MultiopenVar).
+//   k_acc_termmul  one lane per (proof, term) or per two terms of one output:
+//                  [coef] P by GLV and signed 3-bit windows (43 windows of 3
+//                  doublings, shared by a lane's terms, and 2 mixed additions
+//                  per term), XYZZ.
+//   k_acc_sum      lanes or quads per (proof, output): sums its terms, converts
+//                  to the unique affine point (w, zw, f, e order of MultiopenVar).
 // Scalars / points use the Rust in-memory Montgomery layout (pasta_msm.h).
 #pragma once
 #include "accum_plan.hpp"

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round 6: k_acc_sum with a quad per output at large B (sweep), then the accumulator tests.
+set -o pipefail
+OUT=gpurun_out/r06_e
+mkdir -p $OUT
+BS=256,512,1024,1536,2048,3072,4096 REPS=20 timeout -k 10 300 python -u tools/accum_scaling.py > $OUT/sweep.jsonl 2> $OUT/sweep.err || { tail -20 $OUT/sweep.err; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_proof_gpu.py tests/test_accum_gpu.py > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
