@@ -924,7 +924,8 @@ static int dropin_small_msm(Ctx* ctx, int curve, const uint64_t* scalars, const 
       if ((int)ctx->dropin_small.size() < kDropinSmallEntries && held_small + need <= pm::kDropinSmallBytes &&
           held + need <= budget)
         break;
-      if (ctx->dropin_small.empty()) return small();
+      // the large sets alone leave no room: keep the small sets, do not admit
+      if (ctx->dropin_small.empty() || held - held_small + need > budget) return small();
       auto lru = std::min_element(ctx->dropin_small.begin(), ctx->dropin_small.end(),
                                   [](const pm::DropinEntry& x, const pm::DropinEntry& y) { return x.last_use < y.last_use; });
       if (have_info) free_b += lru->bytes;
