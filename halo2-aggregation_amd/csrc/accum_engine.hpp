@@ -774,39 +774,11 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
   h.npp = npp;
   h.sc_off = sc_off;
   h.stride = (uint32_t)stride;
-  // few points on a p = 3 mod 4 curve: one point per row, the square root
-  // row-sliced (k_proof_decode<Cv, true>); up to ~one wave per SIMD
-  const bool sliced = !ctx->sqrt_tab_ts[slot] && (ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1
-                                                                         : B * npp <= kDecodeSlicedPoints);
-  const uint32_t per_blk = sliced ? kDecodeThreads / 16 : kDecodeThreads;
-  h.nblk_pts = (uint32_t)((B * npp + per_blk - 1) / per_blk);
-  const size_t nblk_sc = (B * ((size_t)L.nsc + ninst) + kDecodeThreads - 1) / kDecodeThreads;
-  if (stride > 0xffffffffull) return set_error(PM_ERR_UNSUPPORTED, "proof stride above 4 GiB");
-  AccDecode dec;
-  dec.proofs = d_proofs;
-  dec.stride = stride;
-  dec.inst = d_inst;
-  dec.sliced = sliced;
-  // The twisted ladder (accum_device_impl) and the decode's fence, decided
-  // together before the plan is built.  With the powers tables (split form)
-  // the ladder runs beside the decode (PM_ACC_OPT_TWIST = 0: after it); the
-  // decode's fence then keeps its blocks off the ladder's CUs where the CUs
-  // allow (round 6, profiles/r06/twist_fence_ab.jsonl, B = 128 .. 1024):
-  //  * decode and ladder blocks fit the CUs side by side: kDecodeFence, one
-  //    decode block per CU beside nothing (B <= 128, 384, 512);
-  //  * else, while the decode's blocks alone leave CUs free: kDecodePairFence
-  //    (B = 192: 0.507 ms against 0.540 unfenced, 0.60 without the twist);
-  //  * else unfenced, among the ladder's blocks: the dispatcher spreads the
-  //    first blocks one per CU, so a pair-fenced decode filling every CU kept
-  //    the ladder waiting (B = 256: 0.547 unfenced, 0.600 paired or no twist).
-  // (In round 5 the twist beside a fenced decode lost at B = 256 for that
-  // reason and was kept to the first case.)  PM_ACC_OPT_TWIST = 1 / 2 force
-  // the unfenced / paired decode.  Without the split form (the one-lane GLV
-  // products) the decode is fenced up to num_cus point blocks (beyond,
-  // throughput work).
-  const size_t nblk_dec = h.nblk_pts + nblk_sc;
+  // Plan facts the decode's form and fence depend on (the split form and
+  // the ladder's grid; accum_device_impl recomputes them identically).
   bool twist = false;
-  size_t dec_fence;
+  size_t lad_blocks = 0;
+  const size_t cus = (size_t)ctx->num_cus;
   {
     std::vector<int32_t> rots;
     std::vector<std::vector<AccQuery>> sets;
@@ -814,14 +786,56 @@ int proofs_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* 
     AccTerms tm;
     acc_terms(s, L, sets, tm);
     const bool split = vk_repr && acc_split_lanes(ctx, B, tm) > 0;
-    const size_t nprf = B * (size_t)tm.Tp, cus = (size_t)ctx->num_cus;
-    const size_t lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
+    const size_t nprf = B * (size_t)tm.Tp;
+    lad_blocks = nprf <= kAccSlicedChains ? (nprf + 3) / 4 : (4 * nprf + 255) / 256;
     twist = split && ctx->acc_twist != 0;
-    if (!twist) dec_fence = h.nblk_pts <= cus ? kDecodeFence : 0;
-    else if (ctx->acc_twist == 1) dec_fence = 0;
-    else if (ctx->acc_twist == 2) dec_fence = kDecodePairFence;
-    else dec_fence = nblk_dec + lad_blocks <= cus ? kDecodeFence : nblk_dec < cus ? kDecodePairFence : 0;
   }
+  const size_t nblk_sc = (B * ((size_t)L.nsc + ninst) + kDecodeThreads - 1) / kDecodeThreads;
+  auto pt_blocks = [&](bool sl) {
+    const size_t per = sl ? kDecodeThreads / 16 : kDecodeThreads;
+    return (B * npp + per - 1) / per;
+  };
+  // few points on a p = 3 mod 4 curve: one point per row, the square root
+  // row-sliced (k_proof_decode<Cv, true>); up to ~one wave per SIMD.  Beside
+  // the twisted ladder (automatic schedule) only while its grid fits the CUs
+  // with the ladder's blocks: else the one-lane decode, 16x fewer blocks,
+  // which then fits fenced beside the ladder and leaves it undisturbed --
+  // the decode is off the critical path there, the ladder on it (round 6,
+  // profiles/r06/decode_form_ab.jsonl: B = 256 0.546 -> 0.50 ms)
+  bool sliced = !ctx->sqrt_tab_ts[slot] && (ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1
+                                                                  : B * npp <= kDecodeSlicedPoints);
+  if (sliced && twist && ctx->acc_ladder < 0 && ctx->acc_twist < 0 && pt_blocks(true) + nblk_sc + lad_blocks > cus)
+    sliced = false;
+  h.nblk_pts = (uint32_t)pt_blocks(sliced);
+  if (stride > 0xffffffffull) return set_error(PM_ERR_UNSUPPORTED, "proof stride above 4 GiB");
+  AccDecode dec;
+  dec.proofs = d_proofs;
+  dec.stride = stride;
+  dec.inst = d_inst;
+  dec.sliced = sliced;
+  // The decode's fence beside the twisted ladder: its blocks are kept off the
+  // ladder's CUs where the CUs allow (round 6, profiles/r06/twist_fence_ab.jsonl,
+  // B = 128 .. 1024):
+  //  * decode and ladder blocks fit the CUs side by side: kDecodeFence, one
+  //    decode block per CU beside nothing (B <= 128, 384, 512);
+  //  * else, while the decode's blocks alone leave CUs free: kDecodePairFence
+  //    (B = 192 with the sliced decode: 0.507 ms against 0.540 unfenced, 0.60
+  //    without the twist);
+  //  * else unfenced, among the ladder's blocks: the dispatcher spreads the
+  //    first blocks one per CU, so a pair-fenced decode filling every CU kept
+  //    the ladder waiting (B = 256 sliced: 0.547 unfenced, 0.600 paired or no
+  //    twist).
+  // (In round 5 the twist beside a fenced decode lost at B = 256 for that
+  // reason and was kept to the first case.)  PM_ACC_OPT_TWIST = 1 / 2 force
+  // the unfenced / paired decode (and keep the row-sliced form where it
+  // applies).  Without the split form (the one-lane GLV products) the decode
+  // is fenced up to num_cus point blocks (beyond, throughput work).
+  const size_t nblk_dec = h.nblk_pts + nblk_sc;
+  size_t dec_fence;
+  if (!twist) dec_fence = h.nblk_pts <= cus ? kDecodeFence : 0;
+  else if (ctx->acc_twist == 1) dec_fence = 0;
+  else if (ctx->acc_twist == 2) dec_fence = kDecodePairFence;
+  else dec_fence = nblk_dec + lad_blocks <= cus ? kDecodeFence : nblk_dec < cus ? kDecodePairFence : 0;
   dec.twist = twist;
   dec.off_of.assign(L.npts, kAccNoByte);
   for (size_t i = 0; i + 1 < map.size(); i += 2) dec.off_of[map[i + 1]] = map[i];
