@@ -128,6 +128,11 @@ def leg_summary(leg):
                 matches.append(cb[k])
     if "status_nonzero" in leg:
         matches.append(leg["status_nonzero"] == 0)
+    two = leg.get("two_in_flight")
+    if isinstance(two, dict) and two.get("value") is not None:
+        s["two_in_flight"] = _r(two["value"])
+        if isinstance(two.get("quads_match_single_runs"), bool):
+            matches.append(two["quads_match_single_runs"])
     if matches:
         s["matches"] = all(matches)
     return {k: v for k, v in s.items() if v is not None}
@@ -176,7 +181,7 @@ def compact_line(out, detail_path=None):
     if detail_path:
         line["detail"] = detail_path
     s = json.dumps(line, separators=(",", ":"))
-    for drop in (("bound",), ("cpu",), ("frac", "ms")):
+    for drop in (("bound", "two_in_flight"), ("cpu",), ("frac", "ms")):
         if len(s) < LINE_LIMIT:
             break
         for leg in legs.values():
@@ -433,8 +438,8 @@ def main():
     inst = run_instance_commitments(args, ctx, dist, dev, rank, world) if args.inst_batch > 0 else None
     # many proofs in one pm_accum_batch_proofs_device call (the stream of a
     # busy aggregator): the batch fills the GPU instead of a latency chain
-    accum_large = run_accumulator(args, ctx, dist, dev, rank, world, B=args.accum_large, logn=17, light=True) \
-        if args.accum_large else None
+    accum_large = run_accumulator(args, ctx, dist, dev, rank, world, B=args.accum_large, logn=17, light=True,
+                                  two=True) if args.accum_large else None
 
     if rank == 0:
         out = {
@@ -1021,7 +1026,7 @@ def ntt_cpu_baseline(curve, k, src, w, first, budget_s):
             "matches_gpu": match}
 
 
-def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None, light=False):
+def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None, light=False, two=None):
     """Batch multiopen accumulator: B proofs per rank, timed like the MSM leg.
     One step starts from the proofs' BYTES, resident in HBM as halo2's
     Blake2bWrite serialized them: device decode (read_point decompression /
@@ -1099,7 +1104,7 @@ def run_accumulator(args, ctx, dist, dev, rank, world, B=None, logn=None, light=
            "from_decoded": {"ms_per_batch": round(ms_dec, 4), "value": round(world * B / (ms_dec * 1e-3), 1),
                             "entry": "pm_accum_batch_transcript_device (decoded points / scalars in HBM)",
                             "quads_match_bytes_path": bool(torch.equal(quads_dec, batch.quads))}}
-    if world == 1 and not light:
+    if world == 1 and (not light if two is None else two):
         out["two_in_flight"] = accum_two_in_flight(args, ctx, shape, batch, B)
     if B > 256:  # its first 256 proofs as a batch of their own: the same quads
         sub = 256
