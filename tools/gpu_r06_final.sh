@@ -4,7 +4,7 @@
 # kernel's summary), the small-MSM phases, and the k_accumulate PMC passes of
 # the headline workload (resident row table, 2^20).
 set -o pipefail
-OUT=gpurun_out/r06_final
+OUT=gpurun_out/${TAG:-r06_final}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
@@ -17,5 +17,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt -o run -- p
 find $OUT/kt -name '*kernel_stats.csv' -exec cp {} $OUT/kt_kernel_stats.csv \;
 rm -rf $OUT/kt
 timeout -k 10 200 python -u tools/small_phases.py > $OUT/small_phases.jsonl 2> $OUT/small.err || { tail -20 $OUT/small.err; exit 1; }
-RESIDENT=1 LOGNS="20 22" bash tools/gpu_pmc_r02.sh r06_final/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+RESIDENT=1 LOGNS="20 22" bash tools/gpu_pmc_r02.sh ${TAG:-r06_final}/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
 ls $OUT $OUT/pmc
