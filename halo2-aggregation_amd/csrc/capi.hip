@@ -190,7 +190,9 @@ int pm_ctx::ensure_pinned(size_t bytes) {
   h_pinned_cap = 0;
   // coherent: the small-MSM path's window sums and completion flag live here
   // and are read by the host while the kernel still runs
+  h_pinned_dev = nullptr;
   HIP_TRY(hipHostMalloc(&h_pinned, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer(&h_pinned_dev, h_pinned, 0));
   h_pinned_cap = bytes;
   return PM_OK;
 }
@@ -202,7 +204,9 @@ int pm_ctx::ensure_small_pin(size_t bytes) {
   small_pin_cap = 0;
   // coherent (fine-grained) whatever HIP_HOST_COHERENT says: the host spins on
   // the completion flag and window sums the kernel writes here mid-launch
+  small_pin_dev = nullptr;
   HIP_TRY(hipHostMalloc(&small_pin, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer(&small_pin_dev, small_pin, 0));
   small_pin_cap = bytes;
   return PM_OK;
 }

@@ -220,12 +220,7 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // saves the blit of a D2H copy (~11 us per MSM, profiles/r03/kernel_stats.csv
   // __amd_rocclr_copyBuffer; the copy measured within noise on the headline
   // and 24 us slower on the variable-base path, profiles/r03/ab/).
-  Xyzz<F>* Qd = nullptr;
-  {
-    void* dq = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&dq, hslot, 0));
-    Qd = (Xyzz<F>*)dq;
-  }
+  Xyzz<F>* Qd = (Xyzz<F>*)ctx->h_pinned_dev + (size_t)slot * nQ;
   const uint32_t un = (uint32_t)n;
 
   g.clr_bh = bh + (TOTB - 1);  // zeroed by the histogram kernel's block 0
@@ -656,8 +651,7 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   if (s_host || b_host) {
     const size_t sb = s_host ? n * 32 : 0, bb = b_host ? n * 64 : 0;
     if ((rc = ctx->ensure_small_pin(sb + bb))) return rc;
-    void* dp = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&dp, ctx->small_pin, 0));
+    void* dp = ctx->small_pin_dev;
     if (s_host) {
       std::memcpy(ctx->small_pin, scalars, sb);
       ds = (const uint32_t*)dp;
@@ -685,8 +679,7 @@ int msm_small_impl(Ctx* ctx, const void* scalars, bool s_host, const void* bases
   volatile uint32_t* hflag = (volatile uint32_t*)(hW + kSmallWin);
   *hflag = 0;
   const uint32_t seq = ++ctx->small_seq ? ctx->small_seq : ++ctx->small_seq;
-  void* dW = nullptr;
-  HIP_TRY(hipHostGetDevicePointer(&dW, hW, 0));
+  void* dW = ctx->h_pinned_dev;
   uint32_t* dflag = (uint32_t*)((Xyzz<F>*)dW + kSmallWin);
   if (fused) {
     PM_LAUNCH(ctx, "small_fused",

@@ -337,9 +337,7 @@ int msm_many_impl(Ctx* ctx, const ManyTable* tb, size_t B, const size_t* n, cons
     if (sb <= kManyMappedBytes) {
       if ((rc = ctx->ensure_small_pin(sb))) return rc;
       std::memcpy(ctx->small_pin, scalars, sb);
-      void* dp = nullptr;
-      HIP_TRY(hipHostGetDevicePointer(&dp, ctx->small_pin, 0));
-      ds = (const uint32_t*)dp;
+      ds = (const uint32_t*)ctx->small_pin_dev;
     } else {
       if ((rc = ctx->in_scalars.ensure(sb)) || (rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, sb, st))) return rc;
       ds = (const uint32_t*)ctx->in_scalars.p;
@@ -358,8 +356,7 @@ int msm_many_impl(Ctx* ctx, const ManyTable* tb, size_t B, const size_t* n, cons
   volatile uint32_t* hflag = (volatile uint32_t*)(hR + msms.size());
   *hflag = 0;
   const uint32_t seq = ++ctx->small_seq ? ctx->small_seq : ++ctx->small_seq;
-  void* dR = nullptr;
-  HIP_TRY(hipHostGetDevicePointer(&dR, hR, 0));
+  void* dR = ctx->h_pinned_dev;
   uint32_t* dflag = (uint32_t*)((Xyzz<F>*)dR + msms.size());
   PM_LAUNCH(ctx, "many_sum",
             (k_many_sum<Cv><<<(unsigned)jobs.size(), 256, 0, st>>>(g, djobs, dmsms, ds, (const Xyzz<F>*)tb->d,

@@ -271,9 +271,11 @@ struct pm_ctx {
   std::vector<pm::NttTwiddles> ntt_tw;  // cached twiddle segments (pm_fft*)
   uint64_t ntt_clock = 0;
   void* h_pinned = nullptr;  // MSM host terms: two slots (batch pipelining)
+  void* h_pinned_dev = nullptr;  // its device address (hipHostGetDevicePointer, once per allocation)
   size_t h_pinned_cap = 0;
   size_t small_max = pm::kSmallMaxN;  // small-MSM path threshold (pm_ctx_set_small_msm)
   void* small_pin = nullptr;          // small-MSM host inputs, pinned + mapped (read by k_small_table)
+  void* small_pin_dev = nullptr;      // its device address
   size_t small_pin_cap = 0;
   uint32_t small_seq = 0;             // completion-flag value of the last small MSM
   // timing
