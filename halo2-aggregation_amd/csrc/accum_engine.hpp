@@ -207,6 +207,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
                       bool canon_ready = false, uint32_t* dflags = nullptr, const AccDecode* dec = nullptr) {
   using F = typename Cv::Base;
   using Fs = typename Cv::Scalar;
+  const auto tplan = std::chrono::steady_clock::now();  // host planning (stat "accum_plan_host")
   std::vector<AccQuery> q;
   AccLayout L;
   const std::string err = acc_validate(s, q, L, nullptr);
@@ -429,6 +430,11 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     const size_t chains = nprf + nvk_build;
     const bool sliced = ctx->acc_ladder >= 0 ? ctx->acc_ladder == 1 : chains <= kAccSlicedChains;
     lad_sliced = sliced;
+    if (ctx->timing) {  // entry -> the ladder's launch (filter "accum_host": no kernel events)
+      auto& stt = ctx->stats["accum_plan_host"];
+      stt.first += 1;
+      stt.second += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tplan).count();
+    }
     if (chains > 0 && sliced)
       PM_LAUNCH_ST(ctx, lst, "acc_ladder",
                 (k_acc_powers_s<Cv><<<(unsigned)((chains + 3) / 4), 256, kAccSlicedFence, lst>>>(
