@@ -490,6 +490,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
   // 128 0.454 -> 0.446; B = 16 0.341 -> 0.347 had it followed the ladder too)
   const bool tail_red = ctx->acc_tail != 0;  // PM_ACC_OPT_TAIL_STREAM = 0: always the main stream
   const hipStream_t tst = lgS > 0 && h.twist && !lad_sliced && tail_red ? ctx->red_stream : st;
+  uint32_t pstep = 1;  // k_acc_sum's row step (2 after two-term lanes)
   if (lgS > 0) {
     // the term additions wait for the other stream: the scalar block (side),
     // or with the twist the ladder (or, on the ladder's stream, the scalar block)
@@ -514,6 +515,7 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     const bool pairs_fit = (size_t)B * npair <= kAccLaneBudget / 2;
     const int tpl = ctx->acc_tpl > 0 ? ctx->acc_tpl : (nterm > kAccLaneBudget / 2 && pairs_fit ? 2 : 1);
     const uint32_t* dvk = (const uint32_t*)ctx->acc_vk.buf.p;
+    if (tpl == 2) pstep = 2;
     if (tpl == 2)
       PM_LAUNCH(ctx, "acc_termmul",
                 (k_acc_termmul<Cv, 2><<<(unsigned)(((size_t)B * npair + 255) / 256), 256, 0, st>>>(
@@ -540,11 +542,11 @@ int accum_device_impl(Ctx* ctx, const pm_proof_shape* s, size_t B, const void* d
     if (!done) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     const unsigned nblk = (unsigned)((B * 4 * (1u << lgL) + 63) / 64);
     if (ctx->timing) {
-      PM_LAUNCH_ST(ctx, tst, "acc_sum", (k_acc_sum<Cv><<<nblk, 64, 0, tst>>>(h, dpart, lgL, (uint32_t*)d_out)));
+      PM_LAUNCH_ST(ctx, tst, "acc_sum", (k_acc_sum<Cv><<<nblk, 64, 0, tst>>>(h, dpart, lgL, (uint32_t*)d_out, pstep)));
       HIP_TRY(hipEventRecord(done, tst));
     } else {  // the completion event rides on the dispatch (no marker packet behind it)
       hipExtLaunchKernelGGL(k_acc_sum<Cv>, dim3(nblk), dim3(64), 0, tst, nullptr, done, 0, h, dpart, lgL,
-                            (uint32_t*)d_out);
+                            (uint32_t*)d_out, pstep);
       HIP_TRY(hipGetLastError());
     }
     if (int rc = wait_event(ctx, done)) return rc;

@@ -1125,13 +1125,14 @@ __global__ void __launch_bounds__(256) k_acc_termadd(AccumHdr h, const uint32_t*
 }
 
 // k_acc_sum: 2^lgL lanes per (proof, output) (lgL <= 5): lane l sums terms
-// lo + l, lo + l + 2^lgL, ...; a butterfly of cross-lane shuffles folds the
+// lo + l, lo + l + 2^lgL, ... (pstep = 2 after k_acc_termmul's two-term
+// lanes: only the pairs' first rows hold sums, the second the identity); a butterfly of cross-lane shuffles folds the
 // partials and lane 0 converts to the unique affine point (binary-GCD
 // inversion).  With >= 4 lanes the lanes work in quads (quad-cooperative
 // additions).  Outputs in MultiopenVar order w, zw, f, e.
 template <class Cv>
 __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename Cv::Base>* __restrict__ part,
-                                                uint32_t lgL, uint32_t* __restrict__ out) {
+                                                uint32_t lgL, uint32_t* __restrict__ out, uint32_t pstep) {
   using F = typename Cv::Base;
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t NL = 1u << lgL, g = gl >> lgL, lane = gl & (NL - 1);
@@ -1147,11 +1148,12 @@ __global__ void __launch_bounds__(64) k_acc_sum(AccumHdr h, const Xyzz<typename 
     // quads of lanes act as one lane (coop29.hpp: each addition at ~half the
     // latency); all 4 lanes of a quad see the same terms
     const uint32_t v = lane >> 2, NV = NL >> 2;
-    for (uint32_t t = lo + v; t < hi; t += NV)
+    for (uint32_t t = lo + v * pstep; t < hi; t += NV * pstep)
       acc = xyzz29_add_q<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
     for (uint32_t m = 4; m < NL; m <<= 1) acc = xyzz29_add_q<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
   } else {
-    for (uint32_t t = lo + lane; t < hi; t += NL) acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
+    for (uint32_t t = lo + lane * pstep; t < hi; t += NL * pstep)
+      acc = xyzz29_add<F>(acc, load_xyzz29<F>(&part[(size_t)b * h.T + t]));
     for (uint32_t m = 1; m < NL; m <<= 1) acc = xyzz29_add<F>(acc, xyzz29_shfl_xor<F>(acc, (int)m));
   }
   // affine conversion: by the group's first quad (quad-cooperative inversion,
