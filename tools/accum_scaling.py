@@ -28,6 +28,8 @@ def main():
         ctx.set_accum_ladder(int(os.environ["LADDER"]))
     if os.environ.get("TWIST"):  # pm_ctx_set_accum_option(PM_ACC_OPT_TWIST, v)
         ctx.set_accum_option(H.ACC_OPT_TWIST, int(os.environ["TWIST"]))
+    if os.environ.get("SPLIT"):  # lanes per term of the split form, log2 (pm_ctx_set_accum_split)
+        ctx.set_accum_split(int(os.environ["SPLIT"]))
     shape = Wk.simple_example_shape(ctx, H.BN254, logn)
     for B in bs:
         batch = Wk.SyntheticBatch(ctx, shape, B)
@@ -46,7 +48,8 @@ def main():
             batch.run_bytes(ctx, shape)
         ctx.set_timing(False)
         ks = {k: round(ctx.kernel_stats(k)[1] / 5, 4) for k in KERNELS}
-        print(json.dumps({"B": B, "logn": logn, "ladder": os.environ.get("LADDER", "auto"), "twist": os.environ.get("TWIST", "auto"), "ms_per_batch": round(ms, 4), "proofs_per_s": round(B / ms * 1e3, 1),
+        print(json.dumps({"B": B, "logn": logn, "ladder": os.environ.get("LADDER", "auto"), "twist": os.environ.get("TWIST", "auto"),
+                          "split": os.environ.get("SPLIT", "auto"), "ms_per_batch": round(ms, 4), "proofs_per_s": round(B / ms * 1e3, 1),
                           "kernels_ms": ks, "status_nonzero": int((batch.status != 0).sum().item())}), flush=True)
         del batch
         torch.cuda.empty_cache()
