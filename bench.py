@@ -171,11 +171,14 @@ def compact_line(out, detail_path=None):
                        "matches": all(r.get("match", True) for r in rows.values())}
         elif k == "dropin_pm_msm" and isinstance(v, dict):
             legs[k] = {"value": v.get("warm_Mscalar_s"), "unit": "Mscalar/s", "ms": v.get("warm_ms_per_msm"),
-                       "first_ms": v.get("first_ms"), "matches": v.get("matches")}
+                       "one_copy_ms": v.get("warm_ms_one_copy"), "first_ms": v.get("first_ms"),
+                       "matches": v.get("matches")}
         elif k == "host_scalars" and isinstance(v, dict) and isinstance(v.get("pageable"), dict):
             p = v["pageable"]
+            one = v.get("pageable_one_copy") if isinstance(v.get("pageable_one_copy"), dict) else {}
             legs[k] = {"value": p.get("Mscalar_s"), "unit": "Mscalar/s", "ms": p.get("ms_per_msm"),
-                       "matches": p.get("matches")}
+                       "one_copy_ms": one.get("ms_per_msm"), "matches": bool(p.get("matches") and
+                                                                             one.get("matches", True))}
     if legs:
         line["legs"] = legs
     if detail_path:
@@ -725,6 +728,14 @@ def run_dropin(args, curve, S, B, n, want):
         for _ in range(k):
             got = ctx.msm(curve, S, B)
         warm = (time.perf_counter() - t0) * 1e3 / k
+        # the same warm calls with one scalar copy (no split: MSM_OPT_SPLIT_COPY = 0)
+        ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, 0)
+        ctx.msm(curve, S, B)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            got1 = ctx.msm(curve, S, B)
+        warm1 = (time.perf_counter() - t0) * 1e3 / k
+        ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, -1)
         # host-side phases of a warm call (separate, untimed calls): the keyed
         # digest on the pool (start to join) and the scalar copy call beside it
         ctx.set_timing(True, only="")
@@ -738,10 +749,11 @@ def run_dropin(args, curve, S, B, n, want):
         kept, drained = ctx.dropin_spec_stats()
         return {"call": "pm_msm_ctx(curve, host scalars, host bases, n)", "first_ms": round(first_ms, 3),
                 "admit_ms": round(admit_ms, 3), "warm_ms_per_msm": round(warm, 4),
+                "warm_ms_one_copy": round(warm1, 4),
                 "warm_Mscalar_s": round(n / (warm * 1e-3) / 1e6, 3), "warm_phases_ms": phases, "cache": st,
                 "speculation": {"kept": kept, "drained": drained},
                 "matches": bool(np.array_equal(first, want) and np.array_equal(second, want)
-                                and np.array_equal(got, want))}
+                                and np.array_equal(got, want) and np.array_equal(got1, want))}
     finally:
         ctx.close()
 
@@ -820,12 +832,19 @@ def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
     """The drop-in path a Rust best_multiexp shim takes:
     scalars in (pageable) host memory, bases resident -> pm_msm_resident.
     Reports the PCIe-inclusive rate and the scalar H2D time on its own
-    (HIP events around the copy, one pageable hipMemcpyAsync)."""
+    (HIP events around the copy, one pageable hipMemcpyAsync or the split
+    copy's two parts)."""
     import numpy as np
+
+    import halo2_amd as H
 
     S = d_s.cpu().numpy().view(np.uint64).copy()
     res = {}
-    for label in ("pageable",):
+    # "pageable": the automatic schedule (the split scalar copy from
+    # PM_SPLIT_COPY_MIN_N points: the first 3/8's sort and accumulation beside
+    # the rest's copy); "pageable_one_copy": MSM_OPT_SPLIT_COPY = 0
+    for label, split in (("pageable", -1), ("pageable_one_copy", 0)):
+        ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, split)
         k = max(3, args.steps // 2)
         el, got = timed_steps(lambda: ctx.msm_resident(rb, 0, S), k, 1, None, dev)
         ctx.set_timing(True, only="h2d")
@@ -834,12 +853,13 @@ def run_host_scalars(args, ctx, rb, d_s, n, dist, dev, world, want):
             ctx.msm_resident(rb, 0, S)
         ctx.set_timing(False)
         cnt, h2d_ms = ctx.kernel_stats("h2d")
-        h2d = h2d_ms / max(1, cnt)
+        h2d = h2d_ms / 3  # per MSM: the copy's span, or the two halves' spans summed
         res[label] = {"ms_per_msm": round(el * 1e3 / k, 4), "Mscalar_s": round(n / (el / k) / 1e6, 3),
-                      "scalar_h2d_ms": round(h2d, 4),
+                      "scalar_h2d_ms": round(h2d, 4), "copies_per_msm": round(cnt / 3, 2),
                       # no h2d events on the small-MSM path (its kernel reads pinned host memory)
                       "scalar_h2d_GBps": round(32 * n / (h2d * 1e-3) / 1e9, 2) if h2d > 0 else None,
                       "matches": bool(np.array_equal(np.asarray(got), np.asarray(want)))}
+    ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, -1)
     # the prover's commit of many polynomials: K MSMs per call
     # (pm_msm_resident_batch), the scalar copy of MSM j+1 and the host tail of
     # MSM j-1 overlapping MSM j's kernels

@@ -943,7 +943,8 @@ int vk_repr_impl(const uint8_t digest[64], uint64_t out[4]) {
                                            size_t, uint32_t, uint64_t*);                             \
   template int transcript_device_impl<Cv>(Ctx*, const pm_proof_shape*, size_t, const uint64_t*, const void*, \
                                           const void*, void*, void*);                            \
-  template int msm_start_impl<Cv>(Ctx*, const pm_fixed_bases*, const void*, const void*, size_t, uint32_t, void*); \
+  template int msm_start_impl<Cv>(Ctx*, const pm_fixed_bases*, const void*, const void*, size_t, uint32_t, void*, \
+                                  const void*); \
   template int msm_finish_impl<Cv>(Ctx*, const void*, uint64_t*);                                \
   template int msm_small_impl<Cv>(Ctx*, const void*, bool, const void*, bool, bool, size_t, uint32_t, uint64_t*); \
   template int many_table_impl<Cv>(Ctx*, const void*, size_t, ManyTable*);                       \

@@ -460,6 +460,19 @@ int pm_ctx_set_accum_option(pm_ctx* ctx, int option, int value) {
   }
 }
 
+int pm_ctx_set_msm_option(pm_ctx* ctx, int option, int value) {
+  if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  switch (option) {
+    case PM_MSM_OPT_SPLIT_COPY:
+      if (value < -1 || value > 0) return set_error(PM_ERR_ARG, "msm option value out of range (-1 auto, 0 off)");
+      ctx->msm_split_copy = value;
+      return PM_OK;
+    default:
+      return set_error(PM_ERR_ARG, "unknown msm option");
+  }
+}
+
 int pm_ctx_set_window(pm_ctx* ctx, int c) {
   if (!ctx) return set_error(PM_ERR_ARG, "null ctx");
   if (c != 0 && (c < kMinC || c > kMaxC)) return set_error(PM_ERR_ARG, "window width out of range");
@@ -697,7 +710,7 @@ static int msm_resident(pm_ctx* ctx, const pm_bases* b, size_t offset, const voi
   int rc = ctx->begin_call();
   if (rc) return rc;
   const void* d_s = scalars;
-  if (host) {  // the copy is chunked behind the histogram pass (msm_device_impl)
+  if (host) {  // copied by msm_device_impl (in two parts with a row table)
     if ((rc = ctx->in_scalars.ensure(n * 32))) return rc;
     d_s = ctx->in_scalars.p;
   }
@@ -1013,13 +1026,17 @@ static int dropin_msm(Ctx* ctx, int curve, const uint64_t* scalars, const uint64
   const bool threaded = pool.size() > 1;
   const auto t0 = std::chrono::steady_clock::now();
   if (threaded) pool.start(pool.size(), job);
-  const int copy_rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream);
-  const auto t1 = std::chrono::steady_clock::now();
+  // with a predicted set the MSM copies the scalars itself (a row table's
+  // MSM in two parts, the first part's sort and accumulation beside the
+  // second part's copy: engine.hpp); else one copy here
   alignas(16) unsigned char tail[pm::kTailBytes];
-  int spec_rc = -1;
-  if (spec && !copy_rc)
+  int spec_rc = -1, copy_rc = 0;
+  if (spec)
     spec_rc = curve_ops(curve)->msm_start(ctx, resident_use_table(spec, 0, n) ? spec->table : nullptr, spec->d,
-                                          ctx->in_scalars.p, n, flags, tail);
+                                          ctx->in_scalars.p, n, flags, tail, scalars);
+  else
+    copy_rc = ctx->upload_h2d(ctx->in_scalars.p, scalars, n * 32, ctx->stream);
+  const auto t1 = std::chrono::steady_clock::now();
   if (threaded) pool.wait();
   else job(1, 1);
   if (copy_rc) return copy_rc;

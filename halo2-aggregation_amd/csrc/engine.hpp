@@ -144,59 +144,33 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   const hipStream_t st = ctx->stream;
   const int kmerge = fixed ? ft->rows : 1;
   const int Wr = pl.W / kmerge;                     // bucket sets (reduced windows)
-  const size_t stride = fixed ? ft->npad : n;       // digit row length
-  const size_t E = (size_t)kmerge * stride;         // entries of one sort row
   const size_t TOT = (size_t)Wr * pl.NB + 1;
-  const size_t nW = (size_t)stride * pl.W;
   const int NJ = pl.NB2 + kTJobs;                   // bit-sum jobs per set
   const int NQ = NJ + 1;                            // host terms per set
-  SortGeom g{};  // histogram geometry (blocks of scalars)
-  g.FB = std::max(0, pl.cmax - 1 - 8);
-  // the fixed-base MSM's merged sort rows are W x longer: 4x more coarse bins
-  // once they exceed 2^24 entries (2^23, c = 20: FB 11 -> 9, sort 3.4 -> 2.3 ms)
-  if (fixed && E > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
-  g.NCB = (pl.K >> g.FB) + 1;
-  // points per thread: blocks of 1024 threads x ppt points, ppt the largest
-  // power of two <= 8 that still gives >= 128 blocks (2^20: 8192 points per
-  // block; larger blocks give longer contiguous runs per coarse bin in
-  // k_sort_coarse and a 4x smaller block histogram to scan: sort 0.19 ->
-  // 0.16 ms at 2^20; small n keeps enough blocks)
-  g.ppt = 1;
-  while (g.ppt < kSortPerThread && stride >= (size_t)256 * g.ppt * kSortThreads) g.ppt *= 2;
-  g.nblk = (int)((stride + (size_t)g.ppt * kSortThreads - 1) / ((size_t)g.ppt * kSortThreads));
-  // The histogram pass is compute-bound per block (Montgomery -> canonical,
-  // W signed digits and LDS atomics per scalar); with 8192-point blocks 2^20
-  // gives 128 blocks for 256 CUs.  Split each coarse block's points over 2
-  // histogram blocks when the grid is short of the CUs: the coarse pass keeps
-  // its long runs and reads its start offsets at every hsub-th histogram
-  // block.  The scan doubles with it, so one split only (same box, 2^20:
-  // histogram 0.049-0.050 -> 0.035-0.041 ms, scan 0.014 -> 0.019 ms; below
-  // 128 blocks the scan's growth cancels the gain: 2^19 +-0, 2^18 +3-5 us,
-  // profiles/r02/hs/ab.txt and profiles/r02/p/ab.txt).
-  int hsub = 1;
-  if (g.ppt >= 2 && g.nblk >= 128 && g.nblk < 256) hsub = 2;
-  g.hsub = 1;
-  SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
-  g.ppt /= hsub;    // histogram geometry
-  g.nblk *= hsub;
-  gm.nblk = g.nblk * kmerge;
-  gm.hsub = hsub;
-  const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
-  // 4-B coarse entries when the entry index fits beside the fine bits and the sign
-  const bool wide = E > (size_t(1) << (31 - g.FB));
   const bool d16 = pl.cmax <= 16;
+  // Split scalar copy (round 6): a row-table MSM with scalars in host memory
+  // sorts and accumulates a first part of its points while the rest of the
+  // scalars cross PCIe.  A pageable hipMemcpyAsync blocks the calling thread
+  // for the whole copy but overlaps kernels on other streams
+  // (tools/h2d_overlap.hip: 32 MB in 0.60 ms, 2 x 16 MB 0.62, a 0.45 ms kernel
+  // meanwhile hidden), so: copy part 0 on the context stream (blocks), queue
+  // its sort and accumulation there, copy part 1 on the copy stream (blocks
+  // while part 0 runs), then queue part 1's sort and accumulation on the
+  // context stream behind an event of that copy, and one bucket reduction
+  // over both sorted lists (k_bucket_seg_q<F, 2>).  Part 1's kernels stay on
+  // the context stream: beside part 0's accumulation on a queue of their own
+  // they only slowed it (sort 0.10 -> 0.27 ms, accumulation 0.49 -> 0.52,
+  // same end; rocprofv3 trace, round 6).  Each part is sorted as a table of
+  // its own points (digit rows of its padded length) and k_sort_coarse
+  // writes the full table's indices.
+  const int nch = fixed && h_scalars && ctx->msm_split_copy != 0 && n >= kSplitCopyMinN ? 2 : 1;
+  // The first part is 3/8 of the points: its copy is the exposed one, and the
+  // second part's copy (5/8) still ends before the first part's sort and
+  // accumulation do (2^20 with host scalars: 1/2 1.61 ms, 5/16 1.57-1.58,
+  // 3/8 1.57, 7/16 1.64; 2^22: 3/8 5.68 ms, 1/2 6.00 ms, one copy 7.3-7.4;
+  // profiles/r06/split_copy_ab.jsonl)
+  const size_t part0 = nch == 2 ? (n * 3 / 8 + kSortB - 1) / kSortB * kSortB : n;
   int rc;
-  if ((rc = ctx->digits.ensure(nW * (d16 ? 2 : 4)))) return rc;
-  if ((rc = ctx->sorted.ensure(nW * 4))) return rc;
-  if ((rc = ctx->mid.ensure(nW * (wide ? 8 : 4)))) return rc;
-  if ((rc = ctx->counts.ensure(TOTB * 4))) return rc;
-  if ((rc = ctx->cursor.ensure(TOTB * 4))) return rc;
-  if ((rc = ctx->offsets.ensure(TOT * 4))) return rc;
-  const ScanTiles tiles = scan_tiles((uint32_t)(pl.W * g.NCB), (uint32_t)g.nblk);  // k_sort_hist's layout
-  const uint32_t nb = (uint32_t)((TOTB + tiles.chunk - 1) / tiles.chunk);
-  if ((rc = ctx->bsum.ensure((size_t)nb * 4))) return rc;
-  if ((rc = ctx->buckets.ensure((size_t)Wr * pl.NB * sizeof(Xyzz<F>)))) return rc;
-  if ((rc = ctx->head.ensure((size_t)pl.nthreads * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segS.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segT.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->bitsQ.ensure((size_t)Wr * NQ * sizeof(Xyzz<F>)))) return rc;
@@ -204,15 +178,6 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   if ((rc = ctx->ensure_pinned(2 * nQ * sizeof(Xyzz<F>)))) return rc;  // two slots (batch pipelining)
   if ((rc = ctx->ensure_group_events(2))) return rc;
   Xyzz<F>* hslot = (Xyzz<F>*)ctx->h_pinned + (size_t)slot * nQ;
-
-  uint32_t* sorted = (uint32_t*)ctx->sorted.p;
-  void* mid = ctx->mid.p;
-  uint32_t* bh = (uint32_t*)ctx->counts.p;
-  uint32_t* bofs = (uint32_t*)ctx->cursor.p;
-  uint32_t* offsets = (uint32_t*)ctx->offsets.p;
-  uint32_t* bsum = (uint32_t*)ctx->bsum.p;
-  Xyzz<F>* buckets = (Xyzz<F>*)ctx->buckets.p;
-  Xyzz<F>* head = (Xyzz<F>*)ctx->head.p;
   Xyzz<F>* S = (Xyzz<F>*)ctx->segS.p;
   Xyzz<F>* T = (Xyzz<F>*)ctx->segT.p;
   // host terms: the reduction kernels store them straight into the pinned
@@ -223,7 +188,6 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   Xyzz<F>* Qd = (Xyzz<F>*)ctx->h_pinned_dev + (size_t)slot * nQ;
   const uint32_t un = (uint32_t)n;
 
-  g.clr_bh = bh + (TOTB - 1);  // zeroed by the histogram kernel's block 0
   // bases -> R261 once per MSM.  Running it on a second stream beside the
   // sort measured no faster: both are memory bound (bases 0.04 -> 0.07 ms,
   // histogram 0.048 -> 0.082 ms concurrently).
@@ -239,73 +203,181 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
               (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
   }
   const uint32_t canon = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
-  if (h_scalars) {
-    // one pageable copy on the context stream ahead of the histogram pass (a
-    // copy in 4 chunks, each chunk's histogram blocks launched behind it,
-    // measured ~0.1 ms slower per 2^20 MSM: round 3, profiles/r03/h2d/)
-    if ((rc = ctx->upload_h2d((void*)d_scalars, h_scalars, n * 32, st))) return rc;
+  SegChunk<F> co[2] = {};
+  if (nch == 2) {  // the copy stream starts behind everything queued on the context stream
+    if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    hipEvent_t ev0 = ctx->next_event();
+    if (!ev0) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+    HIP_TRY(hipEventRecord(ev0, st));
+    HIP_TRY(hipStreamWaitEvent(ctx->copy_stream, ev0, 0));
   }
-  PM_LAUNCH(ctx, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, d_scalars, un, canon, g, g.nblk, bh, ctx->digits.p,
-                                                   (uint32_t)stride, (uint32_t)kmerge, st));
-  if (rc) return rc;
-  PM_LAUNCH(ctx, "scan", {
-    k_scan_reduce<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, tiles, bsum);
-    k_scan_down<<<nb, kScanThreads, 0, st>>>(bh, (uint32_t)TOTB, tiles, bsum, bofs, nullptr);
-  });
-  {
-    const size_t lds = (size_t)gm.ppt * kSortThreads * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
-    const dim3 grid(gm.nblk / gm.hsub, Wr);
-    void* dg = ctx->digits.p;
-    const uint32_t ue = (uint32_t)E;
-    if (d16 && !wide)
-      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<true, false>(dg, ue, gm, bofs, mid, grid, lds, st));
-    else if (d16)
-      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<true, true>(dg, ue, gm, bofs, mid, grid, lds, st));
-    else if (!wide)
-      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<false, false>(dg, ue, gm, bofs, mid, grid, lds, st));
+  for (int ch = 0; ch < nch; ch++) {
+    const hipStream_t cs = st;
+    const size_t c0 = (size_t)ch * part0, nc = ch == nch - 1 ? n - c0 : part0;  // the last part takes the rest
+    // digit row length: n, the table's padded rows, or a part's own padded length
+    const size_t stride = !fixed ? n : nch == 2 ? std::max<size_t>(kSortB, (nc + kSortB - 1) / kSortB * kSortB)
+                                                : ft->npad;
+    const size_t E = (size_t)kmerge * stride;  // entries of one sort row
+    const size_t nW = (size_t)stride * pl.W;
+    SortGeom g{};  // histogram geometry (blocks of scalars)
+    g.FB = std::max(0, pl.cmax - 1 - 8);
+    // the fixed-base MSM's merged sort rows are W x longer: 4x more coarse bins
+    // once they exceed 2^24 entries (2^23, c = 20: FB 11 -> 9, sort 3.4 -> 2.3 ms)
+    if (fixed && E > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
+    g.NCB = (pl.K >> g.FB) + 1;
+    // points per thread: blocks of 1024 threads x ppt points, ppt the largest
+    // power of two <= 8 that still gives >= 128 blocks (2^20: 8192 points per
+    // block; larger blocks give longer contiguous runs per coarse bin in
+    // k_sort_coarse and a 4x smaller block histogram to scan: sort 0.19 ->
+    // 0.16 ms at 2^20; small n keeps enough blocks)
+    g.ppt = 1;
+    while (g.ppt < kSortPerThread && stride >= (size_t)256 * g.ppt * kSortThreads) g.ppt *= 2;
+    g.nblk = (int)((stride + (size_t)g.ppt * kSortThreads - 1) / ((size_t)g.ppt * kSortThreads));
+    // The histogram pass is compute-bound per block (Montgomery -> canonical,
+    // W signed digits and LDS atomics per scalar); with 8192-point blocks 2^20
+    // gives 128 blocks for 256 CUs.  Split each coarse block's points over 2
+    // histogram blocks when the grid is short of the CUs: the coarse pass keeps
+    // its long runs and reads its start offsets at every hsub-th histogram
+    // block.  The scan doubles with it, so one split only (same box, 2^20:
+    // histogram 0.049-0.050 -> 0.035-0.041 ms, scan 0.014 -> 0.019 ms; below
+    // 128 blocks the scan's growth cancels the gain: 2^19 +-0, 2^18 +3-5 us,
+    // profiles/r02/hs/ab.txt and profiles/r02/p/ab.txt).
+    int hsub = 1;
+    if (g.ppt >= 2 && g.nblk >= 128 && g.nblk < 256) hsub = 2;
+    g.hsub = 1;
+    SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
+    g.ppt /= hsub;    // histogram geometry
+    g.nblk *= hsub;
+    gm.nblk = g.nblk * kmerge;
+    gm.hsub = hsub;
+    // a part's entries carry table indices j npad + c0 + i (k_sort_coarse)
+    gm.rstride = (uint32_t)stride;
+    gm.rdelta = nch == 2 ? (uint32_t)(ft->npad - stride) : 0u;
+    gm.roff = nch == 2 ? (uint32_t)c0 : 0u;
+    const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
+    // 4-B coarse entries when the entry index fits beside the fine bits and the sign
+    const size_t imax = nch == 2 ? (size_t)kmerge * ft->npad : E;
+    const bool wide = imax > (size_t(1) << (31 - g.FB));
+    Buf& b_digits = ch ? ctx->digits2 : ctx->digits;
+    Buf& b_sorted = ch ? ctx->sorted2 : ctx->sorted;
+    Buf& b_mid = ch ? ctx->mid2 : ctx->mid;
+    Buf& b_counts = ch ? ctx->counts2 : ctx->counts;
+    Buf& b_cursor = ch ? ctx->cursor2 : ctx->cursor;
+    Buf& b_offsets = ch ? ctx->offsets2 : ctx->offsets;
+    Buf& b_bsum = ch ? ctx->bsum2 : ctx->bsum;
+    Buf& b_buckets = ch ? ctx->buckets2 : ctx->buckets;
+    Buf& b_head = ch ? ctx->head2 : ctx->head;
+    // accumulation lanes: each part's own plan (~4 waves per SIMD; a part's
+    // buckets reach as many slices as a full sort's).  The whole MSM's slice
+    // length instead (fewer lanes, shorter chains) measured the same with
+    // equal halves and 0.17 ms slower with a 3/8 first part (1.5 waves per
+    // SIMD in its accumulation)
+    const uint32_t chunk = nch == 2 ? make_plan_fixed(stride, ft->c, ctx->min_chunk).chunk : pl.chunk;
+    const uint32_t nthreads = nch == 2 ? (uint32_t)((nW + chunk - 1) / chunk) : pl.nthreads;
+    if ((rc = b_digits.ensure(nW * (d16 ? 2 : 4)))) return rc;
+    if ((rc = b_sorted.ensure(nW * 4))) return rc;
+    if ((rc = b_mid.ensure(nW * (wide ? 8 : 4)))) return rc;
+    if ((rc = b_counts.ensure(TOTB * 4))) return rc;
+    if ((rc = b_cursor.ensure(TOTB * 4))) return rc;
+    if ((rc = b_offsets.ensure(TOT * 4))) return rc;
+    const ScanTiles tiles = scan_tiles((uint32_t)(pl.W * g.NCB), (uint32_t)g.nblk);  // k_sort_hist's layout
+    const uint32_t nb = (uint32_t)((TOTB + tiles.chunk - 1) / tiles.chunk);
+    if ((rc = b_bsum.ensure((size_t)nb * 4))) return rc;
+    if ((rc = b_buckets.ensure((size_t)Wr * pl.NB * sizeof(Xyzz<F>)))) return rc;
+    if ((rc = b_head.ensure((size_t)nthreads * sizeof(Xyzz<F>)))) return rc;
+
+    uint32_t* sorted = (uint32_t*)b_sorted.p;
+    void* mid = b_mid.p;
+    uint32_t* bh = (uint32_t*)b_counts.p;
+    uint32_t* bofs = (uint32_t*)b_cursor.p;
+    uint32_t* offsets = (uint32_t*)b_offsets.p;
+    uint32_t* bsum = (uint32_t*)b_bsum.p;
+    Xyzz<F>* buckets = (Xyzz<F>*)b_buckets.p;
+    Xyzz<F>* head = (Xyzz<F>*)b_head.p;
+    g.clr_bh = bh + (TOTB - 1);  // zeroed by the histogram kernel's block 0
+    const uint32_t* sc = d_scalars + 8 * c0;
+    const uint32_t unc = (uint32_t)nc;
+    if (h_scalars) {
+      // one pageable copy ahead of this part's histogram pass (without the
+      // split: a copy in 4 chunks, each chunk's histogram blocks launched
+      // behind it, measured ~0.1 ms slower per 2^20 MSM: round 3,
+      // profiles/r03/h2d/)
+      const hipStream_t xs = ch == 0 ? st : ctx->copy_stream;
+      if ((rc = ctx->upload_h2d((void*)sc, (const uint8_t*)h_scalars + 32 * c0, nc * 32, xs))) return rc;
+      if (ch > 0) {
+        hipEvent_t evc = ctx->next_event();
+        if (!evc) return set_error(PM_ERR_HIP, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(evc, xs));
+        HIP_TRY(hipStreamWaitEvent(st, evc, 0));
+      }
+    }
+    PM_LAUNCH_ST(ctx, cs, "sort_hist", rc = launch_sort<Fs>(pl.W, d16, sc, unc, canon, g, g.nblk, bh, b_digits.p,
+                                                            (uint32_t)stride, (uint32_t)kmerge, cs));
+    if (rc) return rc;
+    PM_LAUNCH_ST(ctx, cs, "scan", {
+      k_scan_reduce<<<nb, kScanThreads, 0, cs>>>(bh, (uint32_t)TOTB, tiles, bsum);
+      k_scan_down<<<nb, kScanThreads, 0, cs>>>(bh, (uint32_t)TOTB, tiles, bsum, bofs, nullptr);
+    });
+    {
+      const size_t lds = (size_t)gm.ppt * kSortThreads * ((wide ? 8 : 4) + 2) + (size_t)(2 * g.NCB + 1) * 4 + (kSortThreads / 64 + 1) * 4;
+      const dim3 grid(gm.nblk / gm.hsub, Wr);
+      void* dg = b_digits.p;
+      const uint32_t ue = (uint32_t)E;
+      if (d16 && !wide)
+        PM_LAUNCH_ST(ctx, cs, "sort_coarse", launch_coarse<true, false>(dg, ue, gm, bofs, mid, grid, lds, cs));
+      else if (d16)
+        PM_LAUNCH_ST(ctx, cs, "sort_coarse", launch_coarse<true, true>(dg, ue, gm, bofs, mid, grid, lds, cs));
+      else if (!wide)
+        PM_LAUNCH_ST(ctx, cs, "sort_coarse", launch_coarse<false, false>(dg, ue, gm, bofs, mid, grid, lds, cs));
+      else
+        PM_LAUNCH_ST(ctx, cs, "sort_coarse", launch_coarse<false, true>(dg, ue, gm, bofs, mid, grid, lds, cs));
+    }
+    // fine sort LDS: segment cache + chunk buffer (k_sort_fine).  A mean
+    // segment that fits 24 KiB is cached whole with room for 1.5x its size and
+    // sorted as one chunk; larger ones are re-read from mid in 32 KiB chunks
+    // (2 blocks per CU).  Sweep with 16-B loads (profiles/r03/sort_fine/): 16
+    // KiB chunks 2^20 0.065 / 2^22 0.233 ms, 24-32 KiB 0.056 / 0.210, 40-64 KiB
+    // (one block per CU) 0.064-0.074 / 0.256-0.288; the whole segment cached in
+    // LDS (64-136 KiB) 0.069-0.107 / 0.34-0.44.  PM_FINE_CACHE_KB /
+    // PM_FINE_CHUNK_KB override both (A/B).
+    const size_t esz = wide ? 8 : 4;
+    const size_t mean_seg = E / std::max(1, g.NCB - 1) + 1;
+    const size_t fine_fixed = ((size_t)3 * (1 << g.FB) + kFineThreads / 64 + 1) * 4;  // hist, lcur, lst, scan
+    size_t cache_n = (mean_seg * 3 / 2 + 63) & ~size_t(63), chn;
+    if (cache_n * esz > 24576) cache_n = kFineChunkBytes / esz;
+    chn = cache_n;
+    if (ctx->fine_cache_kb > 0) cache_n = ((size_t)ctx->fine_cache_kb * 1024 / esz) & ~size_t(63);
+    if (ctx->fine_chunk_kb > 0) chn = ((size_t)ctx->fine_chunk_kb * 1024 / esz) & ~size_t(63);
+    chn = std::max<size_t>(64, std::min(chn, cache_n));
+    cache_n = std::max(cache_n, chn);
+    if (fine_fixed + 128 * esz > kMaxLds) return set_error(PM_ERR_UNSUPPORTED, "sort: fine bits too wide");
+    while (cache_n > 64 && (cache_n + chn) * esz + fine_fixed > kMaxLds) {
+      cache_n /= 2;
+      chn = std::min(chn, cache_n);
+    }
+    const size_t lds_fine = (cache_n + chn) * esz + fine_fixed;
+    if (wide)
+      PM_LAUNCH_ST(ctx, cs, "sort_fine", (k_sort_fine<true><<<Wr * g.NCB, kFineThreads, lds_fine, cs>>>(
+                                            (const uint64_t*)mid, bofs, gm, Wr, pl.NB, (uint32_t)cache_n, (uint32_t)chn,
+                                            offsets, sorted)));
     else
-      PM_LAUNCH(ctx, "sort_coarse", launch_coarse<false, true>(dg, ue, gm, bofs, mid, grid, lds, st));
+      PM_LAUNCH_ST(ctx, cs, "sort_fine", (k_sort_fine<false><<<Wr * g.NCB, kFineThreads, lds_fine, cs>>>(
+                                            (const uint32_t*)mid, bofs, gm, Wr, pl.NB, (uint32_t)cache_n, (uint32_t)chn,
+                                            offsets, sorted)));
+    const uint32_t s1 = (uint32_t)((size_t)Wr * pl.NB);
+    PM_LAUNCH_ST(ctx, cs, "accumulate",
+                 (k_accumulate<F><<<(nthreads + 255) / 256, 256, 0, cs>>>(sorted, offsets, s1, bases29, chunk,
+                                                                          buckets, head)));
+    co[ch] = SegChunk<F>{offsets, chunk, nthreads, buckets, head};
   }
-  // fine sort LDS: segment cache + chunk buffer (k_sort_fine).  A mean
-  // segment that fits 24 KiB is cached whole with room for 1.5x its size and
-  // sorted as one chunk; larger ones are re-read from mid in 32 KiB chunks
-  // (2 blocks per CU).  Sweep with 16-B loads (profiles/r03/sort_fine/): 16
-  // KiB chunks 2^20 0.065 / 2^22 0.233 ms, 24-32 KiB 0.056 / 0.210, 40-64 KiB
-  // (one block per CU) 0.064-0.074 / 0.256-0.288; the whole segment cached in
-  // LDS (64-136 KiB) 0.069-0.107 / 0.34-0.44.  PM_FINE_CACHE_KB /
-  // PM_FINE_CHUNK_KB override both (A/B).
-  const size_t esz = wide ? 8 : 4;
-  const size_t mean_seg = E / std::max(1, g.NCB - 1) + 1;
-  const size_t fine_fixed = ((size_t)3 * (1 << g.FB) + kFineThreads / 64 + 1) * 4;  // hist, lcur, lst, scan
-  size_t cache_n = (mean_seg * 3 / 2 + 63) & ~size_t(63), ch;
-  if (cache_n * esz > 24576) cache_n = kFineChunkBytes / esz;
-  ch = cache_n;
-  if (ctx->fine_cache_kb > 0) cache_n = ((size_t)ctx->fine_cache_kb * 1024 / esz) & ~size_t(63);
-  if (ctx->fine_chunk_kb > 0) ch = ((size_t)ctx->fine_chunk_kb * 1024 / esz) & ~size_t(63);
-  ch = std::max<size_t>(64, std::min(ch, cache_n));
-  cache_n = std::max(cache_n, ch);
-  if (fine_fixed + 128 * esz > kMaxLds) return set_error(PM_ERR_UNSUPPORTED, "sort: fine bits too wide");
-  while (cache_n > 64 && (cache_n + ch) * esz + fine_fixed > kMaxLds) {
-    cache_n /= 2;
-    ch = std::min(ch, cache_n);
-  }
-  const size_t lds_fine = (cache_n + ch) * esz + fine_fixed;
-  if (wide)
-    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<true><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
-                                    (const uint64_t*)mid, bofs, gm, Wr, pl.NB, (uint32_t)cache_n, (uint32_t)ch,
-                                    offsets, sorted)));
-  else
-    PM_LAUNCH(ctx, "sort_fine", (k_sort_fine<false><<<Wr * g.NCB, kFineThreads, lds_fine, st>>>(
-                                    (const uint32_t*)mid, bofs, gm, Wr, pl.NB, (uint32_t)cache_n, (uint32_t)ch,
-                                    offsets, sorted)));
-  const uint32_t s1 = (uint32_t)((size_t)Wr * pl.NB);
-  PM_LAUNCH(ctx, "accumulate",
-            (k_accumulate<F><<<(pl.nthreads + 255) / 256, 256, 0, st>>>(sorted, offsets, s1, bases29, pl.chunk,
-                                                                        buckets, head)));
   // chains (long ones wave-cooperatively) + segment sums + the top bucket
-  PM_LAUNCH(ctx, "bucket_seg",
-            (k_bucket_seg_q<F><<<(unsigned)((4ull * Wr * pl.M1 + 255) / 256), 256, 0, st>>>(
-                offsets, pl.chunk, pl.nthreads, buckets, head, Wr, pl.NB, (uint32_t)pl.M1, S, T, Qd, NQ)));
+  const unsigned seg_blocks = (unsigned)((4ull * Wr * pl.M1 + 255) / 256);
+  if (nch == 2)
+    PM_LAUNCH(ctx, "bucket_seg", (k_bucket_seg_q<F, 2><<<seg_blocks, 256, 0, st>>>(co[0], co[1], Wr, pl.NB,
+                                                                                   (uint32_t)pl.M1, S, T, Qd, NQ)));
+  else
+    PM_LAUNCH(ctx, "bucket_seg", (k_bucket_seg_q<F, 1><<<seg_blocks, 256, 0, st>>>(co[0], co[0], Wr, pl.NB,
+                                                                                   (uint32_t)pl.M1, S, T, Qd, NQ)));
   // bit sums of few sets (the row tables, the fixed-base MSM's one set) are
   // split over more blocks.  Every extra lane also adds one tree addition, so
   // the split stops at ~16 blocks per job (c = 20, 2^19 buckets: 16 -> 0.33
@@ -558,12 +630,12 @@ int msm_device_to_aff(Ctx* ctx, const void* d_s, const void* d_b, size_t n, uint
 // the two halves of a resident-bases MSM (CurveOps::msm_start / msm_finish)
 template <class Cv>
 int msm_start_impl(Ctx* ctx, const pm_fixed_bases* ft, const void* d_bases29, const void* d_s, size_t n,
-                   uint32_t flags, void* tail) {
+                   uint32_t flags, void* tail, const void* h_s) {
   using F = typename Cv::Base;
   static_assert(sizeof(MsmTail<F>) <= kTailBytes, "tail storage");
   MsmTail<F>* t = new (tail) MsmTail<F>();
   return msm_device_impl<Cv>(ctx, (const uint32_t*)d_s, (const uint32_t*)d_bases29, n,
-                             ft ? flags & ~kBasesR261 : flags | kBasesR261, nullptr, ft, t, 0, nullptr);
+                             ft ? flags & ~kBasesR261 : flags | kBasesR261, nullptr, ft, t, 0, h_s);
 }
 template <class Cv>
 int msm_finish_impl(Ctx* ctx, const void* tail, uint64_t out[8]) {

@@ -256,6 +256,10 @@ struct SortGeom {
   uint32_t* clr_longs;
   uint32_t clr_stride;  // words between group headers
   int clr_groups;
+  // entry index remap of k_sort_coarse (a part of a row table's points, the
+  // split scalar copy): sort-row entry e = j rstride + i -> table index
+  // e + j rdelta + roff (= j npad + c0 + i); rdelta = roff = 0: e itself
+  uint32_t rstride, rdelta, roff;
 };
 
 // signed digit of window w (WinGeom), carry in/out; returns |d| | neg << 31
@@ -442,6 +446,8 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename Dig
   uint32_t* lstart = cnt + g.NCB;                                            // NCB + 1
   uint32_t* scan_tmp = lstart + g.NCB + 1;                                   // kSortThreads/64 + 1
   const uint32_t w = blockIdx.y, blk = blockIdx.x;
+  // the block's entries lie in one digit row j (sortb divides rstride)
+  const uint32_t remap = (g.rdelta | g.roff) ? blk * sortb / g.rstride * g.rdelta + g.roff : 0u;
   for (int k = threadIdx.x; k < g.NCB; k += kSortThreads) cnt[k] = 0;
   __syncthreads();
   const DT* row = digits + (size_t)w * n;
@@ -479,7 +485,7 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_coarse(const typename Dig
     const uint32_t slot = code[r] & ~kNegBit;
     const uint32_t cb = slot >> g.FB;
     const uint32_t pos = atomicAdd(&cnt[cb], 1u);
-    stage[pos] = E::make(slot, i0 + r, code[r] >> 31, g.FB);
+    stage[pos] = E::make(slot, i0 + r + remap, code[r] >> 31, g.FB);
     stage_cb[pos] = (uint16_t)cb;
   }
   __syncthreads();
@@ -856,29 +862,30 @@ __device__ __forceinline__ void store_r256_q(Xyzz<F>* dst, const Xyzz29<F>& p, u
 // whatever slot 0 holds has weight 0: S_0 enters no bit sum, T_0 weighs lane 0
 // by 0); that quad converts it and stores it as the set's last host term,
 // Q[w * NQ + NQ - 1].
+// One sorted list's share of a bucket (the split scalar copy sorts and
+// accumulates two parts of the points separately, engine.hpp): its partial in
+// buckets[slot] when the bucket has entries in that list, plus the chain
+// head[t_first + 1 .. t_last] of the later slices it reaches.
 template <class F>
-__global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restrict__ offsets, uint32_t chunk,
-                                                      uint32_t nthreads, const Xyzz<F>* __restrict__ buckets,
-                                                      const Xyzz<F>* __restrict__ head, int Wr, int NB,
-                                                      uint32_t M1, Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T,
-                                                      Xyzz<F>* __restrict__ Q, int NQ) {
-  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t g = gl >> 2, q = gl & 3u;
-  // lanes past the last segment stay (inactive values) for the wave-wide fold
-  const bool valid = g < (uint32_t)Wr * M1;
-  const uint32_t w = valid ? g / M1 : 0u, j = valid ? g - w * M1 : 1u;
-  const bool top = valid && j == 0 && q == 0;
-  const size_t slot = (size_t)w * NB + (top ? M1 * kSegQ : j * kSegQ + q);
-  const uint32_t base = offsets[0];
-  const uint32_t bs = valid ? offsets[slot] : 0u, be = valid ? offsets[slot + 1] : 0u;
-  Xyzz29<F> B = xyzz29_inf<F>();
+struct SegChunk {
+  const uint32_t* offsets;
+  uint32_t chunk, nthreads;
+  const Xyzz<F>* buckets;
+  const Xyzz<F>* head;
+};
+// adds chunk c's share of bucket `slot` to B (first: B is still empty)
+template <class F, bool FIRST>
+__device__ __forceinline__ void seg_fold_chunk(const SegChunk<F>& c, bool valid, size_t slot, Xyzz29<F>& B) {
+  const uint32_t base = c.offsets[0];
+  const uint32_t bs = valid ? c.offsets[slot] : 0u, be = valid ? c.offsets[slot + 1] : 0u;
   uint32_t tf = 0, tl = 0;
   if (bs != be) {
-    B = load_xyzz29<F>(&buckets[slot]);
-    tf = (bs - base) / chunk;
-    tl = min((be - 1 - base) / chunk, nthreads - 1);
+    const Xyzz29<F> b0 = load_xyzz29<F>(&c.buckets[slot]);
+    B = FIRST ? b0 : xyzz29_add<F>(B, b0);
+    tf = (bs - base) / c.chunk;
+    tl = min((be - 1 - base) / c.chunk, c.nthreads - 1);
     if (tl - tf <= kSerialChain)
-      for (uint32_t t = tf + 1; t <= tl; t++) B = xyzz29_add<F>(B, load_xyzz29<F>(&head[t]));
+      for (uint32_t t = tf + 1; t <= tl; t++) B = xyzz29_add<F>(B, load_xyzz29<F>(&c.head[t]));
   }
   // giant buckets: the wave folds each long chain in turn (wave-uniform loop)
   uint64_t lm = __ballot(tl - tf > kSerialChain);
@@ -895,7 +902,7 @@ __global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restr
     for (uint64_t r = lm; r; r &= r - 1) coop += (mx + 63) / 64 + 6;
     if (mx <= kSerialChain + coop) {
       if (tl - tf > kSerialChain)
-        for (uint32_t t = tf + 1; t <= tl; t++) B = xyzz29_add<F>(B, load_xyzz29<F>(&head[t]));
+        for (uint32_t t = tf + 1; t <= tl; t++) B = xyzz29_add<F>(B, load_xyzz29<F>(&c.head[t]));
       lm = 0;
     }
   }
@@ -903,12 +910,29 @@ __global__ void __launch_bounds__(256, 2) k_bucket_seg_q(const uint32_t* __restr
     const int L = __ffsll((unsigned long long)lm) - 1;
     lm &= lm - 1;
     const uint32_t a = (uint32_t)__shfl((int)tf, L, 64) + 1u, z = (uint32_t)__shfl((int)tl, L, 64);
-    Xyzz29<F> c = xyzz29_inf<F>();
-    for (uint32_t t = a + ln; t <= z; t += 64) c = xyzz29_add<F>(c, load_xyzz29<F>(&head[t]));
+    Xyzz29<F> cs = xyzz29_inf<F>();
+    for (uint32_t t = a + ln; t <= z; t += 64) cs = xyzz29_add<F>(cs, load_xyzz29<F>(&c.head[t]));
 #pragma unroll 1
-    for (int m = 32; m > 0; m >>= 1) c = xyzz29_add<F>(c, xyzz29_shfl_xor<F>(c, m));
-    if (ln == (uint32_t)L) B = xyzz29_add<F>(B, c);
+    for (int m = 32; m > 0; m >>= 1) cs = xyzz29_add<F>(cs, xyzz29_shfl_xor<F>(cs, m));
+    if (ln == (uint32_t)L) B = xyzz29_add<F>(B, cs);
   }
+}
+// NCH = 2: the bucket sums of the split copy's two sorted lists (c2 unused
+// with NCH = 1)
+template <class F, int NCH>
+__global__ void __launch_bounds__(256, 2) k_bucket_seg_q(SegChunk<F> c1, SegChunk<F> c2, int Wr, int NB,
+                                                      uint32_t M1, Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T,
+                                                      Xyzz<F>* __restrict__ Q, int NQ) {
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = gl >> 2, q = gl & 3u;
+  // lanes past the last segment stay (inactive values) for the wave-wide fold
+  const bool valid = g < (uint32_t)Wr * M1;
+  const uint32_t w = valid ? g / M1 : 0u, j = valid ? g - w * M1 : 1u;
+  const bool top = valid && j == 0 && q == 0;
+  const size_t slot = (size_t)w * NB + (top ? M1 * kSegQ : j * kSegQ + q);
+  Xyzz29<F> B = xyzz29_inf<F>();
+  seg_fold_chunk<F, true>(c1, valid, slot, B);
+  if constexpr (NCH == 2) seg_fold_chunk<F, false>(c2, valid, slot, B);
   // broadcast each lane's sum only when it is consumed (fewer live points)
   const Xyzz29<F> B3 = xyzz29_qbc<3, F>(B);
   const Xyzz29<F> p23 = xyzz29_add_q<F>(xyzz29_qbc<2, F>(B), B3);

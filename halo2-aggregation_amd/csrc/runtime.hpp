@@ -46,6 +46,8 @@ constexpr int kBitsSplitK = 16;
 // kDropinMinN points are kept resident, keyed by a content digest; at most
 // kDropinEntries sets and kDropinBytes of device memory per context
 constexpr size_t kDropinMinN = size_t(1) << 12;
+// the split scalar copy of row-table MSMs with host scalars (engine.hpp)
+constexpr size_t kSplitCopyMinN = PM_SPLIT_COPY_MIN_N;
 constexpr int kDropinEntries = 4;
 constexpr size_t kDropinBytes = size_t(16) << 30;
 // ... and at most this fraction (1/kDropinFreeDiv) of the device memory free
@@ -210,7 +212,9 @@ struct pm_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t red_stream = nullptr;  // accumulator side stream (accum_engine.hpp)
-  hipStream_t copy_stream = nullptr; // pm_msm_resident_batch: H2D of the next MSM's scalars
+  // H2D copies beside the context stream's kernels: pm_msm_resident_batch (the
+  // next MSM's scalars), the split scalar copy's second half (engine.hpp)
+  hipStream_t copy_stream = nullptr;
   pm::HostPool* pool = nullptr;      // lazily created (drop-in digest)
   std::vector<pm::DropinEntry> dropin;  // drop-in base cache (pm_msm / pm_msm_ctx)
   std::vector<pm::DropinEntry> dropin_seen;  // digests seen once (b == nullptr), admitted on the second sighting
@@ -239,6 +243,8 @@ struct pm_ctx {
   // the stream of the term additions / sums (0 main), the one-lane form's
   // terms per lane (1, 2), the streamed transcript replay (0: per record)
   int acc_twist = -1, acc_tail = -1, acc_tpl = -1, acc_tr_stream = -1;
+  // pm_ctx_set_msm_option(PM_MSM_OPT_SPLIT_COPY): -1 auto, 0 one scalar copy
+  int msm_split_copy = -1;
   // the device's CU count (hipDeviceAttributeMultiprocessorCount, 256 on an
   // MI355X): the one-block-per-CU fences of the latency-bound accumulator
   // kernels are sized against it (pm_ctx_create refuses a device with less
@@ -252,6 +258,8 @@ struct pm_ctx {
   pm::Buf in_scalars, in_scalars2, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
       win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, acc_corr, tr_canon, ntt_scratch2,
       acc_vkpow, small_tab, small_dig, small_part, small_tk;
+  // the second part's sort / accumulation buffers of the split scalar copy (engine.hpp)
+  pm::Buf digits2, sorted2, counts2, offsets2, cursor2, bsum2, buckets2, head2, mid2;
   pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
   pm::CachedUpload tr_wtab;  // streamed transcript: word table of the shape's byte stream
   pm::CachedUpload many_prog;  // pm_msm_resident_many*: job + MSM tables
@@ -287,7 +295,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &acc_corr, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &pf_flags, &small_tab, &small_dig, &small_part, &small_tk, &many_prog.buf, &tr_wtab.buf};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &acc_corr, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &pf_flags, &small_tab, &small_dig, &small_part, &small_tk, &many_prog.buf, &tr_wtab.buf, &digits2, &sorted2, &counts2, &offsets2, &cursor2, &bsum2, &buckets2, &head2, &mid2};
   }
   ~pm_ctx();
   int begin_call();
@@ -344,9 +352,11 @@ struct CurveOps {
   // resident-bases MSM in two halves (the drop-in cache's speculative start):
   // msm_start enqueues the device pipeline on ctx->stream (ft: the row table,
   // else d_bases29 in the R = 2^261 form) and fills the opaque tail;
-  // msm_finish waits for it and runs the host Horner
+  // msm_finish waits for it and runs the host Horner.  h_scalars != nullptr:
+  // the scalars are still in host memory and are copied to d_scalars first
+  // (in two halves beside the pipeline with a row table: engine.hpp)
   int (*msm_start)(Ctx* ctx, const pm_fixed_bases* ft, const void* d_bases29, const void* d_scalars, size_t n,
-                   uint32_t flags, void* tail);
+                   uint32_t flags, void* tail, const void* h_scalars);
   int (*msm_finish)(Ctx* ctx, const void* tail, uint64_t out[8]);
   // small-MSM path (msm_small.hpp); s_host / b_host: the input is in host
   // memory; b_r261: bases in the resident R = 2^261 form

@@ -26,6 +26,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "pasta_msm.h")
 
 PALLAS, VESTA, BN254 = 0, 1, 2
 ACC_OPT_TWIST, ACC_OPT_TAIL_STREAM, ACC_OPT_TERMS_PER_LANE, ACC_OPT_TRANSCRIPT = 1, 2, 3, 4  # pm_ctx_set_accum_option
+MSM_OPT_SPLIT_COPY = 1  # pm_ctx_set_msm_option
+SPLIT_COPY_MIN_N = 262144  # PM_SPLIT_COPY_MIN_N
 SCALARS_CANONICAL = 1
 LEGACY_STREAM = 1  # PM_STREAM_LEGACY: the HIP legacy null stream
 # PM_MSM_GPU_MIN_N: below this many terms the Rust shim would keep halo2's CPU
@@ -227,6 +229,7 @@ def _load():
         "pm_ctx_set_accum_split": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_ladder": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_accum_option": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pm_ctx_set_msm_option": ([_vp, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_glv": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing": ([_vp, ctypes.c_int], ctypes.c_int),
         "pm_ctx_set_timing_filter": ([_vp, ctypes.c_char_p], ctypes.c_int),
@@ -588,6 +591,10 @@ class Context:
         """pm_ctx_set_accum_option: ACC_OPT_TWIST / _TAIL_STREAM / _TRANSCRIPT
         (0 off, -1 auto), ACC_OPT_TERMS_PER_LANE (1, 2, -1 auto)."""
         _check(lib().pm_ctx_set_accum_option(self.h, option, value))
+
+    def set_msm_option(self, option, value=-1):
+        """pm_ctx_set_msm_option: MSM_OPT_SPLIT_COPY (0 one scalar copy, -1 auto)."""
+        _check(lib().pm_ctx_set_msm_option(self.h, option, value))
 
     def set_accum_split(self, lg_lanes=-1):
         """Accumulator: 2^lg_lanes lanes (bit segments) per MSM term, 0..5 (-1 = automatic)."""

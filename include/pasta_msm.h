@@ -129,6 +129,19 @@ enum {
   PM_ACC_OPT_TRANSCRIPT = 4
 };
 int pm_ctx_set_accum_option(pm_ctx* ctx, int option, int value);
+/* MSM schedule options (round 6); value -1 = automatic (the default).
+ * Results never depend on them.
+ *   PM_MSM_OPT_SPLIT_COPY   0: one scalar copy.  Automatic: an MSM over a
+ *                           resident row table with scalars in host memory
+ *                           (pm_msm_resident, the drop-in pm_msm's warm
+ *                           calls) of at least PM_SPLIT_COPY_MIN_N points
+ *                           copies the scalars in two parts (3/8, 5/8) and
+ *                           sorts and accumulates the first while the second
+ *                           crosses PCIe.
+ * PM_ERR_ARG for an unknown option or a value out of range. */
+#define PM_SPLIT_COPY_MIN_N 262144
+enum { PM_MSM_OPT_SPLIT_COPY = 1 };
+int pm_ctx_set_msm_option(pm_ctx* ctx, int option, int value);
 /* Per-kernel HIP-event timing on the context stream (for bench/profiling).
  * Every event pair costs ~10 us of stream time on MI355X, so a timed region
  * should restrict events to the kernel it measures:

@@ -37,6 +37,7 @@ def test_null_arguments_rejected():
     assert L.pm_points_sum(0, p1, 1, None) == ARG
     assert L.pm_points_sum(9, p1, 1, po) == ARG
     assert L.pm_ctx_set_accum_option(None, 1, 0) == ARG
+    assert L.pm_ctx_set_msm_option(None, 1, 0) == ARG
     assert L.pm_bases_upload(None, 0, p1, 1, None) == ARG
     assert L.pm_msm_resident(None, None, 0, p1, 1, 0, po) == ARG
     assert L.pm_msm_resident_batch(None, None, 0, None, 1, 1, 0, po) == ARG

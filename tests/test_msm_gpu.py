@@ -442,6 +442,65 @@ def test_dropin_row_table(gpu_ctx):
         ctx.close()
 
 
+@pytest.mark.parametrize("curve", [0, 2])
+def test_split_scalar_copy(gpu_ctx, curve):
+    """Row-table MSMs with host scalars from PM_SPLIT_COPY_MIN_N points copy
+    the scalars in two parts (3/8, 5/8), each sorted and accumulated on its
+    own, with one bucket reduction over both sorted lists
+    (k_bucket_seg_q<F, 2>): ragged parts, lengths at and just above the
+    threshold, a giant bucket that spans both parts, the fixed-base MSM, and
+    the one-copy schedule (pm_ctx_set_msm_option MSM_OPT_SPLIT_COPY = 0) all
+    equal the device-input MSM."""
+    import torch
+
+    n = (1 << 19) + 8195
+    s, b = _torch_inputs(gpu_ctx, curve, n)
+    S = s.cpu().numpy().view(np.uint64).copy()
+    rb = gpu_ctx.upload_bases(curve, d_bases=b.data_ptr(), n=n)
+    try:
+        assert rb.rows > 1
+        for m in (n, (1 << 19) + 17, n - 8192):   # > n / 2: the row-table path
+            want = gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), m)
+            assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S[:m]), want), m
+            gpu_ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, 0)
+            try:
+                assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S[:m]), want), m
+            finally:
+                gpu_ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, -1)
+        # every scalar equal: one giant bucket per window, in both parts' lists
+        e = s[7:8].repeat(n, 1).contiguous()
+        torch.cuda.synchronize()
+        want = gpu_ctx.msm_resident_device(rb, 0, e.data_ptr(), n)
+        assert np.array_equal(gpu_ctx.msm_resident(rb, 0, e.cpu().numpy().view(np.uint64).copy()), want)
+    finally:
+        rb.release()
+    # at the threshold: a fresh table of exactly PM_SPLIT_COPY_MIN_N (+ 1) points
+    for m in (H.SPLIT_COPY_MIN_N, H.SPLIT_COPY_MIN_N + 1):
+        rb = gpu_ctx.upload_bases(curve, d_bases=b.data_ptr(), n=m)
+        try:
+            assert rb.rows > 1
+            want = gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), m)
+            assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S[:m]), want), m
+        finally:
+            rb.release()
+    # the fixed-base MSM (one merged bucket set) with host scalars
+    m = (1 << 18) + 5
+    fb = gpu_ctx.fixed_bases(curve, d_bases=b.data_ptr(), n=m)
+    try:
+        assert np.array_equal(fb.msm(S[:m]), gpu_ctx.msm_device(curve, s.data_ptr(), b.data_ptr(), m))
+    finally:
+        fb.release()
+
+
+def test_msm_option_arguments(gpu_ctx):
+    """pm_ctx_set_msm_option: -1 and 0 accepted, anything else refused."""
+    for v in (0, -1):
+        gpu_ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, v)
+    for opt, v in ((H.MSM_OPT_SPLIT_COPY, 1), (H.MSM_OPT_SPLIT_COPY, -2), (99, 0)):
+        with pytest.raises(H.PmError):
+            gpu_ctx.set_msm_option(opt, v)
+
+
 @pytest.mark.parametrize("logn,rows", [(20, 8), (22, 4)])
 def test_headline_path_vs_c_port(gpu_ctx, logn, rows):
     """The bench's exact headline path with default knobs: Pallas 2^20
