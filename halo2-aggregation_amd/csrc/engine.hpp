@@ -163,13 +163,25 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
   // same end; rocprofv3 trace, round 6).  Each part is sorted as a table of
   // its own points (digit rows of its padded length) and k_sort_coarse
   // writes the full table's indices.
-  const int nch = fixed && h_scalars && ctx->msm_split_copy != 0 && n >= kSplitCopyMinN ? 2 : 1;
-  // The first part is 3/8 of the points: its copy is the exposed one, and the
-  // second part's copy (5/8) still ends before the first part's sort and
-  // accumulation do (2^20 with host scalars: 1/2 1.61 ms, 5/16 1.57-1.58,
-  // 3/8 1.57, 7/16 1.64; 2^22: 3/8 5.68 ms, 1/2 6.00 ms, one copy 7.3-7.4;
-  // profiles/r06/split_copy_ab.jsonl)
-  const size_t part0 = nch == 2 ? (n * 3 / 8 + kSortB - 1) / kSortB * kSortB : n;
+  const int nch = fixed && h_scalars && ctx->msm_split_copy != 0 && n >= kSplitCopyMinN
+                      ? (n >= kSplitCopy3MinN ? 3 : 2) : 1;
+  // Two parts: the first is 3/8 of the points -- its copy is the exposed one,
+  // and the second part's copy (5/8) still ends before the first part's sort
+  // and accumulation do (2^20 with host scalars: 1/2 1.61 ms, 5/16
+  // 1.57-1.58, 3/8 1.57, 7/16 1.64; 2^22: 3/8 5.68 ms, 1/2 6.00 ms, one copy
+  // 7.3-7.4).  Three parts (1/4, 3/8, 3/8) from kSplitCopy3MinN points: the
+  // exposed copy shrinks with n while each extra part costs a fixed sort
+  // (~0.04 ms) and chain fold (2^20: 1.64-1.68 ms against 1.59-1.62 with two;
+  // 2^22: 5.25-5.32 against 5.63-5.66; profiles/r06/split_copy_ab.jsonl)
+  // part starts (multiples of kSortB): two parts 3/8 + 5/8, three 1/4 + 3/8 + 3/8
+  size_t pstart[kMaxParts + 1] = {0, n, n, n};
+  auto rnd = [](size_t v) { return (v + kSortB - 1) / kSortB * kSortB; };
+  if (nch == 2) pstart[1] = rnd(n * 3 / 8);
+  if (nch == 3) {
+    pstart[1] = rnd(n / 4);
+    pstart[2] = rnd(n * 5 / 8);
+  }
+  pstart[nch] = n;
   int rc;
   if ((rc = ctx->segS.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
   if ((rc = ctx->segT.ensure((size_t)Wr * pl.M1 * sizeof(Xyzz<F>)))) return rc;
@@ -203,27 +215,31 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
               (k_bases_to_r261<F><<<(un + 255) / 256, 256, 0, st>>>(d_bases, un, (uint32_t*)ctx->bases29.p)));
   }
   const uint32_t canon = (flags & PM_SCALARS_CANONICAL) ? 1u : 0u;
-  SegChunk<F> co[2] = {};
-  if (nch == 2) {  // the copy stream starts behind everything queued on the context stream
+  SegChunks<F> co = {};
+  if (nch > 1) {  // the copy stream starts behind everything queued on the context stream
     if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     hipEvent_t ev0 = ctx->next_event();
     if (!ev0) return set_error(PM_ERR_HIP, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(ev0, st));
     HIP_TRY(hipStreamWaitEvent(ctx->copy_stream, ev0, 0));
   }
-  for (int ch = 0; ch < nch; ch++) {
-    const hipStream_t cs = st;
-    const size_t c0 = (size_t)ch * part0, nc = ch == nch - 1 ? n - c0 : part0;  // the last part takes the rest
-    // digit row length: n, the table's padded rows, or a part's own padded length
-    const size_t stride = !fixed ? n : nch == 2 ? std::max<size_t>(kSortB, (nc + kSortB - 1) / kSortB * kSortB)
-                                                : ft->npad;
-    const size_t E = (size_t)kmerge * stride;  // entries of one sort row
-    const size_t nW = (size_t)stride * pl.W;
-    SortGeom g{};  // histogram geometry (blocks of scalars)
+  // sort geometry of a digit row length (the whole MSM's, or a part's)
+  struct PartGeom {
+    size_t E, nW, TOTB;
+    SortGeom g, gm;
+    ScanTiles tiles;
+    uint32_t nb;
+    bool wide;
+  };
+  auto geom = [&](size_t stride) {
+    PartGeom r{};
+    r.E = (size_t)kmerge * stride;  // entries of one sort row
+    r.nW = (size_t)stride * pl.W;
+    SortGeom& g = r.g;  // histogram geometry (blocks of scalars)
     g.FB = std::max(0, pl.cmax - 1 - 8);
     // the fixed-base MSM's merged sort rows are W x longer: 4x more coarse bins
     // once they exceed 2^24 entries (2^23, c = 20: FB 11 -> 9, sort 3.4 -> 2.3 ms)
-    if (fixed && E > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
+    if (fixed && r.E > (size_t(1) << 24)) g.FB = std::max(0, pl.cmax - 1 - 10);
     g.NCB = (pl.K >> g.FB) + 1;
     // points per thread: blocks of 1024 threads x ppt points, ppt the largest
     // power of two <= 8 that still gives >= 128 blocks (2^20: 8192 points per
@@ -245,44 +261,68 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     int hsub = 1;
     if (g.ppt >= 2 && g.nblk >= 128 && g.nblk < 256) hsub = 2;
     g.hsub = 1;
-    SortGeom gm = g;  // coarse / fine geometry (blocks of sort-row entries)
+    r.gm = g;         // coarse / fine geometry (blocks of sort-row entries)
     g.ppt /= hsub;    // histogram geometry
     g.nblk *= hsub;
-    gm.nblk = g.nblk * kmerge;
-    gm.hsub = hsub;
+    r.gm.nblk = g.nblk * kmerge;
+    r.gm.hsub = hsub;
+    r.TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
+    r.tiles = scan_tiles((uint32_t)(pl.W * g.NCB), (uint32_t)g.nblk);  // k_sort_hist's layout
+    r.nb = (uint32_t)((r.TOTB + r.tiles.chunk - 1) / r.tiles.chunk);
+    // 4-B coarse entries when the entry index fits beside the fine bits and
+    // the sign (a part's entries carry the full table's indices)
+    const size_t imax = nch > 1 ? (size_t)kmerge * ft->npad : r.E;
+    r.wide = imax > (size_t(1) << (31 - g.FB));
+    return r;
+  };
+  // digit row length: n, the table's padded rows, or a part's own padded length
+  auto part_stride = [&](int ch) -> size_t {
+    return !fixed ? n : nch > 1 ? std::max<size_t>(kSortB, rnd(pstart[ch + 1] - pstart[ch])) : ft->npad;
+  };
+  // the sort scratch, shared by the parts (their kernels run in stream order),
+  // sized for the largest before anything is queued
+  for (int ch = 0; ch < nch; ch++) {
+    const PartGeom q = geom(part_stride(ch));
+    if ((rc = ctx->digits.ensure(q.nW * (d16 ? 2 : 4)))) return rc;
+    if ((rc = ctx->mid.ensure(q.nW * (q.wide ? 8 : 4)))) return rc;
+    if ((rc = ctx->counts.ensure(q.TOTB * 4))) return rc;
+    if ((rc = ctx->cursor.ensure(q.TOTB * 4))) return rc;
+    if ((rc = ctx->bsum.ensure((size_t)q.nb * 4))) return rc;
+  }
+  for (int ch = 0; ch < nch; ch++) {
+    const hipStream_t cs = st;
+    const size_t c0 = pstart[ch], nc = pstart[ch + 1] - c0;
+    const size_t stride = part_stride(ch);
+    const PartGeom q = geom(stride);
+    const size_t E = q.E, nW = q.nW, TOTB = q.TOTB;
+    SortGeom g = q.g;
+    SortGeom gm = q.gm;
+    const ScanTiles tiles = q.tiles;
+    const uint32_t nb = q.nb;
+    const bool wide = q.wide;
     // a part's entries carry table indices j npad + c0 + i (k_sort_coarse)
     gm.rstride = (uint32_t)stride;
-    gm.rdelta = nch == 2 ? (uint32_t)(ft->npad - stride) : 0u;
-    gm.roff = nch == 2 ? (uint32_t)c0 : 0u;
-    const size_t TOTB = (size_t)pl.W * g.NCB * g.nblk + 1;
-    // 4-B coarse entries when the entry index fits beside the fine bits and the sign
-    const size_t imax = nch == 2 ? (size_t)kmerge * ft->npad : E;
-    const bool wide = imax > (size_t(1) << (31 - g.FB));
-    Buf& b_digits = ch ? ctx->digits2 : ctx->digits;
-    Buf& b_sorted = ch ? ctx->sorted2 : ctx->sorted;
-    Buf& b_mid = ch ? ctx->mid2 : ctx->mid;
-    Buf& b_counts = ch ? ctx->counts2 : ctx->counts;
-    Buf& b_cursor = ch ? ctx->cursor2 : ctx->cursor;
-    Buf& b_offsets = ch ? ctx->offsets2 : ctx->offsets;
-    Buf& b_bsum = ch ? ctx->bsum2 : ctx->bsum;
-    Buf& b_buckets = ch ? ctx->buckets2 : ctx->buckets;
-    Buf& b_head = ch ? ctx->head2 : ctx->head;
+    gm.rdelta = nch > 1 ? (uint32_t)(ft->npad - stride) : 0u;
+    gm.roff = nch > 1 ? (uint32_t)c0 : 0u;
+    // each part keeps its sorted list and bucket partials for the reduction
+    Buf& b_digits = ctx->digits;
+    Buf& b_mid = ctx->mid;
+    Buf& b_counts = ctx->counts;
+    Buf& b_cursor = ctx->cursor;
+    Buf& b_bsum = ctx->bsum;
+    Buf& b_sorted = ch ? ctx->part_sorted[ch - 1] : ctx->sorted;
+    Buf& b_offsets = ch ? ctx->part_offsets[ch - 1] : ctx->offsets;
+    Buf& b_buckets = ch ? ctx->part_buckets[ch - 1] : ctx->buckets;
+    Buf& b_head = ch ? ctx->part_head[ch - 1] : ctx->head;
     // accumulation lanes: each part's own plan (~4 waves per SIMD; a part's
     // buckets reach as many slices as a full sort's).  The whole MSM's slice
     // length instead (fewer lanes, shorter chains) measured the same with
     // equal halves and 0.17 ms slower with a 3/8 first part (1.5 waves per
     // SIMD in its accumulation)
-    const uint32_t chunk = nch == 2 ? make_plan_fixed(stride, ft->c, ctx->min_chunk).chunk : pl.chunk;
-    const uint32_t nthreads = nch == 2 ? (uint32_t)((nW + chunk - 1) / chunk) : pl.nthreads;
-    if ((rc = b_digits.ensure(nW * (d16 ? 2 : 4)))) return rc;
+    const uint32_t chunk = nch > 1 ? make_plan_fixed(stride, ft->c, ctx->min_chunk).chunk : pl.chunk;
+    const uint32_t nthreads = nch > 1 ? (uint32_t)((nW + chunk - 1) / chunk) : pl.nthreads;
     if ((rc = b_sorted.ensure(nW * 4))) return rc;
-    if ((rc = b_mid.ensure(nW * (wide ? 8 : 4)))) return rc;
-    if ((rc = b_counts.ensure(TOTB * 4))) return rc;
-    if ((rc = b_cursor.ensure(TOTB * 4))) return rc;
     if ((rc = b_offsets.ensure(TOT * 4))) return rc;
-    const ScanTiles tiles = scan_tiles((uint32_t)(pl.W * g.NCB), (uint32_t)g.nblk);  // k_sort_hist's layout
-    const uint32_t nb = (uint32_t)((TOTB + tiles.chunk - 1) / tiles.chunk);
-    if ((rc = b_bsum.ensure((size_t)nb * 4))) return rc;
     if ((rc = b_buckets.ensure((size_t)Wr * pl.NB * sizeof(Xyzz<F>)))) return rc;
     if ((rc = b_head.ensure((size_t)nthreads * sizeof(Xyzz<F>)))) return rc;
 
@@ -368,16 +408,19 @@ int msm_device_impl(Ctx* ctx, const uint32_t* d_scalars, const uint32_t* d_bases
     PM_LAUNCH_ST(ctx, cs, "accumulate",
                  (k_accumulate<F><<<(nthreads + 255) / 256, 256, 0, cs>>>(sorted, offsets, s1, bases29, chunk,
                                                                           buckets, head)));
-    co[ch] = SegChunk<F>{offsets, chunk, nthreads, buckets, head};
+    co.c[ch] = SegChunk<F>{offsets, chunk, nthreads, buckets, head};
   }
   // chains (long ones wave-cooperatively) + segment sums + the top bucket
   const unsigned seg_blocks = (unsigned)((4ull * Wr * pl.M1 + 255) / 256);
-  if (nch == 2)
-    PM_LAUNCH(ctx, "bucket_seg", (k_bucket_seg_q<F, 2><<<seg_blocks, 256, 0, st>>>(co[0], co[1], Wr, pl.NB,
-                                                                                   (uint32_t)pl.M1, S, T, Qd, NQ)));
+  if (nch == 3)
+    PM_LAUNCH(ctx, "bucket_seg", (k_bucket_seg_q<F, 3><<<seg_blocks, 256, 0, st>>>(co, Wr, pl.NB, (uint32_t)pl.M1, S, T,
+                                                                                   Qd, NQ)));
+  else if (nch == 2)
+    PM_LAUNCH(ctx, "bucket_seg", (k_bucket_seg_q<F, 2><<<seg_blocks, 256, 0, st>>>(co, Wr, pl.NB, (uint32_t)pl.M1, S, T,
+                                                                                   Qd, NQ)));
   else
-    PM_LAUNCH(ctx, "bucket_seg", (k_bucket_seg_q<F, 1><<<seg_blocks, 256, 0, st>>>(co[0], co[0], Wr, pl.NB,
-                                                                                   (uint32_t)pl.M1, S, T, Qd, NQ)));
+    PM_LAUNCH(ctx, "bucket_seg", (k_bucket_seg_q<F, 1><<<seg_blocks, 256, 0, st>>>(co, Wr, pl.NB, (uint32_t)pl.M1, S, T,
+                                                                                   Qd, NQ)));
   // bit sums of few sets (the row tables, the fixed-base MSM's one set) are
   // split over more blocks.  Every extra lane also adds one tree addition, so
   // the split stops at ~16 blocks per job (c = 20, 2^19 buckets: 16 -> 0.33

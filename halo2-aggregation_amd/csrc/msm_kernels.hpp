@@ -917,11 +917,16 @@ __device__ __forceinline__ void seg_fold_chunk(const SegChunk<F>& c, bool valid,
     if (ln == (uint32_t)L) B = xyzz29_add<F>(B, cs);
   }
 }
-// NCH = 2: the bucket sums of the split copy's two sorted lists (c2 unused
-// with NCH = 1)
+// the sorted lists of one MSM: 1, or the split scalar copy's parts
+constexpr int kMaxParts = 3;
+template <class F>
+struct SegChunks {
+  SegChunk<F> c[kMaxParts];
+};
+// NCH > 1: the bucket sums of the split copy's NCH sorted lists
 template <class F, int NCH>
-__global__ void __launch_bounds__(256, 2) k_bucket_seg_q(SegChunk<F> c1, SegChunk<F> c2, int Wr, int NB,
-                                                      uint32_t M1, Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T,
+__global__ void __launch_bounds__(256, 2) k_bucket_seg_q(SegChunks<F> cs, int Wr, int NB, uint32_t M1,
+                                                      Xyzz<F>* __restrict__ S, Xyzz<F>* __restrict__ T,
                                                       Xyzz<F>* __restrict__ Q, int NQ) {
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t g = gl >> 2, q = gl & 3u;
@@ -931,8 +936,9 @@ __global__ void __launch_bounds__(256, 2) k_bucket_seg_q(SegChunk<F> c1, SegChun
   const bool top = valid && j == 0 && q == 0;
   const size_t slot = (size_t)w * NB + (top ? M1 * kSegQ : j * kSegQ + q);
   Xyzz29<F> B = xyzz29_inf<F>();
-  seg_fold_chunk<F, true>(c1, valid, slot, B);
-  if constexpr (NCH == 2) seg_fold_chunk<F, false>(c2, valid, slot, B);
+  seg_fold_chunk<F, true>(cs.c[0], valid, slot, B);
+#pragma unroll
+  for (int k = 1; k < NCH; k++) seg_fold_chunk<F, false>(cs.c[k], valid, slot, B);
   // broadcast each lane's sum only when it is consumed (fewer live points)
   const Xyzz29<F> B3 = xyzz29_qbc<3, F>(B);
   const Xyzz29<F> p23 = xyzz29_add_q<F>(xyzz29_qbc<2, F>(B), B3);

@@ -48,6 +48,7 @@ constexpr int kBitsSplitK = 16;
 constexpr size_t kDropinMinN = size_t(1) << 12;
 // the split scalar copy of row-table MSMs with host scalars (engine.hpp)
 constexpr size_t kSplitCopyMinN = PM_SPLIT_COPY_MIN_N;
+constexpr size_t kSplitCopy3MinN = size_t(1) << 21;  // three parts from here (measured at 2^20 and 2^22)
 constexpr int kDropinEntries = 4;
 constexpr size_t kDropinBytes = size_t(16) << 30;
 // ... and at most this fraction (1/kDropinFreeDiv) of the device memory free
@@ -258,8 +259,9 @@ struct pm_ctx {
   pm::Buf in_scalars, in_scalars2, in_bases, digits, sorted, counts, offsets, cursor, bsum, buckets, head, segS, segT, bits,
       win, longs, mid, acc_coef, acc_part, acc_io, bases29, tr_io, bitsP, tickets, ntt_scratch, bitsQ, acc_lad, acc_corr, tr_canon, ntt_scratch2,
       acc_vkpow, small_tab, small_dig, small_part, small_tk;
-  // the second part's sort / accumulation buffers of the split scalar copy (engine.hpp)
-  pm::Buf digits2, sorted2, counts2, offsets2, cursor2, bsum2, buckets2, head2, mid2;
+  // the later parts' sorted lists and bucket partials of the split scalar
+  // copy (engine.hpp; the sort scratch is shared, its kernels run in order)
+  pm::Buf part_sorted[2], part_offsets[2], part_buckets[2], part_head[2];
   pm::CachedUpload acc_prog, acc_const, acc_vk, tr_prog;
   pm::CachedUpload tr_wtab;  // streamed transcript: word table of the shape's byte stream
   pm::CachedUpload many_prog;  // pm_msm_resident_many*: job + MSM tables
@@ -295,7 +297,7 @@ struct pm_ctx {
   std::vector<pm::Buf*> all_bufs() {
     return {&in_scalars, &in_scalars2, &in_bases, &digits, &sorted, &counts, &offsets, &cursor,
             &bsum,       &buckets,  &head,   &segS,   &segT,   &bits,    &win, &longs, &mid,
-            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &acc_corr, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &pf_flags, &small_tab, &small_dig, &small_part, &small_tk, &many_prog.buf, &tr_wtab.buf, &digits2, &sorted2, &counts2, &offsets2, &cursor2, &bsum2, &buckets2, &head2, &mid2};
+            &acc_prog.buf, &acc_const.buf, &acc_vk.buf, &acc_coef, &acc_part, &acc_io, &bases29, &tr_prog.buf, &tr_io, &bitsP, &tickets, &ntt_scratch, &bitsQ, &acc_lad, &acc_corr, &tr_canon, &ntt_scratch2, &acc_vkpow, &sqrt_tab[0], &sqrt_tab[1], &sqrt_tab[2], &pf_map.buf, &pf_io, &pf_flags, &small_tab, &small_dig, &small_part, &small_tk, &many_prog.buf, &tr_wtab.buf, &part_sorted[0], &part_sorted[1], &part_offsets[0], &part_offsets[1], &part_buckets[0], &part_buckets[1], &part_head[0], &part_head[1]};
   }
   ~pm_ctx();
   int begin_call();

@@ -135,9 +135,10 @@ int pm_ctx_set_accum_option(pm_ctx* ctx, int option, int value);
  *                           resident row table with scalars in host memory
  *                           (pm_msm_resident, the drop-in pm_msm's warm
  *                           calls) of at least PM_SPLIT_COPY_MIN_N points
- *                           copies the scalars in two parts (3/8, 5/8) and
- *                           sorts and accumulates the first while the second
- *                           crosses PCIe.
+ *                           copies the scalars in two parts (3/8, 5/8;
+ *                           three from 2^21 points) and sorts and
+ *                           accumulates each part while the next crosses
+ *                           PCIe.
  * PM_ERR_ARG for an unknown option or a value out of range. */
 #define PM_SPLIT_COPY_MIN_N 262144
 enum { PM_MSM_OPT_SPLIT_COPY = 1 };

@@ -76,7 +76,7 @@ def test_device_code_has_every_launched_kernel():
         return sum(1 for n in names if stem in n)
 
     assert count("11k_sort_hist") == 3 * 16 * 2  # 3 scalar fields x 16 window counts x {2-B, 4-B digits}
-    assert count("14k_bucket_seg_q") == 3 * 2  # one sorted list / the split scalar copy's two (round 6)
+    assert count("14k_bucket_seg_q") == 3 * 3  # one sorted list / the split scalar copy's two or three (round 6)
     for stem in ("12k_accumulate", "13k_bucket_bits", "15k_bases_to_r261",
                  "16k_selftest_field", "9k_acc_sum", "13k_acc_scalars", "12k_acc_powers",
                  "15k_synth_scalars", "13k_synth_bases", "14k_transcript_s", "12k_transcriptI", "14k_acc_powers_s"):

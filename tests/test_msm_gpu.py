@@ -445,10 +445,11 @@ def test_dropin_row_table(gpu_ctx):
 @pytest.mark.parametrize("curve", [0, 2])
 def test_split_scalar_copy(gpu_ctx, curve):
     """Row-table MSMs with host scalars from PM_SPLIT_COPY_MIN_N points copy
-    the scalars in two parts (3/8, 5/8), each sorted and accumulated on its
-    own, with one bucket reduction over both sorted lists
-    (k_bucket_seg_q<F, 2>): ragged parts, lengths at and just above the
-    threshold, a giant bucket that spans both parts, the fixed-base MSM, and
+    the scalars in two parts (3/8, 5/8; three from 2^21 points), each sorted
+    and accumulated on its own, with one bucket reduction over the parts'
+    sorted lists (k_bucket_seg_q<F, 2 | 3>): ragged parts, lengths at and just
+    above the threshold, a giant bucket that spans both parts, three parts,
+    the fixed-base MSM, and
     the one-copy schedule (pm_ctx_set_msm_option MSM_OPT_SPLIT_COPY = 0) all
     equal the device-input MSM."""
     import torch
@@ -483,6 +484,16 @@ def test_split_scalar_copy(gpu_ctx, curve):
             assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S[:m]), want), m
         finally:
             rb.release()
+    # three parts from 2^21 points (ragged last part)
+    m = (1 << 21) + 77
+    s3, b3 = _torch_inputs(gpu_ctx, curve, m)
+    rb = gpu_ctx.upload_bases(curve, d_bases=b3.data_ptr(), n=m)
+    try:
+        want = gpu_ctx.msm_resident_device(rb, 0, s3.data_ptr(), m)
+        assert np.array_equal(gpu_ctx.msm_resident(rb, 0, s3.cpu().numpy().view(np.uint64).copy()), want)
+    finally:
+        rb.release()
+    del s3, b3
     # the fixed-base MSM (one merged bucket set) with host scalars
     m = (1 << 18) + 5
     fb = gpu_ctx.fixed_bases(curve, d_bases=b.data_ptr(), n=m)
