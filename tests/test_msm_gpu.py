@@ -420,6 +420,8 @@ def test_dropin_row_table(gpu_ctx):
     """A full-length repeated set from 2^18 points runs as a resident
     row-table MSM once admitted (second call); pm_msm_resident / pm_msm_fixed
     with host scalars; all equal the device-input MSM."""
+    import torch
+
     n = (1 << 18) + 11
     s, b = _torch_inputs(gpu_ctx, 0, n)
     want = gpu_ctx.msm_device(0, s.data_ptr(), b.data_ptr(), n)
@@ -431,6 +433,15 @@ def test_dropin_row_table(gpu_ctx):
             assert np.array_equal(ctx.msm(0, S, B), want)
         st = ctx.dropin_stats()
         assert st["hits"] == 2 and st["misses"] == 2 and st["entries"] == 1
+        # a middle base changed: the speculative row-table MSM (split scalar
+        # copy) starts on the predicted set, the digest names no set, the
+        # speculative result is drained and the call runs as a miss
+        kept, drained = ctx.dropin_spec_stats()
+        Bm = B.copy()
+        Bm[n // 2] = B[3]
+        wm = gpu_ctx.msm_device(0, s.data_ptr(), torch.from_numpy(Bm.view(np.int64)).to(b.device).data_ptr(), n)
+        assert np.array_equal(ctx.msm(0, S, Bm), wm)
+        assert ctx.dropin_spec_stats() == (kept, drained + 1)
         rb = ctx.upload_bases(0, d_bases=b.data_ptr(), n=n)
         assert rb.rows > 1
         assert np.array_equal(ctx.msm_resident(rb, 0, S), want)
