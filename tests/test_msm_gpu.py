@@ -479,6 +479,9 @@ def test_split_scalar_copy(gpu_ctx, curve):
                 assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S[:m]), want), m
             finally:
                 gpu_ctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, -1)
+        # canonical scalars (PM_SCALARS_CANONICAL) through both parts
+        want = gpu_ctx.msm_resident_device(rb, 0, s.data_ptr(), n, canonical=True)
+        assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S, canonical=True), want)
         # every scalar equal: one giant bucket per window, in both parts' lists
         e = s[7:8].repeat(n, 1).contiguous()
         torch.cuda.synchronize()
