@@ -50,7 +50,14 @@ def main():
                 dctx.set_msm_option(H.MSM_OPT_SPLIT_COPY, mode)
                 ms, got = timed(lambda: ctx.msm_resident(rb, 0, S), reps)
                 dms, dgot = timed(lambda: dctx.msm(curve, S, B), reps)
+                ctx.set_timing(True, only="bucket_seg")
+                ctx.reset_stats()
+                for _ in range(5):
+                    ctx.msm_resident(rb, 0, S)
+                ctx.set_timing(False)
+                seg = ctx.kernel_stats("bucket_seg")[1] / 5
                 print(json.dumps({"logn": lg, "round": rnd, "split_copy": "auto" if mode < 0 else "off",
+                                  "bucket_seg_ms": round(seg, 4),
                                   "pm_msm_resident_ms": round(ms, 4), "dropin_pm_msm_ms": round(dms, 4),
                                   "matches": bool(np.array_equal(got, want) and np.array_equal(dgot, want))}),
                       flush=True)
