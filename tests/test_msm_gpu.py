@@ -498,15 +498,23 @@ def test_split_scalar_copy(gpu_ctx, curve):
             assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S[:m]), want), m
         finally:
             rb.release()
-    # three parts from 2^21 points (ragged last part)
+    # three parts from 2^21 points (ragged last part); and the fixed-base
+    # table past 2^21 points (c = 20, 13 merged windows: 8-B sort entries)
     m = (1 << 21) + 77
     s3, b3 = _torch_inputs(gpu_ctx, curve, m)
+    S3 = s3.cpu().numpy().view(np.uint64).copy()
     rb = gpu_ctx.upload_bases(curve, d_bases=b3.data_ptr(), n=m)
     try:
         want = gpu_ctx.msm_resident_device(rb, 0, s3.data_ptr(), m)
-        assert np.array_equal(gpu_ctx.msm_resident(rb, 0, s3.cpu().numpy().view(np.uint64).copy()), want)
+        assert np.array_equal(gpu_ctx.msm_resident(rb, 0, S3), want)
     finally:
         rb.release()
+    fb = gpu_ctx.fixed_bases(curve, d_bases=b3.data_ptr(), n=m)
+    try:
+        assert fb.c == 20
+        assert np.array_equal(fb.msm(S3), want)
+    finally:
+        fb.release()
     del s3, b3
     # the fixed-base MSM (one merged bucket set) with host scalars
     m = (1 << 18) + 5
