@@ -82,3 +82,16 @@ def test_dry_run_line():
     line = json.loads(last)
     for k in CONTRACT:
         assert k in line
+
+
+def test_final_record_host_scalar_legs():
+    """The final round-6 record (the split scalar copy): the host-scalar legs'
+    summaries carry the one-copy comparison, and the whole line compacts
+    under the limit with every leg matching."""
+    out = json.load(open(os.path.join(ROOT, "profiles", "r06", "bench_r06_final3_detail.json")))
+    line = json.loads(bench.compact_line(out))
+    legs = line["legs"]
+    for k in ("host_scalars", "dropin_pm_msm"):
+        assert legs[k]["one_copy_ms"] > legs[k]["ms"] > 0, k
+        assert legs[k]["matches"] is True, k
+    assert all(v.get("matches", True) for v in legs.values())
